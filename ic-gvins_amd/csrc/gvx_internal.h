@@ -1,0 +1,113 @@
+// gvx_internal.h -- shared host-side definitions of libgvx (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gvx.h"
+
+namespace gvx {
+
+// Pyramid storage (DESIGN.md "HBM layout"): every level is stored
+// with a PAD-pixel BORDER_REFLECT_101 ring so that LK window gathers (including
+// the Scharr halo and 16-byte aligned row loads) never leave the allocation.
+// OpenCV pads by winSize (21); the extra ring beyond 21 px is never read by a
+// valid computation.
+constexpr int PAD = 32;
+constexpr int MAX_LEVELS = 7;
+constexpr int WIN = 21;  // the device LK kernel is specialised for 21x21
+
+struct PyrLayout {
+    int32_t nlev;                  // levels built (maxLevel actually used + 1)
+    int32_t w[MAX_LEVELS], h[MAX_LEVELS];
+    int32_t pitch[MAX_LEVELS];     // bytes per padded row (multiple of 64)
+    int64_t off[MAX_LEVELS];       // byte offset of padded (-PAD,-PAD) of level l
+    int64_t bytes;                 // bytes per image pyramid (multiple of 256)
+};
+
+// buildOpticalFlowPyramid's level count rule (stop when the next level would be
+// <= win on either side) -- identical for both images of a pair.
+PyrLayout make_layout(int w, int h, int max_level, int win);
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Frame {
+    PyrLayout lay;
+    uint8_t* pyr = nullptr;  // device
+    int w = 0, h = 0;
+};
+
+struct ProfEntry {
+    double ms = 0;
+    int64_t launches = 0;
+};
+
+}  // namespace gvx
+
+struct gvx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::unordered_map<uint64_t, gvx::Frame> frames;
+    // scratch (grown on demand, never shrunk)
+    std::map<std::string, gvx::DevBuf> dev;
+    std::map<std::string, gvx::DevBuf> pinned;
+    // profiling
+    bool prof = false;
+    std::map<std::string, gvx::ProfEntry> prof_acc;
+    struct Pending {
+        std::string fam;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace gvx {
+
+gvx_status set_err(gvx_ctx* c, gvx_status s, const char* fmt, ...);
+gvx_status hip_err(gvx_ctx* c, hipError_t e, const char* what);
+void* scratch(gvx_ctx* c, const std::string& name, size_t bytes);   // device
+void* pinned(gvx_ctx* c, const std::string& name, size_t bytes);    // pinned host
+
+// Profiling brackets around a kernel family launch (no-ops when disabled).
+void prof_begin(gvx_ctx* c, const char* fam, hipEvent_t* a);
+void prof_end(gvx_ctx* c, const char* fam, hipEvent_t a);
+void prof_drain(gvx_ctx* c);
+
+// ---- kernel launchers (klt.hip) ----
+// Build pyramids for n_img images (h x w, row stride `stride` bytes, image i at
+// src + i*img_stride) into dst + i*lay.bytes.
+hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride,
+                                 int n_img, const PyrLayout& lay, uint8_t* dst);
+
+struct KltArgs {
+    int32_t n_pairs, n_pts;
+    int32_t max_iter;
+    double crit_eps;         // eps*eps (double, like OpenCV criteria.epsilon)
+    float min_eig;
+    int32_t use_initial_flow;
+    int32_t mode;            // 0: single LK, 1: fwd + bwd + FB
+    double fb_thresh, border;
+    int32_t cam_w, cam_h;
+};
+
+// Pyramid of pair i: prev at pyr_prev + idx_prev[i]*lay.bytes (idx arrays may be
+// null => i); likewise next.
+hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                      const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                      const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                      float* err);
+hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
+                          int32_t* n_kept);
+
+}  // namespace gvx

@@ -1,0 +1,232 @@
+/*
+ * gvx.h -- C ABI of the MI355X-native IC-GVINS front end (libgvx.so).
+ *
+ * Plain C types only (no HIP, torch or C++ types in any signature).  Every call
+ * returns gvx_status (0 = OK, negative = error; gvx_last_error() has the text);
+ * no exception crosses the ABI.  Calls are synchronous unless their name ends in
+ * _dev (device pointers, enqueued on the context stream; gvx_sync() waits).
+ * One context per host thread, or serialise calls on a shared context.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to /root/reference/ic_gvins/ic_gvins/).
+ */
+#ifndef GVX_H
+#define GVX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t gvx_status;
+enum {
+    GVX_OK = 0,
+    GVX_ERR_INVALID = -1,   /* bad argument (the reference would throw cv::Exception / assert) */
+    GVX_ERR_NO_DEVICE = -2, /* no gfx950 device / HIP runtime unavailable */
+    GVX_ERR_HIP = -3,       /* a HIP runtime call failed */
+    GVX_ERR_OOM = -4,       /* device or host allocation failed */
+    GVX_ERR_NOT_FOUND = -5, /* unknown frame id */
+    GVX_ERR_UNSUPPORTED = -6
+};
+
+typedef struct gvx_ctx gvx_ctx;
+
+/* ---------------------------------------------------------------- context */
+gvx_status gvx_create(int32_t device, gvx_ctx** out);
+void gvx_destroy(gvx_ctx* ctx);
+const char* gvx_status_string(gvx_status s);
+const char* gvx_last_error(const gvx_ctx* ctx);
+gvx_status gvx_sync(gvx_ctx* ctx);
+/* The hipStream_t all work of this context is enqueued on (opaque). */
+void* gvx_get_stream(gvx_ctx* ctx);
+/* Library version string, e.g. "gvx 0.1 gfx950". */
+const char* gvx_version(void);
+
+/* Per-kernel-family device time, accumulated with HIP events on the context
+   stream while enabled (used by bench.py's roofline).  family: "pyramid",
+   "klt", "compact", "detect", "preint", "reproj", "preint_factor". */
+gvx_status gvx_profile_enable(gvx_ctx* ctx, int32_t on);
+gvx_status gvx_profile_read(gvx_ctx* ctx, const char* family, double* total_ms, int64_t* launches);
+gvx_status gvx_profile_reset(gvx_ctx* ctx);
+
+/* ------------------------------------------------------------------ KLT  */
+/* cv::calcOpticalFlowPyrLK arguments as used at tracking/tracking.cc:385-393:
+   Size(21,21), maxLevel TRACK_PYRAMID_LEVEL=3 (tracking/tracking.h:113),
+   TermCriteria(COUNT+EPS, 30, 0.01), OPTFLOW_USE_INITIAL_FLOW, minEig 1e-4. */
+typedef struct {
+    int32_t win;              /* window side; the device path supports 21 */
+    int32_t max_level;        /* <= 6 */
+    int32_t max_iter;         /* TermCriteria COUNT, clamped to [0,100] like OpenCV */
+    double eps;               /* TermCriteria EPS (squared internally) */
+    int32_t use_initial_flow; /* OPTFLOW_USE_INITIAL_FLOW */
+    float min_eig;            /* minEigThreshold */
+} gvx_klt_params;
+void gvx_klt_params_default(gvx_klt_params* p);
+
+/* Upload one gray u8 frame (Frame::image() after CLAHE, tracking/frame.h:62-64)
+   and build its padded pyramid on the device once; replaces the per-call
+   buildOpticalFlowPyramid inside each of the four cv::calcOpticalFlowPyrLK calls
+   per frame (tracking/tracking.cc:385,390,487,493).  Re-putting an id replaces it. */
+gvx_status gvx_frame_put(gvx_ctx* ctx, uint64_t id, const uint8_t* gray, int32_t w, int32_t h,
+                         int32_t stride, const gvx_klt_params* p);
+gvx_status gvx_frame_drop(gvx_ctx* ctx, uint64_t id);
+
+/* One cv::calcOpticalFlowPyrLK(prev, next, prevPts, nextPts, status, err, ...)
+   on cached frames.  next_xy is in/out when use_initial_flow.  n may be 0. */
+gvx_status gvx_klt(gvx_ctx* ctx, uint64_t prev_id, uint64_t next_id, const float* prev_xy,
+                   float* next_xy, uint8_t* status, float* err, int32_t n, const gvx_klt_params* p);
+
+/* Fused replacement of tracking/tracking.cc:380-408 (and :482-511):
+   forward LK prev->next with initial flow next_xy, backward LK next->prev with
+   initial flow prev_xy, keep = st_f && st_b && !isOnBorder(next) &&
+   ptsDistance(back, prev) < fb_thresh (tracking.cc:396-403, :841-849), then the
+   order-preserving reduceVector compaction (tracking.cc:831-839) as an index
+   list.  Outputs: next_xy (forward result), back_xy, status_fwd, status_bwd,
+   keep[n], kept_idx[*n_kept].  border = 5.0, fb_thresh = 0.5 in the reference;
+   cam_w/cam_h = camera_->width()/height(). Any output pointer except next_xy and
+   n_kept may be NULL. */
+gvx_status gvx_klt_fb(gvx_ctx* ctx, uint64_t prev_id, uint64_t next_id, const float* prev_xy,
+                      float* next_xy, float* back_xy, uint8_t* status_fwd, uint8_t* status_bwd,
+                      uint8_t* keep, int32_t* kept_idx, int32_t* n_kept, int32_t n,
+                      double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                      const gvx_klt_params* p);
+
+/* Batched frame-pair unit, device pointers, async on the context
+   stream: for each pair i, build the pyramids of prev[i] and next[i]
+   (h x w u8, tightly packed, pair-major), run gvx_klt_fb on n_pts points
+   (prev_xy/next_xy/back_xy: n_pairs x n_pts x 2 f32), write flags
+   (bit0 fwd status, bit1 bwd status, bit2 keep; n_pairs x n_pts u8),
+   kept_idx (n_pairs x n_pts) and n_kept (n_pairs). */
+gvx_status gvx_klt_fb_batch_dev(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h,
+                                const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
+                                const float* d_prev_xy, float* d_next_xy, float* d_back_xy,
+                                uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                const gvx_klt_params* p);
+/* Host-pointer convenience wrapper of the above (copies in and out, synchronous). */
+gvx_status gvx_klt_fb_batch(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h,
+                            const uint8_t* prev, const uint8_t* next, int32_t n_pts,
+                            const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                            int32_t* kept_idx, int32_t* n_kept, double fb_thresh, double border,
+                            int32_t cam_w, int32_t cam_h, const gvx_klt_params* p);
+
+/* Debug/parity hook: copy level `level` of a cached frame's pyramid (unpadded,
+   w_l x h_l, tightly packed) to host.  Returns GVX_ERR_INVALID past the top. */
+gvx_status gvx_frame_level(gvx_ctx* ctx, uint64_t id, int32_t level, uint8_t* out, int32_t* w,
+                           int32_t* h);
+
+/* ------------------------------------------------------ feature detection */
+/* Tracking::featuresDetection (tracking/tracking.cc:576-688): block grid from
+   the Tracking ctor (:65-85), FILLED circle mask of radius
+   track_min_pixel_distance_ (:609-620), per block goodFeaturesToTrack
+   (quality 0.01, blockSize 3) + cornerSubPix(5x5, 20 it, 0.01) (:647-651). */
+typedef struct {
+    double block_size;   /* TRACK_BLOCK_SIZE = 200 */
+    int32_t max_features;/* track_max_features */
+    double quality;      /* 0.01 */
+    int32_t subpix_win;  /* 5 */
+    int32_t subpix_iters;/* 20 */
+    double subpix_eps;   /* 0.01 */
+} gvx_detect_params;
+void gvx_detect_params_default(gvx_detect_params* p);
+
+/* count_xy: key points counted per block (frame->features() + pts2d_new_);
+   mask_xy: circle centres (frame_cur_->features() + pts2d_new_); ismask as in
+   the reference; n_existing = features + pts2d_ref_ for the early exit
+   (*n_out = -1 when it triggers).  out_xy holds up to block_cnts *
+   max_block_features points, block-major like the reference's merge loop;
+   out_block_counts has block_cnts entries. */
+gvx_status gvx_detect(gvx_ctx* ctx, uint64_t frame_id, const float* count_xy, int32_t n_count,
+                      const float* mask_xy, int32_t n_mask, int32_t ismask, int32_t n_existing,
+                      const gvx_detect_params* p, float* out_xy, int32_t* out_block_counts,
+                      int32_t* n_out);
+
+/* --------------------------------------------------- IMU preintegration */
+enum { GVX_PREINT_NORMAL = 0, GVX_PREINT_EARTH = 2 }; /* preintegration.h:38-43 */
+
+/* IMU record, common/types.h:50-58. */
+typedef struct {
+    double time, dt, dtheta[3], dvel[3], odovel;
+} gvx_imu;
+
+/* IntegrationParameters subset on the path (preintegration/integration_state.h:68-89). */
+typedef struct {
+    double acc_vrw, gyr_arw, gyr_bias_std, acc_bias_std, corr_time, gravity;
+} gvx_imu_params;
+
+/* IntegrationState core (integration_state.h:35-51); q = (x, y, z, w). */
+typedef struct {
+    double time;
+    double p[3], q[4], v[3], bg[3], ba[3];
+} gvx_state;
+
+/* A PreintegrationBase after its segment: deltaState(), currentState(),
+   deltaTime(), jacobian_, covariance_ (row-major 15x15), plus what the Earth
+   variant's evaluate() needs (iewn_, gravity_). */
+typedef struct {
+    int32_t variant, m; /* m = imu_buffer_.size() */
+    double delta_time, start_time, end_time;
+    gvx_state current, delta;
+    double gravity[3], iewn[3], q0[4];
+    double jacobian[225];
+    double covariance[225];
+} gvx_preint_result;
+
+/* Preintegration::createPreintegration + addNewImu(series[k]), k = 1..m-1
+   (ic_gvins.cc:946-953, preintegration_base.cc:72-75), batched over segments:
+   segment s uses imu[seg_off[s] .. seg_off[s+1]) and state0[s]; iewn[s] is the
+   Earth rate computed by the caller as PreintegrationEarth::resetState does
+   (gvx_earth_iewn); ignored for NORMAL.  pn (Earth only, may be NULL) receives
+   the pn_ list {dt, p[3]} per integrated step: (seg_off[s]-s) * 4 doubles
+   offset for segment s.  One wavefront per segment. */
+gvx_status gvx_preint_integrate(gvx_ctx* ctx, int32_t variant, const gvx_imu_params* prm,
+                                int32_t n_seg, const gvx_imu* imu, const int32_t* seg_off,
+                                const gvx_state* state0, const double* iewn,
+                                gvx_preint_result* out, double* pn);
+gvx_status gvx_preint_integrate_dev(gvx_ctx* ctx, int32_t variant, const gvx_imu_params* prm,
+                                    int32_t n_seg, const gvx_imu* d_imu, const int32_t* d_seg_off,
+                                    const gvx_state* d_state0, const double* d_iewn,
+                                    gvx_preint_result* d_out, double* d_pn);
+
+/* Earth::iewn(station, p) (common/earth.h:233-237), host-side helper used by
+   resetState (preintegration_earth.cc:320). */
+void gvx_earth_iewn(const double origin[3], const double local[3], double iewn[3]);
+
+/* ------------------------------------------------------ factor batches */
+/* PreintegrationFactor::Evaluate (preintegration/preintegration_factor.h:45-69)
+   for n factors: factor i uses pre[i], pn list at pn[pn_off[i]*4 ...]
+   (pre[i].m - 1 entries), and parameter blocks params + offs[4i+k] (k:
+   pose0[7], mix0[9], pose1[7], mix1[9]).  residuals n x 15; jacobians (may be
+   NULL) n x 480 doubles = [J_pose0 15x7 | J_mix0 15x9 | J_pose1 15x7 |
+   J_mix1 15x9], each row-major like Ceres. */
+gvx_status gvx_preint_factor_eval(gvx_ctx* ctx, int32_t n, const gvx_preint_result* pre,
+                                  const double* pn, const int32_t* pn_off, const double* params,
+                                  const int32_t* offs, double* residuals, double* jacobians);
+gvx_status gvx_preint_factor_eval_dev(gvx_ctx* ctx, int32_t n, const gvx_preint_result* d_pre,
+                                      const double* d_pn, const int32_t* d_pn_off,
+                                      const double* d_params, const int32_t* d_offs,
+                                      double* d_residuals, double* d_jacobians);
+
+/* ReprojectionFactor constants (factors/reprojection_factor.h:47-58). */
+typedef struct {
+    double pts0[3], pts1[3], vel0[3], vel1[3], td0, td1, std;
+} gvx_reproj_const;
+
+/* ReprojectionFactor::Evaluate (factors/reprojection_factor.h:61-161) for n
+   factors; factor i reads params + offs[5i+k] (pose_ref[7], pose_obs[7],
+   ext[7], invdepth[1], td[1]).  residuals n x 2; jacobians (may be NULL)
+   n x 46 doubles = [J0 2x7 | J1 2x7 | J2 2x7 | J3 2x1 | J4 2x1]. */
+gvx_status gvx_reproj_eval(gvx_ctx* ctx, int32_t n, const gvx_reproj_const* c,
+                           const double* params, int32_t n_params, const int32_t* offs,
+                           double* residuals, double* jacobians);
+gvx_status gvx_reproj_eval_dev(gvx_ctx* ctx, int32_t n, const gvx_reproj_const* d_c,
+                               const double* d_params, const int32_t* d_offs,
+                               double* d_residuals, double* d_jacobians);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GVX_H */

@@ -1,0 +1,249 @@
+/*
+ * gvx_oracle.h -- CPU restatement of the IC-GVINS per-frame hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libgvx.so, the C ABI in
+ * include/gvx.h, the host mirror under ic-gvins_amd/) links, loads or calls
+ * this code.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg use it -- as the parity checker and as the timed CPU baseline.
+ *
+ * PARITY STATUS: the reference (WZXTP/IC-GVINS) cannot be built or imported in
+ * this environment (OpenCV, Eigen, Ceres absent -- SURVEY.md section 8c) and it
+ * ships no tests, golden vectors or fixtures for this path.  This restatement is
+ * therefore "parity unpinned" with respect to the real reference binaries.  It is
+ * pinned instead by analytic known-answer tests (integer-shift image pairs,
+ * constant/ramp pyramids, zero-rotation IMU segments, numeric-derivative checks
+ * of every factor Jacobian) in tests/test_oracle_*.py.
+ *
+ * What each function restates (file:line in /root/reference, or the un-vendored
+ * OpenCV 4.x routine the reference calls there):
+ *   orc_build_pyramid      cv::buildOpticalFlowPyramid + pyrDown, called inside
+ *                          cv::calcOpticalFlowPyrLK at
+ *                          ic_gvins/ic_gvins/tracking/tracking.cc:385,390,487,493
+ *   orc_scharr             calcSharrDeriv (same call sites)
+ *   orc_calc_optical_flow_pyr_lk   cv::calcOpticalFlowPyrLK / LKTrackerInvoker
+ *   orc_klt_fb             tracking.cc:383-408 (fwd + bwd LK, FB/border status,
+ *                          reduceVector tracking.cc:831-849)
+ *   orc_features_detection tracking.cc:576-688 (block grid, circle mask,
+ *                          goodFeaturesToTrack + cornerSubPix per block)
+ *   orc_preint_*           preintegration/preintegration_{base,earth,normal}.cc
+ *   orc_preint_factor_eval preintegration/preintegration_factor.h:45-69
+ *   orc_reproj_eval        factors/reprojection_factor.h:61-161
+ *
+ * Documented choices where the upstream arithmetic is build-dependent:
+ *   - LK window sums (A11/A12/A22, b1/b2) are exact int64 sums converted to
+ *     float once (OpenCV's x86 SIMD path accumulates float partials in 4-lane
+ *     groups; the result differs by float rounding only).
+ *   - All float/double expressions are evaluated left-to-right with no FMA
+ *     contraction (-ffp-contract=off), following OpenCV's scalar tail loops and
+ *     Eigen's coefficient-wise expression order.
+ */
+#ifndef GVX_ORACLE_H
+#define GVX_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------- */
+/* KLT (pyramidal Lucas-Kanade)                                               */
+/* ------------------------------------------------------------------------- */
+
+#define ORC_MAX_LEVELS 8
+
+typedef struct {
+    int win;            /* window side, 21 in the reference (tracking.cc:386) */
+    int max_level;      /* TRACK_PYRAMID_LEVEL = 3 (tracking.h:113) */
+    int max_iter;       /* TermCriteria COUNT = 30 */
+    double eps;         /* TermCriteria EPS = 0.01 (squared internally) */
+    int use_initial_flow; /* OPTFLOW_USE_INITIAL_FLOW */
+    float min_eig;      /* minEigThreshold default 1e-4 */
+} orc_klt_params;
+
+/* A padded u8 plane: pixel (x, y) lives at buf[(y + pad) * pitch + x + pad]. */
+typedef struct {
+    int w, h, pad, pitch;
+    uint8_t* buf;
+} orc_u8plane;
+
+/* A padded interleaved int16 (dx, dy) plane. */
+typedef struct {
+    int w, h, pad, pitch; /* pitch in (dx,dy) pairs */
+    int16_t* buf;
+} orc_s16plane;
+
+typedef struct {
+    int nlevels;
+    orc_u8plane lv[ORC_MAX_LEVELS];
+} orc_pyramid;
+
+void orc_klt_params_default(orc_klt_params* p);
+
+/* Returns the highest level built (<= max_level). Levels are padded by `win`
+   pixels with BORDER_REFLECT_101, exactly as buildOpticalFlowPyramid does. */
+int orc_build_pyramid(const uint8_t* img, int w, int h, int stride, int win, int max_level,
+                      orc_pyramid* pyr);
+void orc_free_pyramid(orc_pyramid* pyr);
+
+/* Scharr derivative of an unpadded view (x in [0,w), y in [0,h)) of `src`,
+   written interleaved (dx, dy) into out[(y*w + x)*2 + {0,1}]. */
+void orc_scharr(const orc_u8plane* src, int16_t* out);
+
+/* Exact restatement of cv::calcOpticalFlowPyrLK(prev, next, prevPts, nextPts,
+   status, err, Size(win,win), max_level, TermCriteria(COUNT+EPS, iters, eps),
+   flags, minEig) on u8 gray images.  nextPts is in/out when use_initial_flow.
+   Builds both pyramids itself (as OpenCV does on every call).  nthreads > 1
+   splits the point range like OpenCV's parallel_for_. */
+void orc_calc_optical_flow_pyr_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int stride,
+                                  const float* prev_xy, float* next_xy, uint8_t* status, float* err,
+                                  int n, const orc_klt_params* p, int nthreads);
+
+/* Same, on pyramids built by the caller (pyramid-reuse variant). */
+void orc_lk_on_pyramids(const orc_pyramid* prev, const orc_pyramid* next, const float* prev_xy,
+                        float* next_xy, uint8_t* status, float* err, int n, const orc_klt_params* p,
+                        int nthreads);
+
+/* tracking.cc:383-408: forward LK, backward LK (initial flow = prev points),
+   keep = st_f && st_b && !isOnBorder(next) && ptsDistance(back, prev) < fb_thresh,
+   then order-preserving compaction.  `border` is the isOnBorder margin (5.0),
+   cam_w/cam_h the camera size used by isOnBorder.
+   Outputs: next_xy (in: initial flow, out: forward result), back_xy, st_f, st_b,
+   keep[n], kept_idx[*n_kept].  Returns n_kept.
+   reuse_pyramids = 0 follows the reference's call pattern (each LK call builds
+   both pyramids again); 1 builds each pyramid once. */
+int orc_klt_fb(const uint8_t* prev, const uint8_t* next, int w, int h, int stride,
+               const float* prev_xy, float* next_xy, float* back_xy, uint8_t* st_f, uint8_t* st_b,
+               uint8_t* keep, int* kept_idx, int n, double fb_thresh, double border, int cam_w,
+               int cam_h, const orc_klt_params* p, int reuse_pyramids, int nthreads);
+
+/* ------------------------------------------------------------------------- */
+/* Feature detection (block-grid GFTT + cornerSubPix)                         */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+    double block_size;      /* TRACK_BLOCK_SIZE = 200 (tracking.h:112) */
+    int max_features;       /* track_max_features (config) */
+    double quality;         /* 0.01 (tracking.cc:647) */
+    int subpix_win;         /* 5 (tracking.cc:623) */
+    int subpix_iters;       /* 20 */
+    double subpix_eps;      /* 0.01 */
+} orc_detect_params;
+
+typedef struct {
+    int block_cols, block_rows, block_cnts;
+    int col, row;           /* block_indexs_[0] = (col, row) */
+    int max_block_features; /* track_max_block_features_ */
+    int min_pixel_distance; /* track_min_pixel_distance_ */
+} orc_block_grid;
+
+void orc_detect_params_default(orc_detect_params* p);
+/* Tracking ctor, tracking.cc:65-85. */
+void orc_block_grid_make(int w, int h, const orc_detect_params* p, orc_block_grid* g);
+
+/* cv::circle(mask, Point(cvRound(x), cvRound(y)), r, 0, FILLED) for every point;
+   mask must be pre-filled by the caller. */
+void orc_mask_circles(uint8_t* mask, int w, int h, const float* xy, int n, int radius);
+
+/* cornerMinEigenVal(blockSize 3, ksize 3) of the ROI [x0,x0+rw)x[y0,y0+rh) of the
+   w x h image: Sobel reads the parent image across the ROI edge, the box filter
+   reflects inside the ROI.  eig is rw*rh floats. */
+void orc_corner_min_eigen_val(const uint8_t* img, int w, int h, int stride, int x0, int y0, int rw,
+                              int rh, float* eig);
+
+/* goodFeaturesToTrack on the ROI with mask ROI; returns the number of corners (ROI
+   coordinates, integer-valued floats). */
+int orc_good_features_to_track(const uint8_t* img, int w, int h, int stride, int x0, int y0, int rw,
+                               int rh, const uint8_t* mask, int mask_stride, int max_corners,
+                               double quality, double min_distance, float* out_xy);
+
+/* cornerSubPix on the ROI (ROI coordinates in/out). */
+void orc_corner_subpix(const uint8_t* img, int stride, int x0, int y0, int rw, int rh, float* xy,
+                       int n, int win, int max_iters, double eps);
+
+/* Tracking::featuresDetection (tracking.cc:576-688) on one frame.
+   count_xy: points counted per block (frame->features() key points + pts2d_new_).
+   mask_xy:  points masked with circles (frame_cur_->features() + pts2d_new_).
+   n_existing: num_features for the early-exit test (features + pts2d_ref_).
+   Outputs new corners in image coordinates, block-major; per-block counts.
+   Returns the number of new corners, or -1 if the early exit triggered. */
+int orc_features_detection(const uint8_t* img, int w, int h, int stride, const float* count_xy,
+                           int n_count, const float* mask_xy, int n_mask, int ismask, int n_existing,
+                           const orc_detect_params* p, float* out_xy, int* out_block_counts);
+
+/* ------------------------------------------------------------------------- */
+/* IMU preintegration (fp64)                                                  */
+/* ------------------------------------------------------------------------- */
+
+enum { ORC_PREINT_NORMAL = 0, ORC_PREINT_EARTH = 2 };
+
+/* IMU record, types.h:50-58: {time, dt, dtheta[3], dvel[3], odovel}. */
+typedef struct {
+    double time, dt, dtheta[3], dvel[3], odovel;
+} orc_imu;
+
+/* IntegrationParameters (integration_state.h:68-89) subset used on the path. */
+typedef struct {
+    double acc_vrw, gyr_arw, gyr_bias_std, acc_bias_std, corr_time, gravity;
+} orc_imu_params;
+
+/* IntegrationState core (integration_state.h:35-51); q stored (x, y, z, w). */
+typedef struct {
+    double time;
+    double p[3], q[4], v[3], bg[3], ba[3];
+} orc_state;
+
+/* Everything a PreintegrationBase holds after integrating a segment. */
+typedef struct {
+    int variant, m;          /* m = number of IMU records (imu_buffer_.size()) */
+    double delta_time, start_time, end_time;
+    orc_state current, delta;
+    double gravity[3];
+    double jacobian[225];    /* row-major 15x15 */
+    double covariance[225];
+    double noise[144];       /* 12x12 */
+    double q0[4], iewn[3];   /* Earth variant only */
+    double* pn;              /* (m-1) x {dt, p[3]}; Earth variant only */
+} orc_preint;
+
+/* Preintegration::createPreintegration + addNewImu for k = 1..m-1
+   (ic_gvins.cc:946-953).  iewn is the Earth rate computed by the caller exactly
+   as resetState does (orc_earth_iewn).  pn buffer is allocated. */
+void orc_preint_integrate(orc_preint* s, int variant, const orc_imu_params* prm, const orc_imu* imu,
+                          int m, const orc_state* state0, const double iewn[3]);
+/* PreintegrationBase::reintegration (preintegration_base.cc:77-84). */
+void orc_preint_reintegrate(orc_preint* s, const orc_imu_params* prm, const orc_imu* imu,
+                            const orc_state* state, const double iewn[3]);
+void orc_preint_free(orc_preint* s);
+
+/* PreintegrationFactor::Evaluate: params = {pose0[7], mix0[9], pose1[7], mix1[9]};
+   jac[i] may be NULL; jac == NULL means residual only.  Mutates s->corrected_* like
+   the reference does (kept internal). */
+void orc_preint_factor_eval(const orc_preint* s, const double* const* params, double* residual,
+                            double** jac);
+
+/* Earth::iewn(origin, local) (earth.h:233-237) via local2global/ecef2blh. */
+void orc_earth_iewn(const double origin[3], const double local[3], double iewn[3]);
+
+/* ------------------------------------------------------------------------- */
+/* Reprojection factor                                                        */
+/* ------------------------------------------------------------------------- */
+
+/* Constants of one ReprojectionFactor (reprojection_factor.h:47-58). */
+typedef struct {
+    double pts0[3], pts1[3], vel0[3], vel1[3], td0, td1, std;
+} orc_reproj_const;
+
+/* params = {pose_ref[7], pose_obs[7], ext[7], invdepth[1], td[1]}; jac[i] may be
+   NULL (2x7, 2x7, 2x7, 2x1, 2x1 row-major). */
+void orc_reproj_eval(const orc_reproj_const* c, const double* const* params, double* residual,
+                     double** jac);
+
+/* PoseParameterization::Plus (pose_parameterization.h:34-49). */
+void orc_pose_plus(const double* x, const double* delta, double* x_plus_delta);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GVX_ORACLE_H */

@@ -1,0 +1,462 @@
+/*
+ * klt.c -- TEST INFRASTRUCTURE (parity oracle + CPU baseline), see gvx_oracle.h.
+ *
+ * Restates OpenCV 4.x calcOpticalFlowPyrLK as the reference calls it at
+ * ic_gvins/ic_gvins/tracking/tracking.cc:385-393 and :487-496
+ * (winSize 21x21, maxLevel 3, TermCriteria(COUNT+EPS, 30, 0.01),
+ * OPTFLOW_USE_INITIAL_FLOW, minEigThreshold 1e-4), plus the FB/border status
+ * and reduceVector compaction of tracking.cc:396-408 / :831-849.
+ * The OpenCV sources are not in this environment; the semantics follow
+ * SURVEY.md Appendix A.1-A.3 (modules/video/src/lkpyramid.cpp scalar path).
+ * Parity vs. a real OpenCV binary is unpinned (see gvx_oracle.h).
+ */
+#include "gvx_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+void orc_klt_params_default(orc_klt_params* p) {
+    p->win = 21;
+    p->max_level = 3;
+    p->max_iter = 30;
+    p->eps = 0.01;
+    p->use_initial_flow = 1;
+    p->min_eig = 1e-4f;
+}
+
+/* cv::borderInterpolate(p, len, BORDER_REFLECT_101) */
+static int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0)
+            p = -p;
+        else
+            p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+/* cvRound: round half to even (lrintf in the default rounding mode). */
+static int cv_round(float v) { return (int)lrintf(v); }
+/* cvFloor */
+static int cv_floor(float v) {
+    int i = (int)v;
+    return i - (i > v);
+}
+
+static uint8_t* px(const orc_u8plane* p, int x, int y) {
+    return p->buf + (size_t)(y + p->pad) * p->pitch + (x + p->pad);
+}
+
+static void alloc_plane(orc_u8plane* p, int w, int h, int pad) {
+    p->w = w;
+    p->h = h;
+    p->pad = pad;
+    p->pitch = w + 2 * pad;
+    p->buf = (uint8_t*)malloc((size_t)p->pitch * (h + 2 * pad));
+}
+
+/* copyMakeBorder(..., BORDER_REFLECT_101) of the interior into the pad ring. */
+static void fill_border_reflect101(orc_u8plane* p) {
+    for (int y = -p->pad; y < p->h + p->pad; y++) {
+        int sy = reflect101(y, p->h);
+        for (int x = -p->pad; x < p->w + p->pad; x++) {
+            if (y >= 0 && y < p->h && x >= 0 && x < p->w) continue;
+            *px(p, x, y) = *px(p, reflect101(x, p->w), sy);
+        }
+    }
+}
+
+/* pyrDown (imgproc/src/pyramids.cpp pyrDown_ with FixPtCast<uchar,8>):
+   dst(y,x) = (sum_ij k_i k_j src(refl(2y+i-2), refl(2x+j-2)) + 128) >> 8,
+   k = [1 4 6 4 1].  Integer arithmetic: evaluation order is irrelevant. */
+static void pyr_down(const orc_u8plane* src, orc_u8plane* dst) {
+    static const int k[5] = {1, 4, 6, 4, 1};
+    for (int y = 0; y < dst->h; y++) {
+        for (int x = 0; x < dst->w; x++) {
+            int s = 0;
+            for (int i = 0; i < 5; i++) {
+                int sy = reflect101(2 * y + i - 2, src->h);
+                int row = 0;
+                for (int j = 0; j < 5; j++) {
+                    int sx = reflect101(2 * x + j - 2, src->w);
+                    row += k[j] * (int)*px(src, sx, sy);
+                }
+                s += k[i] * row;
+            }
+            *px(dst, x, y) = (uint8_t)((s + 128) >> 8);
+        }
+    }
+}
+
+int orc_build_pyramid(const uint8_t* img, int w, int h, int stride, int win, int max_level,
+                      orc_pyramid* pyr) {
+    memset(pyr, 0, sizeof(*pyr));
+    orc_u8plane* l0 = &pyr->lv[0];
+    alloc_plane(l0, w, h, win);
+    for (int y = 0; y < h; y++) memcpy(px(l0, 0, y), img + (size_t)y * stride, (size_t)w);
+    fill_border_reflect101(l0);
+    int sw = w, sh = h;
+    for (int level = 0; level <= max_level; level++) {
+        if (level != 0) {
+            alloc_plane(&pyr->lv[level], sw, sh, win);
+            pyr_down(&pyr->lv[level - 1], &pyr->lv[level]);
+            fill_border_reflect101(&pyr->lv[level]);
+        }
+        pyr->nlevels = level + 1;
+        sw = (sw + 1) / 2;
+        sh = (sh + 1) / 2;
+        if (sw <= win || sh <= win) return level;
+    }
+    return max_level;
+}
+
+void orc_free_pyramid(orc_pyramid* pyr) {
+    for (int i = 0; i < pyr->nlevels; i++) free(pyr->lv[i].buf);
+    memset(pyr, 0, sizeof(*pyr));
+}
+
+/* calcSharrDeriv (lkpyramid.cpp): vertical [3 10 3] / [-1 0 1] pass with
+   REFLECT_101 rows, then horizontal [-1 0 1] / [3 10 3] with REFLECT_101 columns. */
+void orc_scharr(const orc_u8plane* src, int16_t* out) {
+    int w = src->w, h = src->h;
+    int* t0 = (int*)malloc(sizeof(int) * (w + 2));
+    int* t1 = (int*)malloc(sizeof(int) * (w + 2));
+    for (int y = 0; y < h; y++) {
+        int y0 = y > 0 ? y - 1 : (h > 1 ? 1 : 0);
+        int y2 = y < h - 1 ? y + 1 : (h > 1 ? h - 2 : 0);
+        for (int x = 0; x < w; x++) {
+            int a = *px(src, x, y0), b = *px(src, x, y), c = *px(src, x, y2);
+            t0[x + 1] = (a + c) * 3 + b * 10;
+            t1[x + 1] = c - a;
+        }
+        int x0 = w > 1 ? 1 : 0, x1 = w > 1 ? w - 2 : 0;
+        t0[0] = t0[x0 + 1];
+        t0[w + 1] = t0[x1 + 1];
+        t1[0] = t1[x0 + 1];
+        t1[w + 1] = t1[x1 + 1];
+        for (int x = 0; x < w; x++) {
+            out[((size_t)y * w + x) * 2 + 0] = (int16_t)(t0[x + 2] - t0[x]);
+            out[((size_t)y * w + x) * 2 + 1] = (int16_t)((t1[x + 2] + t1[x]) * 3 + t1[x + 1] * 10);
+        }
+    }
+    free(t0);
+    free(t1);
+}
+
+/* derivI buffer: Scharr of the level, padded by `win` with zeros
+   (copyMakeBorder BORDER_CONSTANT|BORDER_ISOLATED). */
+static void make_deriv(const orc_u8plane* lv, int win, orc_s16plane* d) {
+    d->w = lv->w;
+    d->h = lv->h;
+    d->pad = win;
+    d->pitch = lv->w + 2 * win;
+    size_t n = (size_t)d->pitch * (lv->h + 2 * win);
+    d->buf = (int16_t*)calloc(n * 2, sizeof(int16_t));
+    int16_t* tmp = (int16_t*)malloc(sizeof(int16_t) * 2 * (size_t)lv->w * lv->h);
+    orc_scharr(lv, tmp);
+    for (int y = 0; y < lv->h; y++)
+        memcpy(d->buf + 2 * ((size_t)(y + win) * d->pitch + win), tmp + 2 * (size_t)y * lv->w,
+               sizeof(int16_t) * 2 * lv->w);
+    free(tmp);
+}
+
+typedef struct {
+    const orc_u8plane* I;
+    const orc_s16plane* dI;
+    const orc_u8plane* J;
+    const float* prev_pts;
+    float* next_pts;
+    uint8_t* status;
+    float* err;
+    int level, max_level, begin, end;
+    const orc_klt_params* p;
+} lk_job;
+
+/* LKTrackerInvoker::operator() for points [begin, end) at one level. */
+static void lk_level(const lk_job* jb) {
+    const orc_u8plane* I = jb->I;
+    const orc_s16plane* dI = jb->dI;
+    const orc_u8plane* J = jb->J;
+    const int win = jb->p->win;
+    const int level = jb->level;
+    const float halfw = (float)((win - 1) * 0.5f);
+    const int W_BITS = 14, W_BITS1 = 14;
+    const float FLT_SCALE = 1.f / (1 << 20);
+    const double crit_eps = jb->p->eps * jb->p->eps;
+    int16_t* Iwin = (int16_t*)malloc(sizeof(int16_t) * win * win);
+    int16_t* dIwin = (int16_t*)malloc(sizeof(int16_t) * win * win * 2);
+    const int dstep = dI->pitch * 2; /* in int16 elements */
+
+    for (int pt = jb->begin; pt < jb->end; pt++) {
+        float scale = (float)(1. / (1 << level));
+        float prevx = jb->prev_pts[2 * pt] * scale;
+        float prevy = jb->prev_pts[2 * pt + 1] * scale;
+        float nextx, nexty;
+        if (level == jb->max_level) {
+            if (jb->p->use_initial_flow) {
+                nextx = jb->next_pts[2 * pt] * scale;
+                nexty = jb->next_pts[2 * pt + 1] * scale;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = jb->next_pts[2 * pt] * 2.f;
+            nexty = jb->next_pts[2 * pt + 1] * 2.f;
+        }
+        jb->next_pts[2 * pt] = nextx;
+        jb->next_pts[2 * pt + 1] = nexty;
+
+        prevx -= halfw;
+        prevy -= halfw;
+        int ipx = cv_floor(prevx), ipy = cv_floor(prevy);
+        if (ipx < -win || ipx >= dI->w || ipy < -win || ipy >= dI->h) {
+            if (level == 0) {
+                jb->status[pt] = 0;
+                jb->err[pt] = 0;
+            }
+            continue;
+        }
+        float a = prevx - ipx;
+        float b = prevy - ipy;
+        int iw00 = cv_round((1.f - a) * (1.f - b) * (1 << W_BITS));
+        int iw01 = cv_round(a * (1.f - b) * (1 << W_BITS));
+        int iw10 = cv_round((1.f - a) * b * (1 << W_BITS));
+        int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+
+        int64_t iA11 = 0, iA12 = 0, iA22 = 0;
+        for (int y = 0; y < win; y++) {
+            const uint8_t* src = px(I, ipx, ipy + y);
+            const int16_t* dsrc = dI->buf + 2 * ((size_t)(ipy + y + dI->pad) * dI->pitch + ipx + dI->pad);
+            int stepI = I->pitch;
+            for (int x = 0; x < win; x++, dsrc += 2) {
+                int ival = DESCALE(src[x] * iw00 + src[x + 1] * iw01 + src[x + stepI] * iw10 +
+                                       src[x + stepI + 1] * iw11,
+                                   W_BITS1 - 5);
+                int ixval = DESCALE(dsrc[0] * iw00 + dsrc[2] * iw01 + dsrc[dstep] * iw10 +
+                                        dsrc[dstep + 2] * iw11,
+                                    W_BITS1);
+                int iyval = DESCALE(dsrc[1] * iw00 + dsrc[3] * iw01 + dsrc[dstep + 1] * iw10 +
+                                        dsrc[dstep + 3] * iw11,
+                                    W_BITS1);
+                Iwin[y * win + x] = (int16_t)ival;
+                dIwin[(y * win + x) * 2] = (int16_t)ixval;
+                dIwin[(y * win + x) * 2 + 1] = (int16_t)iyval;
+                iA11 += (int64_t)ixval * ixval;
+                iA12 += (int64_t)ixval * iyval;
+                iA22 += (int64_t)iyval * iyval;
+            }
+        }
+        float A11 = (float)iA11 * FLT_SCALE;
+        float A12 = (float)iA12 * FLT_SCALE;
+        float A22 = (float)iA22 * FLT_SCALE;
+        float D = A11 * A22 - A12 * A12;
+        float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
+                       (float)(2 * win * win);
+        if (minEig < jb->p->min_eig || D < FLT_EPSILON) {
+            if (level == 0) {
+                jb->status[pt] = 0;
+                jb->err[pt] = 0;
+            }
+            continue;
+        }
+        D = 1.f / D;
+
+        nextx -= halfw;
+        nexty -= halfw;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < jb->p->max_iter; j++) {
+            int inx = cv_floor(nextx), iny = cv_floor(nexty);
+            if (inx < -win || inx >= J->w || iny < -win || iny >= J->h) {
+                if (level == 0) jb->status[pt] = 0;
+                break;
+            }
+            a = nextx - inx;
+            b = nexty - iny;
+            iw00 = cv_round((1.f - a) * (1.f - b) * (1 << W_BITS));
+            iw01 = cv_round(a * (1.f - b) * (1 << W_BITS));
+            iw10 = cv_round((1.f - a) * b * (1 << W_BITS));
+            iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+            int64_t ib1 = 0, ib2 = 0;
+            for (int y = 0; y < win; y++) {
+                const uint8_t* Jp = px(J, inx, iny + y);
+                int stepJ = J->pitch;
+                for (int x = 0; x < win; x++) {
+                    int diff = DESCALE(Jp[x] * iw00 + Jp[x + 1] * iw01 + Jp[x + stepJ] * iw10 +
+                                           Jp[x + stepJ + 1] * iw11,
+                                       W_BITS1 - 5) -
+                               Iwin[y * win + x];
+                    ib1 += (int64_t)diff * dIwin[(y * win + x) * 2];
+                    ib2 += (int64_t)diff * dIwin[(y * win + x) * 2 + 1];
+                }
+            }
+            float b1 = (float)ib1 * FLT_SCALE;
+            float b2 = (float)ib2 * FLT_SCALE;
+            float dx = (A12 * b2 - A22 * b1) * D;
+            float dy = (A12 * b1 - A11 * b2) * D;
+            nextx += dx;
+            nexty += dy;
+            jb->next_pts[2 * pt] = nextx + halfw;
+            jb->next_pts[2 * pt + 1] = nexty + halfw;
+            if ((double)dx * dx + (double)dy * dy <= crit_eps) break;
+            if (j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f) {
+                jb->next_pts[2 * pt] -= dx * 0.5f;
+                jb->next_pts[2 * pt + 1] -= dy * 0.5f;
+                break;
+            }
+            pdx = dx;
+            pdy = dy;
+        }
+
+        if (jb->status[pt] && level == 0) {
+            float nx = jb->next_pts[2 * pt] - halfw;
+            float ny = jb->next_pts[2 * pt + 1] - halfw;
+            int inx = cv_floor(nx), iny = cv_floor(ny);
+            if (inx < -win || inx >= J->w || iny < -win || iny >= J->h) {
+                jb->status[pt] = 0;
+                continue;
+            }
+            float aa = nx - inx, bb = ny - iny;
+            iw00 = cv_round((1.f - aa) * (1.f - bb) * (1 << W_BITS));
+            iw01 = cv_round(aa * (1.f - bb) * (1 << W_BITS));
+            iw10 = cv_round((1.f - aa) * bb * (1 << W_BITS));
+            iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+            /* sum of |diff| < 2^24: the float accumulation of OpenCV is exact. */
+            int64_t errsum = 0;
+            for (int y = 0; y < win; y++) {
+                const uint8_t* Jp = px(J, inx, iny + y);
+                int stepJ = J->pitch;
+                for (int x = 0; x < win; x++) {
+                    int diff = DESCALE(Jp[x] * iw00 + Jp[x + 1] * iw01 + Jp[x + stepJ] * iw10 +
+                                           Jp[x + stepJ + 1] * iw11,
+                                       W_BITS1 - 5) -
+                               Iwin[y * win + x];
+                    errsum += diff < 0 ? -diff : diff;
+                }
+            }
+            /* errval * 1.f/(32*win*win): (errval*1.f) / 14112 by C precedence */
+            jb->err[pt] = (float)errsum * 1.f / (float)(32 * win * win);
+        }
+    }
+    free(Iwin);
+    free(dIwin);
+}
+
+static void* lk_thread(void* arg) {
+    lk_level((const lk_job*)arg);
+    return NULL;
+}
+
+static void run_level(lk_job* base, int n, int nthreads) {
+    if (nthreads <= 1 || n < 2) {
+        base->begin = 0;
+        base->end = n;
+        lk_level(base);
+        return;
+    }
+    if (nthreads > n) nthreads = n;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+    lk_job* jobs = (lk_job*)malloc(sizeof(lk_job) * nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = *base;
+        jobs[t].begin = (int)((long)n * t / nthreads);
+        jobs[t].end = (int)((long)n * (t + 1) / nthreads);
+        pthread_create(&th[t], NULL, lk_thread, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(jobs);
+}
+
+void orc_lk_on_pyramids(const orc_pyramid* prev, const orc_pyramid* next, const float* prev_xy,
+                        float* next_xy, uint8_t* status, float* err, int n, const orc_klt_params* p,
+                        int nthreads) {
+    int max_level = prev->nlevels - 1;
+    if (next->nlevels - 1 < max_level) max_level = next->nlevels - 1;
+    if (!p->use_initial_flow) memcpy(next_xy, prev_xy, sizeof(float) * 2 * n);
+    for (int i = 0; i < n; i++) {
+        status[i] = 1;
+        err[i] = 0.f;
+    }
+    for (int level = max_level; level >= 0; level--) {
+        orc_s16plane d;
+        make_deriv(&prev->lv[level], p->win, &d);
+        lk_job jb;
+        jb.I = &prev->lv[level];
+        jb.dI = &d;
+        jb.J = &next->lv[level];
+        jb.prev_pts = prev_xy;
+        jb.next_pts = next_xy;
+        jb.status = status;
+        jb.err = err;
+        jb.level = level;
+        jb.max_level = max_level;
+        jb.p = p;
+        run_level(&jb, n, nthreads);
+        free(d.buf);
+    }
+}
+
+void orc_calc_optical_flow_pyr_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int stride,
+                                  const float* prev_xy, float* next_xy, uint8_t* status, float* err,
+                                  int n, const orc_klt_params* p, int nthreads) {
+    if (n <= 0) return;
+    orc_pyramid pp, pn;
+    orc_build_pyramid(prev, w, h, stride, p->win, p->max_level, &pp);
+    orc_build_pyramid(next, w, h, stride, p->win, p->max_level, &pn);
+    orc_lk_on_pyramids(&pp, &pn, prev_xy, next_xy, status, err, n, p, nthreads);
+    orc_free_pyramid(&pp);
+    orc_free_pyramid(&pn);
+}
+
+/* Tracking::isOnBorder (tracking.cc:847-849). */
+static int is_on_border(float x, float y, double border, int cam_w, int cam_h) {
+    return x < border || y < border || (x > (cam_w - border)) || (y > (cam_h - border));
+}
+
+/* Tracking::ptsDistance (tracking.cc:841-845): float subtraction, double sqrt. */
+static double pts_distance(const float* a, const float* b) {
+    double dx = a[0] - b[0];
+    double dy = a[1] - b[1];
+    return sqrt(dx * dx + dy * dy);
+}
+
+int orc_klt_fb(const uint8_t* prev, const uint8_t* next, int w, int h, int stride,
+               const float* prev_xy, float* next_xy, float* back_xy, uint8_t* st_f, uint8_t* st_b,
+               uint8_t* keep, int* kept_idx, int n, double fb_thresh, double border, int cam_w,
+               int cam_h, const orc_klt_params* p, int reuse_pyramids, int nthreads) {
+    if (n <= 0) return 0;
+    float* err = (float*)malloc(sizeof(float) * n);
+    /* pts2d_reverse = pts2d_map (tracking.cc:383) */
+    memcpy(back_xy, prev_xy, sizeof(float) * 2 * n);
+    if (reuse_pyramids) {
+        orc_pyramid pp, pn;
+        orc_build_pyramid(prev, w, h, stride, p->win, p->max_level, &pp);
+        orc_build_pyramid(next, w, h, stride, p->win, p->max_level, &pn);
+        orc_lk_on_pyramids(&pp, &pn, prev_xy, next_xy, st_f, err, n, p, nthreads);
+        orc_lk_on_pyramids(&pn, &pp, next_xy, back_xy, st_b, err, n, p, nthreads);
+        orc_free_pyramid(&pp);
+        orc_free_pyramid(&pn);
+    } else {
+        orc_calc_optical_flow_pyr_lk(prev, next, w, h, stride, prev_xy, next_xy, st_f, err, n, p,
+                                     nthreads);
+        orc_calc_optical_flow_pyr_lk(next, prev, w, h, stride, next_xy, back_xy, st_b, err, n, p,
+                                     nthreads);
+    }
+    int kept = 0;
+    for (int k = 0; k < n; k++) {
+        int ok = st_f[k] && st_b[k] && !is_on_border(next_xy[2 * k], next_xy[2 * k + 1], border, cam_w, cam_h) &&
+                 (pts_distance(&back_xy[2 * k], &prev_xy[2 * k]) < fb_thresh);
+        keep[k] = (uint8_t)ok;
+        if (ok) kept_idx[kept++] = k;
+    }
+    free(err);
+    return kept;
+}

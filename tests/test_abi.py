@@ -1,0 +1,52 @@
+"""CPU checks of the C-ABI boundary: libgvx.so loads without a GPU and exports
+every function include/gvx.h declares; the Python mirror fails loudly (no CPU
+fallback) when no device is present."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "gvx.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gvx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_core_entry_points():
+    syms = declared_symbols()
+    for s in ("gvx_create", "gvx_klt", "gvx_klt_fb", "gvx_frame_put", "gvx_klt_fb_batch_dev",
+              "gvx_detect", "gvx_preint_integrate", "gvx_preint_factor_eval", "gvx_reproj_eval"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(gvx_mod):
+    lib = ctypes.CDLL(gvx_mod.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, f"libgvx.so lacks {missing}"
+
+
+def test_version_and_status_strings(gvx_mod):
+    L = gvx_mod.lib()
+    assert L.gvx_version().decode().startswith("gvx")
+    assert L.gvx_status_string(0) == b"ok"
+    assert L.gvx_status_string(-5) == b"not found"
+
+
+def test_params_defaults_match_reference(gvx_mod):
+    # tracking.cc:385-388 / tracking.h:113
+    p = gvx_mod.KltParams()
+    gvx_mod.lib().gvx_klt_params_default(ctypes.byref(p))
+    assert (p.win, p.max_level, p.max_iter, p.use_initial_flow) == (21, 3, 30, 1)
+    assert p.eps == 0.01 and abs(p.min_eig - 1e-4) < 1e-12
+
+
+def test_no_cpu_fallback_without_device(gvx_mod):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    with pytest.raises(gvx_mod.GvxError):
+        gvx_mod.Context(0)

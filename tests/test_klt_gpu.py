@@ -1,0 +1,128 @@
+"""GPU parity of the KLT path (libgvx.so via the C ABI) against the CPU
+restatement (oracle/): pyramid levels, calcOpticalFlowPyrLK outputs and the
+fused fwd/bwd/FB/compaction are required to be BIT-EXACT (integer window sums,
+IEEE fp32 solve without FMA on both sides); this is stricter than the 1e-4 px
+flow tolerance of BASELINE.json's north_star."""
+import numpy as np
+import pytest
+
+from gvx import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    if not np.array_equal(a, b):
+        diff = np.argwhere(a != b)
+        raise AssertionError(f"{what}: {len(diff)} mismatches, first at {diff[:5].tolist()}: "
+                             f"gpu={a[tuple(diff[0])]} oracle={b[tuple(diff[0])]}")
+
+
+@pytest.mark.parametrize("w,h,L", [(160, 70, 3), (161, 71, 3), (1280, 560, 3), (1920, 1200, 4),
+                                   (333, 97, 2)])
+def test_pyramid_levels_bit_exact(ctx, orc, gvx_mod, w, h, L):
+    img = synth.make_image(w, h, np.random.default_rng(w + h))
+    p = gvx_mod.KltParams.default(max_level=L)
+    ctx.frame_put(7, img, p)
+    ref = orc.build_pyramid(img, L)
+    for l, r in enumerate(ref):
+        _assert_same(ctx.frame_level(7, l), r, f"level {l}")
+    ctx.frame_drop(7)
+
+
+@pytest.mark.parametrize("w,h,n,L,seed", [(160, 70, 32, 3, 1), (320, 140, 64, 3, 2),
+                                          (1280, 560, 150, 3, 20261015), (1920, 1200, 500, 4, 5)])
+def test_calc_optical_flow_bit_exact(ctx, orc, gvx_mod, w, h, n, L, seed):
+    I, J, prev, init, _ = synth.make_pair(w, h, n, seed)
+    p = gvx_mod.KltParams.default(max_level=L)
+    ctx.frame_put(1, I, p)
+    ctx.frame_put(2, J, p)
+    g_next, g_st, g_err = ctx.calc_optical_flow_pyr_lk(1, 2, prev, init, p)
+    o_next, o_st, o_err = orc.calc_optical_flow_pyr_lk(I, J, prev, init, orc.KltParams.default(max_level=L))
+    _assert_same(g_st, o_st, "status")
+    _assert_same(g_next, o_next, "nextPts")
+    _assert_same(g_err[o_st == 1], o_err[o_st == 1], "err")
+
+
+@pytest.mark.parametrize("w,h,n,L,seed", [(320, 140, 80, 3, 3), (1280, 560, 150, 3, 20261015),
+                                          (1920, 1200, 500, 4, 20261016)])
+def test_track_fb_bit_exact(ctx, orc, gvx_mod, w, h, n, L, seed):
+    I, J, prev, init, _ = synth.make_pair(w, h, n, seed)
+    p = gvx_mod.KltParams.default(max_level=L)
+    ctx.frame_put(1, I, p)
+    ctx.frame_put(2, J, p)
+    g = ctx.track_fb(1, 2, prev, init, w, h, params=p)
+    o = orc.klt_fb(I, J, prev, init, w, h, params=orc.KltParams.default(max_level=L))
+    for k in ("next", "back", "st_f", "st_b", "keep", "kept_idx"):
+        _assert_same(g[k], o[k], k)
+
+
+def test_batch_bit_exact(ctx, orc, gvx_mod):
+    P, W, H, N = 6, 1280, 560, 150
+    I, J, prev, init = synth.make_batch(P, W, H, N)
+    g = ctx.klt_fb_batch(I, J, prev, init)
+    for i in range(P):
+        o = orc.klt_fb(I[i], J[i], prev[i], init[i], reuse_pyramids=True)
+        _assert_same(g["next"][i], o["next"], f"pair {i} next")
+        _assert_same(g["back"][i], o["back"], f"pair {i} back")
+        flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
+        _assert_same(g["flags"][i], flags, f"pair {i} flags")
+        assert g["n_kept"][i] == len(o["kept_idx"])
+        _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
+
+
+def test_edge_points(ctx, orc, gvx_mod):
+    """Points at / beyond the border, far outside, and on a flat patch."""
+    I, J, _, _, _ = synth.make_pair(320, 140, 8, seed=9)
+    I[40:80, 200:260] = 77
+    J[40:80, 200:260] = 77
+    prev = np.array([[0, 0], [319.9, 139.9], [-25, 10], [10, -25], [1000, 50], [230, 60], [5, 70],
+                     [315, 5], [160.5, 70.25], [-21.0, -21.0], [330.0, 150.0]], np.float32)
+    init = prev + np.float32(0.7)
+    p = gvx_mod.KltParams.default()
+    ctx.frame_put(1, I, p)
+    ctx.frame_put(2, J, p)
+    g_next, g_st, g_err = ctx.calc_optical_flow_pyr_lk(1, 2, prev, init, p)
+    o_next, o_st, o_err = orc.calc_optical_flow_pyr_lk(I, J, prev, init)
+    _assert_same(g_st, o_st, "status")
+    _assert_same(g_next, o_next, "next")
+    g = ctx.track_fb(1, 2, prev, init, 320, 140)
+    o = orc.klt_fb(I, J, prev, init)
+    for k in ("next", "back", "st_f", "st_b", "keep", "kept_idx"):
+        _assert_same(g[k], o[k], k)
+
+
+def test_empty_and_single(ctx, orc, gvx_mod):
+    I, J, prev, init, _ = synth.make_pair(160, 70, 1, seed=10)
+    ctx.frame_put(1, I)
+    ctx.frame_put(2, J)
+    r = ctx.track_fb(1, 2, prev[:0], init[:0], 160, 70)
+    assert r["kept_idx"].size == 0
+    g = ctx.track_fb(1, 2, prev, init, 160, 70)
+    o = orc.klt_fb(I, J, prev, init)
+    for k in ("next", "back", "keep", "kept_idx"):
+        _assert_same(g[k], o[k], k)
+
+
+def test_missing_frame_raises(ctx, gvx_mod):
+    with pytest.raises(gvx_mod.GvxError):
+        ctx.calc_optical_flow_pyr_lk(12345, 54321, np.zeros((1, 2), np.float32))
+
+
+def test_large_batch_invariants(ctx, gvx_mod):
+    """Size-independent properties at the config-3 scale (1920x1200, 500 feat,
+    4-level): determinism across two runs and compaction consistency."""
+    P, W, H, N = 32, 1920, 1200, 500
+    I, J, prev, init = synth.make_batch(P, W, H, N, distinct=4)
+    p = gvx_mod.KltParams.default(max_level=4)
+    a = ctx.klt_fb_batch(I, J, prev, init, params=p)
+    b = ctx.klt_fb_batch(I, J, prev, init, params=p)
+    for k in a:
+        _assert_same(a[k], b[k], k)
+    for i in range(P):
+        keep = np.nonzero(a["flags"][i] & 4)[0]
+        assert a["n_kept"][i] == len(keep)
+        _assert_same(a["kept"][i][:len(keep)], keep, "kept")
+    # tiled pairs are identical inputs -> identical outputs
+    _assert_same(a["next"][0], a["next"][4], "tiling")
