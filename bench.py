@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""bench.py -- KLT frames/s on MI355X (BASELINE.json metric, configs[1]).
+
+A step = one pass of the KLT hot path over one batch of synthetic frame pairs
+resident in HBM: for every pair build both image pyramids, forward LK with the
+initial flow, backward LK, FB/border status and reduceVector compaction
+(SURVEY.md 8d "frame-pair" unit; tracking/tracking.cc:380-408 of the reference).
+Workload (configs[1]): 1280x560 mono, 150 features, maxLevel 3, 21x21 window.
+value = frame pairs processed by all ranks / max-over-ranks wall time.
+
+Multi-GPU: one process per GPU (torch.distributed.run), pairs sharded by rank
+with no data-path collective (weak scaling); like the reference's offline
+batch-replay config, per-step results (n_kept per pair) are gathered to rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ic-gvins_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(w, h, levels, n):
+    """B = 2*A0 + 4*Ap + 16*(A0 + Ap) + 58*N per frame pair."""
+    a0 = w * h
+    ap = 0
+    sw, sh = w, h
+    for _ in range(levels):
+        sw, sh = (sw + 1) // 2, (sh + 1) // 2
+        ap += sw * sh
+    return 2 * a0 + 4 * ap + 16 * (a0 + ap) + 58 * n
+
+
+def cpu_baseline(w, h, n, level, budget_s=12.0):
+    """Oracle (C restatement, 1 thread) on the reference's 4-call pattern
+    (each calcOpticalFlowPyrLK rebuilds both pyramids), bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # test-infrastructure import: cpu_baseline leg only
+    from gvx import synth
+    pairs = [synth.make_pair(w, h, n, synth.SEED + 1000 + i) for i in range(4)]
+    p = orc.KltParams.default(max_level=level)
+    orc.klt_fb(*pairs[0][:4], params=p)  # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        I, J, P, Q, _ = pairs[done % len(pairs)]
+        orc.klt_fb(I, J, P, Q, params=p, reuse_pyramids=False, nthreads=1)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{done} frame pairs {w}x{h}/{n} feat, 4 LK calls each rebuilding pyramids "
+                      f"(tracking.cc:385-393 pattern), 1 thread, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=256, help="frame pairs per GPU per step")
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=560)
+    ap.add_argument("--features", type=int, default=150)
+    ap.add_argument("--levels", type=int, default=3)
+    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic pairs (tiled)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import gvx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    W, H, N, L, Pn = args.width, args.height, args.features, args.levels, args.pairs
+    from gvx import synth
+    I, J, P, Q = synth.make_batch(Pn, W, H, N, seed=synth.SEED + 100000 * rank, distinct=args.distinct)
+    dI = torch.from_numpy(I).to(dev)
+    dJ = torch.from_numpy(J).to(dev)
+    dP = torch.from_numpy(P).to(dev)
+    dQ = torch.from_numpy(Q).to(dev)
+    dN = torch.empty_like(dQ)
+    dB = torch.empty_like(dQ)
+    dF = torch.empty((Pn, N), dtype=torch.uint8, device=dev)
+    dK = torch.empty((Pn, N), dtype=torch.int32, device=dev)
+    dNK = torch.empty((Pn,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    ctx = gvx.Context(local)
+    stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
+    params = gvx.KltParams.default(max_level=L)
+
+    def step():
+        with torch.cuda.stream(stream):
+            dN.copy_(dQ)  # initial flow in (next_xy is in/out)
+        ctx.klt_fb_batch_dev(Pn, W, H, dI.data_ptr(), dJ.data_ptr(), N, dP.data_ptr(), dN.data_ptr(),
+                             dB.data_ptr(), dF.data_ptr(), dK.data_ptr(), dNK.data_ptr(), params=params)
+
+    gathered = [torch.empty_like(dNK) for _ in range(world)] if world > 1 else None
+
+    def collect():
+        if world > 1:
+            ctx.sync()
+            dist.all_gather(gathered, dNK)  # offline batch replay: results to every rank
+
+    for _ in range(args.warmup):
+        step()
+        collect()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    ctx.profile_reset()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        collect()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact")}
+    ctx.profile(False)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kept_frac = float(dNK.float().mean().item()) / N
+    total_pairs = world * Pn * args.steps
+    value = total_pairs / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    B = algorithmic_bytes(W, H, L, N)
+    dev_ms = sum(v[0] for v in fam.values()) / args.steps  # device time per step (all kernels)
+    achieved = B * Pn / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(W, H, N, L, args.cpu_budget)
+        line = {
+            "metric": "KLT frames/sec @1280x560,150 feat",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/i32 windows, f32 solve",
+            "data": "synthetic (KAIST bags unavailable offline): band-limited noise + rectangles, "
+                    "similarity warp, seed 20261015",
+            "config": {"workload": f"configs[1]: batch of {Pn} frame pairs/GPU, {W}x{H} mono, {N} feat, "
+                                   f"maxLevel {L}, win 21, fwd+bwd LK + FB + compaction",
+                       "pairs_per_gpu_per_step": Pn, "parallelism": f"pairs sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "kernel": "klt pipeline (pyramid + LK + compaction)",
+                         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": None, "algorithmic_bytes_per_pair": B,
+                         "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
+            "cpu_baseline": cpu,
+            "kept_fraction": round(kept_frac, 4),
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
