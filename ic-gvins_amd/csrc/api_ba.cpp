@@ -1,0 +1,236 @@
+// api_ba.cpp -- C ABI entry points for IMU preintegration and the BA factor
+// batches (include/gvx.h).  Host-pointer variants stage through one device
+// arena and are synchronous; *_dev variants only enqueue on the context stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "gvx_internal.h"
+
+using namespace gvx;
+
+namespace {
+
+const double WGS84_WIE = 7.2921151467E-5;
+const double WGS84_RA = 6378137.0000000000;
+const double WGS84_E1 = 0.0066943799901413156;
+
+double earth_rn(double lat) {
+    const double s = std::sin(lat);
+    return WGS84_RA / std::sqrt(1.0 - WGS84_E1 * s * s);
+}
+
+gvx_status check_variant(gvx_ctx* c, int v) {
+    if (v != GVX_PREINT_NORMAL && v != GVX_PREINT_EARTH)
+        return set_err(c, GVX_ERR_UNSUPPORTED,
+                       "preintegration variant %d (odometer variants are unreachable in the reference, "
+                       "ic_gvins.cc:115)", v);
+    return GVX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Earth::iewn(origin, local) = iewn(lat of local2global(origin, local)) (common/earth.h).
+void gvx_earth_iewn(const double origin[3], const double local[3], double iewn[3]) {
+    const double cl = std::cos(origin[0]), sl = std::sin(origin[0]);
+    const double co = std::cos(origin[1]), so = std::sin(origin[1]);
+    double rn = earth_rn(origin[0]);
+    const double rnh = rn + origin[2];
+    const double e0[3] = {rnh * cl * co, rnh * cl * so, (rnh - rn * WGS84_E1) * sl};
+    const double C[9] = {-sl * co, -so, -cl * co, -sl * so, co, -cl * so, cl, 0, -sl};
+    double e1[3];
+    for (int i = 0; i < 3; ++i)
+        e1[i] = e0[i] + (C[3 * i] * local[0] + C[3 * i + 1] * local[1] + C[3 * i + 2] * local[2]);
+    const double p = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1]);
+    double lat = std::atan(e1[2] / (p * (1.0 - WGS84_E1)));
+    double h = 0, h2;
+    do {
+        h2 = h;
+        rn = earth_rn(lat);
+        h = p / std::cos(lat) - rn;
+        lat = std::atan(e1[2] / (p * (1.0 - WGS84_E1 * rn / (rn + h))));
+    } while (std::fabs(h - h2) > 1.0e-4);
+    iewn[0] = WGS84_WIE * std::cos(lat);
+    iewn[1] = 0;
+    iewn[2] = -WGS84_WIE * std::sin(lat);
+}
+
+gvx_status gvx_preint_integrate_dev(gvx_ctx* c, int32_t variant, const gvx_imu_params* prm,
+                                    int32_t n_seg, const gvx_imu* d_imu, const int32_t* d_seg_off,
+                                    const gvx_state* d_state0, const double* d_iewn,
+                                    gvx_preint_result* d_out, double* d_pn) {
+    if (!c || !prm) return GVX_ERR_INVALID;
+    gvx_status s = check_variant(c, variant);
+    if (s) return s;
+    if (n_seg < 0) return set_err(c, GVX_ERR_INVALID, "n_seg < 0");
+    if (n_seg == 0) return GVX_OK;
+    if (!d_imu || !d_seg_off || !d_state0 || !d_out || (variant == GVX_PREINT_EARTH && !d_iewn))
+        return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    hipEvent_t ev{};
+    prof_begin(c, "preint", &ev);
+    hipError_t e = launch_preint(c, variant, *prm, n_seg, d_imu, d_seg_off, d_state0, d_iewn, d_out, d_pn);
+    prof_end(c, "preint", ev);
+    return hip_err(c, e, "preint kernel");
+}
+
+gvx_status gvx_preint_integrate(gvx_ctx* c, int32_t variant, const gvx_imu_params* prm, int32_t n_seg,
+                                const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
+                                const double* iewn, gvx_preint_result* out, double* pn) {
+    if (!c || !prm) return GVX_ERR_INVALID;
+    gvx_status s = check_variant(c, variant);
+    if (s) return s;
+    if (n_seg <= 0) return n_seg == 0 ? GVX_OK : set_err(c, GVX_ERR_INVALID, "n_seg < 0");
+    if (!imu || !seg_off || !state0 || !out) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    if (seg_off[0] != 0) return set_err(c, GVX_ERR_INVALID, "seg_off[0] must be 0");
+    for (int i = 0; i < n_seg; ++i)
+        if (seg_off[i + 1] - seg_off[i] < 1) return set_err(c, GVX_ERR_INVALID, "segment %d is empty", i);
+    const bool earth = variant == GVX_PREINT_EARTH;
+    if (earth && !iewn) return set_err(c, GVX_ERR_INVALID, "Earth variant needs iewn");
+    const size_t n_imu = (size_t)seg_off[n_seg];
+    const size_t n_pn = n_imu - (size_t)n_seg;
+    hipSetDevice(c->device);
+    size_t need = arena_size({n_imu * sizeof(gvx_imu), sizeof(int32_t) * (n_seg + 1), sizeof(gvx_state) * n_seg,
+                              sizeof(double) * 3 * n_seg, sizeof(gvx_preint_result) * n_seg,
+                              sizeof(double) * 4 * (n_pn + 1)});
+    Arena a{(char*)scratch(c, "preint", need), need, 0};
+    if (!a.base) return set_err(c, GVX_ERR_OOM, "preint staging");
+    gvx_imu* d_imu = a.take<gvx_imu>(n_imu);
+    int32_t* d_off = a.take<int32_t>(n_seg + 1);
+    gvx_state* d_s0 = a.take<gvx_state>(n_seg);
+    double* d_iewn = a.take<double>(3 * n_seg);
+    gvx_preint_result* d_out = a.take<gvx_preint_result>(n_seg);
+    double* d_pn = a.take<double>(4 * (n_pn + 1));
+    hipError_t e = hipMemcpyAsync(d_imu, imu, n_imu * sizeof(gvx_imu), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_off, seg_off, sizeof(int32_t) * (n_seg + 1), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_s0, state0, sizeof(gvx_state) * n_seg, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && earth) e = hipMemcpyAsync(d_iewn, iewn, sizeof(double) * 3 * n_seg, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "preint H2D");
+    s = gvx_preint_integrate_dev(c, variant, prm, n_seg, d_imu, d_off, d_s0, earth ? d_iewn : nullptr, d_out,
+                                 d_pn);
+    if (s) return s;
+    e = hipMemcpyAsync(out, d_out, sizeof(gvx_preint_result) * n_seg, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && pn && earth && n_pn)
+        e = hipMemcpyAsync(pn, d_pn, sizeof(double) * 4 * n_pn, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "preint D2H");
+    return hip_err(c, hipStreamSynchronize(c->stream), "preint sync");
+}
+
+gvx_status gvx_reproj_eval_dev(gvx_ctx* c, int32_t n, const gvx_reproj_const* d_c, const double* d_params,
+                               const int32_t* d_offs, double* d_res, double* d_jac) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n < 0) return set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (n == 0) return GVX_OK;
+    if (!d_c || !d_params || !d_offs || !d_res) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    hipEvent_t ev{};
+    prof_begin(c, "reproj", &ev);
+    hipError_t e = launch_reproj(c, n, d_c, d_params, d_offs, d_res, d_jac);
+    prof_end(c, "reproj", ev);
+    return hip_err(c, e, "reproj kernel");
+}
+
+gvx_status gvx_reproj_eval(gvx_ctx* c, int32_t n, const gvx_reproj_const* cs, const double* params,
+                           int32_t n_params, const int32_t* offs, double* res, double* jac) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n <= 0) return n == 0 ? GVX_OK : set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (!cs || !params || !offs || !res || n_params <= 0) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    for (int64_t i = 0; i < 5 * (int64_t)n; ++i) {
+        const int need = (i % 5) < 3 ? 7 : 1;
+        if (offs[i] < 0 || offs[i] + need > n_params)
+            return set_err(c, GVX_ERR_INVALID, "factor %lld block %d offset %d out of range",
+                           (long long)(i / 5), (int)(i % 5), offs[i]);
+    }
+    hipSetDevice(c->device);
+    size_t need = arena_size({sizeof(gvx_reproj_const) * n, sizeof(double) * n_params, sizeof(int32_t) * 5 * n,
+                              sizeof(double) * 2 * n, jac ? sizeof(double) * 46 * n : 0});
+    Arena a{(char*)scratch(c, "reproj", need), need, 0};
+    if (!a.base) return set_err(c, GVX_ERR_OOM, "reproj staging");
+    gvx_reproj_const* d_c = a.take<gvx_reproj_const>(n);
+    double* d_p = a.take<double>(n_params);
+    int32_t* d_o = a.take<int32_t>(5 * (size_t)n);
+    double* d_r = a.take<double>(2 * (size_t)n);
+    double* d_j = jac ? a.take<double>(46 * (size_t)n) : nullptr;
+    hipError_t e = hipMemcpyAsync(d_c, cs, sizeof(gvx_reproj_const) * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_o, offs, sizeof(int32_t) * 5 * n, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "reproj H2D");
+    gvx_status s = gvx_reproj_eval_dev(c, n, d_c, d_p, d_o, d_r, d_j);
+    if (s) return s;
+    e = hipMemcpyAsync(res, d_r, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && jac) e = hipMemcpyAsync(jac, d_j, sizeof(double) * 46 * n, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "reproj D2H");
+    return hip_err(c, hipStreamSynchronize(c->stream), "reproj sync");
+}
+
+gvx_status gvx_preint_factor_eval_dev(gvx_ctx* c, int32_t n, const gvx_preint_result* d_pre,
+                                      const double* d_pn, const int32_t* d_pn_off, const double* d_params,
+                                      const int32_t* d_offs, double* d_res, double* d_jac) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n < 0) return set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (n == 0) return GVX_OK;
+    if (!d_pre || !d_params || !d_offs || !d_res) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    hipEvent_t ev{};
+    prof_begin(c, "preint_factor", &ev);
+    hipError_t e = launch_preint_factor(c, n, d_pre, d_pn, d_pn_off, d_params, d_offs, d_res, d_jac);
+    prof_end(c, "preint_factor", ev);
+    return hip_err(c, e, "preint factor kernel");
+}
+
+gvx_status gvx_preint_factor_eval(gvx_ctx* c, int32_t n, const gvx_preint_result* pre, const double* pn,
+                                  int32_t n_pn, const int32_t* pn_off, const double* params, int32_t n_params,
+                                  const int32_t* offs, double* res, double* jac) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n <= 0) return n == 0 ? GVX_OK : set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (!pre || !params || !offs || !res || n_params <= 0) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    bool any_earth = false;
+    for (int i = 0; i < n; ++i) {
+        gvx_status s = check_variant(c, pre[i].variant);
+        if (s) return s;
+        if (pre[i].variant == GVX_PREINT_EARTH) {
+            any_earth = true;
+            if (!pn || !pn_off || pn_off[i] < 0 || pn_off[i] + pre[i].m - 1 > n_pn)
+                return set_err(c, GVX_ERR_INVALID, "factor %d: pn list out of range", i);
+        }
+        const int sz[4] = {7, 9, 7, 9};
+        for (int k = 0; k < 4; ++k)
+            if (offs[4 * i + k] < 0 || offs[4 * i + k] + sz[k] > n_params)
+                return set_err(c, GVX_ERR_INVALID, "factor %d block %d out of range", i, k);
+    }
+    hipSetDevice(c->device);
+    const size_t npn = any_earth ? (size_t)n_pn : 0;
+    size_t need = arena_size({sizeof(gvx_preint_result) * n, sizeof(double) * 4 * (npn + 1), sizeof(int32_t) * n,
+                              sizeof(double) * n_params, sizeof(int32_t) * 4 * n, sizeof(double) * 15 * n,
+                              jac ? sizeof(double) * 480 * n : 0});
+    Arena a{(char*)scratch(c, "pfactor", need), need, 0};
+    if (!a.base) return set_err(c, GVX_ERR_OOM, "preint factor staging");
+    gvx_preint_result* d_pre = a.take<gvx_preint_result>(n);
+    double* d_pn = a.take<double>(4 * (npn + 1));
+    int32_t* d_pno = a.take<int32_t>(n);
+    double* d_p = a.take<double>(n_params);
+    int32_t* d_o = a.take<int32_t>(4 * (size_t)n);
+    double* d_r = a.take<double>(15 * (size_t)n);
+    double* d_j = jac ? a.take<double>(480 * (size_t)n) : nullptr;
+    hipError_t e = hipMemcpyAsync(d_pre, pre, sizeof(gvx_preint_result) * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && any_earth) {
+        e = hipMemcpyAsync(d_pn, pn, sizeof(double) * 4 * npn, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_pno, pn_off, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
+    } else if (e == hipSuccess) {
+        e = hipMemsetAsync(d_pno, 0, sizeof(int32_t) * n, c->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(d_p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_o, offs, sizeof(int32_t) * 4 * n, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "preint factor H2D");
+    gvx_status s = gvx_preint_factor_eval_dev(c, n, d_pre, d_pn, d_pno, d_p, d_o, d_r, d_j);
+    if (s) return s;
+    e = hipMemcpyAsync(res, d_r, sizeof(double) * 15 * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && jac) e = hipMemcpyAsync(jac, d_j, sizeof(double) * 480 * n, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "preint factor D2H");
+    return hip_err(c, hipStreamSynchronize(c->stream), "preint factor sync");
+}
+
+}  // extern "C"

@@ -1,0 +1,490 @@
+// factors.hip -- batched residual + Jacobian evaluation of the two BA factor
+// types on gfx950 (fp64):
+//   ReprojectionFactor::Evaluate    factors/reprojection_factor.h:61-161
+//   PreintegrationFactor::Evaluate  preintegration/preintegration_factor.h:45-69
+//     -> Preintegration{Normal,Earth}::evaluate + residualJacobian{Pose,Mix}{0,1}
+// (paths under /root/reference/ic_gvins/ic_gvins/).
+//
+// Reprojection: one lane per factor; parameter blocks are gathered through the
+// per-factor offset table (the Ceres parameter-block pointers), outputs are
+// staged through LDS so that the 46-double Jacobian rows leave as coalesced
+// stores.  Preintegration: one wavefront per factor; the reference recomputes
+// sqrt_information_ = LLT(P^-1)^T on every call (quirk),
+// done here with a partial-pivot LU, axpy-form substitutions and the
+// left-looking LLT spread over the lanes in LDS, each entry updated in the same
+// k order as the sequential CPU restatement.
+#include <hip/hip_runtime.h>
+
+#include "dmath.h"
+#include "gvx_internal.h"
+
+namespace gvx {
+
+namespace {
+
+constexpr int NS = 15;
+
+// ------------------------------------------------------------ reprojection
+// C(2x3) = A(2x3) * B(3x3)
+__device__ __forceinline__ void m23m33(const double* A, const double* B, double* C) {
+    double t[6];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j)
+            t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    for (int k = 0; k < 6; ++k) C[k] = t[k];
+}
+
+__device__ __forceinline__ void put_2x7(const double* red, const double* L, const double* R, double* J) {
+    double a[6], b[6];
+    m23m33(red, L, a);
+    m23m33(red, R, b);
+    for (int i = 0; i < 2; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            J[7 * i + j] = a[3 * i + j];
+            J[7 * i + 3 + j] = b[3 * i + j];
+        }
+        J[7 * i + 6] = 0.0;
+    }
+}
+
+constexpr int RP_THREADS = 128;
+constexpr int RP_OUT = 48;  // residual 2 + Jacobians 46
+
+__global__ void __launch_bounds__(RP_THREADS) reproj_kernel(int n, const gvx_reproj_const* __restrict__ cs,
+                                                             const double* __restrict__ params,
+                                                             const int32_t* __restrict__ offs,
+                                                             double* __restrict__ res,
+                                                             double* __restrict__ jac) {
+    __shared__ double stage[RP_THREADS * (RP_OUT + 1)];
+    const int t = threadIdx.x;
+    const int base = blockIdx.x * RP_THREADS;
+    const int i = base + t;
+    double* out = stage + t * (RP_OUT + 1);
+    if (i < n) {
+        const gvx_reproj_const c = cs[i];
+        const int32_t* o = offs + 5 * (int64_t)i;
+        const double* P0 = params + o[0];
+        const double* P1 = params + o[1];
+        const double* EX = params + o[2];
+        const dq q0 = dq_make(P0[6], P0[3], P0[4], P0[5]);
+        const dq q1 = dq_make(P1[6], P1[3], P1[4], P1[5]);
+        const dq qic = dq_make(EX[6], EX[3], EX[4], EX[5]);
+        const double p0[3] = {P0[0], P0[1], P0[2]}, p1[3] = {P1[0], P1[1], P1[2]};
+        const double tic[3] = {EX[0], EX[1], EX[2]};
+        const double id0 = params[o[3]];
+        const double td = params[o[4]];
+        const double sq = 1.0 / c.std;
+        const double SI[4] = {sq, 0.0, 0.0, sq};
+        double pts0td[3], pts1td[3], pc0[3], pb0[3], pn[3], pb1[3], pts1[3], tv[3];
+        for (int k = 0; k < 3; ++k) {
+            pts0td[k] = c.pts0[k] - (td - c.td0) * c.vel0[k];
+            pts1td[k] = c.pts1[k] - (td - c.td1) * c.vel1[k];
+        }
+        for (int k = 0; k < 3; ++k) pc0[k] = pts0td[k] / id0;
+        dq_rotate(qic, pc0, tv);
+        for (int k = 0; k < 3; ++k) pb0[k] = tv[k] + tic[k];
+        dq_rotate(q0, pb0, tv);
+        for (int k = 0; k < 3; ++k) pn[k] = tv[k] + p0[k];
+        for (int k = 0; k < 3; ++k) tv[k] = pn[k] - p1[k];
+        dq_rotate(dq_inv(q1), tv, pb1);
+        for (int k = 0; k < 3; ++k) tv[k] = pb1[k] - tic[k];
+        dq_rotate(dq_inv(qic), tv, pts1);
+        const double d1 = pts1[2];
+        const double e0 = pts1[0] / d1 - pts1td[0];
+        const double e1 = pts1[1] / d1 - pts1td[1];
+        out[0] = SI[0] * e0 + SI[1] * e1;
+        out[1] = SI[2] * e0 + SI[3] * e1;
+        if (jac) {
+            double cb0n[9], cnb1[9], cbc[9], R[9];
+            dq_rot(q0, cb0n);
+            dq_rot(q1, R);
+            mt3(R, cnb1);
+            dq_rot(qic, R);
+            mt3(R, cbc);
+            const double red0[6] = {1.0 / d1, 0, -pts1[0] / (d1 * d1), 0, 1.0 / d1, -pts1[1] / (d1 * d1)};
+            double red[6];
+            for (int a = 0; a < 2; ++a)
+                for (int b = 0; b < 3; ++b) red[3 * a + b] = SI[2 * a] * red0[b] + SI[2 * a + 1] * red0[3 + b];
+            double A[9], B[9], C[9], S[9], ncbc[9];
+            for (int k = 0; k < 9; ++k) ncbc[k] = -cbc[k];
+            // J0: pose_i
+            mm3(cbc, cnb1, A);
+            mm3(ncbc, cnb1, B);
+            mm3(B, cb0n, B);
+            skew(pb0, S);
+            mm3(B, S, B);
+            put_2x7(red, A, B, out + 2);
+            // J1: pose_j
+            mm3(ncbc, cnb1, A);
+            skew(pb1, S);
+            mm3(cbc, S, B);
+            put_2x7(red, A, B, out + 16);
+            // J2: extrinsic
+            mm3(cnb1, cb0n, C);
+            for (int k = 0; k < 9; ++k) C[k] = C[k] - ((k % 4) == 0 ? 1.0 : 0.0);
+            mm3(cbc, C, A);
+            double tmp_r[9], cbcT[9], ntr[9], S1[9], S2[9], S3[9], u[3], w[3];
+            mm3(cbc, cnb1, tmp_r);
+            mm3(tmp_r, cb0n, tmp_r);
+            mt3(cbc, cbcT);
+            mm3(tmp_r, cbcT, tmp_r);
+            for (int k = 0; k < 9; ++k) ntr[k] = -tmp_r[k];
+            skew(pc0, S);
+            mm3(ntr, S, S1);
+            mv3(tmp_r, pc0, u);
+            skew(u, S2);
+            mv3(cb0n, tic, u);
+            for (int k = 0; k < 3; ++k) u[k] = u[k] + p0[k] - p1[k];
+            mv3(cnb1, u, w);
+            for (int k = 0; k < 3; ++k) w[k] = w[k] - tic[k];
+            mv3(cbc, w, u);
+            skew(u, S3);
+            for (int k = 0; k < 9; ++k) B[k] = S1[k] + S2[k] + S3[k];
+            put_2x7(red, A, B, out + 30);
+            // J3: inverse depth, J4: td
+            double nred[6], M[6], v2[2];
+            for (int k = 0; k < 6; ++k) nred[k] = -red[k];
+            m23m33(nred, cbc, M);
+            m23m33(M, cnb1, M);
+            m23m33(M, cb0n, M);
+            m23m33(M, cbcT, M);
+            v2[0] = M[0] * pts0td[0] + M[1] * pts0td[1] + M[2] * pts0td[2];
+            v2[1] = M[3] * pts0td[0] + M[4] * pts0td[1] + M[5] * pts0td[2];
+            const double dd = id0 * id0;
+            out[44] = v2[0] / dd;
+            out[45] = v2[1] / dd;
+            v2[0] = M[0] * c.vel0[0] + M[1] * c.vel0[1] + M[2] * c.vel0[2];
+            v2[1] = M[3] * c.vel0[0] + M[4] * c.vel0[1] + M[5] * c.vel0[2];
+            const double s0 = SI[0] * c.vel1[0] + SI[1] * c.vel1[1];
+            const double s1 = SI[2] * c.vel1[0] + SI[3] * c.vel1[1];
+            out[46] = v2[0] / id0 + s0;
+            out[47] = v2[1] / id0 + s1;
+        }
+    }
+    __syncthreads();
+    // coalesced write-out of the block's residuals and Jacobians
+    const int cnt = min(RP_THREADS, n - base);
+    for (int k = t; k < cnt * 2; k += RP_THREADS) {
+        const int f = k >> 1, q = k & 1;
+        res[(int64_t)base * 2 + k] = stage[f * (RP_OUT + 1) + q];
+    }
+    if (jac)
+        for (int k = t; k < cnt * 46; k += RP_THREADS) {
+            const int f = k / 46, q = k - f * 46;
+            jac[(int64_t)base * 46 + k] = stage[f * (RP_OUT + 1) + 2 + q];
+        }
+}
+
+// ------------------------------------------------------ preintegration factor
+__device__ __forceinline__ void set3(double* J, int ld, int r, int c, const double* B) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) J[(r + i) * ld + c + j] = B[3 * i + j];
+}
+
+__global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
+                                                           const double* __restrict__ pn,
+                                                           const int32_t* __restrict__ pn_off,
+                                                           const double* __restrict__ params,
+                                                           const int32_t* __restrict__ offs,
+                                                           double* __restrict__ res,
+                                                           double* __restrict__ jac) {
+    __shared__ double A[NS * NS];   // LU
+    __shared__ double X[NS * NS];   // inverse, then Cholesky factor
+    __shared__ double Jr[NS * 32];  // raw (un-whitened) Jacobians [J0 7 | J1 9 | J2 7 | J3 9]
+    __shared__ double rr[NS];
+    __shared__ int perm[NS];
+    const int fi = blockIdx.x;
+    if (fi >= n) return;
+    const int lane = threadIdx.x;
+    const gvx_preint_result* s = pre + fi;
+    const bool earth = s->variant == GVX_PREINT_EARTH;
+
+    // ---- sqrt_information_ = LLT(covariance_.inverse()).matrixL().transpose() ----
+    for (int e = lane; e < NS * NS; e += 64) A[e] = s->covariance[e];
+    if (lane < NS) perm[lane] = lane;
+    __syncthreads();
+    for (int k = 0; k < NS; ++k) {
+        int piv = k;
+        double best = fabs(A[k * NS + k]);
+        for (int i = k + 1; i < NS; ++i) {
+            const double v = fabs(A[i * NS + k]);
+            if (v > best) {
+                best = v;
+                piv = i;
+            }
+        }
+        __syncthreads();
+        if (piv != k) {
+            if (lane < NS) {
+                const double t = A[k * NS + lane];
+                A[k * NS + lane] = A[piv * NS + lane];
+                A[piv * NS + lane] = t;
+            }
+            if (lane == 0) {
+                const int t = perm[k];
+                perm[k] = perm[piv];
+                perm[piv] = t;
+            }
+            __syncthreads();
+        }
+        const double akk = A[k * NS + k];
+        if (akk != 0.0 && lane > k && lane < NS) A[lane * NS + k] = A[lane * NS + k] / akk;
+        __syncthreads();
+        const int r = NS - 1 - k;  // trailing block r x r
+        for (int e = lane; e < r * r; e += 64) {
+            const int i = k + 1 + e / r, j = k + 1 + e % r;
+            A[i * NS + j] = A[i * NS + j] - A[i * NS + k] * A[k * NS + j];
+        }
+        __syncthreads();
+    }
+    for (int e = lane; e < NS * NS; e += 64) {
+        const int i = e / NS, c = e - i * NS;
+        X[e] = perm[i] == c ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    for (int k = 0; k < NS; ++k) {
+        const int r = NS - 1 - k;
+        for (int e = lane; e < r * NS; e += 64) {
+            const int i = k + 1 + e / NS, c = e % NS;
+            X[i * NS + c] = X[i * NS + c] - A[i * NS + k] * X[k * NS + c];
+        }
+        __syncthreads();
+    }
+    for (int k = NS - 1; k >= 0; --k) {
+        if (lane < NS) X[k * NS + lane] = X[k * NS + lane] / A[k * NS + k];
+        __syncthreads();
+        for (int e = lane; e < k * NS; e += 64) {
+            const int i = e / NS, c = e % NS;
+            X[i * NS + c] = X[i * NS + c] - A[i * NS + k] * X[k * NS + c];
+        }
+        __syncthreads();
+    }
+    // Eigen llt_inplace<Lower>::unblocked on the lower triangle of X
+    for (int k = 0; k < NS; ++k) {
+        double x = X[k * NS + k];
+        if (k > 0) {
+            double sq = 0;
+            for (int j = 0; j < k; ++j) sq = sq + X[k * NS + j] * X[k * NS + j];
+            x = x - sq;
+        }
+        x = sqrt(x);
+        __syncthreads();
+        if (lane == 0) X[k * NS + k] = x;
+        if (lane > k && lane < NS) {
+            double v = X[lane * NS + k];
+            if (k > 0) {
+                double d = 0;
+                for (int j = 0; j < k; ++j) d = d + X[lane * NS + j] * X[k * NS + j];
+                v = v - d;
+            }
+            X[lane * NS + k] = v / x;
+        }
+        __syncthreads();
+    }
+    // sqrt_info[i][j] = L[j][i] for j >= i  (upper triangular)
+
+    // ---- residual and raw Jacobian blocks (uniform, every lane) ----
+    const int32_t* o = offs + 4 * (int64_t)fi;
+    const double *ps0 = params + o[0], *m0 = params + o[1], *ps1 = params + o[2], *m1 = params + o[3];
+    const dq q0 = dq_make(ps0[6], ps0[3], ps0[4], ps0[5]);
+    const dq q1 = dq_make(ps1[6], ps1[3], ps1[4], ps1[5]);
+    const double *p0 = ps0, *p1 = ps1, *v0 = m0, *v1 = m1;
+    const double *bg0 = m0 + 3, *ba0 = m0 + 6, *bg1 = m1 + 3, *ba1 = m1 + 6;
+    const double dtt = s->delta_time;
+    const double* Jc = s->jacobian;
+    double dp_dbg[9], dp_dba[9], dv_dbg[9], dv_dba[9], dq_dbg[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            dp_dbg[3 * i + j] = Jc[i * NS + 9 + j];
+            dp_dba[3 * i + j] = Jc[i * NS + 12 + j];
+            dv_dbg[3 * i + j] = Jc[(3 + i) * NS + 9 + j];
+            dv_dba[3 * i + j] = Jc[(3 + i) * NS + 12 + j];
+            dq_dbg[3 * i + j] = Jc[(6 + i) * NS + 9 + j];
+        }
+    double dbg[3], dba[3], t[3], u[3], cp[3], cv[3];
+    for (int i = 0; i < 3; ++i) {
+        dbg[i] = bg0[i] - s->delta.bg[i];
+        dba[i] = ba0[i] - s->delta.ba[i];
+    }
+    mv3(dp_dba, dba, t);
+    mv3(dp_dbg, dbg, u);
+    for (int i = 0; i < 3; ++i) cp[i] = s->delta.p[i] + t[i] + u[i];
+    mv3(dv_dba, dba, t);
+    mv3(dv_dbg, dbg, u);
+    for (int i = 0; i < 3; ++i) cv[i] = s->delta.v[i] + t[i] + u[i];
+    mv3(dq_dbg, dbg, t);
+    const dq dqd = dq_load(s->delta.q);
+    const dq cq = dq_mul(dqd, dq_from_rotvec(t));
+    const double* g = s->gravity;
+    const dq q0i = dq_inv(q0);
+    double cnb0[9], M[9], N[9];
+    dq_rot(q0i, cnb0);
+    double r[NS];
+    for (int e = lane; e < NS * 32; e += 64) Jr[e] = 0.0;
+    __syncthreads();
+    const bool w0 = lane == 0;  // lane 0 writes the uniform blocks
+    if (earth) {
+        double S[9], S2[9];
+        skew(s->iewn, S);
+        double pc[3] = {0, 0, 0};
+        const double* pl = pn + 4 * (int64_t)pn_off[fi];
+        for (int k = 0; k < s->m - 1; ++k)
+            for (int i = 0; i < 3; ++i) pc[i] = pc[i] + (pl[4 * k + 1 + i] - p0[i]) * pl[4 * k];
+        for (int i = 0; i < 9; ++i) S2[i] = 2.0 * S[i];
+        mv3(S2, pc, pc);
+        double dp[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]}, vc[3];
+        mv3(S2, dp, vc);
+        const double dnn[3] = {-s->iewn[0] * dtt, -s->iewn[1] * dtt, -s->iewn[2] * dtt};
+        const dq qnn = dq_from_rotvec(dnn);
+        double dpn[3], dvn[3];
+        for (int i = 0; i < 3; ++i) {
+            dpn[i] = p1[i] - p0[i] - v0[i] * dtt - 0.5 * g[i] * dtt * dtt + pc[i];
+            dvn[i] = v1[i] - v0[i] - g[i] * dtt + vc[i];
+        }
+        const dq qb0b1 = dq_mul(dq_mul(dq_inv(q1), qnn), q0);
+        mv3(cnb0, dpn, t);
+        for (int i = 0; i < 3; ++i) r[i] = t[i] - cp[i];
+        mv3(cnb0, dvn, t);
+        for (int i = 0; i < 3; ++i) r[3 + i] = t[i] - cv[i];
+        const dq e = dq_mul(qb0b1, cq);
+        r[6] = 2 * e.x;
+        r[7] = 2 * e.y;
+        r[8] = 2 * e.z;
+        if (jac && w0) {
+            double C2[9];
+            for (int i = 0; i < 9; ++i) C2[i] = 2.0 * cnb0[i];
+            mm3(C2, S, M);
+            for (int i = 0; i < 9; ++i) N[i] = -cnb0[i] - M[i] * dtt;
+            set3(Jr, 32, 0, 0, N);
+            mv3(cnb0, dpn, t);
+            skew(t, N);
+            set3(Jr, 32, 0, 3, N);
+            for (int i = 0; i < 9; ++i) C2[i] = -2.0 * cnb0[i];
+            mm3(C2, S, N);
+            set3(Jr, 32, 3, 0, N);
+            mv3(cnb0, dvn, t);
+            skew(t, N);
+            set3(Jr, 32, 3, 3, N);
+            qlr_br(qb0b1, cq, N);
+            set3(Jr, 32, 6, 3, N);
+            // pose1 (columns 16..22)
+            set3(Jr, 32, 0, 16, cnb0);
+            for (int i = 0; i < 9; ++i) C2[i] = 2.0 * cnb0[i];
+            mm3(C2, S, N);
+            set3(Jr, 32, 3, 16, N);
+            qright_br(dq_mul(qb0b1, cq), N);
+            for (int i = 0; i < 9; ++i) N[i] = -N[i];
+            set3(Jr, 32, 6, 19, N);
+            // mix0 (columns 7..15)
+            qleft_br(dq_mul(qb0b1, dqd), M);
+            mm3(M, dq_dbg, N);
+            set3(Jr, 32, 6, 10, N);
+        }
+    } else {
+        double dp[3], dv[3], rp[3], rv[3];
+        for (int i = 0; i < 3; ++i) {
+            dp[i] = p1[i] - p0[i] - v0[i] * dtt - 0.5 * g[i] * dtt * dtt;
+            dv[i] = v1[i] - v0[i] - g[i] * dtt;
+        }
+        dq_rotate(q0i, dp, rp);
+        dq_rotate(q0i, dv, rv);
+        for (int i = 0; i < 3; ++i) {
+            r[i] = rp[i] - cp[i];
+            r[3 + i] = rv[i] - cv[i];
+        }
+        const dq e = dq_mul(dq_mul(dq_inv(cq), q0i), q1);
+        r[6] = 2 * e.x;
+        r[7] = 2 * e.y;
+        r[8] = 2 * e.z;
+        if (jac && w0) {
+            for (int i = 0; i < 9; ++i) N[i] = -cnb0[i];
+            set3(Jr, 32, 0, 0, N);
+            skew(rp, N);
+            set3(Jr, 32, 0, 3, N);
+            skew(rv, N);
+            set3(Jr, 32, 3, 3, N);
+            qlr_br(dq_mul(dq_inv(q1), q0), cq, N);
+            for (int i = 0; i < 9; ++i) N[i] = -N[i];
+            set3(Jr, 32, 6, 3, N);
+            set3(Jr, 32, 0, 16, cnb0);
+            qleft_br(e, N);
+            set3(Jr, 32, 6, 19, N);
+            qleft_br(dq_mul(dq_mul(dq_inv(q1), q0), dqd), M);
+            for (int i = 0; i < 9; ++i) M[i] = -M[i];
+            mm3(M, dq_dbg, N);
+            set3(Jr, 32, 6, 10, N);
+        }
+    }
+    for (int i = 0; i < 3; ++i) {
+        r[9 + i] = bg1[i] - bg0[i];
+        r[12 + i] = ba1[i] - ba0[i];
+    }
+    if (jac && w0) {
+        // common mix0 / mix1 blocks
+        for (int i = 0; i < 9; ++i) N[i] = -cnb0[i] * dtt;
+        set3(Jr, 32, 0, 7, N);
+        for (int i = 0; i < 9; ++i) N[i] = -dp_dbg[i];
+        set3(Jr, 32, 0, 10, N);
+        for (int i = 0; i < 9; ++i) N[i] = -dp_dba[i];
+        set3(Jr, 32, 0, 13, N);
+        for (int i = 0; i < 9; ++i) N[i] = -cnb0[i];
+        set3(Jr, 32, 3, 7, N);
+        for (int i = 0; i < 9; ++i) N[i] = -dv_dbg[i];
+        set3(Jr, 32, 3, 10, N);
+        for (int i = 0; i < 9; ++i) N[i] = -dv_dba[i];
+        set3(Jr, 32, 3, 13, N);
+        for (int i = 0; i < 3; ++i) {
+            Jr[(9 + i) * 32 + 10 + i] = -1.0;
+            Jr[(12 + i) * 32 + 13 + i] = -1.0;
+            Jr[(9 + i) * 32 + 26 + i] = 1.0;
+            Jr[(12 + i) * 32 + 29 + i] = 1.0;
+        }
+        set3(Jr, 32, 3, 23, cnb0);
+    }
+    if (w0)
+        for (int i = 0; i < NS; ++i) rr[i] = r[i];
+    __syncthreads();
+    // ---- whitening: sqrt_info (upper, = L^T) times residual / Jacobians ----
+    if (lane < NS) {
+        const int i = lane;
+        double sacc = X[i * NS + i] * rr[i];
+        for (int k = i + 1; k < NS; ++k) sacc = sacc + X[k * NS + i] * rr[k];
+        res[(int64_t)fi * NS + i] = sacc;
+    }
+    if (jac) {
+        double* jo = jac + (int64_t)fi * 480;
+        // output layout [J0 15x7 | J1 15x9 | J2 15x7 | J3 15x9], Jr columns [0..7 | 7..16 | 16..23 | 23..32]
+        for (int e = lane; e < NS * 32; e += 64) {
+            int blk, i, c, col;
+            if (e < 105) { blk = 0; i = e / 7; c = e % 7; col = c; }
+            else if (e < 240) { blk = 105; i = (e - 105) / 9; c = (e - 105) % 9; col = 7 + c; }
+            else if (e < 345) { blk = 240; i = (e - 240) / 7; c = (e - 240) % 7; col = 16 + c; }
+            else { blk = 345; i = (e - 345) / 9; c = (e - 345) % 9; col = 23 + c; }
+            (void)blk;
+            double sacc = X[i * NS + i] * Jr[i * 32 + col];
+            for (int k = i + 1; k < NS; ++k) sacc = sacc + X[k * NS + i] * Jr[k * 32 + col];
+            jo[e] = sacc;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
+                         const int32_t* offs, double* res, double* jac) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(reproj_kernel, dim3((n + RP_THREADS - 1) / RP_THREADS), dim3(RP_THREADS), 0,
+                       c->stream, n, cs, params, offs, res, jac);
+    return hipGetLastError();
+}
+
+hipError_t launch_preint_factor(gvx_ctx* c, int n, const gvx_preint_result* pre, const double* pn,
+                                const int32_t* pn_off, const double* params, const int32_t* offs,
+                                double* res, double* jac) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(preint_factor_kernel, dim3(n), dim3(64), 0, c->stream, n, pre, pn, pn_off, params,
+                       offs, res, jac);
+    return hipGetLastError();
+}
+
+}  // namespace gvx

@@ -110,4 +110,34 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
 hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
                           int32_t* n_kept);
 
+// ---- preint.hip / factors.hip ----
+hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
+                         const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
+                         const double* iewn, gvx_preint_result* out, double* pn);
+hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
+                         const int32_t* offs, double* res, double* jac);
+hipError_t launch_preint_factor(gvx_ctx* c, int n, const gvx_preint_result* pre, const double* pn,
+                                const int32_t* pn_off, const double* params, const int32_t* offs,
+                                double* res, double* jac);
+
+// Device staging arena: bump-allocates 256-byte aligned slices of one scratch
+// buffer (named) for host-pointer API calls.
+struct Arena {
+    char* base = nullptr;
+    size_t cap = 0, used = 0;
+    template <class T>
+    T* take(size_t count) {
+        size_t b = (count * sizeof(T) + 255) & ~size_t(255);
+        if (used + b > cap) return nullptr;
+        T* p = reinterpret_cast<T*>(base + used);
+        used += b;
+        return p;
+    }
+};
+inline size_t arena_size(std::initializer_list<size_t> bytes) {
+    size_t s = 0;
+    for (size_t b : bytes) s += (b + 255) & ~size_t(255);
+    return s + 256;
+}
+
 }  // namespace gvx

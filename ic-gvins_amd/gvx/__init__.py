@@ -43,6 +43,23 @@ class KltParams(C.Structure):
         return p
 
 
+IMU_DTYPE = np.dtype([("time", "f8"), ("dt", "f8"), ("dtheta", "f8", 3), ("dvel", "f8", 3),
+                      ("odovel", "f8")], align=True)
+STATE_DTYPE = np.dtype([("time", "f8"), ("p", "f8", 3), ("q", "f8", 4), ("v", "f8", 3), ("bg", "f8", 3),
+                        ("ba", "f8", 3)], align=True)
+PREINT_DTYPE = np.dtype([("variant", "i4"), ("m", "i4"), ("delta_time", "f8"), ("start_time", "f8"),
+                         ("end_time", "f8"), ("current", STATE_DTYPE), ("delta", STATE_DTYPE),
+                         ("gravity", "f8", 3), ("iewn", "f8", 3), ("q0", "f8", 4),
+                         ("jacobian", "f8", 225), ("covariance", "f8", 225)], align=True)
+REPROJ_DTYPE = np.dtype([("pts0", "f8", 3), ("pts1", "f8", 3), ("vel0", "f8", 3), ("vel1", "f8", 3),
+                         ("td0", "f8"), ("td1", "f8"), ("std", "f8")], align=True)
+
+
+class ImuParams(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("acc_vrw", "gyr_arw", "gyr_bias_std", "acc_bias_std",
+                                           "corr_time", "gravity")]
+
+
 _lib = None
 
 
@@ -82,6 +99,13 @@ def _declare(L):
                                        i32, C.POINTER(KltParams)]),
         "gvx_klt_fb_batch": (i32, [P, i32, i32, i32, P, P, i32, P, P, P, P, P, P, f64, f64, i32, i32,
                                    C.POINTER(KltParams)]),
+        "gvx_preint_integrate": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
+        "gvx_preint_integrate_dev": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
+        "gvx_earth_iewn": (None, [P, P, P]),
+        "gvx_preint_factor_eval": (i32, [P, i32, P, P, i32, P, P, i32, P, P, P]),
+        "gvx_preint_factor_eval_dev": (i32, [P, i32, P, P, P, P, P, P, P]),
+        "gvx_reproj_eval": (i32, [P, i32, P, P, i32, P, P, P]),
+        "gvx_reproj_eval_dev": (i32, [P, i32, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -227,6 +251,55 @@ class Context:
                     "gvx_klt_fb_batch")
         return dict(next=nxt, back=back, flags=flags, kept=kept, n_kept=nk)
 
+    # ------------------------------------------------------- preintegration
+    def preint_integrate(self, variant: int, prm, segments, states, iewn=None):
+        """Preintegrate a batch of IMU segments (list of IMU_DTYPE arrays, each the
+        vector<IMU> of one time-node interval, ic_gvins.cc:940-953).
+        prm: (acc_vrw, gyr_arw, gyr_bias_std, acc_bias_std, corr_time, gravity).
+        states: STATE_DTYPE array [n_seg]; iewn: [n_seg, 3] (Earth variant).
+        Returns (PREINT_DTYPE results [n_seg], pn [sum(m-1), 4], pn offsets [n_seg])."""
+        segs = [np.ascontiguousarray(s, dtype=IMU_DTYPE) for s in segments]
+        n = len(segs)
+        off = np.zeros(n + 1, np.int32)
+        off[1:] = np.cumsum([len(s) for s in segs])
+        imu = np.concatenate(segs) if n else np.zeros(0, IMU_DTYPE)
+        st = np.ascontiguousarray(states, dtype=STATE_DTYPE).reshape(n)
+        iw = None if iewn is None else np.ascontiguousarray(iewn, np.float64).reshape(n, 3)
+        out = np.zeros(n, PREINT_DTYPE)
+        pn_off = (off[:-1] - np.arange(n)).astype(np.int32)
+        pn = np.zeros((max(int(off[-1]) - n, 1), 4))
+        p = ImuParams(*prm)
+        self._check(self._L.gvx_preint_integrate(self._h, variant, C.byref(p), n, _ptr(imu), _ptr(off), _ptr(st),
+                                                 _ptr(iw), _ptr(out), _ptr(pn)), "gvx_preint_integrate")
+        return out, pn[:int(off[-1]) - n], pn_off
+
+    def preint_factor_eval(self, pre, pn, pn_off, params, offs, jacobians=True):
+        """PreintegrationFactor::Evaluate batch -> (residuals [n,15], jacobians [n,480] or None)."""
+        pre = np.ascontiguousarray(pre, dtype=PREINT_DTYPE)
+        n = pre.shape[0]
+        pn = np.ascontiguousarray(pn, np.float64).reshape(-1, 4)
+        pno = np.ascontiguousarray(pn_off, np.int32)
+        prm = np.ascontiguousarray(params, np.float64).reshape(-1)
+        o = np.ascontiguousarray(offs, np.int32).reshape(n, 4)
+        res = np.zeros((n, 15))
+        jac = np.zeros((n, 480)) if jacobians else None
+        self._check(self._L.gvx_preint_factor_eval(self._h, n, _ptr(pre), _ptr(pn), pn.shape[0], _ptr(pno),
+                                                   _ptr(prm), prm.size, _ptr(o), _ptr(res), _ptr(jac)),
+                    "gvx_preint_factor_eval")
+        return res, jac
+
+    def reproj_eval(self, consts, params, offs, jacobians=True):
+        """ReprojectionFactor::Evaluate batch -> (residuals [n,2], jacobians [n,46] or None)."""
+        cs = np.ascontiguousarray(consts, dtype=REPROJ_DTYPE)
+        n = cs.shape[0]
+        prm = np.ascontiguousarray(params, np.float64).reshape(-1)
+        o = np.ascontiguousarray(offs, np.int32).reshape(n, 5)
+        res = np.zeros((n, 2))
+        jac = np.zeros((n, 46)) if jacobians else None
+        self._check(self._L.gvx_reproj_eval(self._h, n, _ptr(cs), _ptr(prm), prm.size, _ptr(o), _ptr(res),
+                                            _ptr(jac)), "gvx_reproj_eval")
+        return res, jac
+
     def klt_fb_batch_dev(self, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_back_xy,
                          d_flags, d_kept, d_nkept, cam_w=None, cam_h=None, fb_thresh=0.5, border=5.0,
                          params: Optional[KltParams] = None):
@@ -236,3 +309,12 @@ class Context:
                                                  d_prev_xy, d_next_xy, d_back_xy, d_flags, d_kept,
                                                  d_nkept, fb_thresh, border, cam_w or w, cam_h or h,
                                                  C.byref(p)), "gvx_klt_fb_batch_dev")
+
+
+def earth_iewn(origin, local) -> np.ndarray:
+    """Earth::iewn(station, p) as PreintegrationEarth::resetState computes it."""
+    o = np.ascontiguousarray(origin, np.float64)
+    l_ = np.ascontiguousarray(local, np.float64)
+    out = np.zeros(3)
+    lib().gvx_earth_iewn(_ptr(o), _ptr(l_), _ptr(out))
+    return out

@@ -197,13 +197,16 @@ void gvx_earth_iewn(const double origin[3], const double local[3], double iewn[3
 /* ------------------------------------------------------ factor batches */
 /* PreintegrationFactor::Evaluate (preintegration/preintegration_factor.h:45-69)
    for n factors: factor i uses pre[i], pn list at pn[pn_off[i]*4 ...]
-   (pre[i].m - 1 entries), and parameter blocks params + offs[4i+k] (k:
+   (pre[i].m - 1 entries of 4 doubles; n_pn entries in total, Earth only --
+   pn/pn_off may be NULL when every factor is NORMAL), and parameter blocks
+   params + offs[4i+k] (params holds n_params doubles) (k:
    pose0[7], mix0[9], pose1[7], mix1[9]).  residuals n x 15; jacobians (may be
    NULL) n x 480 doubles = [J_pose0 15x7 | J_mix0 15x9 | J_pose1 15x7 |
    J_mix1 15x9], each row-major like Ceres. */
 gvx_status gvx_preint_factor_eval(gvx_ctx* ctx, int32_t n, const gvx_preint_result* pre,
-                                  const double* pn, const int32_t* pn_off, const double* params,
-                                  const int32_t* offs, double* residuals, double* jacobians);
+                                  const double* pn, int32_t n_pn, const int32_t* pn_off,
+                                  const double* params, int32_t n_params, const int32_t* offs,
+                                  double* residuals, double* jacobians);
 gvx_status gvx_preint_factor_eval_dev(gvx_ctx* ctx, int32_t n, const gvx_preint_result* d_pre,
                                       const double* d_pn, const int32_t* d_pn_off,
                                       const double* d_params, const int32_t* d_offs,

@@ -196,3 +196,121 @@ def klt_fb(prev, nxt, prev_pts, init_pts, cam_w=None, cam_h=None, fb=0.5, border
                          _p(kept), n, fb, border, cam_w or w, cam_h or h, C.byref(p),
                          1 if reuse_pyramids else 0, nthreads)
     return dict(next=nx, back=back, st_f=stf, st_b=stb, keep=keep, kept_idx=kept[:k].copy())
+
+
+# ------------------------------------------------------------- preintegration
+IMU_DTYPE = np.dtype([("time", "f8"), ("dt", "f8"), ("dtheta", "f8", 3), ("dvel", "f8", 3), ("odovel", "f8")])
+
+
+def imu_params(acc_vrw, gyr_arw, gyr_bias_std, acc_bias_std, corr_time, gravity):
+    return ImuParams(acc_vrw, gyr_arw, gyr_bias_std, acc_bias_std, corr_time, gravity)
+
+
+def make_state(time=0.0, p=(0, 0, 0), q=(0, 0, 0, 1), v=(0, 0, 0), bg=(0, 0, 0), ba=(0, 0, 0)):
+    s = State()
+    s.time = time
+    for name, val in (("p", p), ("q", q), ("v", v), ("bg", bg), ("ba", ba)):
+        arr = getattr(s, name)
+        for i, x in enumerate(val):
+            arr[i] = float(x)
+    return s
+
+
+def state_dict(s: State):
+    return dict(time=s.time, p=np.array(s.p[:]), q=np.array(s.q[:]), v=np.array(s.v[:]),
+                bg=np.array(s.bg[:]), ba=np.array(s.ba[:]))
+
+
+class PreintSeg:
+    """Owns an orc_preint (freed on deletion)."""
+
+    def __init__(self, variant, prm, imu: np.ndarray, state0: State, iewn=(0.0, 0.0, 0.0)):
+        self.imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+        self.prm = prm
+        self.iewn = np.asarray(iewn, np.float64)
+        self.s = Preint()
+        lib().orc_preint_integrate(C.byref(self.s), variant, C.byref(prm), _p(self.imu), len(self.imu),
+                                   C.byref(state0), _p(self.iewn))
+
+    def reintegrate(self, state: State, iewn=None):
+        if iewn is not None:
+            self.iewn = np.asarray(iewn, np.float64)
+        lib().orc_preint_reintegrate(C.byref(self.s), C.byref(self.prm), _p(self.imu), C.byref(state),
+                                     _p(self.iewn))
+
+    def __del__(self):
+        try:
+            lib().orc_preint_free(C.byref(self.s))
+        except Exception:
+            pass
+
+    @property
+    def jacobian(self):
+        return np.array(self.s.jacobian[:]).reshape(15, 15)
+
+    @property
+    def covariance(self):
+        return np.array(self.s.covariance[:]).reshape(15, 15)
+
+    @property
+    def pn(self):
+        m = self.s.m - 1
+        return np.ctypeslib.as_array(self.s.pn, shape=(max(m, 1) * 4,))[:m * 4].reshape(m, 4).copy()
+
+    def delta(self):
+        return state_dict(self.s.delta)
+
+    def current(self):
+        return state_dict(self.s.current)
+
+    def evaluate(self, pose0, mix0, pose1, mix1, jacobians=True):
+        blocks = [np.ascontiguousarray(b, np.float64) for b in (pose0, mix0, pose1, mix1)]
+        params = (C.c_void_p * 4)(*[b.ctypes.data for b in blocks])
+        res = np.zeros(15)
+        if not jacobians:
+            lib().orc_preint_factor_eval(C.byref(self.s), params, _p(res), None)
+            return res, None
+        J = [np.zeros((15, 7)), np.zeros((15, 9)), np.zeros((15, 7)), np.zeros((15, 9))]
+        jp = (C.c_void_p * 4)(*[j.ctypes.data for j in J])
+        lib().orc_preint_factor_eval(C.byref(self.s), params, _p(res), jp)
+        return res, J
+
+
+def earth_iewn(origin, local):
+    o = np.ascontiguousarray(origin, np.float64)
+    l_ = np.ascontiguousarray(local, np.float64)
+    out = np.zeros(3)
+    lib().orc_earth_iewn(_p(o), _p(l_), _p(out))
+    return out
+
+
+# ------------------------------------------------------------- reprojection
+def reproj_const(pts0, pts1, vel0, vel1, td0, td1, std):
+    c = ReprojConst()
+    for name, val in (("pts0", pts0), ("pts1", pts1), ("vel0", vel0), ("vel1", vel1)):
+        arr = getattr(c, name)
+        for i in range(3):
+            arr[i] = float(val[i])
+    c.td0, c.td1, c.std = float(td0), float(td1), float(std)
+    return c
+
+
+def reproj_eval(c: ReprojConst, pose_i, pose_j, ext, invdepth, td, jacobians=True):
+    blocks = [np.ascontiguousarray(b, np.float64).reshape(-1) for b in (pose_i, pose_j, ext, [invdepth], [td])]
+    params = (C.c_void_p * 5)(*[b.ctypes.data for b in blocks])
+    res = np.zeros(2)
+    if not jacobians:
+        lib().orc_reproj_eval(C.byref(c), params, _p(res), None)
+        return res, None
+    J = [np.zeros((2, 7)), np.zeros((2, 7)), np.zeros((2, 7)), np.zeros((2, 1)), np.zeros((2, 1))]
+    jp = (C.c_void_p * 5)(*[j.ctypes.data for j in J])
+    lib().orc_reproj_eval(C.byref(c), params, _p(res), jp)
+    return res, J
+
+
+def pose_plus(x, delta):
+    x = np.ascontiguousarray(x, np.float64)
+    d = np.ascontiguousarray(delta, np.float64)
+    out = np.zeros(7)
+    lib().orc_pose_plus(_p(x), _p(d), _p(out))
+    return out
