@@ -1,0 +1,436 @@
+// detect.hip -- block-grid feature detection for gfx950: replaces
+// Tracking::featuresDetection (/root/reference/ic_gvins/ic_gvins/tracking/tracking.cc:576-688):
+// circle mask (:609-620), per-block cv::goodFeaturesToTrack (:647-648) and
+// cv::cornerSubPix (:651), whose TBB fan-out over blocks (:656) becomes the grid.
+//
+// Kernels:
+//  mask_kernel    FILLED integer-midpoint circles (cv::circle, LINE_8) as a
+//                 per-row half-width table -> u8 mask (255 / 0).
+//  eig_kernel     cornerMinEigenVal(blockSize 3, ksize 3) per block ROI: the
+//                 Sobel reads the parent image across the ROI edge (padded
+//                 level 0 supplies REFLECT_101 at the image border), the 3x3 box
+//                 of the covariance reflects inside the ROI; fp32 products and
+//                 fp64 box sums in the CPU restatement's order.
+//  select_kernel  one workgroup per block: max over the mask, TOZERO threshold,
+//                 3x3 dilate, local-max candidates (keys = value, raster index),
+//                 then the greedy minDistance suppression as <= maxCorners
+//                 rounds of a block-wide argmax -- identical to sorting by
+//                 (value desc, address desc) and scanning (goodFeaturesToTrack).
+//  subpix_kernel  one wavefront per corner: getRectSubPix + gradient normal
+//                 equations; the five fp64 sums run sequentially in one lane
+//                 each, in OpenCV's row-major order, so corners are bit-exact.
+#include <hip/hip_runtime.h>
+
+#include "gvx_internal.h"
+
+namespace gvx {
+
+namespace {
+
+__device__ __forceinline__ int refl(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        p = p < 0 ? -p : 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+// ------------------------------------------------------------------ mask
+__global__ void __launch_bounds__(256) mask_kernel(int w, int h, const int2* __restrict__ centers, int n,
+                                                   const int* __restrict__ hw, int r,
+                                                   uint8_t* __restrict__ mask) {
+    __shared__ int2 sc[256];
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    bool hit = false;
+    for (int base = 0; base < n; base += 256) {
+        __syncthreads();
+        if (base + (int)threadIdx.x < n) sc[threadIdx.x] = centers[base + threadIdx.x];
+        __syncthreads();
+        const int cnt = min(256, n - base);
+        for (int i = 0; i < cnt && !hit; ++i) {
+            const int dy = abs(y - sc[i].y);
+            if (dy > r) continue;
+            const int hwv = hw[dy];
+            hit = hwv >= 0 && abs(x - sc[i].x) <= hwv;
+        }
+    }
+    if (x < w && y < h) mask[(int64_t)y * w + x] = hit ? 0 : 255;
+}
+
+// ------------------------------------------------------------------ eig
+constexpr int ET_W = 64, ET_H = 16;
+
+__global__ void __launch_bounds__(256) eig_kernel(const uint8_t* __restrict__ img0, int pitch,
+                                                  const int4* __restrict__ rois, const int* __restrict__ blk_ids,
+                                                  int64_t eig_stride, float* __restrict__ eig, float sc,
+                                                  float sc2) {
+    __shared__ uint8_t px[ET_H + 4][ET_W + 4];
+    __shared__ float cov[3][ET_H + 2][ET_W + 2];
+    const int k = blk_ids[blockIdx.z];
+    const int4 roi = rois[k];  // x0, y0, rw, rh
+    const int rw = roi.z, rh = roi.w;
+    const int tx0 = blockIdx.x * ET_W, ty0 = blockIdx.y * ET_H;
+    if (tx0 >= rw || ty0 >= rh) return;
+    // parent pixels for ROI coords [tx0-2, tx0+ET_W+1] x [ty0-2, ty0+ET_H+1]
+    // (ROI coords beyond rw+1 / rh+1 are never used; clamp them so the reads stay
+    // inside the PAD ring of the padded level)
+    for (int i = threadIdx.x; i < (ET_H + 4) * (ET_W + 4); i += 256) {
+        const int r = i / (ET_W + 4), c = i - r * (ET_W + 4);
+        const int yy = min(ty0 - 2 + r, rh + 1), xx = min(tx0 - 2 + c, rw + 1);
+        px[r][c] = img0[(int64_t)(roi.y + yy) * pitch + roi.x + xx];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (ET_H + 2) * (ET_W + 2); i += 256) {
+        const int r = i / (ET_W + 2), c = i - r * (ET_W + 2);
+        const int ry = refl(ty0 + r - 1, rh) - ty0 + 2;  // staged coords of the centre
+        const int rx = refl(tx0 + c - 1, rw) - tx0 + 2;
+        float dx = 0.f, dy = 0.f;
+        if (ry >= 1 && ry <= ET_H + 2 && rx >= 1 && rx <= ET_W + 2) {
+            float rdx[3], rdy[3];
+            for (int q = 0; q < 3; ++q) {
+                const float s0 = (float)px[ry - 1 + q][rx - 1];
+                const float s1 = (float)px[ry - 1 + q][rx];
+                const float s2 = (float)px[ry - 1 + q][rx + 1];
+                float a = -1.f * s0;
+                a = a + 0.f * s1;
+                a = a + 1.f * s2;
+                rdx[q] = a;
+                float b = sc * s0;
+                b = b + sc2 * s1;
+                b = b + sc * s2;
+                rdy[q] = b;
+            }
+            dx = (rdx[0] + rdx[2]) * sc + rdx[1] * sc2;
+            dx = dx + 0.f;
+            dy = rdy[2] - rdy[0];
+            dy = dy + 0.f;
+        }
+        cov[0][r][c] = dx * dx;
+        cov[1][r][c] = dx * dy;
+        cov[2][r][c] = dy * dy;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ET_H * ET_W; i += 256) {
+        const int r = i / ET_W, c = i - r * ET_W;
+        const int x = tx0 + c, y = ty0 + r;
+        if (x >= rw || y >= rh) continue;
+        double s[3];
+        for (int q = 0; q < 3; ++q) {
+            double acc = 0;
+            for (int d = 0; d < 3; ++d) {
+                double rs = (double)cov[q][r + d][c];
+                rs = rs + (double)cov[q][r + d][c + 1];
+                rs = rs + (double)cov[q][r + d][c + 2];
+                acc = acc + rs;
+            }
+            s[q] = acc;
+        }
+        const float a = (float)s[0] * 0.5f;
+        const float b = (float)s[1];
+        const float cc = (float)s[2] * 0.5f;
+        eig[k * eig_stride + (int64_t)y * rw + x] = (a + cc) - __fsqrt_rn((a - cc) * (a - cc) + b * b);
+    }
+}
+
+// ------------------------------------------------------------------ select
+__device__ __forceinline__ uint32_t fkey(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+
+constexpr int SEL_T = 1024;
+
+__global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__ eig, int64_t eig_stride,
+                                                       const uint8_t* __restrict__ mask, int w,
+                                                       const int4* __restrict__ rois,
+                                                       const int* __restrict__ blk_ids,
+                                                       const int* __restrict__ want, double quality,
+                                                       float min_dist, unsigned long long* __restrict__ cand,
+                                                       int2* __restrict__ corners, int max_per_block,
+                                                       int* __restrict__ ncorner) {
+    __shared__ float s_max[SEL_T / 64];
+    __shared__ int s_found[SEL_T / 64];
+    __shared__ unsigned long long s_key[SEL_T / 64];
+    __shared__ int s_ncand;
+    __shared__ float s_acc[64][2];
+    __shared__ int s_nacc;
+    const int k = blk_ids[blockIdx.x];
+    const int4 roi = rois[k];
+    const int rw = roi.z, rh = roi.w;
+    const float* E = eig + k * eig_stride;
+    const uint8_t* M = mask + (int64_t)roi.y * w + roi.x;
+    unsigned long long* CK = cand + k * eig_stride;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int npx = rw * rh;
+    // minMaxLoc(eig, 0, &maxVal, 0, 0, mask)
+    float mx = -__FLT_MAX__;
+    int found = 0;
+    for (int i = t; i < npx; i += SEL_T) {
+        const int y = i / rw, x = i - y * rw;
+        if (M[(int64_t)y * w + x]) {
+            mx = fmaxf(mx, E[i]);
+            found = 1;
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        found |= __shfl_xor(found, o, 64);
+    }
+    if (lane == 0) {
+        s_max[wv] = mx;
+        s_found[wv] = found;
+    }
+    if (t == 0) {
+        s_ncand = 0;
+        s_nacc = 0;
+    }
+    __syncthreads();
+    float mxa = -__FLT_MAX__;
+    int fa = 0;
+    for (int q = 0; q < SEL_T / 64; ++q) {
+        mxa = fmaxf(mxa, s_max[q]);
+        fa |= s_found[q];
+    }
+    const double maxv = fa ? (double)mxa : 0.0;
+    const float thr = (float)(maxv * quality);
+    // candidates: thresholded local maxima of the 3x3 dilation, inside the
+    // 1-pixel ROI ring, on the mask
+    for (int i = t; i < npx; i += SEL_T) {
+        const int y = i / rw, x = i - y * rw;
+        if (y < 1 || y > rh - 2 || x < 1 || x > rw - 2) continue;
+        float v = E[i];
+        v = v > thr ? v : 0.f;
+        if (v == 0.f || !M[(int64_t)y * w + x]) continue;
+        float d = -__FLT_MAX__;
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                float u = E[(y + dy) * rw + x + dx];
+                u = u > thr ? u : 0.f;
+                d = fmaxf(d, u);
+            }
+        if (v == d) {
+            const int slot = atomicAdd(&s_ncand, 1);
+            CK[slot] = ((unsigned long long)fkey(v) << 32) | (unsigned)i;
+        }
+    }
+    __syncthreads();
+    const int nc = s_ncand;
+    const int maxc = want[k];
+    const float md2 = min_dist * min_dist;
+    for (int round = 0; round < maxc; ++round) {
+        unsigned long long best = 0;
+        const int na = s_nacc;
+        for (int i = t; i < nc; i += SEL_T) {
+            const unsigned long long key = CK[i];
+            if (key <= best) continue;
+            const int idx = (int)(key & 0xffffffffu);
+            const int y = idx / rw, x = idx - y * rw;
+            bool good = true;
+            for (int j = 0; j < na && good; ++j) {
+                const float dx = (float)x - s_acc[j][0];
+                const float dy = (float)y - s_acc[j][1];
+                if (dx * dx + dy * dy < md2) good = false;
+            }
+            if (good) best = key;
+        }
+        best = wave_max_u64(best);
+        if (lane == 0) s_key[wv] = best;
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long b = 0;
+            for (int q = 0; q < SEL_T / 64; ++q) b = s_key[q] > b ? s_key[q] : b;
+            if (b != 0) {
+                const int idx = (int)(b & 0xffffffffu);
+                const int y = idx / rw, x = idx - y * rw;
+                s_acc[s_nacc][0] = (float)x;
+                s_acc[s_nacc][1] = (float)y;
+                corners[k * max_per_block + s_nacc] = make_int2(x, y);
+                s_nacc = s_nacc + 1;
+            } else {
+                s_key[0] = 0;  // signal: no more candidates
+            }
+        }
+        __syncthreads();
+        if (s_nacc == round) break;  // nothing accepted this round
+    }
+    if (t == 0) ncorner[k] = s_nacc;
+}
+
+// ------------------------------------------------------------------ subpix
+constexpr int SP_WIN = 5;
+constexpr int SP_W = 2 * SP_WIN + 1;  // 11
+constexpr int SP_B = SP_W + 2;        // 13
+
+// getRectSubPix(ROI, 13x13, centre, CV_32F): value of patch pixel (i, j).
+__device__ float rect_subpix_px(const uint8_t* __restrict__ src, int pitch, int sw, int sh, float cx0,
+                                float cy0, int i, int j) {
+    const float cx = cx0 - (SP_B - 1) * 0.5f;
+    const float cy = cy0 - (SP_B - 1) * 0.5f;
+    const int ipx = (int)floorf(cx), ipy = (int)floorf(cy);
+    if (0 <= ipx && ipx + SP_B < sw && 0 <= ipy && ipy + SP_B < sh) {
+        float a = cx - ipx;
+        const float b = cy - ipy;
+        a = a > 0.0001f ? a : 0.0001f;
+        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
+        const double s = (1. - a) / a;
+        const uint8_t* p = src + (int64_t)(ipy + i) * pitch + ipx;
+        const float t = a12 * (float)p[j + 1] + a22 * (float)p[j + 1 + pitch];
+        float prev;
+        if (j == 0) {
+            prev = (1 - a) * (b1 * (float)p[0] + b2 * (float)p[pitch]);
+        } else {
+            const float tp = a12 * (float)p[j] + a22 * (float)p[j + pitch];
+            prev = (float)(tp * s);
+        }
+        return prev + t;
+    }
+    const float a = cx - ipx, b = cy - ipy;
+    const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+    const float b1 = 1.f - b, b2 = b;
+    // adjustRect
+    int64_t off = 0;
+    int rx, rwid, ry, rhei;
+    if (ipx >= 0) {
+        off += ipx;
+        rx = 0;
+    } else {
+        rx = -ipx;
+        if (rx > SP_B) rx = SP_B;
+    }
+    if (ipx < sw - SP_B)
+        rwid = SP_B;
+    else {
+        rwid = sw - ipx - 1;
+        if (rwid < 0) {
+            off += rwid;
+            rwid = 0;
+        }
+    }
+    if (ipy >= 0) {
+        off += (int64_t)ipy * pitch;
+        ry = 0;
+    } else
+        ry = -ipy;
+    if (ipy < sh - SP_B)
+        rhei = SP_B;
+    else {
+        rhei = sh - ipy - 1;
+        if (rhei < 0) {
+            off += (int64_t)rhei * pitch;
+            rhei = 0;
+        }
+    }
+    const uint8_t* s = src + off - rx;
+    for (int q = 0; q < i; ++q) {
+        const uint8_t* s2 = s + pitch;
+        if (q < ry || q >= rhei) s2 -= pitch;
+        if (q < rhei) s = s2;
+    }
+    const uint8_t* s2 = s + pitch;
+    if (i < ry || i >= rhei) s2 -= pitch;
+    if (j < rx) return (float)s[rx] * b1 + (float)s2[rx] * b2;
+    if (j >= rwid) return (float)s[rwid] * b1 + (float)s2[rwid] * b2;
+    return (float)s[j] * a11 + (float)s[j + 1] * a12 + (float)s2[j] * a21 + (float)s2[j + 1] * a22;
+}
+
+__global__ void __launch_bounds__(64) subpix_kernel(const uint8_t* __restrict__ img0, int pitch,
+                                                    const int4* __restrict__ rois,
+                                                    const int2* __restrict__ corners,
+                                                    const int* __restrict__ ncorner, int max_per_block,
+                                                    const float* __restrict__ gmask, int max_iters,
+                                                    double eps2, float2* __restrict__ out) {
+    __shared__ float patch[SP_B * SP_B];
+    __shared__ double terms[5][SP_W * SP_W];
+    __shared__ double sums[5];
+    const int k = blockIdx.y;
+    const int ci = blockIdx.x;
+    if (ci >= ncorner[k]) return;
+    const int lane = threadIdx.x;
+    const int4 roi = rois[k];
+    const uint8_t* src = img0 + (int64_t)roi.y * pitch + roi.x;
+    const int2 c0 = corners[k * max_per_block + ci];
+    const float cTx = (float)c0.x, cTy = (float)c0.y;
+    float cIx = cTx, cIy = cTy;
+    int iter = 0;
+    double err = 0;
+    do {
+        for (int e = lane; e < SP_B * SP_B; e += 64)
+            patch[e] = rect_subpix_px(src, pitch, roi.z, roi.w, cIx, cIy, e / SP_B, e % SP_B);
+        __syncthreads();
+        for (int e = lane; e < SP_W * SP_W; e += 64) {
+            const int i = e / SP_W, j = e - i * SP_W;
+            const float* sp = patch + (i + 1) * SP_B + 1;
+            const double m = gmask[e];
+            const double tgx = sp[j + 1] - sp[j - 1];
+            const double tgy = sp[j + SP_B] - sp[j - SP_B];
+            const double gxx = tgx * tgx * m;
+            const double gxy = tgx * tgy * m;
+            const double gyy = tgy * tgy * m;
+            const double pxx = j - SP_WIN, py = i - SP_WIN;
+            terms[0][e] = gxx;
+            terms[1][e] = gxy;
+            terms[2][e] = gyy;
+            terms[3][e] = gxx * pxx + gxy * py;
+            terms[4][e] = gxy * pxx + gyy * py;
+        }
+        __syncthreads();
+        if (lane < 5) {
+            double acc = 0;
+            for (int e = 0; e < SP_W * SP_W; ++e) acc += terms[lane][e];
+            sums[lane] = acc;
+        }
+        __syncthreads();
+        const double a = sums[0], b = sums[1], c = sums[2], bb1 = sums[3], bb2 = sums[4];
+        const double det = a * c - b * b;
+        if (fabs(det) <= __DBL_EPSILON__ * __DBL_EPSILON__) break;
+        const double scale = 1.0 / det;
+        const float nx = (float)(cIx + c * scale * bb1 - b * scale * bb2);
+        const float ny = (float)(cIy - b * scale * bb1 + a * scale * bb2);
+        err = (nx - cIx) * (nx - cIx) + (ny - cIy) * (ny - cIy);
+        cIx = nx;
+        cIy = ny;
+        if (cIx < 0 || cIx >= roi.z || cIy < 0 || cIy >= roi.w) break;
+    } while (++iter < max_iters && err > eps2);
+    if (fabsf(cIx - cTx) > SP_WIN || fabsf(cIy - cTy) > SP_WIN) {
+        cIx = cTx;
+        cIy = cTy;
+    }
+    if (lane == 0) out[k * max_per_block + ci] = make_float2(cIx, cIy);
+}
+
+}  // namespace
+
+hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d) {
+    if (d.n_circles > 0 || d.fill_mask) {
+        dim3 g((d.w + 63) / 64, (d.h + 3) / 4);
+        hipLaunchKernelGGL(mask_kernel, g, dim3(256), 0, c->stream, d.w, d.h, d.centers, d.n_circles, d.hw,
+                           d.radius, d.mask);
+    }
+    if (d.n_active <= 0) return hipGetLastError();
+    {
+        dim3 g((d.max_rw + ET_W - 1) / ET_W, (d.max_rh + ET_H - 1) / ET_H, d.n_active);
+        hipLaunchKernelGGL(eig_kernel, g, dim3(256), 0, c->stream, d.img0, d.pitch, d.rois, d.blk_ids,
+                           d.eig_stride, d.eig, d.sc, d.sc2);
+    }
+    hipLaunchKernelGGL(select_kernel, dim3(d.n_active), dim3(SEL_T), 0, c->stream, d.eig, d.eig_stride, d.mask,
+                       d.w, d.rois, d.blk_ids, d.want, d.quality, d.min_dist, d.cand, d.corners,
+                       d.max_per_block, d.ncorner);
+    {
+        dim3 g(d.max_per_block, d.n_blocks);
+        hipLaunchKernelGGL(subpix_kernel, g, dim3(64), 0, c->stream, d.img0, d.pitch, d.rois, d.corners,
+                           d.ncorner, d.max_per_block, d.gmask, d.max_iters, d.eps2, d.out);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gvx

@@ -120,6 +120,37 @@ hipError_t launch_preint_factor(gvx_ctx* c, int n, const gvx_preint_result* pre,
                                 const int32_t* pn_off, const double* params, const int32_t* offs,
                                 double* res, double* jac);
 
+// ---- detect.hip ----
+struct DetectLaunch {
+    int w, h;
+    const uint8_t* img0;  // padded level 0 at image (0,0)
+    int pitch;
+    // circle mask
+    const int2* centers;
+    int n_circles, radius, fill_mask;
+    const int* hw;        // half-width per row offset 0..radius (-1 = none)
+    uint8_t* mask;        // w x h
+    // blocks
+    const int4* rois;     // (x0, y0, rw, rh) per block
+    const int* blk_ids;   // active blocks (want > 0)
+    int n_active, n_blocks, max_rw, max_rh;
+    const int* want;      // maxCorners per block
+    int64_t eig_stride;
+    float* eig;
+    unsigned long long* cand;
+    int2* corners;
+    int* ncorner;
+    int max_per_block;
+    double quality;
+    float min_dist;
+    float sc, sc2;        // Sobel scale 1/(4*3*255) and 2x
+    const float* gmask;   // 11x11 cornerSubPix weights
+    int max_iters;
+    double eps2;
+    float2* out;
+};
+hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d);
+
 // Device staging arena: bump-allocates 256-byte aligned slices of one scratch
 // buffer (named) for host-pointer API calls.
 struct Arena {

@@ -60,6 +60,18 @@ class ImuParams(C.Structure):
                                            "corr_time", "gravity")]
 
 
+class DetectParams(C.Structure):
+    _fields_ = [("block_size", C.c_double), ("max_features", C.c_int32), ("quality", C.c_double),
+                ("subpix_win", C.c_int32), ("subpix_iters", C.c_int32), ("subpix_eps", C.c_double)]
+
+    @classmethod
+    def default(cls, **kw) -> "DetectParams":
+        p = cls(200.0, 150, 0.01, 5, 20, 0.01)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+
 _lib = None
 
 
@@ -106,6 +118,8 @@ def _declare(L):
         "gvx_preint_factor_eval_dev": (i32, [P, i32, P, P, P, P, P, P, P]),
         "gvx_reproj_eval": (i32, [P, i32, P, P, i32, P, P, P]),
         "gvx_reproj_eval_dev": (i32, [P, i32, P, P, P, P, P]),
+        "gvx_detect_params_default": (None, [C.POINTER(DetectParams)]),
+        "gvx_detect": (i32, [P, u64, P, i32, P, i32, i32, i32, C.POINTER(DetectParams), P, P, C.POINTER(i32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -250,6 +264,26 @@ class Context:
                                              border, cam_w or W, cam_h or H, C.byref(p)),
                     "gvx_klt_fb_batch")
         return dict(next=nxt, back=back, flags=flags, kept=kept, n_kept=nk)
+
+    # ------------------------------------------------------------ detection
+    def detect(self, frame_id: int, count_xy=None, mask_xy=None, ismask: bool = True, n_existing: int = 0,
+               params: Optional[DetectParams] = None):
+        """Tracking::featuresDetection on a cached frame -> (corners [n,2] f32 or
+        None when the early exit triggers, per-block counts)."""
+        p = params or DetectParams.default()
+        cxy = np.zeros((0, 2), np.float32) if count_xy is None else _f32xy(count_xy)
+        mxy = np.zeros((0, 2), np.float32) if mask_xy is None else _f32xy(mask_xy)
+        # block_cnts * max_block_features bounds the output
+        cap = 4096
+        out = np.zeros((cap, 2), np.float32)
+        blk = np.zeros(1024, np.int32)
+        n = C.c_int32()
+        self._check(self._L.gvx_detect(self._h, frame_id, _ptr(cxy), cxy.shape[0], _ptr(mxy), mxy.shape[0],
+                                       1 if ismask else 0, n_existing, C.byref(p), _ptr(out), _ptr(blk),
+                                       C.byref(n)), "gvx_detect")
+        if n.value < 0:
+            return None, blk[:0]
+        return out[:n.value].copy(), blk
 
     # ------------------------------------------------------- preintegration
     def preint_integrate(self, variant: int, prm, segments, states, iewn=None):

@@ -314,3 +314,53 @@ def pose_plus(x, delta):
     out = np.zeros(7)
     lib().orc_pose_plus(_p(x), _p(d), _p(out))
     return out
+
+
+# ------------------------------------------------------------- detection
+def block_grid(w, h, params=None):
+    g = BlockGrid()
+    lib().orc_block_grid_make(w, h, C.byref(params or DetectParams.default()), C.byref(g))
+    return g
+
+
+def mask_circles(w, h, xy, radius):
+    mask = np.full((h, w), 255, np.uint8)
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    lib().orc_mask_circles(_p(mask), w, h, _p(xy), xy.shape[0], radius)
+    return mask
+
+
+def corner_min_eigen_val(img, x0, y0, rw, rh):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    eig = np.zeros((rh, rw), np.float32)
+    lib().orc_corner_min_eigen_val(_p(img), w, h, w, x0, y0, rw, rh, _p(eig))
+    return eig
+
+
+def good_features_to_track(img, x0, y0, rw, rh, mask_roi, max_corners, quality, min_distance):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    m = None if mask_roi is None else np.ascontiguousarray(mask_roi, np.uint8)
+    out = np.zeros((max(max_corners, 1) if max_corners > 0 else rw * rh, 2), np.float32)
+    n = lib().orc_good_features_to_track(_p(img), w, h, w, x0, y0, rw, rh, _p(m),
+                                         0 if m is None else m.shape[1], max_corners, quality,
+                                         min_distance, _p(out))
+    return out[:n].copy()
+
+
+def features_detection(img, count_xy=None, mask_xy=None, ismask=True, n_existing=0, params=None):
+    """-> (corners [n,2] or None on early exit, per-block counts)."""
+    p = params or DetectParams.default()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    g = block_grid(w, h, p)
+    cxy = np.zeros((0, 2), np.float32) if count_xy is None else np.ascontiguousarray(count_xy, np.float32).reshape(-1, 2)
+    mxy = np.zeros((0, 2), np.float32) if mask_xy is None else np.ascontiguousarray(mask_xy, np.float32).reshape(-1, 2)
+    out = np.zeros((max(g.block_cnts * max(g.max_block_features, 1), 1), 2), np.float32)
+    blk = np.zeros(max(g.block_cnts, 1), np.int32)
+    n = lib().orc_features_detection(_p(img), w, h, w, _p(cxy), cxy.shape[0], _p(mxy), mxy.shape[0],
+                                     1 if ismask else 0, n_existing, C.byref(p), _p(out), _p(blk))
+    if n < 0:
+        return None, blk[:0]
+    return out[:n].copy(), blk[:g.block_cnts]

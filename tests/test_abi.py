@@ -5,6 +5,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -41,7 +42,7 @@ def test_params_defaults_match_reference(gvx_mod):
     p = gvx_mod.KltParams()
     gvx_mod.lib().gvx_klt_params_default(ctypes.byref(p))
     assert (p.win, p.max_level, p.max_iter, p.use_initial_flow) == (21, 3, 30, 1)
-    assert p.eps == 0.01 and abs(p.min_eig - 1e-4) < 1e-12
+    assert p.eps == 0.01 and p.min_eig == np.float32(1e-4)
 
 
 def test_no_cpu_fallback_without_device(gvx_mod):
