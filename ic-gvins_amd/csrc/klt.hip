@@ -1,18 +1,21 @@
-// klt.hip -- pyramid build, pyramidal LK (fwd / fwd+bwd+FB) and compaction
-// kernels for gfx950.  Replaces the four cv::calcOpticalFlowPyrLK calls per
-// frame at /root/reference/ic_gvins/ic_gvins/tracking/tracking.cc:385,390,487,493
-// and the status/reduceVector logic at tracking.cc:396-408, :831-849.
+// klt.hip -- pyramidal Lucas-Kanade (fwd / fwd+bwd+FB) and compaction kernels
+// for gfx950.  Replaces the four cv::calcOpticalFlowPyrLK calls per frame at
+// /root/reference/ic_gvins/ic_gvins/tracking/tracking.cc:385,390,487,493 and the
+// status / reduceVector logic at tracking.cc:396-408, :831-849.
 //
 // Design (DESIGN.md "KLT"):
-//  * pyramids are built once per image into a padded layout (gvx::PAD ring,
-//    BORDER_REFLECT_101) -- the reference rebuilds them in each of its 4 calls;
-//  * the Scharr derivative planes are never materialised: each LK wavefront
-//    computes the derivative of its 22x22 window from the padded pyramid in
-//    registers (zero outside the image, as OpenCV's BORDER_CONSTANT deriv pad);
-//  * one 64-lane wavefront per point; lane = 3*row + segment owns 7 consecutive
-//    window pixels of one of the 21 rows, loaded as aligned dwords and realigned
-//    with v_alignbyte; window sums are exact integer wave reductions, so the
-//    fp32 2x2 solve sees bit-identical inputs to the CPU restatement.
+//  * pyramids are built once per image (pyramid.hip) into a padded layout;
+//  * the Scharr derivative planes are never materialised: each window's
+//    derivative is computed in registers from the padded pyramid (zero outside
+//    the image, as OpenCV's BORDER_CONSTANT derivative padding);
+//  * one point per 64-lane wavefront: lane k < 63 owns the 7-pixel "unit"
+//    (window row k/3, segment k%3) of the 21x21 window; window rows are read
+//    with aligned dword loads and realigned with v_alignbyte;
+//  * window values are kept as packed int16 pairs and the bilinear weights,
+//    gradients and mismatch products run on v_dot2_i32_i16; every per-pixel
+//    quantity is an exact integer, and the window sums are exact 64-bit DPP
+//    wave reductions -- so the fp32 2x2 solve sees bit-identical inputs to
+//    the CPU restatement (oracle/klt.c), whose LK outputs are matched bit-exactly.
 #include <hip/hip_runtime.h>
 
 #include "gvx_internal.h"
@@ -21,149 +24,55 @@ namespace gvx {
 
 namespace {
 
-__device__ __forceinline__ int reflect101(int p, int len) {
-    if ((unsigned)p < (unsigned)len) return p;
-    if (len == 1) return 0;
-    do {
-        p = p < 0 ? -p : 2 * len - 2 - p;
-    } while ((unsigned)p >= (unsigned)len);
-    return p;
-}
-
-// ----------------------------------------------------------------- pyramid
-
-// Level 0: padded copy of the source image (copyMakeBorder REFLECT_101).
-// One thread per output dword; the source is read through the reflect map.
-__global__ void __launch_bounds__(256) pyr_level0_kernel(const uint8_t* __restrict__ src,
-                                                         int64_t img_stride, int stride, int w,
-                                                         int h, int pitch, int64_t pyr_bytes,
-                                                         uint8_t* __restrict__ dst) {
-    const int img = blockIdx.z;
-    const int row = blockIdx.y;           // padded row 0 .. h+2P-1
-    const int dw = blockIdx.x * 256 + threadIdx.x;  // dword column
-    const int x0 = dw * 4 - PAD;
-    if (dw * 4 >= w + 2 * PAD) return;
-    const int y = reflect101(row - PAD, h);
-    const uint8_t* s = src + img * img_stride + (int64_t)y * stride;
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        int x = x0 + k;
-        uint32_t b = (x < w + PAD) ? s[reflect101(x, w)] : 0u;
-        v |= b << (8 * k);
-    }
-    uint8_t* d = dst + img * pyr_bytes + (int64_t)row * pitch + dw * 4;
-    *reinterpret_cast<uint32_t*>(d) = v;
-}
-
-// pyrDown interior of level l+1 from padded level l (pyramids.cpp pyrDown_):
-// out(y,x) = (sum k_i k_j in(2y+i-2, 2x+j-2) + 128) >> 8, k = [1 4 6 4 1].
-// LDS tile: 16 output rows x 64 output cols <- 35 x 131 input bytes.
-constexpr int PD_TW = 64, PD_TH = 16;
-constexpr int PD_IN_ROWS = 2 * PD_TH + 3;     // 35
-constexpr int PD_IN_DW = (2 * PD_TW + 3 + 3 + 3) / 4 + 1;  // dwords per input row (36)
-
-__global__ void __launch_bounds__(256) pyr_down_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                                       int64_t off_src, int pitch_src, int w_src,
-                                                       int h_src, int64_t off_dst, int pitch_dst,
-                                                       int w_dst, int h_dst) {
-    __shared__ uint32_t tile[PD_IN_ROWS][PD_IN_DW];
-    __shared__ int hsum[PD_IN_ROWS][PD_TW + 1];
-    const int img = blockIdx.z;
-    uint8_t* base = pyr + img * pyr_bytes;
-    const int x0 = blockIdx.x * PD_TW, y0 = blockIdx.y * PD_TH;
-    // input region: X in [2*x0-2, 2*x0+2*PD_TW+1), Y in [2*y0-2, 2*y0+2*PD_TH+1)
-    const int64_t row0 = off_src + (int64_t)(2 * y0 - 2 + PAD) * pitch_src;
-    const int xb = 2 * x0 - 2 + PAD;   // byte column of the first input pixel
-    const int xa = xb & ~3, sh = xb - xa;
-    const int max_y = h_src + PAD - 1 + PAD;  // last valid padded row index (inclusive)
-    for (int i = threadIdx.x; i < PD_IN_ROWS * PD_IN_DW; i += 256) {
-        int r = i / PD_IN_DW, c = i - r * PD_IN_DW;
-        int prow = 2 * y0 - 2 + PAD + r;
-        int pcol = xa + 4 * c;
-        uint32_t v = 0;
-        if (prow <= max_y && pcol + 3 < pitch_src)
-            v = *reinterpret_cast<const uint32_t*>(base + row0 + (int64_t)r * pitch_src + pcol);
-        tile[r][c] = v;
-    }
-    __syncthreads();
-    const uint8_t* tb = reinterpret_cast<const uint8_t*>(&tile[0][0]);
-    // horizontal pass
-    for (int i = threadIdx.x; i < PD_IN_ROWS * PD_TW; i += 256) {
-        int r = i / PD_TW, c = i - r * PD_TW;
-        const uint8_t* p = tb + r * (PD_IN_DW * 4) + sh + 2 * c;
-        hsum[r][c] = (int)p[0] + 4 * (int)p[1] + 6 * (int)p[2] + 4 * (int)p[3] + (int)p[4];
-    }
-    __syncthreads();
-    // vertical pass + store
-    for (int i = threadIdx.x; i < PD_TH * PD_TW; i += 256) {
-        int r = i / PD_TW, c = i - r * PD_TW;
-        int x = x0 + c, y = y0 + r;
-        if (x >= w_dst || y >= h_dst) continue;
-        int s = hsum[2 * r][c] + 4 * hsum[2 * r + 1][c] + 6 * hsum[2 * r + 2][c] +
-                4 * hsum[2 * r + 3][c] + hsum[2 * r + 4][c];
-        base[off_dst + (int64_t)(y + PAD) * pitch_dst + x + PAD] = (uint8_t)((s + 128) >> 8);
-    }
-}
-
-// Fill the PAD ring of a level from its interior (copyMakeBorder REFLECT_101).
-__global__ void __launch_bounds__(256) pyr_ring_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes,
-                                                       int64_t off, int pitch, int w, int h) {
-    const int img = blockIdx.z;
-    const int prow = blockIdx.y;  // 0 .. h+2P-1
-    const int y = prow - PAD;
-    const int x = blockIdx.x * 256 + threadIdx.x - PAD;
-    if (x >= w + PAD) return;
-    const bool inside_row = (unsigned)y < (unsigned)h;
-    if (inside_row && (unsigned)x < (unsigned)w) return;
-    uint8_t* base = pyr + img * pyr_bytes + off;
-    const int sy = reflect101(y, h), sx = reflect101(x, w);
-    base[(int64_t)prow * pitch + x + PAD] = base[(int64_t)(sy + PAD) * pitch + sx + PAD];
-}
-
-// ----------------------------------------------------------------- LK
-
 constexpr int W_BITS = 14;
 constexpr float FLT_SCALE = 1.f / (1 << 20);
 
-__device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
+typedef short v2s __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ long long wave_sum(long long v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// a.lo*b.lo + a.hi*b.hi + c on signed int16 halves (v_dot2_i32_i16)
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c, false);
 }
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// (lo & 0xffff) | (hi << 16)
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) {
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+// bytes (b[t], b[t+1]) of the 8-byte value {d1:d0} zero-extended to int16 halves
+template <int T>
+__device__ __forceinline__ uint32_t byte_pair(uint32_t d0, uint32_t d1) {
+    return __builtin_amdgcn_perm(d1, d0, 0x0c000c00u | ((uint32_t)(T + 1) << 16) | (uint32_t)T);
+}
+__device__ __forceinline__ uint32_t psub16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) - __builtin_bit_cast(v2s, b));
 }
 
-// Load 16 bytes around p from dword-aligned addresses and realign so that the
-// returned d[k] holds bytes p[4k .. 4k+3].
+// Load NDW dwords starting at byte p (any alignment) from dword-aligned
+// addresses and realign: d[k] = bytes p[4k .. 4k+3].  The pointer stays derived
+// from p so the loads remain global_load (address-space inference).
 template <int NDW>
 __device__ __forceinline__ void load_aligned(const uint8_t* p, uint32_t (&d)[NDW]) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
     uint32_t w[NDW + 1];
 #pragma unroll
     for (int k = 0; k <= NDW; ++k) w[k] = q[k];
 #pragma unroll
     for (int k = 0; k < NDW; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
 }
-
 template <int NDW>
 __device__ __forceinline__ int byte_at(const uint32_t (&d)[NDW], int c) {
     return (int)((d[c >> 2] >> (8 * (c & 3))) & 0xffu);
 }
 
-__device__ __forceinline__ void bilinear_weights(float a, float b, int& w00, int& w01, int& w10,
-                                                 int& w11) {
-    w00 = __float2int_rn((1.f - a) * (1.f - b) * (float)(1 << W_BITS));
-    w01 = __float2int_rn(a * (1.f - b) * (float)(1 << W_BITS));
-    w10 = __float2int_rn((1.f - a) * b * (float)(1 << W_BITS));
-    w11 = (1 << W_BITS) - w00 - w01 - w10;
+// cvRound((1-a)(1-b) 2^14) ... in fp32 (LKTrackerInvoker), packed as int16 pairs
+// W0 = (w00, w01), W1 = (w10, w11).
+__device__ __forceinline__ void weights(float a, float b, uint32_t& W0, uint32_t& W1) {
+    const int w00 = __float2int_rn((1.f - a) * (1.f - b) * (float)(1 << W_BITS));
+    const int w01 = __float2int_rn(a * (1.f - b) * (float)(1 << W_BITS));
+    const int w10 = __float2int_rn((1.f - a) * b * (float)(1 << W_BITS));
+    const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+    W0 = pack16(w00, w01);
+    W1 = pack16(w10, w11);
 }
 
 struct LkCfg {
@@ -173,23 +82,147 @@ struct LkCfg {
     int use_initial_flow;
 };
 
-// LKTrackerInvoker::operator() for one point across all levels (coarse to fine),
-// executed by one wavefront.  I/J are the padded pyramids of prev/next image.
-__device__ void lk_point(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
-                         const PyrLayout& lay, const LkCfg& cfg, float p0x, float p0y, float& nx,
-                         float& ny, int& status, float& err, int lane) {
-    const bool valid = lane < 63;
-    const int wy = valid ? lane / 3 : 20;   // window row owned by this lane
-    const int ws = valid ? lane - 3 * (lane / 3) : 2;  // 7-pixel segment
+// One window unit: 7 pixels (cols 7*seg .. 7*seg+6 of window row `row`).
+struct Unit {
+    int row, seg;
+    bool valid;
+    uint32_t iv[4], ix[4], iy[4];  // packed int16 pairs (pixel 2k, 2k+1); pair 3 high = 0
+};
+
+// Extract I (5 fractional bits) and the Scharr gradient at the bilinear
+// window positions of one unit (LKTrackerInvoker window extraction), and
+// accumulate its structure-tensor partial sums.
+__device__ __forceinline__ void extract_unit(Unit& u, const uint8_t* Il, int pitch, int W, int H, int ipx,
+                                             int ipy, uint32_t W0, uint32_t W1, int& a11, int& a12,
+                                             int& a22) {
+    // rows ipy+row-1 .. ipy+row+2 as packed bytes (12 registers); the two
+    // bilinear rows are processed in turn, accumulating the dot products in place
+    const int X = ipx + 7 * u.seg - 1;
+    uint32_t d[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) load_aligned<3>(Il + __mul24(ipy + u.row - 1 + r, pitch) + X, d[r]);
+    int iv[8], ix[8], iy[8];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const uint32_t Wr = rr ? W1 : W0;
+        const bool row_in = (unsigned)(ipy + u.row + rr) < (unsigned)H;
+        int t0[10], t1[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            const int a = byte_at<3>(d[rr], c), b = byte_at<3>(d[rr + 1], c), e = byte_at<3>(d[rr + 2], c);
+            t0[c] = (a + e) * 3 + b * 10;
+            t1[c] = e - a;
+        }
+        int dx[8], dy[8];
+#pragma unroll
+        for (int c = 1; c <= 8; ++c) {
+            const bool in = row_in && (unsigned)(X + c) < (unsigned)W;
+            dx[c - 1] = in ? (t0[c + 1] - t0[c - 1]) : 0;
+            dy[c - 1] = in ? ((t1[c + 1] + t1[c - 1]) * 3 + t1[c] * 10) : 0;
+        }
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            // CV_DESCALE(sum, 9) for I, CV_DESCALE(sum, 14) for the derivatives
+            const uint32_t pp = pack16(byte_at<3>(d[rr + 1], t + 1), byte_at<3>(d[rr + 1], t + 2));
+            iv[t] = dot2(pp, Wr, rr ? iv[t] : 1 << (W_BITS - 6));
+            ix[t] = dot2(pack16(dx[t], dx[t + 1]), Wr, rr ? ix[t] : 1 << (W_BITS - 1));
+            iy[t] = dot2(pack16(dy[t], dy[t + 1]), Wr, rr ? iy[t] : 1 << (W_BITS - 1));
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        iv[t] >>= (W_BITS - 5);
+        ix[t] >>= W_BITS;
+        iy[t] >>= W_BITS;
+    }
+    iv[7] = ix[7] = iy[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        u.iv[k] = pack16(iv[2 * k], iv[2 * k + 1]);
+        u.ix[k] = pack16(ix[2 * k], ix[2 * k + 1]);
+        u.iy[k] = pack16(iy[2 * k], iy[2 * k + 1]);
+    }
+    if (u.valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            a11 = dot2(u.ix[k], u.ix[k], a11);
+            a12 = dot2(u.ix[k], u.iy[k], a12);
+            a22 = dot2(u.iy[k], u.iy[k], a22);
+        }
+    }
+}
+
+// Mismatch of one unit against J at integer offset (jx, jy) with weights
+// (W0, W1): accumulates b1 += diff*Ix, b2 += diff*Iy (or es += |diff| for ERR).
+template <bool ERR>
+__device__ __forceinline__ void match_unit(const Unit& u, const uint8_t* Jl, int pitch, int jx, int jy,
+                                           uint32_t W0, uint32_t W1, int& b1, int& b2, int& es) {
+    const uint8_t* jp = Jl + __mul24(jy + u.row, pitch) + jx + 7 * u.seg;
+    uint32_t r0[2], r1[2];
+    load_aligned<2>(jp, r0);
+    load_aligned<2>(jp + pitch, r1);
+    constexpr int RND = 1 << (W_BITS - 6);
+    int jv[8];
+    jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2(byte_pair<0>(r0[0], r0[1]), W0, RND));
+    jv[1] = dot2(byte_pair<1>(r1[0], r1[1]), W1, dot2(byte_pair<1>(r0[0], r0[1]), W0, RND));
+    jv[2] = dot2(byte_pair<2>(r1[0], r1[1]), W1, dot2(byte_pair<2>(r0[0], r0[1]), W0, RND));
+    jv[3] = dot2(byte_pair<3>(r1[0], r1[1]), W1, dot2(byte_pair<3>(r0[0], r0[1]), W0, RND));
+    jv[4] = dot2(byte_pair<4>(r1[0], r1[1]), W1, dot2(byte_pair<4>(r0[0], r0[1]), W0, RND));
+    jv[5] = dot2(byte_pair<5>(r1[0], r1[1]), W1, dot2(byte_pair<5>(r0[0], r0[1]), W0, RND));
+    jv[6] = dot2(byte_pair<6>(r1[0], r1[1]), W1, dot2(byte_pair<6>(r0[0], r0[1]), W0, RND));
+#pragma unroll
+    for (int t = 0; t < 7; ++t) jv[t] >>= (W_BITS - 5);
+    jv[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);  // diff pair
+        if (ERR) {
+            const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
+            es += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
+        } else {
+            b1 = dot2(d, u.ix[k], b1);
+            b2 = dot2(d, u.iy[k], b2);
+        }
+    }
+}
+
+// Exact wave-wide sum of per-lane values |v| < 2^28 (one 7-pixel unit of
+// products per lane): 14-bit halves keep both DPP reductions within int32.
+__device__ __forceinline__ int wave_total(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm 2,3,0,1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);  // row_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1,3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2,3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ long long wave_sum64(int v) {
+    const long long sh = (long long)wave_total(v >> 14);
+    const long long sl = (long long)wave_total(v & 0x3fff);
+    return sh * 16384 + sl;
+}
+
+// LKTrackerInvoker::operator() for one point across all levels (coarse to
+// fine), one wavefront per point, one 7-pixel window unit per lane (lane 63
+// idle).  I/J: padded pyramids of the prev / next image.
+__device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
+                                        const PyrLayout& lay, const LkCfg& cfg, float p0x, float p0y, float& nx,
+                                        float& ny, int& status, float& err, int lane) {
+    Unit u;
+    u.valid = lane < 63;
+    const int uc = u.valid ? lane : 62;
+    u.row = uc / 3;
+    u.seg = uc - 3 * u.row;
     const float halfw = (float)((WIN - 1) * 0.5f);
     const int max_level = lay.nlev - 1;
     status = 1;
     err = 0.f;
     for (int l = max_level; l >= 0; --l) {
         const int W = lay.w[l], H = lay.h[l], pitch = lay.pitch[l];
-        const uint8_t* Il = I + lay.off[l] + (int64_t)PAD * pitch + PAD;  // (0,0)
-        const uint8_t* Jl = J + lay.off[l] + (int64_t)PAD * pitch + PAD;
-        const float sc = (float)(1. / (1 << l));
+        const uint8_t* Il = I + lay.off[l] + __mul24(PAD, pitch) + PAD;  // (0,0)
+        const uint8_t* Jl = J + lay.off[l] + __mul24(PAD, pitch) + PAD;
+        const float sc = ldexpf(1.f, -l);  // == (float)(1./(1 << l)), exact
         float prevx = p0x * sc, prevy = p0y * sc;
         float nextx, nexty;
         if (l == max_level) {
@@ -216,69 +249,16 @@ __device__ void lk_point(const uint8_t* __restrict__ I, const uint8_t* __restric
             }
             continue;
         }
-        int iw00, iw01, iw10, iw11;
-        bilinear_weights(prevx - ipx, prevy - ipy, iw00, iw01, iw10, iw11);
-
-        // ---- window of I and its Scharr derivative (rows wy-1 .. wy+2) ----
-        int P[4][10];
-        {
-            const int X = ipx + 7 * ws - 1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                uint32_t d[3];
-                load_aligned<3>(Il + (int64_t)(ipy + wy - 1 + r) * pitch + X, d);
-#pragma unroll
-                for (int c = 0; c < 10; ++c) P[r][c] = byte_at<3>(d, c);
-            }
-        }
-        int Iv[7], Ix[7], Iy[7];
-        int dxv[2][8], dyv[2][8];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const int r = rr + 1;
-            const int Yd = ipy + wy + rr;
-            const bool row_in = (unsigned)Yd < (unsigned)H;
-            int t0[10], t1[10];
-#pragma unroll
-            for (int c = 0; c < 10; ++c) {
-                t0[c] = (P[r - 1][c] + P[r + 1][c]) * 3 + P[r][c] * 10;
-                t1[c] = P[r + 1][c] - P[r - 1][c];
-            }
-#pragma unroll
-            for (int c = 1; c <= 8; ++c) {
-                const int Xd = ipx + 7 * ws + c - 1;
-                const bool in = row_in && (unsigned)Xd < (unsigned)W;
-                dxv[rr][c - 1] = in ? (t0[c + 1] - t0[c - 1]) : 0;
-                dyv[rr][c - 1] = in ? ((t1[c + 1] + t1[c - 1]) * 3 + t1[c] * 10) : 0;
-            }
-        }
+        uint32_t W0, W1;
+        weights(prevx - ipx, prevy - ipy, W0, W1);
         int a11 = 0, a12 = 0, a22 = 0;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            Iv[t] = descale(P[1][t + 1] * iw00 + P[1][t + 2] * iw01 + P[2][t + 1] * iw10 +
-                                P[2][t + 2] * iw11,
-                            W_BITS - 5);
-            Ix[t] = descale(dxv[0][t] * iw00 + dxv[0][t + 1] * iw01 + dxv[1][t] * iw10 +
-                                dxv[1][t + 1] * iw11,
-                            W_BITS);
-            Iy[t] = descale(dyv[0][t] * iw00 + dyv[0][t + 1] * iw01 + dyv[1][t] * iw10 +
-                                dyv[1][t + 1] * iw11,
-                            W_BITS);
-            a11 += Ix[t] * Ix[t];
-            a12 += Ix[t] * Iy[t];
-            a22 += Iy[t] * Iy[t];
-        }
-        if (!valid) a11 = a12 = a22 = 0;
-        const long long iA11 = wave_sum((long long)a11);
-        const long long iA12 = wave_sum((long long)a12);
-        const long long iA22 = wave_sum((long long)a22);
-        const float A11 = (float)iA11 * FLT_SCALE;
-        const float A12 = (float)iA12 * FLT_SCALE;
-        const float A22 = (float)iA22 * FLT_SCALE;
+        extract_unit(u, Il, pitch, W, H, ipx, ipy, W0, W1, a11, a12, a22);
+        const float A11 = (float)wave_sum64(a11) * FLT_SCALE;
+        const float A12 = (float)wave_sum64(a12) * FLT_SCALE;
+        const float A22 = (float)wave_sum64(a22) * FLT_SCALE;
         float D = A11 * A22 - A12 * A12;
         const float minEig =
-            __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12),
-                      (float)(2 * WIN * WIN));
+            __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12), (float)(2 * WIN * WIN));
         if (minEig < cfg.min_eig || D < __FLT_EPSILON__) {
             if (l == 0) {
                 status = 0;
@@ -297,25 +277,13 @@ __device__ void lk_point(const uint8_t* __restrict__ I, const uint8_t* __restric
                 if (l == 0) status = 0;
                 break;
             }
-            int jw00, jw01, jw10, jw11;
-            bilinear_weights(nextx - inx, nexty - iny, jw00, jw01, jw10, jw11);
-            const uint8_t* jp = Jl + (int64_t)(iny + wy) * pitch + inx + 7 * ws;
-            uint32_t d0[2], d1[2];
-            load_aligned<2>(jp, d0);
-            load_aligned<2>(jp + pitch, d1);
-            int b1 = 0, b2 = 0;
-#pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                const int jv = descale(byte_at<2>(d0, t) * jw00 + byte_at<2>(d0, t + 1) * jw01 +
-                                           byte_at<2>(d1, t) * jw10 + byte_at<2>(d1, t + 1) * jw11,
-                                       W_BITS - 5);
-                const int diff = jv - Iv[t];
-                b1 += diff * Ix[t];
-                b2 += diff * Iy[t];
-            }
-            if (!valid) b1 = b2 = 0;
-            const float fb1 = (float)wave_sum((long long)b1) * FLT_SCALE;
-            const float fb2 = (float)wave_sum((long long)b2) * FLT_SCALE;
+            uint32_t J0, J1;
+            weights(nextx - inx, nexty - iny, J0, J1);
+            int b1 = 0, b2 = 0, es = 0;
+            match_unit<false>(u, Jl, pitch, inx, iny, J0, J1, b1, b2, es);
+            if (!u.valid) b1 = b2 = 0;
+            const float fb1 = (float)wave_sum64(b1) * FLT_SCALE;
+            const float fb2 = (float)wave_sum64(b2) * FLT_SCALE;
             const float dx = (A12 * fb2 - A22 * fb1) * D;
             const float dy = (A12 * fb1 - A11 * fb2) * D;
             nextx += dx;
@@ -332,45 +300,33 @@ __device__ void lk_point(const uint8_t* __restrict__ I, const uint8_t* __restric
             pdy = dy;
         }
         if (status && l == 0) {
-            const float ex = nx - halfw, ey = ny - halfw;
-            const int inx = (int)floorf(ex), iny = (int)floorf(ey);
+            // final error (OPTFLOW_LK_GET_MIN_EIGENVALS not set)
+            const float exf = nx - halfw, eyf = ny - halfw;
+            const int inx = (int)floorf(exf), iny = (int)floorf(eyf);
             if (inx < -WIN || inx >= W || iny < -WIN || iny >= H) {
                 status = 0;
                 continue;
             }
-            int jw00, jw01, jw10, jw11;
-            bilinear_weights(ex - inx, ey - iny, jw00, jw01, jw10, jw11);
-            const uint8_t* jp = Jl + (int64_t)(iny + wy) * pitch + inx + 7 * ws;
-            uint32_t d0[2], d1[2];
-            load_aligned<2>(jp, d0);
-            load_aligned<2>(jp + pitch, d1);
-            int es = 0;
-#pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                const int jv = descale(byte_at<2>(d0, t) * jw00 + byte_at<2>(d0, t + 1) * jw01 +
-                                           byte_at<2>(d1, t) * jw10 + byte_at<2>(d1, t + 1) * jw11,
-                                       W_BITS - 5);
-                const int diff = jv - Iv[t];
-                es += diff < 0 ? -diff : diff;
-            }
-            if (!valid) es = 0;
-            err = __fdiv_rn((float)wave_sum_i(es) * 1.f, (float)(32 * WIN * WIN));
+            uint32_t J0, J1;
+            weights(exf - inx, eyf - iny, J0, J1);
+            int b1 = 0, b2 = 0, es = 0;
+            match_unit<true>(u, Jl, pitch, inx, iny, J0, J1, b1, b2, es);
+            if (!u.valid) es = 0;
+            err = __fdiv_rn((float)wave_total(es) * 1.f, (float)(32 * WIN * WIN));
         }
     }
 }
 
-__global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay,
-                                                  const uint8_t* __restrict__ pyr_prev,
-                                                  const uint8_t* __restrict__ pyr_next,
-                                                  int64_t prev_stride, int64_t next_stride,
-                                                  const float* __restrict__ prev_xy,
-                                                  float* __restrict__ next_xy,
-                                                  float* __restrict__ back_xy,
-                                                  uint8_t* __restrict__ flags,
-                                                  float* __restrict__ err_out) {
+__global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
+                                                  const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
+                                                  int64_t next_stride, const float* __restrict__ prev_xy,
+                                                  float* __restrict__ next_xy, float* __restrict__ back_xy,
+                                                  uint8_t* __restrict__ flags, float* __restrict__ err_out) {
     const int lane = threadIdx.x & 63;
-    const int64_t gp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
+    // wave-uniform point index in an SGPR: the per-point state, the level /
+    // iteration control and the 2x2 solve then stay scalar (uniform branches)
+    const int64_t gp = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (gp >= total) return;
     const int64_t pair = gp / a.n_pts;
     const uint8_t* I = pyr_prev + pair * prev_stride;
@@ -380,7 +336,7 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay,
     float nx = next_xy[2 * gp], ny = next_xy[2 * gp + 1];
     int st = 1;
     float e = 0.f;
-    lk_point(I, J, lay, cfg, p0x, p0y, nx, ny, st, e, lane);
+    lk_wave(I, J, lay, cfg, p0x, p0y, nx, ny, st, e, lane);
     if (a.mode == 0) {
         if (lane == 0) {
             next_xy[2 * gp] = nx;
@@ -395,7 +351,7 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay,
     int st2 = 1;
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
-    lk_point(J, I, lay, cfg, nx, ny, bx, by, st2, e2, lane);
+    lk_wave(J, I, lay, cfg, nx, ny, bx, by, st2, e2, lane);
     if (lane == 0) {
         const double B = a.border;
         const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
@@ -416,8 +372,7 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay,
 // reduceVector (tracking.cc:831-839): order-preserving index compaction of the
 // keep bit, one workgroup per pair.
 __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* __restrict__ flags,
-                                                      int32_t* __restrict__ kept_idx,
-                                                      int32_t* __restrict__ n_kept) {
+                                                      int32_t* __restrict__ kept_idx, int32_t* __restrict__ n_kept) {
     __shared__ int wsum[4];
     const int pair = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -443,64 +398,21 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 
 }  // namespace
 
-PyrLayout make_layout(int w, int h, int max_level, int win) {
-    PyrLayout L{};
-    int64_t off = 0;
-    int sw = w, sh = h;
-    L.nlev = 0;
-    for (int level = 0; level <= max_level && level < MAX_LEVELS; ++level) {
-        L.w[level] = sw;
-        L.h[level] = sh;
-        L.pitch[level] = ((sw + 2 * PAD) + 63) / 64 * 64;
-        L.off[level] = off;
-        off += (int64_t)L.pitch[level] * (sh + 2 * PAD);
-        off = (off + 255) / 256 * 256;
-        L.nlev = level + 1;
-        sw = (sw + 1) / 2;
-        sh = (sh + 1) / 2;
-        if (sw <= win || sh <= win) break;
-    }
-    L.bytes = off;
-    return L;
-}
-
-hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride,
-                                 int n_img, const PyrLayout& lay, uint8_t* dst) {
-    if (n_img <= 0) return hipSuccess;
-    {
-        dim3 grid((lay.w[0] + 2 * PAD + 1023) / 1024, lay.h[0] + 2 * PAD, n_img);
-        hipLaunchKernelGGL(pyr_level0_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride,
-                           lay.w[0], lay.h[0], lay.pitch[0], lay.bytes, dst);
-    }
-    for (int l = 1; l < lay.nlev; ++l) {
-        dim3 g1((lay.w[l] + PD_TW - 1) / PD_TW, (lay.h[l] + PD_TH - 1) / PD_TH, n_img);
-        hipLaunchKernelGGL(pyr_down_kernel, g1, dim3(256), 0, c->stream, dst, lay.bytes,
-                           lay.off[l - 1], lay.pitch[l - 1], lay.w[l - 1], lay.h[l - 1], lay.off[l],
-                           lay.pitch[l], lay.w[l], lay.h[l]);
-        dim3 g2((lay.w[l] + 2 * PAD + 255) / 256, lay.h[l] + 2 * PAD, n_img);
-        hipLaunchKernelGGL(pyr_ring_kernel, g2, dim3(256), 0, c->stream, dst, lay.bytes, lay.off[l],
-                           lay.pitch[l], lay.w[l], lay.h[l]);
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
                       const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
-                      const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
-                      float* err) {
+                      const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags, float* err) {
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     if (total <= 0) return hipSuccess;
     dim3 grid((unsigned)((total + 3) / 4));
-    hipLaunchKernelGGL(klt_kernel, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next,
-                       prev_pair_stride, next_pair_stride, prev_xy, next_xy, back_xy, flags, err);
+    hipLaunchKernelGGL(klt_kernel, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
+                       next_pair_stride, prev_xy, next_xy, back_xy, flags, err);
     return hipGetLastError();
 }
 
 hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
                           int32_t* n_kept) {
     if (n_pairs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(compact_kernel, dim3(n_pairs), dim3(256), 0, c->stream, n_pts, flags, kept_idx,
-                       n_kept);
+    hipLaunchKernelGGL(compact_kernel, dim3(n_pairs), dim3(256), 0, c->stream, n_pts, flags, kept_idx, n_kept);
     return hipGetLastError();
 }
 

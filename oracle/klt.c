@@ -20,6 +20,10 @@
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
+/* Work counters (diagnostics only): [0] point-levels that reached the
+   Gauss-Newton loop, [1] Gauss-Newton iterations executed. */
+long long orc_lk_stats[2];
+
 void orc_klt_params_default(orc_klt_params* p) {
     p->win = 21;
     p->max_level = 3;
@@ -272,7 +276,9 @@ static void lk_level(const lk_job* jb) {
         nextx -= halfw;
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
+        __atomic_fetch_add(&orc_lk_stats[0], 1, __ATOMIC_RELAXED); /* point-levels */
         for (int j = 0; j < jb->p->max_iter; j++) {
+            __atomic_fetch_add(&orc_lk_stats[1], 1, __ATOMIC_RELAXED); /* iterations */
             int inx = cv_floor(nextx), iny = cv_floor(nexty);
             if (inx < -win || inx >= J->w || iny < -win || iny >= J->h) {
                 if (level == 0) jb->status[pt] = 0;
