@@ -138,6 +138,7 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return GVX_ERR_HIP;
     gvx_ctx* c = new gvx_ctx();
     c->device = device;
+    c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return GVX_ERR_HIP;
@@ -259,7 +260,7 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
     if (e != hipSuccess) return hip_err(c, e, "hipMemcpyAsync(frame)");
     hipEvent_t ev{};
     prof_begin(c, "pyramid", &ev);
-    e = launch_build_pyramids(c, dsrc, (int64_t)nb, w, 1, lay, f.pyr);
+    e = launch_build_pyramids(c, dsrc, (int64_t)nb, w, 1, lay, f.pyr, true);
     prof_end(c, "pyramid", ev);
     if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
     return hip_err(c, hipStreamSynchronize(c->stream), "frame_put sync");
@@ -347,7 +348,9 @@ static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, con
     a.cam_h = cam_h;
     hipEvent_t ev{};
     prof_begin(c, "klt", &ev);
-    e = launch_klt(c, a, lay, fp.pyr, fn.pyr, 0, 0, d_prev, d_next, mode ? d_back : nullptr, d_flags,
+    const int64_t o0 = lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
+    const Level0 l0{fp.pyr + o0, fn.pyr + o0, 0, 0, lay.pitch[0], 0};
+    e = launch_klt(c, a, lay, fp.pyr, fn.pyr, 0, 0, l0, d_prev, d_next, mode ? d_back : nullptr, d_flags,
                    d_err);
     prof_end(c, "klt", ev);
     if (e != hipSuccess) return hip_err(c, e, "klt kernel");
@@ -436,8 +439,9 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
     uint8_t* pyr_next = pyr + (size_t)lay.bytes * n_pairs;
     hipEvent_t ev{};
     prof_begin(c, "pyramid", &ev);
-    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, n_pairs, lay, pyr_prev);
-    if (e == hipSuccess) e = launch_build_pyramids(c, d_next, (int64_t)w * h, w, n_pairs, lay, pyr_next);
+    // level 0 stays in the caller's images; levels >= 1 go to the pyramid slots
+    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, n_pairs, lay, pyr_prev, false);
+    if (e == hipSuccess) e = launch_build_pyramids(c, d_next, (int64_t)w * h, w, n_pairs, lay, pyr_next, false);
     prof_end(c, "pyramid", ev);
     if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
     if (n_pts == 0) {
@@ -458,7 +462,8 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
         if (e != hipSuccess) return hip_err(c, e, "init flow");
     }
     prof_begin(c, "klt", &ev);
-    e = launch_klt(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, d_prev_xy, d_next_xy, d_back_xy,
+    const Level0 l0{d_prev, d_next, (int64_t)w * h, (int64_t)w * h, w, 1};
+    e = launch_klt(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, l0, d_prev_xy, d_next_xy, d_back_xy,
                    d_flags, nullptr);
     prof_end(c, "klt", ev);
     if (e != hipSuccess) return hip_err(c, e, "klt kernel");

@@ -55,6 +55,7 @@ struct ProfEntry {
 
 struct gvx_ctx {
     int device = 0;
+    int n_cu = 256;  // compute units (persistent-grid sizing)
     hipStream_t stream = nullptr;
     std::string err;
     std::unordered_map<uint64_t, gvx::Frame> frames;
@@ -86,9 +87,10 @@ void prof_drain(gvx_ctx* c);
 
 // ---- kernel launchers (klt.hip) ----
 // Build pyramids for n_img images (h x w, row stride `stride` bytes, image i at
-// src + i*img_stride) into dst + i*lay.bytes.
+// src + i*img_stride) into dst + i*lay.bytes: levels >= 1 always; the padded
+// level-0 copy only when write_l0 (otherwise level 0 stays the caller's image).
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride,
-                                 int n_img, const PyrLayout& lay, uint8_t* dst);
+                                 int n_img, const PyrLayout& lay, uint8_t* dst, bool write_l0);
 
 struct KltArgs {
     int32_t n_pairs, n_pts;
@@ -101,11 +103,22 @@ struct KltArgs {
     int32_t cam_w, cam_h;
 };
 
-// Pyramid of pair i: prev at pyr_prev + idx_prev[i]*lay.bytes (idx arrays may be
-// null => i); likewise next.
+// Level 0 of pair i: prev plane at prev + i*prev_stride (pointer to pixel (0,0),
+// rows `pitch` bytes apart), likewise next.  raw = 1: the caller's unpadded
+// images (border windows are gathered with REFLECT_101); raw = 0: the padded
+// level-0 slot of a pyramid.
+struct Level0 {
+    const uint8_t* prev;
+    const uint8_t* next;
+    int64_t prev_stride, next_stride;
+    int32_t pitch, raw;
+};
+
+// Pyramid (levels >= 1) of pair i: prev at pyr_prev + i*prev_pair_stride, next
+// at pyr_next + i*next_pair_stride.
 hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
                       const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
-                      const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                      const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
                       float* err);
 hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
                           int32_t* n_kept);

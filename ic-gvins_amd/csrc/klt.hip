@@ -64,6 +64,53 @@ __device__ __forceinline__ int byte_at(const uint32_t (&d)[NDW], int c) {
     return (int)((d[c >> 2] >> (8 * (c & 3))) & 0xffu);
 }
 
+__device__ __forceinline__ int refl(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        p = p < 0 ? -p : 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+// Border windows of an unpadded plane (level 0 read in place): the wave gathers
+// its window -- rows y0 .. y0+rows-1, bytes x0 .. x0+31, REFLECT_101 outside
+// the image (the values the padded ring of OpenCV's pyramid level holds there)
+// -- into its own LDS tile once (byte buffer loads off the wave-uniform plane
+// base), then every lane reads its rows from LDS like the aligned global path.
+constexpr int WIN_DW = 8;  // dwords per LDS tile row
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void fill_win(uint32_t* win, const uint8_t* plane, int pitch, int W, int H, int x0,
+                                         int y0, int rows, int lane) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(plane), (short)0, 0x7fffffff, 0x00020000);
+    wave_lds_sync();  // earlier reads of the tile are done
+#pragma unroll 1
+    for (int i = lane; i < rows * WIN_DW; i += 64) {
+        const int r = i >> 3, q = i & 7;
+        const int ro = refl(y0 + r, H) * pitch;
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, ro + refl(x0 + 4 * q + b, W), 0, 0) << (8 * b);
+        win[i] = v;
+    }
+    wave_lds_sync();
+}
+template <int NDW>
+__device__ __forceinline__ void read_win(const uint32_t* win, int row, int byteoff, uint32_t (&d)[NDW]) {
+    const uint32_t* p = win + row * WIN_DW + (byteoff >> 2);
+    const uint32_t sh = (uint32_t)(byteoff & 3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for (int k = 0; k <= NDW; ++k) w[k] = p[k];
+#pragma unroll
+    for (int k = 0; k < NDW; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+}
+
 // cvRound((1-a)(1-b) 2^14) ... in fp32 (LKTrackerInvoker), packed as int16 pairs
 // W0 = (w00, w01), W1 = (w10, w11).
 __device__ __forceinline__ void weights(float a, float b, uint32_t& W0, uint32_t& W1) {
@@ -92,15 +139,13 @@ struct Unit {
 // Extract I (5 fractional bits) and the Scharr gradient at the bilinear
 // window positions of one unit (LKTrackerInvoker window extraction), and
 // accumulate its structure-tensor partial sums.
-__device__ __forceinline__ void extract_unit(Unit& u, const uint8_t* Il, int pitch, int W, int H, int ipx,
+// d[r]: bytes X .. X+11 (X = ipx + 7*seg - 1) of rows ipy+row-1+r, r = 0..3.
+__device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3], int W, int H, int ipx,
                                              int ipy, uint32_t W0, uint32_t W1, int& a11, int& a12,
                                              int& a22) {
-    // rows ipy+row-1 .. ipy+row+2 as packed bytes (12 registers); the two
-    // bilinear rows are processed in turn, accumulating the dot products in place
+    // the two bilinear rows are processed in turn, accumulating the dot
+    // products in place
     const int X = ipx + 7 * u.seg - 1;
-    uint32_t d[4][3];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) load_aligned<3>(Il + __mul24(ipy + u.row - 1 + r, pitch) + X, d[r]);
     int iv[8], ix[8], iy[8];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
@@ -154,13 +199,10 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint8_t* Il, int pit
 
 // Mismatch of one unit against J at integer offset (jx, jy) with weights
 // (W0, W1): accumulates b1 += diff*Ix, b2 += diff*Iy (or es += |diff| for ERR).
+// r0 / r1: bytes jx+7*seg .. +7 of rows jy+row and jy+row+1.
 template <bool ERR>
-__device__ __forceinline__ void match_unit(const Unit& u, const uint8_t* Jl, int pitch, int jx, int jy,
+__device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
                                            uint32_t W0, uint32_t W1, int& b1, int& b2, int& es) {
-    const uint8_t* jp = Jl + __mul24(jy + u.row, pitch) + jx + 7 * u.seg;
-    uint32_t r0[2], r1[2];
-    load_aligned<2>(jp, r0);
-    load_aligned<2>(jp + pitch, r1);
     constexpr int RND = 1 << (W_BITS - 6);
     int jv[8];
     jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2(byte_pair<0>(r0[0], r0[1]), W0, RND));
@@ -203,12 +245,56 @@ __device__ __forceinline__ long long wave_sum64(int v) {
     return sh * 16384 + sl;
 }
 
+// Window rows of one unit: 4 rows x 12 bytes of I for the extraction, 2 rows x
+// 8 bytes of J for a match.  `raw` planes (level 0 read in place from the
+// caller's image) take the aligned-load path only when every byte it touches is
+// inside the image, and gather with REFLECT_101 otherwise; padded levels always
+// take the aligned path (their PAD ring covers every window the LK loop admits).
+__device__ __forceinline__ void load_i_rows(const Unit& u, const uint8_t* Il, int pitch, int W, int H, int ipx,
+                                            int ipy, bool raw, uint32_t* win, int lane, uint32_t (&d)[4][3]) {
+    if (!raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H)) {
+        const int X = ipx + 7 * u.seg - 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) load_aligned<3>(Il + __mul24(ipy + u.row - 1 + r, pitch) + X, d[r]);
+    } else {
+        // tile: rows ipy-1 .., bytes ipx-1 ..; the unit reads 4 rows x 12 bytes
+        fill_win(win, Il, pitch, W, H, ipx - 1, ipy - 1, WIN + 3, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) read_win<3>(win, u.row + r, 7 * u.seg, d[r]);
+    }
+}
+__device__ __forceinline__ void load_j_rows(const Unit& u, const uint8_t* Jl, int pitch, int W, int H, int jx,
+                                            int jy, bool raw, uint32_t* win, int lane, uint32_t (&r0)[2],
+                                            uint32_t (&r1)[2]) {
+    if (!raw || (jx >= 3 && jx + 26 <= W && jy >= 0 && jy + 22 <= H)) {
+        const uint8_t* jp = Jl + __mul24(jy + u.row, pitch) + jx + 7 * u.seg;
+        load_aligned<2>(jp, r0);
+        load_aligned<2>(jp + pitch, r1);
+    } else {
+        // tile: rows jy .., bytes jx ..; the unit reads 2 rows x 8 bytes
+        fill_win(win, Jl, pitch, W, H, jx, jy, WIN + 1, lane);
+        read_win<2>(win, u.row, 7 * u.seg, r0);
+        read_win<2>(win, u.row + 1, 7 * u.seg, r1);
+    }
+}
+
+// Level-0 planes of one pair: pointers to pixel (0,0), row pitch, and whether
+// they are the caller's unpadded images.
+struct L0Planes {
+    const uint8_t* i;
+    const uint8_t* j;
+    int pitch;
+    bool raw;
+};
+
 // LKTrackerInvoker::operator() for one point across all levels (coarse to
 // fine), one wavefront per point, one 7-pixel window unit per lane (lane 63
-// idle).  I/J: padded pyramids of the prev / next image.
+// idle).  I/J: padded pyramids of the prev / next image (levels >= 1); level 0
+// from `p0`.
 __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
-                                        const PyrLayout& lay, const LkCfg& cfg, float p0x, float p0y, float& nx,
-                                        float& ny, int& status, float& err, int lane) {
+                                        const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
+                                        float p0y, float& nx, float& ny, int& status, float& err, int lane,
+                                        uint32_t* win) {
     Unit u;
     u.valid = lane < 63;
     const int uc = u.valid ? lane : 62;
@@ -219,9 +305,11 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
     status = 1;
     err = 0.f;
     for (int l = max_level; l >= 0; --l) {
-        const int W = lay.w[l], H = lay.h[l], pitch = lay.pitch[l];
-        const uint8_t* Il = I + lay.off[l] + __mul24(PAD, pitch) + PAD;  // (0,0)
-        const uint8_t* Jl = J + lay.off[l] + __mul24(PAD, pitch) + PAD;
+        const int W = lay.w[l], H = lay.h[l];
+        const bool raw = l == 0 && p0.raw;
+        const int pitch = l == 0 ? p0.pitch : lay.pitch[l];
+        const uint8_t* Il = l == 0 ? p0.i : I + lay.off[l] + __mul24(PAD, pitch) + PAD;  // (0,0)
+        const uint8_t* Jl = l == 0 ? p0.j : J + lay.off[l] + __mul24(PAD, pitch) + PAD;
         const float sc = ldexpf(1.f, -l);  // == (float)(1./(1 << l)), exact
         float prevx = p0x * sc, prevy = p0y * sc;
         float nextx, nexty;
@@ -252,7 +340,11 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         uint32_t W0, W1;
         weights(prevx - ipx, prevy - ipy, W0, W1);
         int a11 = 0, a12 = 0, a22 = 0;
-        extract_unit(u, Il, pitch, W, H, ipx, ipy, W0, W1, a11, a12, a22);
+        {
+            uint32_t d[4][3];
+            load_i_rows(u, Il, pitch, W, H, ipx, ipy, raw, win, lane, d);
+            extract_unit(u, d, W, H, ipx, ipy, W0, W1, a11, a12, a22);
+        }
         const float A11 = (float)wave_sum64(a11) * FLT_SCALE;
         const float A12 = (float)wave_sum64(a12) * FLT_SCALE;
         const float A22 = (float)wave_sum64(a22) * FLT_SCALE;
@@ -280,7 +372,11 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
             uint32_t J0, J1;
             weights(nextx - inx, nexty - iny, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
-            match_unit<false>(u, Jl, pitch, inx, iny, J0, J1, b1, b2, es);
+            {
+                uint32_t r0[2], r1[2];
+                load_j_rows(u, Jl, pitch, W, H, inx, iny, raw, win, lane, r0, r1);
+                match_unit<false>(u, r0, r1, J0, J1, b1, b2, es);
+            }
             if (!u.valid) b1 = b2 = 0;
             const float fb1 = (float)wave_sum64(b1) * FLT_SCALE;
             const float fb2 = (float)wave_sum64(b2) * FLT_SCALE;
@@ -310,7 +406,11 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
             uint32_t J0, J1;
             weights(exf - inx, eyf - iny, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
-            match_unit<true>(u, Jl, pitch, inx, iny, J0, J1, b1, b2, es);
+            {
+                uint32_t r0[2], r1[2];
+                load_j_rows(u, Jl, pitch, W, H, inx, iny, raw, win, lane, r0, r1);
+                match_unit<true>(u, r0, r1, J0, J1, b1, b2, es);
+            }
             if (!u.valid) es = 0;
             err = __fdiv_rn((float)wave_total(es) * 1.f, (float)(32 * WIN * WIN));
         }
@@ -319,10 +419,12 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
 
 __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
                                                   const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
-                                                  int64_t next_stride, const float* __restrict__ prev_xy,
+                                                  int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
                                                   float* __restrict__ next_xy, float* __restrict__ back_xy,
                                                   uint8_t* __restrict__ flags, float* __restrict__ err_out) {
+    __shared__ uint32_t wins[4][(WIN + 3) * WIN_DW];  // per-wave border tiles
     const int lane = threadIdx.x & 63;
+    uint32_t* win = wins[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     // wave-uniform point index in an SGPR: the per-point state, the level /
     // iteration control and the 2x2 solve then stay scalar (uniform branches)
@@ -331,12 +433,14 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
     const int64_t pair = gp / a.n_pts;
     const uint8_t* I = pyr_prev + pair * prev_stride;
     const uint8_t* J = pyr_next + pair * next_stride;
+    const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.pitch, l0.raw != 0};
+    const L0Planes pb{pf.j, pf.i, pf.pitch, pf.raw};
     LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow};
     const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
     float nx = next_xy[2 * gp], ny = next_xy[2 * gp + 1];
     int st = 1;
     float e = 0.f;
-    lk_wave(I, J, lay, cfg, p0x, p0y, nx, ny, st, e, lane);
+    lk_wave(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, lane, win);
     if (a.mode == 0) {
         if (lane == 0) {
             next_xy[2 * gp] = nx;
@@ -351,7 +455,7 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
     int st2 = 1;
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
-    lk_wave(J, I, lay, cfg, nx, ny, bx, by, st2, e2, lane);
+    lk_wave(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, lane, win);
     if (lane == 0) {
         const double B = a.border;
         const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
@@ -400,12 +504,13 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 
 hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
                       const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
-                      const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags, float* err) {
+                      const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                      float* err) {
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     if (total <= 0) return hipSuccess;
     dim3 grid((unsigned)((total + 3) / 4));
     hipLaunchKernelGGL(klt_kernel, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
-                       next_pair_stride, prev_xy, next_xy, back_xy, flags, err);
+                       next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
     return hipGetLastError();
 }
 

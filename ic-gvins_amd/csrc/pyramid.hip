@@ -3,17 +3,24 @@
 // /root/reference/ic_gvins/ic_gvins/tracking/tracking.cc:385,390,487,493
 // (each image's pyramid is built once here and reused by every LK direction).
 //
-// Layout (gvx::PyrLayout): level l is stored with a PAD-pixel ring; the
-// interior is the exact pyrDown result, the ring replicates OpenCV's
-// copyMakeBorder(BORDER_REFLECT_101) padding.
-//   level0_kernel  padded copy of the source image, 16 bytes per thread
-//                  (16-byte loads/stores in the interior, reflect map in the ring)
-//   down_kernel    pyrDown interior: 64x32-output tiles; coalesced dword loads of
-//                  the 131x67 input tile into LDS, horizontal [1 4 6 4 1] pass on
-//                  8-byte LDS reads into an int16 LDS tile, vertical pass in
-//                  registers, one dword store per 4 outputs
-//   ring_kernel    the PAD ring of a level, only ring pixels are launched
+// Layout (gvx::PyrLayout): level l >= 1 is stored with a PAD-pixel ring; the
+// interior is the exact pyrDown result ((sum of [1 4 6 4 1]^T[1 4 6 4 1] + 128)
+// >> 8 over the REFLECT_101-extended source), the ring replicates OpenCV's
+// copyMakeBorder(BORDER_REFLECT_101) padding.  Level 0 is either read in place
+// from the caller's image (batched path; the LK kernel handles its border) or
+// copied into the padded slot of the layout (frame cache, whose detection pass
+// reads across ROI edges).
+//
+//   level0_kernel   padded copy of level 0 (frame cache only)
+//   fused_kernel<NL> NL pyrDown levels in one pass: a 128x64 tile of the source
+//                   level (+ the 5-tap halo of every level below it) is staged in
+//                   LDS with 16-byte loads, each level is filtered in LDS
+//                   (horizontal taps on v_dot4_u32_u8, vertical taps as packed u16)
+//                   and written once; intermediate levels never round-trip HBM
+//   ring_kernel     the PAD rings of all built levels >= 1, one launch
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "gvx_internal.h"
 
@@ -21,13 +28,15 @@ namespace gvx {
 
 namespace {
 
+// BORDER_REFLECT_101 index, branchless: exact for -(2*len-2) <= p <= 3*len-3
+// (two bounces), which covers every position these kernels read (halo and ring
+// overshoot <= 32 < 2*len-2 since levels are > 21 px); the final clamp keeps
+// addresses of unused positions in range.
 __device__ __forceinline__ int refl(int p, int len) {
-    if ((unsigned)p < (unsigned)len) return p;
-    if (len == 1) return 0;
-    do {
-        p = p < 0 ? -p : 2 * len - 2 - p;
-    } while ((unsigned)p >= (unsigned)len);
-    return p;
+    int a = abs(p);
+    a = min(a, 2 * len - 2 - a);
+    a = abs(a);
+    return min(a, len - 1);
 }
 
 // ------------------------------------------------------------------ level 0
@@ -40,7 +49,7 @@ __global__ void __launch_bounds__(256) level0_kernel(const uint8_t* __restrict__
     const int item = blockIdx.x * 256 + threadIdx.x;
     const int prow = item / groups, q = item - prow * groups;
     if (prow >= h + 2 * PAD) return;
-    const int X = q * 16 - PAD;                        // first source column
+    const int X = q * 16 - PAD;  // first source column
     const int sy = refl(prow - PAD, h);
     const uint8_t* s = src + img * img_stride + (int64_t)sy * stride;
     uint8_t* d = dst + img * pyr_bytes + (int64_t)prow * pitch + q * 16;
@@ -66,119 +75,321 @@ __global__ void __launch_bounds__(256) level0_kernel(const uint8_t* __restrict__
     *reinterpret_cast<uint4*>(d) = v;
 }
 
-// ------------------------------------------------------------------ pyrDown
-constexpr int TW = 64, TH = 32;             // output tile
-constexpr int IN_ROWS = 2 * TH + 3;         // 67
-constexpr int IN_DW = 34;                   // 136 bytes >= 2 + 2*TW + 3
-constexpr int HS_STRIDE = TW + 4;           // int16 per hsum row (8-byte aligned rows)
+// Workgroup barrier ordering LDS only: __syncthreads() also waits for every
+// outstanding global load (vmcnt(0)), which would serialise the next tile's
+// prefetch with this tile's filtering.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
-__global__ void __launch_bounds__(256) down_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes, int64_t off_src,
-                                                   int pitch_src, int h_src, int64_t off_dst, int pitch_dst,
-                                                   int w_dst, int h_dst) {
-    __shared__ uint32_t tile[IN_ROWS * IN_DW];
-    __shared__ short hs[IN_ROWS * HS_STRIDE];
-    const int img = blockIdx.z;
-    uint8_t* base = pyr + img * pyr_bytes;
-    const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
-    // input pixels X in [2*x0-2, 2*x0+2*TW+1), Y in [2*y0-2, 2*y0+2*TH+1); the
-    // byte column of X = 2*x0-2 is 2*x0+PAD-2 = 2 (mod 4): load from 2 earlier.
-    const int col0 = 2 * x0 + PAD - 4;   // dword aligned
-    const int row0 = 2 * y0 - 2 + PAD;   // padded row of the first input row
-    const int last_row = h_src + 2 * PAD - 1;
-    const uint8_t* src = base + off_src;
-    for (int i = threadIdx.x; i < IN_ROWS * IN_DW; i += 256) {
-        const int r = i / IN_DW, c = i - r * IN_DW;
-        const int prow = row0 + r, pcol = col0 + 4 * c;
-        uint32_t v = 0;
-        if (prow <= last_row && pcol + 4 <= pitch_src)
-            v = *reinterpret_cast<const uint32_t*>(src + (int64_t)prow * pitch_src + pcol);
-        tile[i] = v;
+// ------------------------------------------------------------ fused pyrDown
+// Tile geometry: the deepest of the NL output levels owns a (128>>NL) x (64>>NL)
+// tile; level k (k = 0 source .. NL) is computed over a region that starts
+// REG_OFF(k) pixels before the tile's owned origin at that level and spans
+// REG_N(k) x REG_M(k) pixels -- exactly the 5-tap dependency cone of the deepest
+// tile (region(k) = 2*region(k+1) + 3, starting 2*off(k+1)+2 earlier).
+template <int NL>
+struct Geo {
+    static constexpr int TXD = 128 >> NL, TYD = 64 >> NL;
+    static constexpr int n(int k) { return k >= NL ? TXD : 2 * n(k + 1) + 3; }
+    static constexpr int m(int k) { return k >= NL ? TYD : 2 * m(k + 1) + 3; }
+    static constexpr int off(int k) { return k >= NL ? 0 : 2 * off(k + 1) + 2; }
+    // groups of 4 outputs per row at level k >= 1
+    static constexpr int g(int k) { return (n(k) + 3) / 4; }
+    // LDS byte row stride of level k (k = 0: the 160-byte staged source rows)
+    static constexpr int rs(int k) { return k == 0 ? 160 : (4 * g(k) + 7) / 8 * 8; }
+};
+
+struct DownLevels {
+    int64_t off[3];  // padded-level offsets (bytes) inside one pyramid
+    int32_t pitch[3], w[3], h[3];
+};
+
+// Horizontal [1 4 6 4 1] taps of one source row into four u16 outputs: outputs
+// 4g..4g+3 read source bytes 8g .. 8g+10 of the row (`sh` = byte shift of the row
+// start inside its first dword, 0 or 2).
+template <int SH>
+__device__ __forceinline__ uint2 hsum4(const uint32_t* row, int g) {
+    const uint32_t* p = row + 2 * g;
+    const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
+    uint32_t d0, d1, d2;
+    if (SH == 0) {
+        d0 = w0;
+        d1 = w1;
+        d2 = w2;
+    } else {
+        const uint32_t w3 = p[3];
+        d0 = __builtin_amdgcn_alignbyte(w1, w0, SH);
+        d1 = __builtin_amdgcn_alignbyte(w2, w1, SH);
+        d2 = __builtin_amdgcn_alignbyte(w3, w2, SH);
     }
-    __syncthreads();
-    // horizontal pass: item = (row r, group g of 4 output columns)
-    for (int i = threadIdx.x; i < IN_ROWS * (TW / 4); i += 256) {
-        const int r = i / (TW / 4), g = i - r * (TW / 4);
-        // input bytes for outputs 4g..4g+3 start at tile byte 2 + 8g: read dwords 2g..2g+3
-        const uint2 lo = *reinterpret_cast<const uint2*>(&tile[r * IN_DW + 2 * g]);
-        const uint2 hi = *reinterpret_cast<const uint2*>(&tile[r * IN_DW + 2 * g + 2]);
-        const uint32_t d0 = __builtin_amdgcn_alignbyte(lo.y, lo.x, 2);
-        const uint32_t d1 = __builtin_amdgcn_alignbyte(hi.x, lo.y, 2);
-        const uint32_t d2 = __builtin_amdgcn_alignbyte(hi.y, hi.x, 2);
-        int p[12];
+    constexpr uint32_t K = 0x04060401u;  // taps 1 4 6 4 on bytes 0..3
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(d1, d0, 2), e3 = __builtin_amdgcn_alignbyte(d2, d1, 2);
+    const uint32_t o0 = __builtin_amdgcn_udot4(d0, K, d1 & 0xffu, false);
+    const uint32_t o1 = __builtin_amdgcn_udot4(e1, K, (d1 >> 16) & 0xffu, false);
+    const uint32_t o2 = __builtin_amdgcn_udot4(d1, K, d2 & 0xffu, false);
+    const uint32_t o3 = __builtin_amdgcn_udot4(e3, K, (d2 >> 16) & 0xffu, false);
+    return make_uint2(o0 | (o1 << 16), o2 | (o3 << 16));
+}
+
+// Vertical taps on packed u16 pairs: (a + 4b + 6c + 4d + e + 128) per half.
+// Every partial sum stays < 2^16 (inputs <= 4080, result <= 65408), so the two
+// halves never interact.
+__device__ __forceinline__ uint32_t vsum2(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+    typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+    const v2u A = __builtin_bit_cast(v2u, a), B = __builtin_bit_cast(v2u, b), C = __builtin_bit_cast(v2u, c),
+              D = __builtin_bit_cast(v2u, d), E = __builtin_bit_cast(v2u, e);
+    const v2u r = A + E + (B + D) * (unsigned short)4 + C * (unsigned short)6 + (unsigned short)128;
+    return __builtin_bit_cast(uint32_t, r);
+}
+// high bytes of the four u16 lanes of (lo, hi) = the (s + 128) >> 8 results
+__device__ __forceinline__ uint32_t hibytes(uint32_t lo, uint32_t hi) {
+    return __builtin_amdgcn_perm(hi, lo, 0x07050301u);
+}
+
+// Persistent: workgroup w builds tiles [w*per_wg, (w+1)*per_wg) of the
+// (image, tile row, tile column)-ordered tile list.  Consecutive tiles are
+// horizontal neighbours, so their shared halo lines stay in this CU's XCD L2,
+// and the next tile's source rows are fetched into registers while the
+// current tile is filtered (global latency off the critical path).
+template <int NL>
+__global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ src, int64_t src_img_stride,
+                                                    int src_pitch, int src_w, int src_h, int vec16,
+                                                    uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
+                                                    int tiles_x, int tiles_y, int n_tiles, int per_wg) {
+    using G = Geo<NL>;
+    constexpr int M0 = G::m(0);
+    constexpr int OFF0 = G::off(0);
+    constexpr int NITEM = M0 * 10;                // 16-byte chunks of the staged source region
+    constexpr int NST = (NITEM + 255) / 256;      // per thread
+    // LDS: staged source rows, reused for the byte planes of levels 1..NL-1; the
+    // u16 horizontal sums of the level being built.
+    constexpr int BYTES_A = (M0 * G::rs(0) > G::m(1) * G::rs(1) ? M0 * G::rs(0) : G::m(1) * G::rs(1)) + 64;
+    constexpr int HS_A = (M0 + 2) * 4 * G::g(1);  // u16 entries (largest level)
+    __shared__ __attribute__((aligned(16))) uint8_t bufA[BYTES_A];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[HS_A];
+    __shared__ __attribute__((aligned(16))) uint8_t bufB[NL > 1 ? G::m(2) * G::rs(2) + 64 : 16];
+
+    const int tid = threadIdx.x;
+    const int t_begin = blockIdx.x * per_wg;
+    const int t_end = min(t_begin + per_wg, n_tiles);
+    if (t_begin >= t_end) return;
+
+    // source region of tile t: rows [64*by - OFF0, +M0), bytes [128*bx - 16, +160).
+    // Rows are reflected per chunk (cheap); a 16-byte chunk whose columns are
+    // all inside the image is one vector load even in border tiles, only chunks
+    // straddling the left / right edge gather bytes.
+    uint4 pre[NST];
+    auto stage_load = [&](int t) {
+        const int bx = t % tiles_x, rest = t / tiles_x;
+        const int by = rest % tiles_y, img = rest / tiles_y;
+        const uint8_t* S = src + img * src_img_stride;
+        const int A = 128 * bx - 16, Y0 = 64 * by - OFF0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            p[k] = (d0 >> (8 * k)) & 255;
-            p[4 + k] = (d1 >> (8 * k)) & 255;
-            p[8 + k] = (d2 >> (8 * k)) & 255;
-        }
-        short o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            o[k] = (short)(p[2 * k] + 4 * p[2 * k + 1] + 6 * p[2 * k + 2] + 4 * p[2 * k + 3] + p[2 * k + 4]);
-        uint2 packed;
-        packed.x = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
-        packed.y = (uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16);
-        *reinterpret_cast<uint2*>(&hs[r * HS_STRIDE + 4 * g]) = packed;
-    }
-    __syncthreads();
-    // vertical pass: thread = (row pair rp, group g); 16 row pairs x 16 groups
-    {
-        const int g = threadIdx.x & 15, rp = threadIdx.x >> 4;
-        const int y = y0 + 2 * rp;
-        int v[7][4];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const uint2 u = *reinterpret_cast<const uint2*>(&hs[(4 * rp + k) * HS_STRIDE + 4 * g]);
-            v[k][0] = (short)(u.x & 0xffff);
-            v[k][1] = (short)(u.x >> 16);
-            v[k][2] = (short)(u.y & 0xffff);
-            v[k][3] = (short)(u.y >> 16);
-        }
-        const int x = x0 + 4 * g;
-        if (x < w_dst) {
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr) {
-                if (y + rr >= h_dst) break;
-                uint32_t out = 0;
+        for (int j = 0; j < NST; ++j) {
+            const int i = tid + 256 * j;
+            if (i >= NITEM) break;
+            const int r = i / 10, c = i - r * 10;
+            const uint8_t* row = S + (int64_t)refl(Y0 + r, src_h) * src_pitch;
+            const int x = A + 16 * c;
+            if (vec16 && x >= 0 && x + 16 <= src_w) {
+                pre[j] = *reinterpret_cast<const uint4*>(row + x);
+            } else {
+                uint32_t q[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int s = v[2 * rr][k] + 4 * v[2 * rr + 1][k] + 6 * v[2 * rr + 2][k] +
-                                  4 * v[2 * rr + 3][k] + v[2 * rr + 4][k];
-                    out |= (uint32_t)((s + 128) >> 8) << (8 * k);
+                    uint32_t d = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) d |= (uint32_t)row[refl(x + 4 * k + b, src_w)] << (8 * b);
+                    q[k] = d;
                 }
-                // bytes past w_dst land in the ring, which ring_kernel rewrites
-                *reinterpret_cast<uint32_t*>(base + off_dst + (int64_t)(y + rr + PAD) * pitch_dst + x + PAD) = out;
+                pre[j] = make_uint4(q[0], q[1], q[2], q[3]);
             }
         }
+    };
+    stage_load(t_begin);
+
+    for (int t = t_begin; t < t_end; ++t) {
+        const int bx = t % tiles_x, rest = t / tiles_x;
+        const int by = rest % tiles_y, img = rest / tiles_y;
+        uint8_t* P = pyr + img * pyr_bytes;
+        const int X0 = 128 * bx, Yo = 64 * by;  // owned origin at the source level
+#pragma unroll
+        for (int j = 0; j < NST; ++j) {
+            const int i = tid + 256 * j;
+            if (i < NITEM) *reinterpret_cast<uint4*>(&bufA[16 * i]) = pre[j];  // row r = i/10, chunk c
+        }
+        lds_barrier();
+        if (t + 1 < t_end) stage_load(t + 1);
+
+        // ---- levels 1..NL ----
+        auto build = [&](auto kc, const uint8_t* in, int in_rs, uint8_t* out) {
+            constexpr int k = decltype(kc)::value;  // output level 1..NL
+            constexpr int NG = G::g(k), MO = G::m(k), MI = G::m(k - 1), RSO = G::rs(k);
+            constexpr int SH = k == 1 ? 2 : 0;
+            constexpr int DW0 = k == 1 ? (16 - OFF0 - 2) / 4 : 0;  // first dword of the row's taps
+            constexpr int OFFK = G::off(k);
+            const int lw = L.w[k - 1], lh = L.h[k - 1], lp = L.pitch[k - 1];
+            // horizontal pass
+            for (int i = tid; i < MI * NG; i += 256) {
+                const int r = i / NG, g = i - r * NG;
+                const uint2 o = hsum4<SH>(reinterpret_cast<const uint32_t*>(in + r * in_rs) + DW0, g);
+                *reinterpret_cast<uint2*>(&hs[r * 4 * NG + 4 * g]) = o;
+            }
+            lds_barrier();
+            // vertical pass: item = (output row pair, group)
+            const int ox = (X0 >> k) - OFFK, oy = (Yo >> k) - OFFK;  // region origin
+            for (int i = tid; i < ((MO + 1) / 2) * NG; i += 256) {
+                const int rp = i / NG, g = i - rp * NG;
+                uint2 h[7];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) h[q] = *reinterpret_cast<const uint2*>(&hs[(4 * rp + q) * 4 * NG + 4 * g]);
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    const int row = 2 * rp + rr;
+                    if (row >= MO) continue;
+                    const uint32_t lo =
+                        vsum2(h[2 * rr].x, h[2 * rr + 1].x, h[2 * rr + 2].x, h[2 * rr + 3].x, h[2 * rr + 4].x);
+                    const uint32_t hi =
+                        vsum2(h[2 * rr].y, h[2 * rr + 1].y, h[2 * rr + 2].y, h[2 * rr + 3].y, h[2 * rr + 4].y);
+                    const uint32_t q = hibytes(lo, hi);
+                    if (k < NL) {
+                        *reinterpret_cast<uint32_t*>(&out[row * RSO + 4 * g]) = q;
+                    } else {
+                        // deepest level: region == owned tile, store in place
+                        const int gx = ox + 4 * g, gy = oy + row;
+                        if (gx < lw && gy < lh)
+                            *reinterpret_cast<uint32_t*>(P + L.off[k - 1] + (int64_t)(gy + PAD) * lp + gx + PAD) = q;
+                    }
+                }
+            }
+            lds_barrier();
+            if (k < NL) {
+                // owned tile of this level -> global (owned columns start at region
+                // offset OFF = 2 (mod 4): realign pairs of LDS dwords)
+                constexpr int OFF = OFFK, OW = 128 >> k, OH = 64 >> k;
+                const int gx0 = X0 >> k, gy0 = Yo >> k;
+                for (int i = tid; i < OH * (OW / 4); i += 256) {
+                    const int r = i / (OW / 4), q = i - r * (OW / 4);
+                    const int gx = gx0 + 4 * q, gy = gy0 + r;
+                    if (gx >= lw || gy >= lh) continue;
+                    const uint32_t* p = reinterpret_cast<const uint32_t*>(&out[(OFF + r) * RSO + OFF + 4 * q - 2]);
+                    const uint32_t v = __builtin_amdgcn_alignbyte(p[1], p[0], 2);
+                    *reinterpret_cast<uint32_t*>(P + L.off[k - 1] + (int64_t)(gy + PAD) * lp + gx + PAD) = v;
+                }
+                // region entries outside the level's image take their REFLECT_101
+                // value (the next level's taps read them); the sources are inside
+                // the image and inside the region for every entry the owned tiles need
+                constexpr int NO = G::n(k);
+                // in-image part of the region: rows [r0, r1), columns [c0, c1)
+                const int c0 = max(0, -ox), c1 = min(NO, lw - ox);
+                const int r0 = max(0, -oy), r1 = min(MO, lh - oy);
+                if (c0 > 0 || c1 < NO || r0 > 0 || r1 < MO) {
+                    auto fix = [&](int r, int c) {
+                        const int sr = refl(oy + r, lh) - oy, sc = refl(ox + c, lw) - ox;
+                        if ((unsigned)sr < (unsigned)MO && (unsigned)sc < (unsigned)NO)
+                            out[r * RSO + c] = out[sr * RSO + sc];
+                    };
+                    // out-of-image columns over all rows, then out-of-image rows
+                    // over the in-image columns (sources are in-image entries only)
+                    const int ncl = c0, ncr = NO - c1, ncol = ncl + ncr;
+                    for (int i = tid; i < MO * ncol; i += 256) {
+                        const int r = i / ncol, j = i - r * ncol;
+                        fix(r, j < ncl ? j : c1 + (j - ncl));
+                    }
+                    const int nrt = r0, nrb = MO - r1, nrow = nrt + nrb, ncin = c1 - c0;
+                    for (int i = tid; i < nrow * ncin; i += 256) {
+                        const int j = i / ncin, c = c0 + (i - j * ncin);
+                        fix(j < nrt ? j : r1 + (j - nrt), c);
+                    }
+                }
+                lds_barrier();
+            }
+        };
+        // level 1 from the staged source (its byte plane overwrites the staged
+        // rows only after the horizontal pass has consumed them)
+        build(std::integral_constant<int, 1>{}, bufA, 160, bufA);
+        constexpr int RS1 = G::rs(1), RS2 = G::rs(2);
+        if constexpr (NL >= 2) build(std::integral_constant<int, 2>{}, bufA, RS1, bufB);
+        if constexpr (NL >= 3) build(std::integral_constant<int, 3>{}, bufB, RS2, bufA);
+        lds_barrier();  // the last level's LDS reads precede the next staging store
     }
 }
 
-// ------------------------------------------------------------------ ring
-// Ring pixels only: the top/bottom PAD rows over the full padded width, plus the
-// left/right PAD columns of the interior rows.
-__global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes, int64_t off,
-                                                   int pitch, int w, int h) {
-    const int img = blockIdx.y;
-    uint8_t* base = pyr + img * pyr_bytes + off;
-    const int wp = w + 2 * PAD;
-    const int n_band = 2 * PAD * wp;      // top + bottom bands
-    const int n_side = h * 2 * PAD;       // side bands of interior rows
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    int x, y;
-    if (i < n_band) {
-        const int r = i / wp, c = i - r * wp;
-        y = r < PAD ? r - PAD : h + (r - PAD);
-        x = c - PAD;
-    } else if (i < n_band + n_side) {
-        const int j = i - n_band;
-        const int r = j / (2 * PAD), c = j - r * (2 * PAD);
-        y = r;
-        x = c < PAD ? c - PAD : w + (c - PAD);
+// ------------------------------------------------------------------ rings
+// REFLECT_101 rings of levels lo..hi of every image in one launch.  Item = one
+// dword of ring: the top / bottom PAD rows over the padded width, then per
+// interior row the left PAD columns and the right columns [w, w+PAD) (dword
+// aligned; bytes of the last interior dword rewrite their own value).
+struct RingLevels {
+    int32_t n;                  // levels
+    int64_t off[MAX_LEVELS];
+    int32_t pitch[MAX_LEVELS], w[MAX_LEVELS], h[MAX_LEVELS];
+    int32_t dw[MAX_LEVELS];     // dwords per padded row (top/bottom bands)
+    int32_t rd0[MAX_LEVELS];    // first dword (padded col / 4) of the right band
+    int32_t rdn[MAX_LEVELS];    // dwords of the right band
+    int32_t items[MAX_LEVELS];  // ring dwords of the level
+};
+
+__global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes, RingLevels R) {
+    const int l = blockIdx.z;  // level slot (wave-uniform)
+    int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= R.items[l]) return;
+    const int w = R.w[l], h = R.h[l], pitch = R.pitch[l];
+    uint8_t* base = pyr + (int64_t)blockIdx.y * pyr_bytes + R.off[l];
+    int prow, pcol;  // padded row, padded byte column of the dword
+    const int nb = 2 * PAD * R.dw[l];
+    if (j < nb) {
+        const int r = j / R.dw[l];
+        prow = r < PAD ? r : h + r;
+        pcol = 4 * (j - r * R.dw[l]);
     } else {
-        return;
+        j -= nb;
+        const int per = PAD / 4 + R.rdn[l];
+        const int r = j / per, c = j - r * per;
+        prow = PAD + r;
+        pcol = c < PAD / 4 ? 4 * c : 4 * (R.rd0[l] + c - PAD / 4);
     }
-    const int sy = refl(y, h), sx = refl(x, w);
-    base[(int64_t)(y + PAD) * pitch + x + PAD] = base[(int64_t)(sy + PAD) * pitch + sx + PAD];
+    const int sy = refl(prow - PAD, h) + PAD;
+    const int x0 = pcol - PAD;
+    uint32_t v;
+    if (x0 >= 0 && x0 + 4 <= w) {
+        v = *reinterpret_cast<const uint32_t*>(base + (int64_t)sy * pitch + pcol);
+    } else {
+        v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int x = x0 + b;
+            if (x >= w + PAD) break;  // past the ring (pitch slack): leave 0
+            v |= (uint32_t)base[(int64_t)sy * pitch + refl(x, w) + PAD] << (8 * b);
+        }
+    }
+    *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = v;
+}
+
+template <int NL>
+void launch_fused(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int src_pitch, int src_w, int src_h,
+                  int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
+    // l0: source level index; builds levels l0+1 .. l0+NL
+    DownLevels D{};
+    for (int k = 0; k < NL; ++k) {
+        D.off[k] = lay.off[l0 + 1 + k];
+        D.pitch[k] = lay.pitch[l0 + 1 + k];
+        D.w[k] = lay.w[l0 + 1 + k];
+        D.h[k] = lay.h[l0 + 1 + k];
+    }
+    const int vec16 = (src_pitch % 16 == 0) && (src_img_stride % 16 == 0) &&
+                      (reinterpret_cast<uintptr_t>(src) % 16 == 0);
+    const int tiles_x = (src_w + 127) / 128, tiles_y = (src_h + 63) / 64;
+    const int n_tiles = tiles_x * tiles_y * n_img;
+    // resident workgroups per CU (LDS-bound: 27.7 / 21.9 / 19.6 KB for NL = 3 / 2 / 1)
+    const int slots = c->n_cu * (NL == 3 ? 5 : NL == 2 ? 7 : 8);
+    const int per_wg = (n_tiles + slots - 1) / slots;
+    const int n_wg = (n_tiles + per_wg - 1) / per_wg;
+    hipLaunchKernelGGL(fused_kernel<NL>, dim3(n_wg), dim3(256), 0, c->stream, src, src_img_stride, src_pitch,
+                       src_w, src_h, vec16, dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
 }
 
 }  // namespace
@@ -206,23 +417,55 @@ PyrLayout make_layout(int w, int h, int max_level, int win) {
 }
 
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride, int n_img,
-                                 const PyrLayout& lay, uint8_t* dst) {
+                                 const PyrLayout& lay, uint8_t* dst, bool write_l0) {
     if (n_img <= 0) return hipSuccess;
-    {
+    const uint8_t* s0 = src;
+    int64_t s0_img = img_stride;
+    int s0_pitch = stride;
+    if (write_l0) {
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
         const int items = groups * (lay.h[0] + 2 * PAD);
         dim3 grid((items + 255) / 256, n_img);
         hipLaunchKernelGGL(level0_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride, lay.w[0],
                            lay.h[0], lay.pitch[0], lay.bytes, dst);
+        // build the other levels from the aligned padded copy
+        s0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
+        s0_img = lay.bytes;
+        s0_pitch = lay.pitch[0];
     }
-    for (int l = 1; l < lay.nlev; ++l) {
-        dim3 g1((lay.w[l] + TW - 1) / TW, (lay.h[l] + TH - 1) / TH, n_img);
-        hipLaunchKernelGGL(down_kernel, g1, dim3(256), 0, c->stream, dst, lay.bytes, lay.off[l - 1],
-                           lay.pitch[l - 1], lay.h[l - 1], lay.off[l], lay.pitch[l], lay.w[l], lay.h[l]);
-        const int n_ring = 2 * PAD * (lay.w[l] + 2 * PAD) + lay.h[l] * 2 * PAD;
-        dim3 g2((n_ring + 255) / 256, n_img);
-        hipLaunchKernelGGL(ring_kernel, g2, dim3(256), 0, c->stream, dst, lay.bytes, lay.off[l], lay.pitch[l],
-                           lay.w[l], lay.h[l]);
+    // levels 1.. in fused passes of up to 3 levels
+    int l = 0;
+    while (l + 1 < lay.nlev) {
+        const int nl = lay.nlev - 1 - l >= 3 ? 3 : lay.nlev - 1 - l;
+        const uint8_t* s = l == 0 ? s0 : dst + lay.off[l] + (int64_t)PAD * lay.pitch[l] + PAD;
+        const int64_t si = l == 0 ? s0_img : lay.bytes;
+        const int sp = l == 0 ? s0_pitch : lay.pitch[l];
+        if (nl == 3)
+            launch_fused<3>(c, s, si, sp, lay.w[l], lay.h[l], n_img, lay, l, dst);
+        else if (nl == 2)
+            launch_fused<2>(c, s, si, sp, lay.w[l], lay.h[l], n_img, lay, l, dst);
+        else
+            launch_fused<1>(c, s, si, sp, lay.w[l], lay.h[l], n_img, lay, l, dst);
+        l += nl;
+    }
+    if (lay.nlev > 1) {
+        RingLevels R{};
+        R.n = lay.nlev - 1;
+        int most = 0;
+        for (int k = 0; k < R.n; ++k) {
+            const int lv = k + 1, w = lay.w[lv];
+            R.off[k] = lay.off[lv];
+            R.pitch[k] = lay.pitch[lv];
+            R.w[k] = w;
+            R.h[k] = lay.h[lv];
+            R.dw[k] = (w + 2 * PAD + 3) / 4;
+            R.rd0[k] = (w + PAD) / 4;
+            R.rdn[k] = (w + 2 * PAD + 3) / 4 - R.rd0[k];
+            R.items[k] = 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
+            most = R.items[k] > most ? R.items[k] : most;
+        }
+        dim3 grid((most + 255) / 256, n_img, R.n);
+        hipLaunchKernelGGL(ring_kernel, grid, dim3(256), 0, c->stream, dst, lay.bytes, R);
     }
     return hipGetLastError();
 }

@@ -126,3 +126,38 @@ def test_large_batch_invariants(ctx, gvx_mod):
         _assert_same(a["kept"][i][:len(keep)], keep, "kept")
     # tiled pairs are identical inputs -> identical outputs
     _assert_same(a["next"][0], a["next"][4], "tiling")
+
+
+def _border_points(w, h, n, rng):
+    """Points hugging / crossing every border at level 0 (the in-place level-0
+    read takes its REFLECT_101 gather path there) plus a few interior ones."""
+    side = rng.integers(0, 4, n)
+    t = rng.uniform(-30, 30, n)
+    pts = np.empty((n, 2), np.float32)
+    pts[:, 0] = np.where(side == 0, t, np.where(side == 1, w - 1 - t, rng.uniform(0, w, n)))
+    pts[:, 1] = np.where(side == 2, t, np.where(side == 3, h - 1 - t, rng.uniform(0, h, n)))
+    pts[:4] = [[0.5, 0.5], [w - 1.5, h - 1.5], [w / 2, h / 2], [3.25, h - 4.75]]
+    return pts
+
+
+@pytest.mark.parametrize("w,h,L", [(1280, 560, 3), (333, 149, 3), (324, 150, 2), (1000, 77, 1)])
+def test_batch_border_and_odd_sizes(ctx, orc, gvx_mod, w, h, L):
+    """Batched path with level 0 read in place: windows on the image border,
+    widths that are not multiples of 16 (no 16-byte staging loads), odd level
+    sizes, and 1- and 2-level pyramids (other fused-pyramid variants)."""
+    P, N = 3, 96
+    rng = np.random.default_rng(w * 7 + h)
+    I = np.stack([synth.make_image(w, h, rng) for _ in range(P)])
+    J = np.stack([np.roll(I[i], (1, -2), axis=(0, 1)) for i in range(P)])
+    prev = np.stack([_border_points(w, h, N, rng) for _ in range(P)])
+    init = (prev + rng.uniform(-1.5, 1.5, prev.shape)).astype(np.float32)
+    p = gvx_mod.KltParams.default(max_level=L)
+    g = ctx.klt_fb_batch(I, J, prev, init, params=p)
+    for i in range(P):
+        o = orc.klt_fb(I[i], J[i], prev[i], init[i], params=orc.KltParams.default(max_level=L),
+                       reuse_pyramids=True)
+        _assert_same(g["next"][i], o["next"], f"pair {i} next")
+        _assert_same(g["back"][i], o["back"], f"pair {i} back")
+        flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
+        _assert_same(g["flags"][i], flags, f"pair {i} flags")
+        _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
