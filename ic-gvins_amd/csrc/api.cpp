@@ -348,8 +348,7 @@ static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, con
     a.cam_h = cam_h;
     hipEvent_t ev{};
     prof_begin(c, "klt", &ev);
-    const int64_t o0 = lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
-    const Level0 l0{fp.pyr + o0, fn.pyr + o0, 0, 0, lay.pitch[0], 0};
+    const Level0 l0{fp.pyr + lay.off[0], fn.pyr + lay.off[0], 0, 0, PAD * lay.pitch[0] + PAD, lay.pitch[0], 0};
     e = launch_klt(c, a, lay, fp.pyr, fn.pyr, 0, 0, l0, d_prev, d_next, mode ? d_back : nullptr, d_flags,
                    d_err);
     prof_end(c, "klt", ev);
@@ -462,7 +461,7 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
         if (e != hipSuccess) return hip_err(c, e, "init flow");
     }
     prof_begin(c, "klt", &ev);
-    const Level0 l0{d_prev, d_next, (int64_t)w * h, (int64_t)w * h, w, 1};
+    const Level0 l0{d_prev, d_next, (int64_t)w * h, (int64_t)w * h, 0, w, 1};
     e = launch_klt(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, l0, d_prev_xy, d_next_xy, d_back_xy,
                    d_flags, nullptr);
     prof_end(c, "klt", ev);

@@ -103,15 +103,15 @@ struct KltArgs {
     int32_t cam_w, cam_h;
 };
 
-// Level 0 of pair i: prev plane at prev + i*prev_stride (pointer to pixel (0,0),
-// rows `pitch` bytes apart), likewise next.  raw = 1: the caller's unpadded
-// images (border windows are gathered with REFLECT_101); raw = 0: the padded
-// level-0 slot of a pyramid.
+// Level 0 of pair i: prev plane at prev + i*prev_stride, pixel (x, y) at byte
+// o0 + y*pitch + x, likewise next.  raw = 1: the caller's unpadded images
+// (o0 = 0; border windows are gathered with REFLECT_101); raw = 0: the padded
+// level-0 slot of a pyramid (base at the ring's corner, o0 = PAD*pitch + PAD).
 struct Level0 {
     const uint8_t* prev;
     const uint8_t* next;
     int64_t prev_stride, next_stride;
-    int32_t pitch, raw;
+    int32_t o0, pitch, raw;
 };
 
 // Pyramid (levels >= 1) of pair i: prev at pyr_prev + i*prev_pair_stride, next

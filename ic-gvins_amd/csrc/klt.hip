@@ -29,9 +29,19 @@ constexpr float FLT_SCALE = 1.f / (1 << 20);
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 
+typedef uint32_t v3u __attribute__((ext_vector_type(3)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
 // a.lo*b.lo + a.hi*b.hi + c on signed int16 halves (v_dot2_i32_i16)
 __device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c, false);
+}
+// the same with a wave-uniform addend taken straight from an SGPR (the VOP3P
+// form: no per-accumulator v_mov of the rounding constant)
+__device__ __forceinline__ int dot2k(uint32_t a, uint32_t b, int k) {
+    int r;
+    __asm__("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
 }
 // (lo & 0xffff) | (hi << 16)
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) {
@@ -42,26 +52,56 @@ template <int T>
 __device__ __forceinline__ uint32_t byte_pair(uint32_t d0, uint32_t d1) {
     return __builtin_amdgcn_perm(d1, d0, 0x0c000c00u | ((uint32_t)(T + 1) << 16) | (uint32_t)T);
 }
+// the same for byte T of a 12-byte row held in three dwords (T <= 10)
+template <int T>
+__device__ __forceinline__ uint32_t byte_pair3(const uint32_t (&d)[3]) {
+    return byte_pair<(T & 3)>(d[T >> 2], d[(T >> 2) + 1 < 3 ? (T >> 2) + 1 : 2]);
+}
 __device__ __forceinline__ uint32_t psub16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) - __builtin_bit_cast(v2s, b));
 }
-
-// Load NDW dwords starting at byte p (any alignment) from dword-aligned
-// addresses and realign: d[k] = bytes p[4k .. 4k+3].  The pointer stays derived
-// from p so the loads remain global_load (address-space inference).
-template <int NDW>
-__device__ __forceinline__ void load_aligned(const uint8_t* p, uint32_t (&d)[NDW]) {
-    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
-    uint32_t w[NDW + 1];
-#pragma unroll
-    for (int k = 0; k <= NDW; ++k) w[k] = q[k];
-#pragma unroll
-    for (int k = 0; k < NDW; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+__device__ __forceinline__ uint32_t padd16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) + __builtin_bit_cast(v2s, b));
 }
+// a*k + c on int16 halves (k small)
+__device__ __forceinline__ uint32_t pmad16(uint32_t a, short k, uint32_t c) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) * k + __builtin_bit_cast(v2s, c));
+}
+__device__ __forceinline__ uint32_t pmul16(uint32_t a, short k) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) * k);
+}
+// (hi half of a, lo half of b): the pair starting one column later
+__device__ __forceinline__ uint32_t shift_pair(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_alignbit(b, a, 16);
+}
+
+// A pyramid level (or level-0 image) as a buffer resource: pixel (x, y) is at
+// byte o0 + y*pitch + x (every offset the LK loop produces is non-negative).
+struct Plane {
+    __amdgpu_buffer_rsrc_t rs;
+    int o0, pitch;
+};
+__device__ __forceinline__ Plane make_plane(const uint8_t* base, int o0, int pitch) {
+    Plane p;
+    p.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, 0x7fffffff, 0x00020000);
+    p.o0 = o0;
+    p.pitch = pitch;
+    return p;
+}
+// NDW realigned dwords of a row starting at byte `off` (any alignment), the row
+// `soff` bytes further (soff wave-uniform, in the SGPR soffset).
 template <int NDW>
-__device__ __forceinline__ int byte_at(const uint32_t (&d)[NDW], int c) {
-    return (int)((d[c >> 2] >> (8 * (c & 3))) & 0xffu);
+__device__ __forceinline__ void brow(const Plane& P, int off_al, uint32_t sh, int soff, uint32_t (&d)[NDW]) {
+    if constexpr (NDW == 3) {
+        const v4u w = __builtin_amdgcn_raw_buffer_load_b128(P.rs, off_al, soff, 0);
+        d[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+        d[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+        d[2] = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
+    } else {
+        const v3u w = __builtin_amdgcn_raw_buffer_load_b96(P.rs, off_al, soff, 0);
+        d[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+        d[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+    }
 }
 
 __device__ __forceinline__ int refl(int p, int len) {
@@ -83,19 +123,17 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ void fill_win(uint32_t* win, const uint8_t* plane, int pitch, int W, int H, int x0,
-                                         int y0, int rows, int lane) {
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(plane), (short)0, 0x7fffffff, 0x00020000);
+__device__ __forceinline__ void fill_win(uint32_t* win, const Plane& P, int W, int H, int x0, int y0, int rows,
+                                         int lane) {
     wave_lds_sync();  // earlier reads of the tile are done
 #pragma unroll 1
     for (int i = lane; i < rows * WIN_DW; i += 64) {
         const int r = i >> 3, q = i & 7;
-        const int ro = refl(y0 + r, H) * pitch;
+        const int ro = P.o0 + refl(y0 + r, H) * P.pitch;
         uint32_t v = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, ro + refl(x0 + 4 * q + b, W), 0, 0) << (8 * b);
+            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(P.rs, ro + refl(x0 + 4 * q + b, W), 0, 0) << (8 * b);
         win[i] = v;
     }
     wave_lds_sync();
@@ -136,65 +174,98 @@ struct Unit {
     uint32_t iv[4], ix[4], iy[4];  // packed int16 pairs (pixel 2k, 2k+1); pair 3 high = 0
 };
 
+// byte pair (T, T+1) of a 12-byte row in three dwords, as int16 halves (T <= 9;
+// T is a constant after unrolling)
+__device__ __forceinline__ uint32_t bpair(const uint32_t (&d)[3], int T) {
+    const int q = T >> 2, r = T & 3;
+    const uint32_t lo = d[q], hi = d[q + 1 < 3 ? q + 1 : 2];
+    return __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | ((uint32_t)(r + 1) << 16) | (uint32_t)r);
+}
+
 // Extract I (5 fractional bits) and the Scharr gradient at the bilinear
 // window positions of one unit (LKTrackerInvoker window extraction), and
 // accumulate its structure-tensor partial sums.
 // d[r]: bytes X .. X+11 (X = ipx + 7*seg - 1) of rows ipy+row-1+r, r = 0..3.
+// The Scharr taps run on int16 column pairs (v_pk_*): t0 = 3(a+e)+10b and
+// t1 = e-a per column, dx = t0[c+1]-t0[c-1], dy = 3(t1[c+1]+t1[c-1])+10 t1[c],
+// every value an exact integer of at most 13 bits.  `interior`: the whole
+// window of every unit is inside the image (no derivative masking).
 __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3], int W, int H, int ipx,
-                                             int ipy, uint32_t W0, uint32_t W1, int& a11, int& a12,
-                                             int& a22) {
-    // the two bilinear rows are processed in turn, accumulating the dot
-    // products in place
+                                             int ipy, bool interior, uint32_t W0, uint32_t W1, int& a11,
+                                             int& a12, int& a22) {
     const int X = ipx + 7 * u.seg - 1;
-    int iv[8], ix[8], iy[8];
+    constexpr int RNDV = 1 << (W_BITS - 6), RNDD = 1 << (W_BITS - 1);
+    // even-aligned column pairs (2k, 2k+1), k = 0..4, of the four rows
+    uint32_t E[4][5];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) E[r][k] = bpair(d[r], 2 * k);
+    int iv[7], ix[7], iy[7];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
         const uint32_t Wr = rr ? W1 : W0;
-        const bool row_in = (unsigned)(ipy + u.row + rr) < (unsigned)H;
-        int t0[10], t1[10];
+        uint32_t T0[5], T1[5];
 #pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            const int a = byte_at<3>(d[rr], c), b = byte_at<3>(d[rr + 1], c), e = byte_at<3>(d[rr + 2], c);
-            t0[c] = (a + e) * 3 + b * 10;
-            t1[c] = e - a;
+        for (int k = 0; k < 5; ++k) {
+            T0[k] = pmad16(padd16(E[rr][k], E[rr + 2][k]), 3, pmul16(E[rr + 1][k], 10));
+            T1[k] = psub16(E[rr + 2][k], E[rr][k]);
         }
-        int dx[8], dy[8];
+        // derivative pairs at columns (2k+1, 2k+2), k = 0..3
+        uint32_t DX[4], DY[4];
 #pragma unroll
-        for (int c = 1; c <= 8; ++c) {
-            const bool in = row_in && (unsigned)(X + c) < (unsigned)W;
-            dx[c - 1] = in ? (t0[c + 1] - t0[c - 1]) : 0;
-            dy[c - 1] = in ? ((t1[c + 1] + t1[c - 1]) * 3 + t1[c] * 10) : 0;
+        for (int k = 0; k < 4; ++k) {
+            DX[k] = psub16(T0[k + 1], T0[k]);
+            DY[k] = pmad16(padd16(T1[k + 1], T1[k]), 3, pmul16(shift_pair(T1[k], T1[k + 1]), 10));
+        }
+        if (!interior) {
+            // derivatives are zero outside the image (BORDER_CONSTANT padding of
+            // OpenCV's derivative pyramid)
+            const bool row_in = (unsigned)(ipy + u.row + rr) < (unsigned)H;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool lo = row_in && (unsigned)(X + 2 * k + 1) < (unsigned)W;
+                const bool hi = row_in && (unsigned)(X + 2 * k + 2) < (unsigned)W;
+                const uint32_t m = (lo ? 0xffffu : 0u) | (hi ? 0xffff0000u : 0u);
+                DX[k] &= m;
+                DY[k] &= m;
+            }
         }
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
-            // CV_DESCALE(sum, 9) for I, CV_DESCALE(sum, 14) for the derivatives
-            const uint32_t pp = pack16(byte_at<3>(d[rr + 1], t + 1), byte_at<3>(d[rr + 1], t + 2));
-            iv[t] = dot2(pp, Wr, rr ? iv[t] : 1 << (W_BITS - 6));
-            ix[t] = dot2(pack16(dx[t], dx[t + 1]), Wr, rr ? ix[t] : 1 << (W_BITS - 1));
-            iy[t] = dot2(pack16(dy[t], dy[t + 1]), Wr, rr ? iy[t] : 1 << (W_BITS - 1));
+            // pixel pair (t+1, t+2): CV_DESCALE(sum, 9) for I, (sum, 14) for dI
+            const int k = t >> 1;
+            const uint32_t pv = (t & 1) ? E[rr + 1][k + 1] : bpair(d[rr + 1], t + 1);
+            const uint32_t px = (t & 1) ? shift_pair(DX[k], DX[k + 1]) : DX[k];
+            const uint32_t py = (t & 1) ? shift_pair(DY[k], DY[k + 1]) : DY[k];
+            if (rr == 0) {
+                iv[t] = dot2k(pv, Wr, RNDV);
+                ix[t] = dot2k(px, Wr, RNDD);
+                iy[t] = dot2k(py, Wr, RNDD);
+            } else {
+                iv[t] = dot2(pv, Wr, iv[t]);
+                ix[t] = dot2(px, Wr, ix[t]);
+                iy[t] = dot2(py, Wr, iy[t]);
+            }
         }
     }
-#pragma unroll
-    for (int t = 0; t < 7; ++t) {
-        iv[t] >>= (W_BITS - 5);
-        ix[t] >>= W_BITS;
-        iy[t] >>= W_BITS;
-    }
-    iv[7] = ix[7] = iy[7] = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        u.iv[k] = pack16(iv[2 * k], iv[2 * k + 1]);
-        u.ix[k] = pack16(ix[2 * k], ix[2 * k + 1]);
-        u.iy[k] = pack16(iy[2 * k], iy[2 * k + 1]);
+        const int h = 2 * k + 1 < 7 ? 2 * k + 1 : 0;
+        u.iv[k] = pack16(iv[2 * k] >> (W_BITS - 5), 2 * k + 1 < 7 ? iv[h] >> (W_BITS - 5) : 0);
+        u.ix[k] = pack16(ix[2 * k] >> W_BITS, 2 * k + 1 < 7 ? ix[h] >> W_BITS : 0);
+        u.iy[k] = pack16(iy[2 * k] >> W_BITS, 2 * k + 1 < 7 ? iy[h] >> W_BITS : 0);
     }
-    if (u.valid) {
+    int s11 = dot2k(u.ix[0], u.ix[0], 0), s12 = dot2k(u.ix[0], u.iy[0], 0), s22 = dot2k(u.iy[0], u.iy[0], 0);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            a11 = dot2(u.ix[k], u.ix[k], a11);
-            a12 = dot2(u.ix[k], u.iy[k], a12);
-            a22 = dot2(u.iy[k], u.iy[k], a22);
-        }
+    for (int k = 1; k < 4; ++k) {
+        s11 = dot2(u.ix[k], u.ix[k], s11);
+        s12 = dot2(u.ix[k], u.iy[k], s12);
+        s22 = dot2(u.iy[k], u.iy[k], s22);
     }
+    a11 = u.valid ? s11 : 0;
+    a12 = u.valid ? s12 : 0;
+    a22 = u.valid ? s22 : 0;
 }
 
 // Mismatch of one unit against J at integer offset (jx, jy) with weights
@@ -205,26 +276,34 @@ __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2
                                            uint32_t W0, uint32_t W1, int& b1, int& b2, int& es) {
     constexpr int RND = 1 << (W_BITS - 6);
     int jv[8];
-    jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2(byte_pair<0>(r0[0], r0[1]), W0, RND));
-    jv[1] = dot2(byte_pair<1>(r1[0], r1[1]), W1, dot2(byte_pair<1>(r0[0], r0[1]), W0, RND));
-    jv[2] = dot2(byte_pair<2>(r1[0], r1[1]), W1, dot2(byte_pair<2>(r0[0], r0[1]), W0, RND));
-    jv[3] = dot2(byte_pair<3>(r1[0], r1[1]), W1, dot2(byte_pair<3>(r0[0], r0[1]), W0, RND));
-    jv[4] = dot2(byte_pair<4>(r1[0], r1[1]), W1, dot2(byte_pair<4>(r0[0], r0[1]), W0, RND));
-    jv[5] = dot2(byte_pair<5>(r1[0], r1[1]), W1, dot2(byte_pair<5>(r0[0], r0[1]), W0, RND));
-    jv[6] = dot2(byte_pair<6>(r1[0], r1[1]), W1, dot2(byte_pair<6>(r0[0], r0[1]), W0, RND));
+    jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2k(byte_pair<0>(r0[0], r0[1]), W0, RND));
+    jv[1] = dot2(byte_pair<1>(r1[0], r1[1]), W1, dot2k(byte_pair<1>(r0[0], r0[1]), W0, RND));
+    jv[2] = dot2(byte_pair<2>(r1[0], r1[1]), W1, dot2k(byte_pair<2>(r0[0], r0[1]), W0, RND));
+    jv[3] = dot2(byte_pair<3>(r1[0], r1[1]), W1, dot2k(byte_pair<3>(r0[0], r0[1]), W0, RND));
+    jv[4] = dot2(byte_pair<4>(r1[0], r1[1]), W1, dot2k(byte_pair<4>(r0[0], r0[1]), W0, RND));
+    jv[5] = dot2(byte_pair<5>(r1[0], r1[1]), W1, dot2k(byte_pair<5>(r0[0], r0[1]), W0, RND));
+    jv[6] = dot2(byte_pair<6>(r1[0], r1[1]), W1, dot2k(byte_pair<6>(r0[0], r0[1]), W0, RND));
 #pragma unroll
     for (int t = 0; t < 7; ++t) jv[t] >>= (W_BITS - 5);
     jv[7] = 0;
+    if (ERR) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);  // diff pair
-        if (ERR) {
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);  // diff pair
             const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
             es += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
-        } else {
-            b1 = dot2(d, u.ix[k], b1);
-            b2 = dot2(d, u.iy[k], b2);
         }
+    } else {
+        const uint32_t d0 = psub16(pack16(jv[0], jv[1]), u.iv[0]);
+        int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);
+            s1 = dot2(d, u.ix[k], s1);
+            s2 = dot2(d, u.iy[k], s2);
+        }
+        b1 += s1;
+        b2 += s2;
     }
 }
 
@@ -250,29 +329,36 @@ __device__ __forceinline__ long long wave_sum64(int v) {
 // caller's image) take the aligned-load path only when every byte it touches is
 // inside the image, and gather with REFLECT_101 otherwise; padded levels always
 // take the aligned path (their PAD ring covers every window the LK loop admits).
-__device__ __forceinline__ void load_i_rows(const Unit& u, const uint8_t* Il, int pitch, int W, int H, int ipx,
+// lane_off = row*pitch + 7*seg of the unit at this level.
+__device__ __forceinline__ void load_i_rows(const Unit& u, const Plane& P, int lane_off, int W, int H, int ipx,
                                             int ipy, bool raw, uint32_t* win, int lane, uint32_t (&d)[4][3]) {
     if (!raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H)) {
-        const int X = ipx + 7 * u.seg - 1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) load_aligned<3>(Il + __mul24(ipy + u.row - 1 + r, pitch) + X, d[r]);
+        const int off = lane_off + (P.o0 + (ipy - 1) * P.pitch + ipx - 1);
+        const int al = off & ~3;
+        const uint32_t sh = (uint32_t)off & 3u;
+        brow<3>(P, al, sh, 0, d[0]);
+        brow<3>(P, al, sh, P.pitch, d[1]);
+        brow<3>(P, al, sh, 2 * P.pitch, d[2]);
+        brow<3>(P, al, sh, 3 * P.pitch, d[3]);
     } else {
         // tile: rows ipy-1 .., bytes ipx-1 ..; the unit reads 4 rows x 12 bytes
-        fill_win(win, Il, pitch, W, H, ipx - 1, ipy - 1, WIN + 3, lane);
+        fill_win(win, P, W, H, ipx - 1, ipy - 1, WIN + 3, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) read_win<3>(win, u.row + r, 7 * u.seg, d[r]);
     }
 }
-__device__ __forceinline__ void load_j_rows(const Unit& u, const uint8_t* Jl, int pitch, int W, int H, int jx,
+__device__ __forceinline__ void load_j_rows(const Unit& u, const Plane& P, int lane_off, int W, int H, int jx,
                                             int jy, bool raw, uint32_t* win, int lane, uint32_t (&r0)[2],
                                             uint32_t (&r1)[2]) {
     if (!raw || (jx >= 3 && jx + 26 <= W && jy >= 0 && jy + 22 <= H)) {
-        const uint8_t* jp = Jl + __mul24(jy + u.row, pitch) + jx + 7 * u.seg;
-        load_aligned<2>(jp, r0);
-        load_aligned<2>(jp + pitch, r1);
+        const int off = lane_off + (P.o0 + jy * P.pitch + jx);
+        const int al = off & ~3;
+        const uint32_t sh = (uint32_t)off & 3u;
+        brow<2>(P, al, sh, 0, r0);
+        brow<2>(P, al, sh, P.pitch, r1);
     } else {
         // tile: rows jy .., bytes jx ..; the unit reads 2 rows x 8 bytes
-        fill_win(win, Jl, pitch, W, H, jx, jy, WIN + 1, lane);
+        fill_win(win, P, W, H, jx, jy, WIN + 1, lane);
         read_win<2>(win, u.row, 7 * u.seg, r0);
         read_win<2>(win, u.row + 1, 7 * u.seg, r1);
     }
@@ -281,9 +367,9 @@ __device__ __forceinline__ void load_j_rows(const Unit& u, const uint8_t* Jl, in
 // Level-0 planes of one pair: pointers to pixel (0,0), row pitch, and whether
 // they are the caller's unpadded images.
 struct L0Planes {
-    const uint8_t* i;
+    const uint8_t* i;  // plane bases; pixel (0,0) at byte o0
     const uint8_t* j;
-    int pitch;
+    int o0, pitch;
     bool raw;
 };
 
@@ -308,8 +394,10 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         const int W = lay.w[l], H = lay.h[l];
         const bool raw = l == 0 && p0.raw;
         const int pitch = l == 0 ? p0.pitch : lay.pitch[l];
-        const uint8_t* Il = l == 0 ? p0.i : I + lay.off[l] + __mul24(PAD, pitch) + PAD;  // (0,0)
-        const uint8_t* Jl = l == 0 ? p0.j : J + lay.off[l] + __mul24(PAD, pitch) + PAD;
+        const int o0 = l == 0 ? p0.o0 : PAD * pitch + PAD;
+        const Plane PI = make_plane(l == 0 ? p0.i : I + lay.off[l], o0, pitch);
+        const Plane PJ = make_plane(l == 0 ? p0.j : J + lay.off[l], o0, pitch);
+        const int lane_off = __mul24(u.row, pitch) + 7 * u.seg;
         const float sc = ldexpf(1.f, -l);  // == (float)(1./(1 << l)), exact
         float prevx = p0x * sc, prevy = p0y * sc;
         float nextx, nexty;
@@ -342,8 +430,10 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         int a11 = 0, a12 = 0, a22 = 0;
         {
             uint32_t d[4][3];
-            load_i_rows(u, Il, pitch, W, H, ipx, ipy, raw, win, lane, d);
-            extract_unit(u, d, W, H, ipx, ipy, W0, W1, a11, a12, a22);
+            load_i_rows(u, PI, lane_off, W, H, ipx, ipy, raw, win, lane, d);
+            // every unit's derivative columns / rows inside the image
+            const bool interior = ipx >= 0 && ipx + WIN + 1 <= W && ipy >= 0 && ipy + WIN + 1 <= H;
+            extract_unit(u, d, W, H, ipx, ipy, interior, W0, W1, a11, a12, a22);
         }
         const float A11 = (float)wave_sum64(a11) * FLT_SCALE;
         const float A12 = (float)wave_sum64(a12) * FLT_SCALE;
@@ -374,7 +464,7 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
             int b1 = 0, b2 = 0, es = 0;
             {
                 uint32_t r0[2], r1[2];
-                load_j_rows(u, Jl, pitch, W, H, inx, iny, raw, win, lane, r0, r1);
+                load_j_rows(u, PJ, lane_off, W, H, inx, iny, raw, win, lane, r0, r1);
                 match_unit<false>(u, r0, r1, J0, J1, b1, b2, es);
             }
             if (!u.valid) b1 = b2 = 0;
@@ -408,7 +498,7 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
             int b1 = 0, b2 = 0, es = 0;
             {
                 uint32_t r0[2], r1[2];
-                load_j_rows(u, Jl, pitch, W, H, inx, iny, raw, win, lane, r0, r1);
+                load_j_rows(u, PJ, lane_off, W, H, inx, iny, raw, win, lane, r0, r1);
                 match_unit<true>(u, r0, r1, J0, J1, b1, b2, es);
             }
             if (!u.valid) es = 0;
@@ -433,8 +523,9 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
     const int64_t pair = gp / a.n_pts;
     const uint8_t* I = pyr_prev + pair * prev_stride;
     const uint8_t* J = pyr_next + pair * next_stride;
-    const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.pitch, l0.raw != 0};
-    const L0Planes pb{pf.j, pf.i, pf.pitch, pf.raw};
+    const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.o0, l0.pitch,
+                      l0.raw != 0};
+    const L0Planes pb{pf.j, pf.i, pf.o0, pf.pitch, pf.raw};
     LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow};
     const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
     float nx = next_xy[2 * gp], ny = next_xy[2 * gp + 1];
