@@ -9,10 +9,17 @@ Workload (configs[1]): 1280x560 mono, 150 features, maxLevel 3, 21x21 window.
 value = frame pairs processed by all ranks / max-over-ranks wall time.
 
 Multi-GPU: one process per GPU (torch.distributed.run), pairs sharded by rank
-with no data-path collective (weak scaling); like the reference's offline
-batch-replay config, per-step results (n_kept per pair) are gathered to rank 0.
+with no data-path collective (weak scaling).  --gather adds the offline
+batch-replay exchange (configs[4]): per-step results (n_kept per pair) are
+all-gathered over RCCL inside the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+roofline.achieved = SURVEY.md 8d algorithmic bytes x pairs / device time of the
+pipeline's kernels (HIP events on the context stream, timed region only);
+roofline.traffic = PMC HBM bytes per step from profiles/pmc_traffic.json
+(tools/pmc.sh + tools/traffic.py) when it was measured on this workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--gather]
+    python bench.py --mock [--backend gloo]   # launcher / aggregation logic without a GPU
 """
 from __future__ import annotations
 
@@ -41,24 +48,54 @@ def algorithmic_bytes(w, h, levels, n):
     return 2 * a0 + 4 * ap + 16 * (a0 + ap) + 58 * n
 
 
-def cpu_baseline(w, h, n, level, budget_s=12.0):
-    """Oracle (C restatement, 1 thread) on the reference's 4-call pattern
-    (each calcOpticalFlowPyrLK rebuilds both pyramids), bounded sample."""
+def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1):
+    """Oracle (C restatement) on the reference's 4-call pattern (each
+    calcOpticalFlowPyrLK rebuilds both pyramids; LK points split over `threads`
+    like OpenCV's parallel_for_), bounded sample of about budget_s seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc  # test-infrastructure import: cpu_baseline leg only
     from gvx import synth
     pairs = [synth.make_pair(w, h, n, synth.SEED + 1000 + i) for i in range(4)]
     p = orc.KltParams.default(max_level=level)
-    orc.klt_fb(*pairs[0][:4], params=p)  # warm
+    half = n // 2  # Tracking::trackMappoint / trackReferencePoint point sets
+
+    def frame(I, J, P, Q):
+        # tracking.cc:385/390 (map points, fwd + bwd) and :487/493 (reference
+        # points): four calcOpticalFlowPyrLK calls, each rebuilding both pyramids
+        orc.klt_fb(I, J, P[:half], Q[:half], params=p, reuse_pyramids=False, nthreads=threads)
+        orc.klt_fb(I, J, P[half:], Q[half:], params=p, reuse_pyramids=False, nthreads=threads)
+
+    frame(*pairs[0][:4])  # warm
     done, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         I, J, P, Q, _ = pairs[done % len(pairs)]
-        orc.klt_fb(I, J, P, Q, params=p, reuse_pyramids=False, nthreads=1)
+        frame(I, J, P, Q)
         done += 1
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} frame pairs {w}x{h}/{n} feat, 4 LK calls each rebuilding pyramids "
-                      f"(tracking.cc:385-393 pattern), 1 thread, {dt:.1f} s"}
+    return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{done} frame pairs {w}x{h}/{n} feat ({half} map + {n - half} reference points), "
+                      f"4 LK calls each rebuilding both pyramids (tracking.cc:385,390,487,493), "
+                      f"{threads} thread(s), {dt:.1f} s"}
+
+
+def traffic_for(workload):
+    """PMC HBM bytes per step measured on this workload (tools/traffic.py)."""
+    f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    return d if d.get("workload") == workload else None
+
+
+def host_threads():
+    """CPU share for the baseline: the affinity mask, capped at 16 (the GPU box's
+    per-GPU CPU share; os.cpu_count() reports the whole machine there)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
 def main():
@@ -73,8 +110,13 @@ def main():
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic pairs (tiled)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
+    ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
+    ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
+    ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
+    if args.mock:
+        return mock_main(args)
 
     import torch
     import gvx
@@ -87,7 +129,7 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -119,7 +161,7 @@ def main():
     gathered = [torch.empty_like(dNK) for _ in range(world)] if world > 1 else None
 
     def collect():
-        if world > 1:
+        if world > 1 and args.gather:
             ctx.sync()
             dist.all_gather(gathered, dNK)  # offline batch replay: results to every rank
 
@@ -143,10 +185,10 @@ def main():
     elapsed = time.perf_counter() - t0
     fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact")}
     ctx.profile(False)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, dev)
+    if world > 1 and not args.gather:
+        collect_once = [torch.empty_like(dNK) for _ in range(world)]
+        dist.all_gather(collect_once, dNK)  # results check, outside the timed region
 
     kept_frac = float(dNK.float().mean().item()) / N
     total_pairs = world * Pn * args.steps
@@ -155,11 +197,18 @@ def main():
     B = algorithmic_bytes(W, H, L, N)
     dev_ms = sum(v[0] for v in fam.values()) / args.steps  # device time per step (all kernels)
     achieved = B * Pn / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
+    workload = f"klt_fb_batch {Pn}x{W}x{H} N{N} L{L}"
+    tr = traffic_for(workload)
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(W, H, N, L, args.cpu_budget)
+            nt = host_threads()
+            cpu = cpu_baseline(W, H, N, L, args.cpu_budget, threads=nt)
+            if nt > 1:
+                one = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=1)
+                cpu["single_thread_value"] = one["value"]
+                cpu["single_thread_sample"] = one["sample"]
         line = {
             "metric": "KLT frames/sec @1280x560,150 feat",
             "value": round(value, 2),
@@ -177,10 +226,13 @@ def main():
             "config": {"workload": f"configs[1]: batch of {Pn} frame pairs/GPU, {W}x{H} mono, {N} feat, "
                                    f"maxLevel {L}, win 21, fwd+bwd LK + FB + compaction",
                        "pairs_per_gpu_per_step": Pn, "parallelism": f"pairs sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "kernel": "klt pipeline (pyramid + LK + compaction)",
+            "roofline": {"bound": "hbm", "kernel": "klt pipeline (pyramid + LK + compaction) per step",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": None, "algorithmic_bytes_per_pair": B,
+                         "traffic": round(tr["bytes_per_step"]) if tr else None,
+                         "traffic_unit": "HBM bytes per step (PMC 2*FETCH_SIZE+WRITE_SIZE)",
+                         "traffic_source": tr["source"] if tr else None,
+                         "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
@@ -189,6 +241,48 @@ def main():
     if dist:
         dist.destroy_process_group()
     ctx.close()
+
+
+def max_over_ranks(elapsed, dist, dev=None):
+    if not dist:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def mock_main(args):
+    """The launcher contract without a GPU: same rank handling, barrier-bracketed
+    timing, max over ranks and rank-0 JSON line; a step is a fixed host sleep.
+    Used by tests/test_bench_dist.py (gloo, world_size 2)."""
+    import torch
+    import torch.distributed as tdist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group(args.backend or "gloo")
+        dist = tdist
+    step_s = 0.002 * (1 + rank)  # ranks deliberately unequal: the max must win
+    for _ in range(args.warmup):
+        time.sleep(step_s)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(step_s)
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+    if rank == 0:
+        print(json.dumps({"metric": "mock", "value": world * args.pairs * args.steps / elapsed, "unit": "frames/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "elapsed_s": elapsed}))
+    if dist:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

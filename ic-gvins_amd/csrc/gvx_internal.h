@@ -92,6 +92,15 @@ void prof_drain(gvx_ctx* c);
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride,
                                  int n_img, const PyrLayout& lay, uint8_t* dst, bool write_l0);
 
+// Workgroups are dispatched to the 8 XCDs round-robin by id (each XCD has its
+// own L2).  xcd_swizzle maps the dispatch id to a logical id so that XCD k runs
+// the contiguous logical range [k*per, (k+1)*per): neighbouring work (points of
+// one frame pair, adjacent image tiles) shares one L2.  The grid must hold
+// 8*per workgroups; logical ids >= n are idle.
+constexpr int N_XCD = 8;
+__host__ __device__ inline int xcd_per(int n) { return (n + N_XCD - 1) / N_XCD; }
+__device__ inline int xcd_swizzle(int b, int n) { return (b % N_XCD) * xcd_per(n) + b / N_XCD; }
+
 struct KltArgs {
     int32_t n_pairs, n_pts;
     int32_t max_iter;

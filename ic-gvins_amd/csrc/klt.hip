@@ -518,7 +518,8 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     // wave-uniform point index in an SGPR: the per-point state, the level /
     // iteration control and the 2x2 solve then stay scalar (uniform branches)
-    const int64_t gp = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nb = (int)((total + 3) / 4);
+    const int64_t gp = (int64_t)xcd_swizzle(blockIdx.x, nb) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (gp >= total) return;
     const int64_t pair = gp / a.n_pts;
     const uint8_t* I = pyr_prev + pair * prev_stride;
@@ -599,7 +600,7 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
                       float* err) {
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     if (total <= 0) return hipSuccess;
-    dim3 grid((unsigned)((total + 3) / 4));
+    dim3 grid((unsigned)(N_XCD * xcd_per((int)((total + 3) / 4))));
     hipLaunchKernelGGL(klt_kernel, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
                        next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
     return hipGetLastError();

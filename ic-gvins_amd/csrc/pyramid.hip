@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ 
     __shared__ __attribute__((aligned(16))) uint8_t bufB[NL > 1 ? G::m(2) * G::rs(2) + 64 : 16];
 
     const int tid = threadIdx.x;
-    const int t_begin = blockIdx.x * per_wg;
+    const int t_begin = xcd_swizzle(blockIdx.x, (n_tiles + per_wg - 1) / per_wg) * per_wg;
     const int t_end = min(t_begin + per_wg, n_tiles);
     if (t_begin >= t_end) return;
 
@@ -398,7 +398,7 @@ void launch_fused(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int sr
     const int slots = c->n_cu * (NL == 3 ? 5 : NL == 2 ? 7 : 8);
     const int per_wg = (n_tiles + slots - 1) / slots;
     const int n_wg = (n_tiles + per_wg - 1) / per_wg;
-    hipLaunchKernelGGL(fused_kernel<NL>, dim3(n_wg), dim3(256), 0, c->stream, src, src_img_stride, src_pitch,
+    hipLaunchKernelGGL(fused_kernel<NL>, dim3(N_XCD * xcd_per(n_wg)), dim3(256), 0, c->stream, src, src_img_stride, src_pitch,
                        src_w, src_h, vec16, dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
 }
 

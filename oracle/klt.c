@@ -14,15 +14,11 @@
 
 #include <float.h>
 #include <math.h>
-#include <pthread.h>
+#include "orc_pool.h"
 #include <stdlib.h>
 #include <string.h>
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
-
-/* Work counters (diagnostics only): [0] point-levels that reached the
-   Gauss-Newton loop, [1] Gauss-Newton iterations executed. */
-long long orc_lk_stats[2];
 
 void orc_klt_params_default(orc_klt_params* p) {
     p->win = 21;
@@ -79,28 +75,58 @@ static void fill_border_reflect101(orc_u8plane* p) {
 
 /* pyrDown (imgproc/src/pyramids.cpp pyrDown_ with FixPtCast<uchar,8>):
    dst(y,x) = (sum_ij k_i k_j src(refl(2y+i-2), refl(2x+j-2)) + 128) >> 8,
-   k = [1 4 6 4 1].  Integer arithmetic: evaluation order is irrelevant. */
-static void pyr_down(const orc_u8plane* src, orc_u8plane* dst) {
-    static const int k[5] = {1, 4, 6, 4, 1};
-    for (int y = 0; y < dst->h; y++) {
-        for (int x = 0; x < dst->w; x++) {
-            int s = 0;
-            for (int i = 0; i < 5; i++) {
-                int sy = reflect101(2 * y + i - 2, src->h);
-                int row = 0;
-                for (int j = 0; j < 5; j++) {
-                    int sx = reflect101(2 * x + j - 2, src->w);
-                    row += k[j] * (int)*px(src, sx, sy);
-                }
-                s += k[i] * row;
+   k = [1 4 6 4 1].  Integer arithmetic: evaluation order is irrelevant, so the
+   separable form (horizontal taps per source row, then vertical) and any row
+   split over threads give the identical result. */
+typedef struct {
+    const orc_u8plane* src;
+    orc_u8plane* dst;
+    const int* xtab; /* 5 reflected source columns per destination column */
+} pyr_job;
+
+static void pyr_rows(void* vctx, int y0, int y1) {
+    const pyr_job* jb = (const pyr_job*)vctx;
+    const orc_u8plane* src = jb->src;
+    orc_u8plane* dst = jb->dst;
+    int* rows = (int*)malloc(sizeof(int) * 5 * (size_t)dst->w);
+    for (int y = y0; y < y1; y++) {
+        for (int i = 0; i < 5; i++) {
+            const uint8_t* s = px(src, 0, reflect101(2 * y + i - 2, src->h));
+            int* r = rows + (size_t)i * dst->w;
+            for (int x = 0; x < dst->w; x++) {
+                const int* t = jb->xtab + 5 * x;
+                r[x] = s[t[0]] + 4 * s[t[1]] + 6 * s[t[2]] + 4 * s[t[3]] + s[t[4]];
             }
-            *px(dst, x, y) = (uint8_t)((s + 128) >> 8);
+        }
+        uint8_t* d = px(dst, 0, y);
+        for (int x = 0; x < dst->w; x++) {
+            int v = rows[x] + 4 * rows[dst->w + x] + 6 * rows[2 * dst->w + x] + 4 * rows[3 * dst->w + x] +
+                    rows[4 * dst->w + x];
+            d[x] = (uint8_t)((v + 128) >> 8);
         }
     }
+    free(rows);
 }
+
+static void pyr_down(const orc_u8plane* src, orc_u8plane* dst, int nthreads) {
+    int* xtab = (int*)malloc(sizeof(int) * 5 * (size_t)dst->w);
+    for (int x = 0; x < dst->w; x++)
+        for (int j = 0; j < 5; j++) xtab[5 * x + j] = reflect101(2 * x + j - 2, src->w);
+    pyr_job jb = {src, dst, xtab};
+    orc_parallel_for(dst->h, nthreads, pyr_rows, &jb);
+    free(xtab);
+}
+
+static int build_pyramid_mt(const uint8_t* img, int w, int h, int stride, int win, int max_level,
+                            orc_pyramid* pyr, int nthreads);
 
 int orc_build_pyramid(const uint8_t* img, int w, int h, int stride, int win, int max_level,
                       orc_pyramid* pyr) {
+    return build_pyramid_mt(img, w, h, stride, win, max_level, pyr, 1);
+}
+
+static int build_pyramid_mt(const uint8_t* img, int w, int h, int stride, int win, int max_level,
+                            orc_pyramid* pyr, int nthreads) {
     memset(pyr, 0, sizeof(*pyr));
     orc_u8plane* l0 = &pyr->lv[0];
     alloc_plane(l0, w, h, win);
@@ -110,7 +136,7 @@ int orc_build_pyramid(const uint8_t* img, int w, int h, int stride, int win, int
     for (int level = 0; level <= max_level; level++) {
         if (level != 0) {
             alloc_plane(&pyr->lv[level], sw, sh, win);
-            pyr_down(&pyr->lv[level - 1], &pyr->lv[level]);
+            pyr_down(&pyr->lv[level - 1], &pyr->lv[level], nthreads);
             fill_border_reflect101(&pyr->lv[level]);
         }
         pyr->nlevels = level + 1;
@@ -127,12 +153,21 @@ void orc_free_pyramid(orc_pyramid* pyr) {
 }
 
 /* calcSharrDeriv (lkpyramid.cpp): vertical [3 10 3] / [-1 0 1] pass with
-   REFLECT_101 rows, then horizontal [-1 0 1] / [3 10 3] with REFLECT_101 columns. */
-void orc_scharr(const orc_u8plane* src, int16_t* out) {
+   REFLECT_101 rows, then horizontal [-1 0 1] / [3 10 3] with REFLECT_101
+   columns.  Rows are independent (integer arithmetic): split over threads. */
+typedef struct {
+    const orc_u8plane* src;
+    int16_t* out;
+    int out_pitch; /* int16 pairs per output row */
+} scharr_job;
+
+static void scharr_rows(void* vctx, int ya, int yb) {
+    const scharr_job* jb = (const scharr_job*)vctx;
+    const orc_u8plane* src = jb->src;
     int w = src->w, h = src->h;
     int* t0 = (int*)malloc(sizeof(int) * (w + 2));
     int* t1 = (int*)malloc(sizeof(int) * (w + 2));
-    for (int y = 0; y < h; y++) {
+    for (int y = ya; y < yb; y++) {
         int y0 = y > 0 ? y - 1 : (h > 1 ? 1 : 0);
         int y2 = y < h - 1 ? y + 1 : (h > 1 ? h - 2 : 0);
         for (int x = 0; x < w; x++) {
@@ -145,30 +180,33 @@ void orc_scharr(const orc_u8plane* src, int16_t* out) {
         t0[w + 1] = t0[x1 + 1];
         t1[0] = t1[x0 + 1];
         t1[w + 1] = t1[x1 + 1];
+        int16_t* o = jb->out + 2 * (size_t)y * jb->out_pitch;
         for (int x = 0; x < w; x++) {
-            out[((size_t)y * w + x) * 2 + 0] = (int16_t)(t0[x + 2] - t0[x]);
-            out[((size_t)y * w + x) * 2 + 1] = (int16_t)((t1[x + 2] + t1[x]) * 3 + t1[x + 1] * 10);
+            o[2 * x + 0] = (int16_t)(t0[x + 2] - t0[x]);
+            o[2 * x + 1] = (int16_t)((t1[x + 2] + t1[x]) * 3 + t1[x + 1] * 10);
         }
     }
     free(t0);
     free(t1);
 }
 
+static void scharr_mt(const orc_u8plane* src, int16_t* out, int out_pitch, int nthreads) {
+    scharr_job jb = {src, out, out_pitch};
+    orc_parallel_for(src->h, nthreads, scharr_rows, &jb);
+}
+
+void orc_scharr(const orc_u8plane* src, int16_t* out) { scharr_mt(src, out, src->w, 1); }
+
 /* derivI buffer: Scharr of the level, padded by `win` with zeros
    (copyMakeBorder BORDER_CONSTANT|BORDER_ISOLATED). */
-static void make_deriv(const orc_u8plane* lv, int win, orc_s16plane* d) {
+static void make_deriv(const orc_u8plane* lv, int win, orc_s16plane* d, int nthreads) {
     d->w = lv->w;
     d->h = lv->h;
     d->pad = win;
     d->pitch = lv->w + 2 * win;
     size_t n = (size_t)d->pitch * (lv->h + 2 * win);
     d->buf = (int16_t*)calloc(n * 2, sizeof(int16_t));
-    int16_t* tmp = (int16_t*)malloc(sizeof(int16_t) * 2 * (size_t)lv->w * lv->h);
-    orc_scharr(lv, tmp);
-    for (int y = 0; y < lv->h; y++)
-        memcpy(d->buf + 2 * ((size_t)(y + win) * d->pitch + win), tmp + 2 * (size_t)y * lv->w,
-               sizeof(int16_t) * 2 * lv->w);
-    free(tmp);
+    scharr_mt(lv, d->buf + 2 * ((size_t)win * d->pitch + win), d->pitch, nthreads);
 }
 
 typedef struct {
@@ -276,9 +314,7 @@ static void lk_level(const lk_job* jb) {
         nextx -= halfw;
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
-        __atomic_fetch_add(&orc_lk_stats[0], 1, __ATOMIC_RELAXED); /* point-levels */
         for (int j = 0; j < jb->p->max_iter; j++) {
-            __atomic_fetch_add(&orc_lk_stats[1], 1, __ATOMIC_RELAXED); /* iterations */
             int inx = cv_floor(nextx), iny = cv_floor(nexty);
             if (inx < -win || inx >= J->w || iny < -win || iny >= J->h) {
                 if (level == 0) jb->status[pt] = 0;
@@ -355,31 +391,14 @@ static void lk_level(const lk_job* jb) {
     free(dIwin);
 }
 
-static void* lk_thread(void* arg) {
-    lk_level((const lk_job*)arg);
-    return NULL;
+static void lk_range(void* vctx, int begin, int end) {
+    lk_job jb = *(const lk_job*)vctx;
+    jb.begin = begin;
+    jb.end = end;
+    lk_level(&jb);
 }
 
-static void run_level(lk_job* base, int n, int nthreads) {
-    if (nthreads <= 1 || n < 2) {
-        base->begin = 0;
-        base->end = n;
-        lk_level(base);
-        return;
-    }
-    if (nthreads > n) nthreads = n;
-    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
-    lk_job* jobs = (lk_job*)malloc(sizeof(lk_job) * nthreads);
-    for (int t = 0; t < nthreads; t++) {
-        jobs[t] = *base;
-        jobs[t].begin = (int)((long)n * t / nthreads);
-        jobs[t].end = (int)((long)n * (t + 1) / nthreads);
-        pthread_create(&th[t], NULL, lk_thread, &jobs[t]);
-    }
-    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
-    free(th);
-    free(jobs);
-}
+static void run_level(lk_job* base, int n, int nthreads) { orc_parallel_for(n, nthreads, lk_range, base); }
 
 void orc_lk_on_pyramids(const orc_pyramid* prev, const orc_pyramid* next, const float* prev_xy,
                         float* next_xy, uint8_t* status, float* err, int n, const orc_klt_params* p,
@@ -393,7 +412,7 @@ void orc_lk_on_pyramids(const orc_pyramid* prev, const orc_pyramid* next, const 
     }
     for (int level = max_level; level >= 0; level--) {
         orc_s16plane d;
-        make_deriv(&prev->lv[level], p->win, &d);
+        make_deriv(&prev->lv[level], p->win, &d, nthreads);
         lk_job jb;
         jb.I = &prev->lv[level];
         jb.dI = &d;
@@ -415,8 +434,8 @@ void orc_calc_optical_flow_pyr_lk(const uint8_t* prev, const uint8_t* next, int 
                                   int n, const orc_klt_params* p, int nthreads) {
     if (n <= 0) return;
     orc_pyramid pp, pn;
-    orc_build_pyramid(prev, w, h, stride, p->win, p->max_level, &pp);
-    orc_build_pyramid(next, w, h, stride, p->win, p->max_level, &pn);
+    build_pyramid_mt(prev, w, h, stride, p->win, p->max_level, &pp, nthreads);
+    build_pyramid_mt(next, w, h, stride, p->win, p->max_level, &pn, nthreads);
     orc_lk_on_pyramids(&pp, &pn, prev_xy, next_xy, status, err, n, p, nthreads);
     orc_free_pyramid(&pp);
     orc_free_pyramid(&pn);
@@ -444,8 +463,8 @@ int orc_klt_fb(const uint8_t* prev, const uint8_t* next, int w, int h, int strid
     memcpy(back_xy, prev_xy, sizeof(float) * 2 * n);
     if (reuse_pyramids) {
         orc_pyramid pp, pn;
-        orc_build_pyramid(prev, w, h, stride, p->win, p->max_level, &pp);
-        orc_build_pyramid(next, w, h, stride, p->win, p->max_level, &pn);
+        build_pyramid_mt(prev, w, h, stride, p->win, p->max_level, &pp, nthreads);
+        build_pyramid_mt(next, w, h, stride, p->win, p->max_level, &pn, nthreads);
         orc_lk_on_pyramids(&pp, &pn, prev_xy, next_xy, st_f, err, n, p, nthreads);
         orc_lk_on_pyramids(&pn, &pp, next_xy, back_xy, st_b, err, n, p, nthreads);
         orc_free_pyramid(&pp);

@@ -1,0 +1,33 @@
+"""bench.py's multi-process contract on CPU (gloo, world_size 2): launched like
+the driver launches it (torch.distributed.run, 127.0.0.1), rank 0 prints one
+JSON line, the timed region is max-over-ranks, value is the whole-job
+aggregate (weak scaling)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_mock_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--mock", "--backend", "gloo", "--gpus", "2", "--steps", "20", "--warmup", "2", "--pairs", "8"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 20 and d["scaling"] == "weak"
+    # rank 1 sleeps 4 ms per step: the max over ranks must be >= 20 * 4 ms
+    assert d["elapsed_s"] >= 0.08
+    assert abs(d["value"] - 2 * 8 * 20 / d["elapsed_s"]) < 1e-6 * d["value"]

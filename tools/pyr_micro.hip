@@ -48,11 +48,11 @@ float run(const uint8_t* src, uint8_t* dst, const PyrLayout& lay, int n_img, int
     hipEventCreate(&a);
     hipEventCreate(&b);
     for (int i = 0; i < 3; ++i)
-        hipLaunchKernelGGL((fused_kernel<3, STOP>), dim3(n_wg), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, 1,
+        hipLaunchKernelGGL((fused_kernel<3, STOP>), dim3(N_XCD * xcd_per(n_wg)), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, 1,
                            dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
     hipEventRecord(a);
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((fused_kernel<3, STOP>), dim3(n_wg), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, 1,
+        hipLaunchKernelGGL((fused_kernel<3, STOP>), dim3(N_XCD * xcd_per(n_wg)), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, 1,
                            dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
     hipEventRecord(b);
     hipEventSynchronize(b);

@@ -1,0 +1,41 @@
+"""HBM traffic per bench step from rocprofv3 PMC passes (tools/pmc.sh with a
+"FETCH_SIZE" pass and a "WRITE_SIZE" pass over `bench.py`), corrected as
+MI355X_MICROARCH.md "HBM" prescribes: bytes = 2 * FETCH_SIZE + WRITE_SIZE
+(FETCH_SIZE reads half on gfx950; both counters in KiB).
+
+Writes profiles/pmc_traffic.json, which bench.py reports as roofline.traffic.
+Usage: python3 tools/traffic.py gpurun_out/<tag> [--workload KEY]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(__file__))
+from pmc_summary import load  # noqa: E402
+
+# launches per bench step of the KLT pipeline (prev + next pyramids, one LK
+# launch for fwd+bwd, one compaction)
+PER_STEP = {"fused_kernel": 2, "ring_kernel": 2, "klt_kernel": 1, "compact_kernel": 1}
+
+ap = argparse.ArgumentParser()
+ap.add_argument("pmc_dir")
+ap.add_argument("--workload", default="klt_fb_batch 256x1280x560 N150 L3")
+ap.add_argument("--pairs", type=int, default=256)
+ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
+a = ap.parse_args()
+res = load(a.pmc_dir)
+kern = {}
+step = 0.0
+for name, n in PER_STEP.items():
+    d = res.get(name)
+    if d is None or "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+        sys.exit(f"{name}: FETCH_SIZE / WRITE_SIZE missing in {a.pmc_dir}")
+    b = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+    kern[name] = {"bytes_per_launch": b, "fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
+                  "launches_per_step": n}
+    step += n * b
+out = {"workload": a.workload, "pairs_per_step": a.pairs, "bytes_per_step": step,
+       "bytes_per_pair": step / a.pairs, "kernels": kern, "source": os.path.relpath(a.pmc_dir),
+       "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md HBM"}
+json.dump(out, open(a.out, "w"), indent=1)
+print(json.dumps(out, indent=1))
