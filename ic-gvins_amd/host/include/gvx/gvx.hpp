@@ -1,0 +1,454 @@
+// gvx.hpp -- C++ host mirror of the reference interfaces on the accelerated
+// path, layered on the C ABI (include/gvx.h).  Header-only, C++17, no OpenCV /
+// Eigen / Ceres dependency: the types are layout- and meaning-compatible stand-ins
+// so the reference's call sites change only in the object they call.
+//
+//   reference (paths under /root/reference/ic_gvins/ic_gvins/)      here
+//   cv::calcOpticalFlowPyrLK (tracking/tracking.cc:385,390,487,493)  gvx::calcOpticalFlowPyrLK
+//   fwd/bwd/FB/reduceVector (tracking/tracking.cc:380-408, :831-849) gvx::trackFB, gvx::reduceVector
+//   Tracking::featuresDetection (tracking/tracking.cc:576-688)       gvx::featuresDetection
+//   PreintegrationBase / Earth / Normal (preintegration/*.h)          gvx::Preintegration
+//   PreintegrationFactor::Evaluate (preintegration_factor.h:45-69)    gvx::PreintegrationFactor
+//   ReprojectionFactor::Evaluate (factors/reprojection_factor.h:61)   gvx::ReprojectionFactor
+//
+// Errors: the C ABI never throws; this layer converts a non-OK status into
+// gvx::Error (the role cv::Exception plays for bad arguments in the reference).
+// There is no CPU fallback: without a gfx950 device gvx::Context throws.
+#pragma once
+
+#include <gvx.h>
+
+#include <array>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace gvx {
+
+class Error : public std::runtime_error {
+public:
+    Error(gvx_status s, const std::string& what) : std::runtime_error(what), status_(s) {}
+    gvx_status status() const { return status_; }
+
+private:
+    gvx_status status_;
+};
+
+inline void check(gvx_status s, const gvx_ctx* c, const char* what) {
+    if (s == GVX_OK) return;
+    std::string msg = std::string(what) + ": " + gvx_status_string(s);
+    if (c && gvx_last_error(c) && *gvx_last_error(c)) msg += std::string(" (") + gvx_last_error(c) + ")";
+    throw Error(s, msg);
+}
+
+// One device context (stream, frame cache, scratch).  One per host thread, as
+// the reference's tracking thread / Ceres workers would hold.
+class Context {
+public:
+    explicit Context(int device = 0) { check(gvx_create(device, &c_), nullptr, "gvx_create"); }
+    ~Context() { gvx_destroy(c_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    gvx_ctx* get() const { return c_; }
+    void sync() const { check(gvx_sync(c_), c_, "gvx_sync"); }
+
+private:
+    gvx_ctx* c_ = nullptr;
+};
+
+// ------------------------------------------------------------------ KLT
+// OpenCV-shaped value types (layout of cv::Point2f / cv::Size / cv::TermCriteria).
+struct Point2f {
+    float x = 0.f, y = 0.f;
+};
+static_assert(sizeof(Point2f) == 8, "Point2f must be two packed floats");
+struct Size {
+    int width = 21, height = 21;
+};
+struct TermCriteria {
+    enum { COUNT = 1, MAX_ITER = 1, EPS = 2 };
+    int type = COUNT + EPS;
+    int maxCount = 30;
+    double epsilon = 0.01;
+};
+enum { OPTFLOW_USE_INITIAL_FLOW = 4, OPTFLOW_LK_GET_MIN_EIGENVALS = 8 };
+
+// A gray frame (Frame::image() after CLAHE, tracking/frame.h:62-64) resident on
+// the device with its pyramid built once; replaces the per-call
+// buildOpticalFlowPyramid of every cv::calcOpticalFlowPyrLK on that image.
+class GpuFrame {
+public:
+    GpuFrame(Context& ctx, const uint8_t* gray, int w, int h, int stride, int maxLevel = 3)
+        : ctx_(&ctx), id_(next_id()), w_(w), h_(h), max_level_(maxLevel) {
+        gvx_klt_params p;
+        gvx_klt_params_default(&p);
+        p.max_level = maxLevel;
+        check(gvx_frame_put(ctx.get(), id_, gray, w, h, stride, &p), ctx.get(), "gvx_frame_put");
+    }
+    ~GpuFrame() {
+        if (ctx_) gvx_frame_drop(ctx_->get(), id_);
+    }
+    GpuFrame(GpuFrame&& o) noexcept : ctx_(o.ctx_), id_(o.id_), w_(o.w_), h_(o.h_), max_level_(o.max_level_) {
+        o.ctx_ = nullptr;
+    }
+    GpuFrame(const GpuFrame&) = delete;
+    GpuFrame& operator=(const GpuFrame&) = delete;
+    uint64_t id() const { return id_; }
+    int width() const { return w_; }
+    int height() const { return h_; }
+    int maxLevel() const { return max_level_; }
+    Context& context() const { return *ctx_; }
+
+private:
+    static uint64_t next_id() {
+        static std::atomic<uint64_t> n{1ull << 40};
+        return n++;
+    }
+    Context* ctx_;
+    uint64_t id_;
+    int w_, h_, max_level_;
+};
+
+namespace detail {
+// cv::calcOpticalFlowPyrLK's criteria handling (lkpyramid.cpp): COUNT clamped
+// to [0, 100] (default 30), EPS clamped to [0, 10] (default 0.01).
+inline gvx_klt_params klt_params(Size win, int maxLevel, TermCriteria c, int flags, double minEig) {
+    if (win.width != 21 || win.height != 21)
+        throw Error(GVX_ERR_UNSUPPORTED, "calcOpticalFlowPyrLK: the device path is specialised for 21x21");
+    if (flags & OPTFLOW_LK_GET_MIN_EIGENVALS)
+        throw Error(GVX_ERR_UNSUPPORTED, "calcOpticalFlowPyrLK: OPTFLOW_LK_GET_MIN_EIGENVALS is not on the path");
+    gvx_klt_params p;
+    gvx_klt_params_default(&p);
+    p.win = 21;
+    p.max_level = maxLevel;
+    p.max_iter = (c.type & TermCriteria::COUNT) ? (c.maxCount < 0 ? 0 : c.maxCount > 100 ? 100 : c.maxCount) : 30;
+    p.eps = (c.type & TermCriteria::EPS) ? (c.epsilon < 0 ? 0 : c.epsilon > 10 ? 10 : c.epsilon) : 0.01;
+    p.use_initial_flow = (flags & OPTFLOW_USE_INITIAL_FLOW) ? 1 : 0;
+    p.min_eig = (float)minEig;
+    return p;
+}
+}  // namespace detail
+
+// cv::calcOpticalFlowPyrLK(prevImg, nextImg, prevPts, nextPts, status, err,
+// winSize, maxLevel, criteria, flags, minEigThreshold) on device-resident frames.
+inline void calcOpticalFlowPyrLK(const GpuFrame& prev, const GpuFrame& next, const std::vector<Point2f>& prevPts,
+                                 std::vector<Point2f>& nextPts, std::vector<uint8_t>& status,
+                                 std::vector<float>& err, Size winSize = Size(), int maxLevel = 3,
+                                 TermCriteria criteria = TermCriteria(), int flags = 0,
+                                 double minEigThreshold = 1e-4) {
+    gvx_klt_params p = detail::klt_params(winSize, maxLevel, criteria, flags, minEigThreshold);
+    const size_t n = prevPts.size();
+    if (p.use_initial_flow) {
+        if (nextPts.size() != n) throw Error(GVX_ERR_INVALID, "calcOpticalFlowPyrLK: nextPts size != prevPts size");
+    } else {
+        nextPts = prevPts;
+    }
+    status.assign(n, 0);
+    err.assign(n, 0.f);
+    gvx_ctx* c = prev.context().get();
+    check(gvx_klt(c, prev.id(), next.id(), reinterpret_cast<const float*>(prevPts.data()),
+                  reinterpret_cast<float*>(nextPts.data()), status.data(), err.data(), (int32_t)n, &p),
+          c, "gvx_klt");
+}
+
+// Fused tracking/tracking.cc:380-408: forward LK with initial flow, backward LK
+// seeded with prevPts, keep = st_f && st_b && !isOnBorder(next) &&
+// ptsDistance(back, prev) < fbThresh, plus the reduceVector index list.
+struct TrackFB {
+    std::vector<Point2f> next, back;
+    std::vector<uint8_t> statusFwd, statusBwd, keep;
+    std::vector<int32_t> kept;  // order-preserving indices with keep == 1
+};
+inline TrackFB trackFB(const GpuFrame& prev, const GpuFrame& next, const std::vector<Point2f>& prevPts,
+                       const std::vector<Point2f>& initPts, int camWidth, int camHeight, double fbThresh = 0.5,
+                       double border = 5.0, int maxLevel = 3) {
+    const size_t n = prevPts.size();
+    if (initPts.size() != n) throw Error(GVX_ERR_INVALID, "trackFB: initPts size != prevPts size");
+    gvx_klt_params p = detail::klt_params(Size(), maxLevel, TermCriteria(), OPTFLOW_USE_INITIAL_FLOW, 1e-4);
+    TrackFB r;
+    r.next = initPts;
+    r.back.resize(n);
+    r.statusFwd.resize(n);
+    r.statusBwd.resize(n);
+    r.keep.resize(n);
+    r.kept.resize(n);
+    int32_t nk = 0;
+    gvx_ctx* c = prev.context().get();
+    check(gvx_klt_fb(c, prev.id(), next.id(), reinterpret_cast<const float*>(prevPts.data()),
+                     reinterpret_cast<float*>(r.next.data()), reinterpret_cast<float*>(r.back.data()),
+                     r.statusFwd.data(), r.statusBwd.data(), r.keep.data(), r.kept.data(), &nk, (int32_t)n,
+                     fbThresh, border, camWidth, camHeight, &p),
+          c, "gvx_klt_fb");
+    r.kept.resize((size_t)nk);
+    return r;
+}
+
+// Tracking::reduceVector (tracking/tracking.cc:831-839): keep the entries whose
+// status is non-zero, in order.
+template <class T>
+void reduceVector(std::vector<T>& vec, const std::vector<uint8_t>& status) {
+    size_t j = 0;
+    for (size_t i = 0; i < vec.size(); ++i)
+        if (status[i]) vec[j++] = vec[i];
+    vec.resize(j);
+}
+
+// Tracking::featuresDetection (tracking/tracking.cc:576-688) on a device frame:
+// block grid of the Tracking ctor, circle mask around maskPts (when ismask),
+// per-block goodFeaturesToTrack + cornerSubPix.  countPts are the points counted
+// per block (frame->features() + pts2d_new_), nExisting = features + pts2d_ref_
+// for the early exit.  Returns false when the early exit triggers.
+struct DetectParams {
+    gvx_detect_params p;
+    DetectParams() { gvx_detect_params_default(&p); }
+};
+inline bool featuresDetection(const GpuFrame& frame, const std::vector<Point2f>& countPts,
+                              const std::vector<Point2f>& maskPts, bool ismask, int nExisting,
+                              const DetectParams& prm, std::vector<Point2f>& corners,
+                              std::vector<int32_t>* blockCounts = nullptr) {
+    // upper bound of block_cnts * track_max_block_features_
+    const double bs = prm.p.block_size;
+    const int cols = (int)(frame.width() / bs + 1.5), rows = (int)(frame.height() / bs + 1.5);
+    const size_t cap = (size_t)(cols + 1) * (rows + 1) * (size_t)(prm.p.max_features + 1);
+    std::vector<Point2f> out(cap);
+    std::vector<int32_t> blk((size_t)(cols + 1) * (rows + 1));
+    int32_t n = 0;
+    gvx_ctx* c = frame.context().get();
+    check(gvx_detect(c, frame.id(), reinterpret_cast<const float*>(countPts.data()), (int32_t)countPts.size(),
+                     reinterpret_cast<const float*>(maskPts.data()), (int32_t)maskPts.size(), ismask ? 1 : 0,
+                     nExisting, &prm.p, reinterpret_cast<float*>(out.data()), blk.data(), &n),
+          c, "gvx_detect");
+    if (n < 0) {
+        corners.clear();
+        return false;
+    }
+    out.resize((size_t)n);
+    corners = std::move(out);
+    if (blockCounts) *blockCounts = blk;
+    return true;
+}
+
+// ------------------------------------------------------ preintegration
+using IMU = gvx_imu;  // common/types.h:50-58 {time, dt, dtheta[3], dvel[3], odovel}
+
+// IntegrationParameters (preintegration/integration_state.h:68-89): the
+// fields the NORMAL / EARTH variants read.  station stays zero unless set, as
+// in the reference (resetState computes iewn from it).
+struct IntegrationParameters {
+    double acc_vrw = 0, gyr_arw = 0, gyr_bias_std = 0, acc_bias_std = 0, corr_time = 0, gravity = 9.8;
+    std::array<double, 3> station{0, 0, 0};
+};
+
+// IntegrationState core (integration_state.h:35-51); q = (x, y, z, w).
+struct IntegrationState {
+    double time = 0;
+    std::array<double, 3> p{0, 0, 0};
+    std::array<double, 4> q{0, 0, 0, 1};
+    std::array<double, 3> v{0, 0, 0}, bg{0, 0, 0}, ba{0, 0, 0};
+};
+
+namespace detail {
+inline gvx_state to_c(const IntegrationState& s) {
+    gvx_state o;
+    o.time = s.time;
+    std::memcpy(o.p, s.p.data(), sizeof o.p);
+    std::memcpy(o.q, s.q.data(), sizeof o.q);
+    std::memcpy(o.v, s.v.data(), sizeof o.v);
+    std::memcpy(o.bg, s.bg.data(), sizeof o.bg);
+    std::memcpy(o.ba, s.ba.data(), sizeof o.ba);
+    return o;
+}
+inline IntegrationState from_c(const gvx_state& s) {
+    IntegrationState o;
+    o.time = s.time;
+    std::memcpy(o.p.data(), s.p, sizeof s.p);
+    std::memcpy(o.q.data(), s.q, sizeof s.q);
+    std::memcpy(o.v.data(), s.v, sizeof s.v);
+    std::memcpy(o.bg.data(), s.bg, sizeof s.bg);
+    std::memcpy(o.ba.data(), s.ba, sizeof s.ba);
+    return o;
+}
+}  // namespace detail
+
+// PreintegrationBase with the NORMAL or EARTH variant
+// (preintegration/preintegration_base.h:38-70, preintegration_earth.h,
+// preintegration_normal.h): same constructor arguments, addNewImu /
+// reintegration / getters, and the factor-side evaluate + Jacobian blocks.
+// The IMU buffer lives on the host; the integration runs on the device (one
+// wavefront) when a result is first needed after a change -- integrating the
+// whole buffer at once is the same arithmetic, step by step, as the
+// reference's per-sample integrationProcess.
+class Preintegration {
+public:
+    enum Variant { NORMAL = GVX_PREINT_NORMAL, EARTH = GVX_PREINT_EARTH };
+
+    Preintegration(Context& ctx, Variant variant, const IntegrationParameters& prm, const IMU& imu0,
+                   const IntegrationState& state)
+        : ctx_(&ctx), variant_(variant), prm_(prm), state0_(state) {
+        imu_buffer_.push_back(imu0);
+    }
+
+    void addNewImu(const IMU& imu) {
+        imu_buffer_.push_back(imu);
+        dirty_ = true;
+    }
+    // preintegration_base.cc:77-84: restart from `state`, re-integrate the buffer
+    void reintegration(IntegrationState& state) {
+        state0_ = state;
+        dirty_ = true;
+    }
+
+    IntegrationState currentState() { return detail::from_c(result().current); }
+    IntegrationState deltaState() { return detail::from_c(result().delta); }
+    double deltaTime() { return result().delta_time; }
+    double startTime() { return result().start_time; }
+    double endTime() { return result().end_time; }
+    std::array<double, 3> gravity() { return {result().gravity[0], result().gravity[1], result().gravity[2]}; }
+    const std::vector<IMU>& imuBuffer() const { return imu_buffer_; }
+    const gvx_preint_result& raw() { return result(); }
+    const std::vector<double>& pn() {
+        result();
+        return pn_;
+    }
+
+    static constexpr int numResiduals() { return 15; }
+    static std::vector<int> numBlocksParameters() { return {7, 9, 7, 9}; }
+    int numMixParametersBlocks() const { return 9; }
+
+    // constructState (preintegration_earth.cc:186-203): pose[7] = p, q(x,y,z,w);
+    // mix[9] = v, bg, ba
+    static void constructState(const double* const* parameters, IntegrationState& s0, IntegrationState& s1) {
+        auto fill = [](const double* pose, const double* mix, IntegrationState& s) {
+            s.p = {pose[0], pose[1], pose[2]};
+            s.q = {pose[3], pose[4], pose[5], pose[6]};
+            s.v = {mix[0], mix[1], mix[2]};
+            s.bg = {mix[3], mix[4], mix[5]};
+            s.ba = {mix[6], mix[7], mix[8]};
+        };
+        fill(parameters[0], parameters[1], s0);
+        fill(parameters[2], parameters[3], s1);
+    }
+
+    // PreintegrationFactor::Evaluate semantics on one parameter set: residuals
+    // (15) and, for every non-null jacobians[k], the Ceres row-major block
+    // (15x7, 15x9, 15x7, 15x9), each already multiplied by sqrt_info.
+    void evaluateAll(const double* const* parameters, double* residuals, double** jacobians) {
+        const gvx_preint_result& r = result();
+        double params[32];
+        std::memcpy(params, parameters[0], 7 * sizeof(double));
+        std::memcpy(params + 7, parameters[1], 9 * sizeof(double));
+        std::memcpy(params + 16, parameters[2], 7 * sizeof(double));
+        std::memcpy(params + 23, parameters[3], 9 * sizeof(double));
+        const int32_t offs[4] = {0, 7, 16, 23};
+        const int32_t pn_off = 0;
+        double res[15];
+        std::vector<double> jac(jacobians ? 480 : 0);
+        const bool earth = variant_ == EARTH;
+        check(gvx_preint_factor_eval(ctx_->get(), 1, &r, earth ? pn_.data() : nullptr,
+                                     earth ? (int32_t)(pn_.size() / 4) : 0, earth ? &pn_off : nullptr, params, 32,
+                                     offs, res, jacobians ? jac.data() : nullptr),
+              ctx_->get(), "gvx_preint_factor_eval");
+        if (residuals) std::memcpy(residuals, res, sizeof res);
+        if (jacobians) {
+            static const int cols[4] = {7, 9, 7, 9}, start[4] = {0, 105, 240, 345};
+            for (int k = 0; k < 4; ++k)
+                if (jacobians[k]) std::memcpy(jacobians[k], jac.data() + start[k], sizeof(double) * 15 * cols[k]);
+        }
+    }
+
+private:
+    const gvx_preint_result& result() {
+        if (!dirty_) return res_;
+        const int32_t m = (int32_t)imu_buffer_.size();
+        const int32_t seg_off[2] = {0, m};
+        const gvx_state s0 = detail::to_c(state0_);
+        double iewn[3] = {0, 0, 0};
+        if (variant_ == EARTH) gvx_earth_iewn(prm_.station.data(), state0_.p.data(), iewn);
+        gvx_imu_params p{prm_.acc_vrw, prm_.gyr_arw, prm_.gyr_bias_std, prm_.acc_bias_std, prm_.corr_time,
+                         prm_.gravity};
+        pn_.assign((size_t)(m > 1 ? m - 1 : 0) * 4 + 4, 0.0);
+        check(gvx_preint_integrate(ctx_->get(), (int32_t)variant_, &p, 1, imu_buffer_.data(), seg_off, &s0, iewn,
+                                   &res_, variant_ == EARTH ? pn_.data() : nullptr),
+              ctx_->get(), "gvx_preint_integrate");
+        pn_.resize((size_t)(m > 1 ? m - 1 : 0) * 4);
+        dirty_ = false;
+        return res_;
+    }
+
+    Context* ctx_;
+    Variant variant_;
+    IntegrationParameters prm_;
+    IntegrationState state0_;
+    std::vector<IMU> imu_buffer_;
+    std::vector<double> pn_;
+    gvx_preint_result res_{};
+    bool dirty_ = true;
+};
+
+// ceres::CostFunction-shaped wrappers: Evaluate(parameters, residuals,
+// jacobians) with the reference's block sizes.  A ceres::CostFunction subclass
+// forwarding to these is all the integration needs.
+class PreintegrationFactor {
+public:
+    explicit PreintegrationFactor(Preintegration& pre) : pre_(&pre) {}
+    std::vector<int> parameter_block_sizes() const { return Preintegration::numBlocksParameters(); }
+    int num_residuals() const { return Preintegration::numResiduals(); }
+    bool Evaluate(const double* const* parameters, double* residuals, double** jacobians) const {
+        pre_->evaluateAll(parameters, residuals, jacobians);
+        return true;
+    }
+
+private:
+    Preintegration* pre_;
+};
+
+// ReprojectionFactor (factors/reprojection_factor.h:35-161): SizedCostFunction
+// <2, 7, 7, 7, 1, 1>, constructed from the two normalized points, their pixel
+// velocities, time delays and the normalized-plane std.
+class ReprojectionFactor {
+public:
+    using Vec3 = std::array<double, 3>;
+    ReprojectionFactor(Context& ctx, const Vec3& pts0, const Vec3& pts1, const Vec3& vel0, const Vec3& vel1,
+                       double td0, double td1, double std)
+        : ctx_(&ctx) {
+        std::memcpy(c_.pts0, pts0.data(), sizeof c_.pts0);
+        std::memcpy(c_.pts1, pts1.data(), sizeof c_.pts1);
+        std::memcpy(c_.vel0, vel0.data(), sizeof c_.vel0);
+        std::memcpy(c_.vel1, vel1.data(), sizeof c_.vel1);
+        c_.td0 = td0;
+        c_.td1 = td1;
+        c_.std = std;
+    }
+    std::vector<int> parameter_block_sizes() const { return {7, 7, 7, 1, 1}; }
+    int num_residuals() const { return 2; }
+    bool Evaluate(const double* const* parameters, double* residuals, double** jacobians) const {
+        double params[23];
+        std::memcpy(params, parameters[0], 7 * sizeof(double));
+        std::memcpy(params + 7, parameters[1], 7 * sizeof(double));
+        std::memcpy(params + 14, parameters[2], 7 * sizeof(double));
+        params[21] = parameters[3][0];
+        params[22] = parameters[4][0];
+        const int32_t offs[5] = {0, 7, 14, 21, 22};
+        double res[2], jac[46];
+        check(gvx_reproj_eval(ctx_->get(), 1, &c_, params, 23, offs, res, jacobians ? jac : nullptr), ctx_->get(),
+              "gvx_reproj_eval");
+        if (residuals) std::memcpy(residuals, res, sizeof res);
+        if (jacobians) {
+            static const int cols[5] = {7, 7, 7, 1, 1}, start[5] = {0, 14, 28, 42, 44};
+            for (int k = 0; k < 5; ++k)
+                if (jacobians[k]) std::memcpy(jacobians[k], jac + start[k], sizeof(double) * 2 * cols[k]);
+        }
+        return true;
+    }
+    const gvx_reproj_const& constants() const { return c_; }
+
+private:
+    Context* ctx_;
+    gvx_reproj_const c_{};
+};
+
+}  // namespace gvx

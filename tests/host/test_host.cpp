@@ -1,0 +1,146 @@
+// C++ host-mirror check (tests/test_host_cpp.py builds and drives this).
+//   test_host nodev       -> constructing gvx::Context without a device must throw
+//                            gvx::Error(GVX_ERR_NO_DEVICE) (no CPU fallback)
+//   test_host run <dir>   -> reads inputs written by the test, runs the reference-
+//                            shaped calls through include/gvx/gvx.hpp, writes outputs
+#include <gvx/gvx.hpp>
+
+#include <cstdio>
+#include <fstream>
+#include <string>
+#include <vector>
+
+template <class T>
+static std::vector<T> readf(const std::string& path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) throw std::runtime_error("cannot read " + path);
+    const size_t bytes = (size_t)f.tellg();
+    std::vector<T> v(bytes / sizeof(T));
+    f.seekg(0);
+    f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+    return v;
+}
+template <class T>
+static void writef(const std::string& path, const T* p, size_t n) {
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(p), (std::streamsize)(n * sizeof(T)));
+}
+
+static gvx::IntegrationState state_from(const double* d) {
+    gvx::IntegrationState s;
+    s.time = d[0];
+    for (int k = 0; k < 3; ++k) s.p[k] = d[1 + k];
+    for (int k = 0; k < 4; ++k) s.q[k] = d[4 + k];
+    for (int k = 0; k < 3; ++k) s.v[k] = d[8 + k], s.bg[k] = d[11 + k], s.ba[k] = d[14 + k];
+    return s;
+}
+static void state_to(const gvx::IntegrationState& s, double* d) {
+    d[0] = s.time;
+    for (int k = 0; k < 3; ++k) d[1 + k] = s.p[k];
+    for (int k = 0; k < 4; ++k) d[4 + k] = s.q[k];
+    for (int k = 0; k < 3; ++k) d[8 + k] = s.v[k], d[11 + k] = s.bg[k], d[14 + k] = s.ba[k];
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "";
+    if (mode == "nodev") {
+        try {
+            gvx::Context c(0);
+            std::printf("HAVE_DEVICE\n");
+            return 0;
+        } catch (const gvx::Error& e) {
+            std::printf("ERROR %d %s\n", (int)e.status(), e.what());
+            return e.status() == GVX_ERR_NO_DEVICE ? 0 : 1;
+        }
+    }
+    if (mode != "run" || argc < 3) {
+        std::fprintf(stderr, "usage: test_host nodev | run <dir>\n");
+        return 2;
+    }
+    const std::string d = std::string(argv[2]) + "/";
+    const auto meta = readf<int32_t>(d + "meta.bin");  // w h n variant
+    const int w = meta[0], h = meta[1], n = meta[2];
+    const auto I = readf<uint8_t>(d + "I.bin"), J = readf<uint8_t>(d + "J.bin");
+    const auto prev = readf<gvx::Point2f>(d + "prev.bin"), init = readf<gvx::Point2f>(d + "init.bin");
+    if ((int)prev.size() != n || (int)init.size() != n) throw std::runtime_error("point count mismatch");
+    gvx::Context ctx(0);
+    gvx::GpuFrame fI(ctx, I.data(), w, h, w), fJ(ctx, J.data(), w, h, w);
+
+    // cv::calcOpticalFlowPyrLK as called at tracking.cc:385
+    std::vector<gvx::Point2f> next = init;
+    std::vector<uint8_t> status;
+    std::vector<float> err;
+    gvx::calcOpticalFlowPyrLK(fI, fJ, prev, next, status, err, gvx::Size{21, 21}, 3,
+                              gvx::TermCriteria{gvx::TermCriteria::COUNT + gvx::TermCriteria::EPS, 30, 0.01},
+                              gvx::OPTFLOW_USE_INITIAL_FLOW);
+    writef(d + "lk_next.bin", next.data(), next.size());
+    writef(d + "lk_status.bin", status.data(), status.size());
+    writef(d + "lk_err.bin", err.data(), err.size());
+
+    // fused fwd/bwd/FB + reduceVector (tracking.cc:380-408)
+    gvx::TrackFB fb = gvx::trackFB(fI, fJ, prev, init, w, h);
+    writef(d + "fb_next.bin", fb.next.data(), fb.next.size());
+    writef(d + "fb_back.bin", fb.back.data(), fb.back.size());
+    writef(d + "fb_keep.bin", fb.keep.data(), fb.keep.size());
+    writef(d + "fb_kept.bin", fb.kept.data(), fb.kept.size());
+    std::vector<gvx::Point2f> reduced = fb.next;
+    gvx::reduceVector(reduced, fb.keep);
+    writef(d + "fb_reduced.bin", reduced.data(), reduced.size());
+
+    // featuresDetection on the first frame, no tracked points
+    std::vector<gvx::Point2f> corners;
+    gvx::DetectParams dp;
+    const bool ran = gvx::featuresDetection(fI, {}, {}, false, 0, dp, corners);
+    if (!ran) corners.clear();
+    writef(d + "det.bin", corners.data(), corners.size());
+
+    // preintegration: constructor(imu0) + addNewImu per sample, then reintegration
+    const auto imu = readf<gvx::IMU>(d + "imu.bin");
+    const auto st = readf<double>(d + "state.bin");
+    const auto prm = readf<double>(d + "prm.bin");
+    gvx::IntegrationParameters ip;
+    ip.acc_vrw = prm[0], ip.gyr_arw = prm[1], ip.gyr_bias_std = prm[2], ip.acc_bias_std = prm[3];
+    ip.corr_time = prm[4], ip.gravity = prm[5];
+    gvx::Preintegration pre(ctx, (gvx::Preintegration::Variant)meta[3], ip, imu[0], state_from(st.data()));
+    for (size_t k = 1; k < imu.size(); ++k) pre.addNewImu(imu[k]);
+    double out[2 * 17 + 1];
+    state_to(pre.deltaState(), out);
+    state_to(pre.currentState(), out + 17);
+    out[34] = pre.deltaTime();
+    writef(d + "pre_state.bin", out, 35);
+    writef(d + "pre_pn.bin", pre.pn().data(), pre.pn().size());
+
+    // PreintegrationFactor::Evaluate with all four Jacobian blocks
+    const auto fp = readf<double>(d + "fparams.bin");
+    const double* blocks[4] = {fp.data(), fp.data() + 7, fp.data() + 16, fp.data() + 23};
+    std::vector<double> res(15), j0(105), j1(135), j2(105), j3(135);
+    double* jac[4] = {j0.data(), j1.data(), j2.data(), j3.data()};
+    gvx::PreintegrationFactor pf(pre);
+    pf.Evaluate(blocks, res.data(), jac);
+    std::vector<double> all(res);
+    for (auto* v : {&j0, &j1, &j2, &j3}) all.insert(all.end(), v->begin(), v->end());
+    writef(d + "pf.bin", all.data(), all.size());
+
+    // reintegration from a modified state (bias step, as after an LM update)
+    gvx::IntegrationState s2 = state_from(st.data());
+    s2.bg[0] += 1e-3;
+    s2.ba[2] -= 2e-3;
+    pre.reintegration(s2);
+    state_to(pre.deltaState(), out);
+    state_to(pre.currentState(), out + 17);
+    out[34] = pre.deltaTime();
+    writef(d + "pre_state2.bin", out, 35);
+
+    // ReprojectionFactor::Evaluate
+    const auto rc = readf<double>(d + "rconst.bin");
+    const auto rp = readf<double>(d + "rparams.bin");
+    gvx::ReprojectionFactor rf(ctx, {rc[0], rc[1], rc[2]}, {rc[3], rc[4], rc[5]}, {rc[6], rc[7], rc[8]},
+                               {rc[9], rc[10], rc[11]}, rc[12], rc[13], rc[14]);
+    const double* rb[5] = {rp.data(), rp.data() + 7, rp.data() + 14, rp.data() + 21, rp.data() + 22};
+    std::vector<double> rr(2 + 46);
+    double* rj[5] = {rr.data() + 2, rr.data() + 16, rr.data() + 30, rr.data() + 44, rr.data() + 46};
+    rf.Evaluate(rb, rr.data(), rj);
+    writef(d + "rf.bin", rr.data(), rr.size());
+    std::printf("OK\n");
+    return 0;
+}

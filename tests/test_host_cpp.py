@@ -1,0 +1,120 @@
+"""The C++ host mirror (ic-gvins_amd/host/include/gvx/gvx.hpp) of the reference
+interfaces -- cv::calcOpticalFlowPyrLK, the fused FB tracking + reduceVector,
+featuresDetection, PreintegrationBase (addNewImu / reintegration / getters),
+PreintegrationFactor / ReprojectionFactor::Evaluate -- compiled with g++ against
+libgvx.so (tests/host/test_host.cpp).  CPU: it builds, links and fails loudly
+without a device.  GPU: its outputs equal the oracle's (bit-exact KLT /
+detection / reprojection, 1e-10 / 1e-9 for the fp64 preintegration path)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NORMAL, EARTH = 0, 2
+
+
+@pytest.fixture(scope="module")
+def host_bin(tmp_path_factory, gvx_mod):
+    out = str(tmp_path_factory.mktemp("host") / "test_host")
+    libdir = os.path.dirname(gvx_mod.LIB_PATH)
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(ROOT, "ic-gvins_amd", "host", "include"),
+           os.path.join(ROOT, "tests", "host", "test_host.cpp"), "-o", out, "-L", libdir, "-lgvx",
+           f"-Wl,-rpath,{libdir}", "-Wl,-rpath-link,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return out
+
+
+def test_host_mirror_builds_and_fails_loudly_without_device(host_bin):
+    import torch
+    r = subprocess.run([host_bin, "nodev"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    if not torch.cuda.is_available():
+        assert r.stdout.startswith("ERROR -2"), r.stdout
+
+
+def _close(g, o, what, rtol):
+    g, o = np.asarray(g, np.float64), np.asarray(o, np.float64)
+    scale = max(np.abs(o).max(), 1e-300)
+    assert np.abs(g - o).max() <= rtol * scale, f"{what}: {np.abs(g - o).max():.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [NORMAL, EARTH])
+def test_host_mirror_matches_oracle(host_bin, orc, tmp_path, variant):
+    from gvx import synth, synth_ba
+    d = str(tmp_path)
+    w, h, n = 640, 280, 96
+    I, J, prev, init, _ = synth.make_pair(w, h, n, seed=77 + variant)
+    rng = np.random.default_rng(5 + variant)
+    imu = synth_ba.make_imu_segment(rng, 60)
+    s = synth_ba.random_state(rng)
+    st = np.r_[s["time"], s["p"], s["q"], s["v"], s["bg"], s["ba"]].astype(np.float64)
+    prm = np.array(synth_ba.imu_params(), np.float64)
+    np.array([w, h, n, variant], np.int32).tofile(f"{d}/meta.bin")
+    I.tofile(f"{d}/I.bin"), J.tofile(f"{d}/J.bin")
+    prev.astype(np.float32).tofile(f"{d}/prev.bin"), init.astype(np.float32).tofile(f"{d}/init.bin")
+    imu.tofile(f"{d}/imu.bin"), st.tofile(f"{d}/state.bin"), prm.tofile(f"{d}/prm.bin")
+    iewn = orc.earth_iewn(np.zeros(3), s["p"])  # IntegrationParameters::station defaults to 0
+    seg = orc.PreintSeg(variant, orc.imu_params(*prm), imu,
+                        orc.make_state(float(s["time"]), s["p"], s["q"], s["v"], s["bg"], s["ba"]), iewn)
+    c = seg.current()
+    blocks = (np.r_[s["p"], s["q"]], np.r_[s["v"], s["bg"], s["ba"]] + 1e-4,
+              np.r_[c["p"] + 0.01, c["q"]], np.r_[c["v"], c["bg"], c["ba"]] - 1e-4)
+    np.concatenate(blocks).tofile(f"{d}/fparams.bin")
+    prob = synth_ba.make_ba_problem(n_kf=3, n_lm=4)
+    rc, o = prob["consts"][0], prob["offs"][0]
+    rconst = np.r_[rc["pts0"], rc["pts1"], rc["vel0"], rc["vel1"], rc["td0"], rc["td1"], rc["std"]]
+    rconst.astype(np.float64).tofile(f"{d}/rconst.bin")
+    pr = prob["params"]
+    rblocks = [pr[o[0]:o[0] + 7], pr[o[1]:o[1] + 7], pr[o[2]:o[2] + 7], pr[o[3]:o[3] + 1], pr[o[4]:o[4] + 1]]
+    np.concatenate(rblocks).tofile(f"{d}/rparams.bin")
+
+    r = subprocess.run([host_bin, "run", d], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+    rd = lambda name, dt: np.fromfile(f"{d}/{name}", dt)  # noqa: E731
+    o_next, o_st, o_err = orc.calc_optical_flow_pyr_lk(I, J, prev, init)
+    assert np.array_equal(rd("lk_next.bin", np.float32).reshape(-1, 2), o_next)
+    assert np.array_equal(rd("lk_status.bin", np.uint8), o_st)
+    assert np.array_equal(rd("lk_err.bin", np.float32)[o_st == 1], o_err[o_st == 1])
+    fb = orc.klt_fb(I, J, prev, init, w, h, reuse_pyramids=True)
+    assert np.array_equal(rd("fb_next.bin", np.float32).reshape(-1, 2), fb["next"])
+    assert np.array_equal(rd("fb_back.bin", np.float32).reshape(-1, 2), fb["back"])
+    assert np.array_equal(rd("fb_keep.bin", np.uint8), fb["keep"])
+    assert np.array_equal(rd("fb_kept.bin", np.int32), fb["kept_idx"])
+    assert np.array_equal(rd("fb_reduced.bin", np.float32).reshape(-1, 2), fb["next"][fb["kept_idx"]])
+    det, _ = orc.features_detection(I, None, None, False, 0, orc.DetectParams.default())
+    assert np.array_equal(rd("det.bin", np.float32).reshape(-1, 2), det)
+
+    ps = rd("pre_state.bin", np.float64)
+    dlt, cur = seg.delta(), seg.current()
+    for k, (lo, hi) in (("p", (1, 4)), ("q", (4, 8)), ("v", (8, 11))):
+        _close(ps[lo:hi], dlt[k], f"delta.{k}", 1e-10)
+        _close(ps[17 + lo:17 + hi], cur[k], f"current.{k}", 1e-10)
+    assert ps[34] == pytest.approx(seg.s.delta_time, rel=1e-15)
+    if variant == EARTH:
+        _close(rd("pre_pn.bin", np.float64).reshape(-1, 4), seg.pn, "pn", 1e-10)
+    pf = rd("pf.bin", np.float64)
+    res, Jo = seg.evaluate(*blocks)
+    _close(pf[:15], res, "factor residual", 1e-9)
+    oj = np.concatenate([x.ravel() for x in Jo])
+    for b, (lo, hi) in enumerate([(0, 105), (105, 240), (240, 345), (345, 480)]):
+        _close(pf[15 + lo:15 + hi], oj[lo:hi], f"factor J{b}", 1e-9)
+    s2 = dict(s)
+    bg2, ba2 = s["bg"].copy(), s["ba"].copy()
+    bg2[0] += 1e-3
+    ba2[2] -= 2e-3
+    seg2 = orc.PreintSeg(variant, orc.imu_params(*prm), imu,
+                         orc.make_state(float(s["time"]), s["p"], s["q"], s["v"], bg2, ba2), iewn)
+    ps2 = rd("pre_state2.bin", np.float64)
+    for k, (lo, hi) in (("p", (1, 4)), ("q", (4, 8)), ("v", (8, 11))):
+        _close(ps2[lo:hi], seg2.delta()[k], f"reintegrated delta.{k}", 1e-10)
+    rf = rd("rf.bin", np.float64)
+    rcc = orc.reproj_const(rc["pts0"], rc["pts1"], rc["vel0"], rc["vel1"], rc["td0"], rc["td1"], rc["std"])
+    rr, rj = orc.reproj_eval(rcc, *rblocks)
+    assert np.array_equal(rf[:2], rr)
+    assert np.array_equal(rf[2:], np.concatenate([x.ravel() for x in rj]))
