@@ -104,7 +104,6 @@ def test_host_mirror_matches_oracle(host_bin, orc, tmp_path, variant):
     oj = np.concatenate([x.ravel() for x in Jo])
     for b, (lo, hi) in enumerate([(0, 105), (105, 240), (240, 345), (345, 480)]):
         _close(pf[15 + lo:15 + hi], oj[lo:hi], f"factor J{b}", 1e-9)
-    s2 = dict(s)
     bg2, ba2 = s["bg"].copy(), s["ba"].copy()
     bg2[0] += 1e-3
     ba2[2] -= 2e-3
