@@ -113,10 +113,17 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
     ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
+    ap.add_argument("--config", type=int, default=1, choices=(1, 3, 4),
+                    help="BASELINE.json config: 1 = 1280x560/150 L3 (default, the metric), "
+                         "3 = 1920x1200/500 L4 batch, 4 = sliding-window BA factor batch")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
     if args.mock:
         return mock_main(args)
+    if args.config == 3:
+        args.width, args.height, args.features, args.levels = 1920, 1200, 500, 4
+    if args.config == 4:
+        return factors_main(args)
 
     import torch
     import gvx
@@ -210,7 +217,7 @@ def main():
                 cpu["single_thread_value"] = one["value"]
                 cpu["single_thread_sample"] = one["sample"]
         line = {
-            "metric": "KLT frames/sec @1280x560,150 feat",
+            "metric": f"KLT frames/sec @{W}x{H},{N} feat",
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -223,7 +230,7 @@ def main():
             "dtype": "u8/i32 windows, f32 solve",
             "data": "synthetic (KAIST bags unavailable offline): band-limited noise + rectangles, "
                     "similarity warp, seed 20261015",
-            "config": {"workload": f"configs[1]: batch of {Pn} frame pairs/GPU, {W}x{H} mono, {N} feat, "
+            "config": {"workload": f"configs[{args.config - 1}]: batch of {Pn} frame pairs/GPU, {W}x{H} mono, {N} feat, "
                                    f"maxLevel {L}, win 21, fwd+bwd LK + FB + compaction",
                        "pairs_per_gpu_per_step": Pn, "parallelism": f"pairs sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": "klt pipeline (pyramid + LK + compaction) per step",
@@ -236,6 +243,144 @@ def main():
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def factors_main(args):
+    """configs[3]: sliding-window BA factor evaluation (10 keyframes x 200
+    landmarks -> 1800 ReprojectionFactor + 9 Earth PreintegrationFactor with
+    M = 100 IMU samples), replicated to >= 2^20 reprojection
+    factors per launch (the window's parameter blocks are shared, read once per
+    batch).  A step = one LM iteration's residual + Jacobian evaluation of the
+    whole batch (reprojection + preintegration factors); preintegration steps/s
+    (9 x replicas segments) are timed separately."""
+    import torch
+    import gvx
+    from gvx import synth_ba
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    ctx = gvx.Context(local)
+    stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
+
+    prob = synth_ba.make_ba_problem()
+    n_kf = prob["poses"].shape[0]
+    n_rp = len(prob["consts"])
+    reps = -(-(1 << 20) // n_rp)
+    rng = np.random.default_rng(synth_ba.SEED if hasattr(synth_ba, "SEED") else 20261015)
+    # Earth preintegration segments between consecutive keyframes
+    M = 100
+    segs = [synth_ba.make_imu_segment(rng, M, t0=0.5 * k) for k in range(n_kf - 1)]
+    states = np.zeros(n_kf - 1, gvx.STATE_DTYPE)
+    for k in range(n_kf - 1):
+        states[k]["time"] = 0.5 * k
+        states[k]["p"] = prob["poses"][k, :3]
+        states[k]["q"] = prob["poses"][k, 3:]
+        states[k]["v"] = [5.0, 0.0, 0.0]
+    iewn = np.array([gvx.earth_iewn(np.zeros(3), st["p"]) for st in states])
+    pre, pn, pn_off = ctx.preint_integrate(2, synth_ba.imu_params(), segs, states, iewn)
+    # parameter array: poses | ext | invdepth | td | mix blocks (v, bg, ba) per keyframe
+    mix = np.zeros((n_kf, 9))
+    mix[:, 0] = 5.0
+    params = np.concatenate([prob["params"], mix.reshape(-1)])
+    o_mix = prob["params"].size
+    poffs = np.array([[7 * k, o_mix + 9 * k, 7 * (k + 1), o_mix + 9 * (k + 1)] for k in range(n_kf - 1)], np.int32)
+
+    def dev_t(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    d_consts = dev_t(np.tile(prob["consts"], reps).view(np.uint8))
+    d_offs = dev_t(np.tile(prob["offs"], (reps, 1)))
+    d_params = dev_t(params)
+    n_r = n_rp * reps
+    d_res = torch.empty((n_r, 2), dtype=torch.float64, device=dev)
+    d_jac = torch.empty((n_r, 46), dtype=torch.float64, device=dev)
+    n_p = (n_kf - 1) * reps
+    d_pre = dev_t(np.tile(pre, reps).view(np.uint8))
+    d_pn = dev_t(pn)
+    d_pn_off = dev_t(np.tile(pn_off, reps))
+    d_poffs = dev_t(np.tile(poffs, (reps, 1)))
+    d_pres = torch.empty((n_p, 15), dtype=torch.float64, device=dev)
+    d_pjac = torch.empty((n_p, 480), dtype=torch.float64, device=dev)
+    # preintegration batch: (n_kf-1) * reps segments of M samples
+    S = (n_kf - 1) * reps
+    imu_all = np.concatenate(segs * reps)
+    seg_off = np.arange(S + 1, dtype=np.int32) * M
+    d_imu = dev_t(imu_all.astype(gvx.IMU_DTYPE).view(np.uint8))
+    d_seg_off = dev_t(seg_off)
+    d_states = dev_t(np.tile(states, reps).view(np.uint8))
+    d_iewn = dev_t(np.tile(iewn, (reps, 1)))
+    d_out = torch.empty(S * gvx.PREINT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_pnall = torch.empty((S * (M - 1), 4), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        ctx.reproj_eval_dev(n_r, d_consts.data_ptr(), d_params.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(),
+                            d_jac.data_ptr())
+        ctx.preint_factor_eval_dev(n_p, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
+                                   d_params.data_ptr(), d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr())
+
+    def integ():
+        ctx.preint_integrate_dev(2, synth_ba.imu_params(), S, d_imu.data_ptr(), d_seg_off.data_ptr(),
+                                 d_states.data_ptr(), d_iewn.data_ptr(), d_out.data_ptr(), d_pnall.data_ptr())
+
+    def timed(fn, k):
+        for _ in range(args.warmup):
+            fn()
+        ctx.sync()
+        if dist:
+            dist.barrier()
+        ctx.profile_reset()
+        ctx.profile(True)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        ctx.sync()
+        if dist:
+            dist.barrier()
+        el = max_over_ranks(time.perf_counter() - t0, dist, dev)
+        fam = {f: ctx.profile_read(f) for f in ("reproj", "preint_factor", "preint")}
+        ctx.profile(False)
+        return el, fam
+
+    el, fam = timed(step, args.steps)
+    el_i, fam_i = timed(integ, max(1, args.steps // 4))
+    k_i = max(1, args.steps // 4)
+    evals = world * (n_r + n_p) * args.steps
+    value = evals / el
+    rp_ms = fam["reproj"][0] / args.steps
+    B_rp = 15 * 8 + 5 * 4 + 48 * 8  # consts + offsets in, residual + 5 Jacobian blocks out
+    achieved = B_rp * n_r / (rp_ms * 1e-3) / 1e9 if rp_ms > 0 else None
+    if rank == 0:
+        line = {
+            "metric": "BA factor-Jacobian evaluations/s (configs[3])",
+            "value": round(value, 1), "unit": "factor evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic sliding window (seed 20261015)",
+            "config": {"workload": f"configs[3]: {n_kf} keyframes x 200 landmarks = {n_rp} ReprojectionFactor + "
+                                   f"{n_kf - 1} Earth PreintegrationFactor (M={M}), x{reps} windows per launch",
+                       "reproj_factors_per_step": n_r, "preint_factors_per_step": n_p},
+            "roofline": {"bound": "hbm", "kernel": "reproj_kernel", "achieved": round(achieved, 1) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
+                         "algorithmic_bytes_per_factor": B_rp,
+                         "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
+            "preint_steps_per_s": round(world * S * (M - 1) * k_i / el_i, 1),
+            "preint_device_ms_per_launch": round(fam_i["preint"][0] / k_i, 4),
+            "cpu_baseline": None,
         }
         print(json.dumps(line))
     if dist:

@@ -344,6 +344,22 @@ class Context:
                                                  d_nkept, fb_thresh, border, cam_w or w, cam_h or h,
                                                  C.byref(p)), "gvx_klt_fb_batch_dev")
 
+    def preint_integrate_dev(self, variant, prm, n_seg, d_imu, d_seg_off, d_state0, d_iewn, d_out, d_pn):
+        """Device-pointer preintegration batch (pointers as ints), async on the context stream."""
+        p = ImuParams(*prm)
+        self._check(self._L.gvx_preint_integrate_dev(self._h, variant, C.byref(p), n_seg, d_imu, d_seg_off,
+                                                     d_state0, d_iewn, d_out, d_pn), "gvx_preint_integrate_dev")
+
+    def preint_factor_eval_dev(self, n, d_pre, d_pn, d_pn_off, d_params, d_offs, d_res, d_jac):
+        """Device-pointer PreintegrationFactor batch, async on the context stream."""
+        self._check(self._L.gvx_preint_factor_eval_dev(self._h, n, d_pre, d_pn, d_pn_off, d_params, d_offs,
+                                                       d_res, d_jac), "gvx_preint_factor_eval_dev")
+
+    def reproj_eval_dev(self, n, d_consts, d_params, d_offs, d_res, d_jac):
+        """Device-pointer ReprojectionFactor batch, async on the context stream."""
+        self._check(self._L.gvx_reproj_eval_dev(self._h, n, d_consts, d_params, d_offs, d_res, d_jac),
+                    "gvx_reproj_eval_dev")
+
 
 def earth_iewn(origin, local) -> np.ndarray:
     """Earth::iewn(station, p) as PreintegrationEarth::resetState computes it."""
