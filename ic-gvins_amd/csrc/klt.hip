@@ -104,13 +104,13 @@ __device__ __forceinline__ void brow(const Plane& P, int off_al, uint32_t sh, in
     }
 }
 
+// BORDER_REFLECT_101 index, branchless: exact for -(2*len-2) <= p <= 3*len-3;
+// LK windows overshoot a level (> 21 px) by at most 26 px.
 __device__ __forceinline__ int refl(int p, int len) {
-    if ((unsigned)p < (unsigned)len) return p;
-    if (len == 1) return 0;
-    do {
-        p = p < 0 ? -p : 2 * len - 2 - p;
-    } while ((unsigned)p >= (unsigned)len);
-    return p;
+    int a = abs(p);
+    a = min(a, 2 * len - 2 - a);
+    a = abs(a);
+    return min(a, len - 1);
 }
 // Border windows of an unpadded plane (level 0 read in place): the wave gathers
 // its window -- rows y0 .. y0+rows-1, bytes x0 .. x0+31, REFLECT_101 outside
@@ -307,21 +307,25 @@ __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2
     }
 }
 
-// Exact wave-wide sum of per-lane values |v| < 2^28 (one 7-pixel unit of
-// products per lane): 14-bit halves keep both DPP reductions within int32.
-__device__ __forceinline__ int wave_total(int v) {
+// Exact wave-wide sums of per-lane values |v| < 2^28 (one 7-pixel unit of
+// products per lane).  The DPP chain leaves the total in lane 63.
+__device__ __forceinline__ int wave_dpp(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm 2,3,0,1
     v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
     v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);  // row_mirror
     v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1,3
     v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2,3
-    return __builtin_amdgcn_readlane(v, 63);
+    return v;
 }
-__device__ __forceinline__ long long wave_sum64(int v) {
-    const long long sh = (long long)wave_total(v >> 14);
-    const long long sl = (long long)wave_total(v & 0x3fff);
-    return sh * 16384 + sl;
+__device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_dpp(v), 63); }
+// (float) of the exact 64-bit sum, round-to-nearest-even: 14-bit halves keep
+// both DPP sums in int32; hi*2^14 + lo is exact in fp64 (|sum| < 2^35) and the
+// single fp64 -> fp32 conversion rounds once -- all on the VALU, one readlane.
+__device__ __forceinline__ float wave_sum_f32(int v) {
+    const int hi = wave_dpp(v >> 14), lo = wave_dpp(v & 0x3fff);
+    const double d = (double)hi * 16384.0 + (double)lo;
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, (float)d), 63));
 }
 
 // Window rows of one unit: 4 rows x 12 bytes of I for the extraction, 2 rows x
@@ -435,9 +439,9 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
             const bool interior = ipx >= 0 && ipx + WIN + 1 <= W && ipy >= 0 && ipy + WIN + 1 <= H;
             extract_unit(u, d, W, H, ipx, ipy, interior, W0, W1, a11, a12, a22);
         }
-        const float A11 = (float)wave_sum64(a11) * FLT_SCALE;
-        const float A12 = (float)wave_sum64(a12) * FLT_SCALE;
-        const float A22 = (float)wave_sum64(a22) * FLT_SCALE;
+        const float A11 = wave_sum_f32(a11) * FLT_SCALE;
+        const float A12 = wave_sum_f32(a12) * FLT_SCALE;
+        const float A22 = wave_sum_f32(a22) * FLT_SCALE;
         float D = A11 * A22 - A12 * A12;
         const float minEig =
             __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12), (float)(2 * WIN * WIN));
@@ -468,8 +472,8 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
                 match_unit<false>(u, r0, r1, J0, J1, b1, b2, es);
             }
             if (!u.valid) b1 = b2 = 0;
-            const float fb1 = (float)wave_sum64(b1) * FLT_SCALE;
-            const float fb2 = (float)wave_sum64(b2) * FLT_SCALE;
+            const float fb1 = wave_sum_f32(b1) * FLT_SCALE;
+            const float fb2 = wave_sum_f32(b2) * FLT_SCALE;
             const float dx = (A12 * fb2 - A22 * fb1) * D;
             const float dy = (A12 * fb1 - A11 * fb2) * D;
             nextx += dx;

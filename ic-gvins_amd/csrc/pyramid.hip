@@ -328,6 +328,312 @@ __global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ 
     if constexpr (STOP < 99) reinterpret_cast<uint32_t*>(pyr)[blockIdx.x * 256 + tid] = sink;
 }
 
+// ------------------------------------------------------- streaming pyrDown
+// Row-streaming build of NL levels (the production path).  One wavefront owns
+// a column strip of the source level and a band of rows, and walks the rows
+// with rolling registers: no LDS, no barriers.
+//   lane L loads 16 source bytes per row at x0 = 480*strip + 8L - 20 and makes
+//   the four level-1 outputs at columns 240*strip + 4(L-2) + {0..3} (horizontal
+//   [1 4 6 4 1] on v_dot4_u32_u8, vertical on packed u16);
+//   level 2 (two outputs per lane) and level 3 (one) take their horizontal
+//   neighbours from lanes L-1 / L+1 with DPP wave shifts, so valid results
+//   shrink by one lane per level and lanes 2..61 own the strip (480 source
+//   columns per strip, 7 % overlap).
+// Band b owns level-1 rows [64b, 64b+64) (level k: [64b, 64b+64) >> (k-1)).
+// Borders: source rows / columns are REFLECT_101-extended at load.  Because the
+// filter is symmetric, the extension of a level computed from an extended
+// source IS the REFLECT_101 extension of that level at the left / top edges;
+// at the right / bottom edges it is not when the level size is even, so the
+// columns >= w are re-gathered from their mirror lanes (ds_bpermute) and the
+// rows >= h are taken from their mirror rows in the rolling registers.
+constexpr int ST_COLS = 480;  // source columns owned per strip
+
+// Levels of at least RING_MIRROR_H rows get their top / bottom ring rows from
+// the streaming pass (each ring row is a single-bounce REFLECT_101 copy of one
+// interior row); shorter levels get the whole ring from ring_kernel.
+constexpr int RING_MIRROR_H = 2 * PAD + 2;
+// The top / bottom ring row that is the REFLECT_101 copy of row r (rows 1..PAD
+// -> -r, rows h-1-PAD..h-2 -> 2h-2-r), or r itself when none is.
+__device__ __forceinline__ int mirror_row(int r, int h) {
+    if (h < RING_MIRROR_H) return r;
+    if (r >= 1 && r <= PAD) return -r;
+    if (r >= h - 1 - PAD && r <= h - 2) return 2 * h - 2 - r;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane L <- lane L-1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane L <- lane L+1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_fetch(uint32_t v, int src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+// Edge bands: for every source row, the REFLECT_101-extended columns
+// [-32, 64) and [w-64, w+32) are stored in a padded plane (the pyramid's unused
+// level-0 slot on the batched path, the padded level 0 itself in the frame
+// cache).  Lanes whose 16-byte window leaves [48, w-48) read the band instead
+// of the source, so the streaming loop never gathers bytes: every row is one
+// 16-byte load per lane and the prefetched rows stay in flight.
+struct EdgePlane {
+    const uint8_t* base;  // pixel (0,0) of image 0
+    int64_t img_stride;
+    int pitch;
+};
+constexpr int EDGE_L = 64, EDGE_R = 64;  // band extents inside the image
+
+__device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pitch, const uint8_t* __restrict__ E,
+                                           int epitch, int w, int h, int x, int y) {
+    const int ry = refl(y, h);
+    const bool edge = x < EDGE_L - 16 || x + 16 > w - (EDGE_R - 16);
+    const int xc = min(x, w + 16);  // lanes past the band are never used: keep them in range
+    const uint8_t* p = edge ? E + (int64_t)ry * epitch + xc : S + (int64_t)ry * pitch + x;
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);  // 4-byte aligned
+    return make_uint4(q[0], q[1], q[2], q[3]);
+}
+
+// Fill the edge bands of n_img source images into the padded plane E: per row
+// six 16-byte chunks on each side.  Inside and outside chunks are separate item
+// ranges, so waves never mix paths: chunks inside the image are vector copies;
+// the two outside chunks per side are the byte-reversed
+// mirror ranges, built from aligned 16-byte loads and v_perm (w % 4 == 0; other
+// widths gather bytes).
+__global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ src, int64_t img_stride, int pitch,
+                                                   int w, int h, uint8_t* __restrict__ E, int64_t e_img_stride,
+                                                   int epitch) {
+    const int img = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= h * 12) return;
+    // items [0, 8h): the 8 chunks per row inside the image (row-major, so a wave
+    // reads 8 rows x 64 contiguous bytes per side); [8h, 12h): the 4 mirrored chunks
+    int q, y;
+    if (i < 8 * h) {
+        y = i >> 3;
+        q = (i & 7) < 4 ? (i & 7) + 2 : (i & 7) + 2;
+    } else {
+        const int j = i - 8 * h;
+        y = j >> 2;
+        q = (j & 3) < 2 ? (j & 3) : (j & 3) + 8;
+    }
+    const int x = q < 6 ? -32 + 16 * q : w - EDGE_R + 16 * (q - 6);
+    const uint8_t* row = src + img * img_stride + (int64_t)y * pitch;
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);  // 4-byte aligned rows
+    uint32_t d[4];
+    if (x >= 0 && x + 16 <= w) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = rw[(x >> 2) + k];
+    } else if (x < 0 && w >= 40) {
+        // columns x..x+15 mirror to -x .. -x-15 (descending): output dword k
+        // holds source bytes m-4k .. m-4k-3 with m = -x, a multiple of 16
+        const int m4 = (-x) >> 2;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = __builtin_amdgcn_perm(rw[m4 - k], rw[m4 - k - 1], 0x01020304u);
+    } else if (x >= w && (w & 3) == 0 && w >= 40) {
+        // columns x..x+15 mirror to 2w-2-x .. 2w-17-x (descending)
+        const int m4 = (2 * w - 2 - x) >> 2;  // dword holding the first source byte (its byte 2)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = __builtin_amdgcn_perm(rw[m4 - k], rw[m4 - k - 1], 0x03040506u);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t t = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) t |= (uint32_t)row[refl(x + 4 * k + b, w)] << (8 * b);
+            d[k] = t;
+        }
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(E + img * e_img_stride + (int64_t)y * epitch + x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = d[k];
+}
+
+// four level-1 horizontal sums (u16 pairs) from the lane's 16 bytes (outputs
+// read bytes 2+2j .. 6+2j)
+__device__ __forceinline__ uint2 hsum_row(uint4 r) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    return hsum4<2>(w, 0);
+}
+// Replace the bytes of `v` (NB bytes per lane, lane column base c0 + NB*(L-2))
+// whose columns are >= w by their REFLECT_101 mirrors 2w-2-c.
+template <int NB>
+__device__ __forceinline__ uint32_t fix_right(uint32_t v, int lane, int c0, int w) {
+    uint32_t out = v;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int c = c0 + NB * (lane - 2) + b;
+        const int m = 2 * w - 2 - c;  // mirror column (valid when c >= w)
+        const int rel = m - c0;
+        const int sl = c >= w ? (rel >= 0 ? rel / NB : -((-rel + NB - 1) / NB)) + 2 : lane;
+        const int sb = c >= w ? rel - NB * (sl - 2) : b;
+        const uint32_t src = lane_fetch(v, sl < 0 ? 0 : (sl > 63 ? 63 : sl));
+        const uint32_t byte = (src >> (8 * sb)) & 0xffu;
+        out = c >= w ? ((out & ~(0xffu << (8 * b))) | (byte << (8 * b))) : out;
+    }
+    return out;
+}
+
+template <int NL>
+__global__ void __launch_bounds__(256) stream_kernel(const uint8_t* __restrict__ src, int64_t src_img_stride,
+                                                     int src_pitch, int w0, int h0, EdgePlane ep,
+                                                     uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
+                                                     int n_strips, int n_bands, int n_units) {
+    const int lane = threadIdx.x & 63;
+    const int nblk = (n_units + 3) / 4;
+    const int unit = xcd_swizzle(blockIdx.x, nblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (unit >= n_units) return;
+    const int st = unit % n_strips, rest = unit / n_strips;
+    const int bd = rest % n_bands, img = rest / n_bands;
+    const uint8_t* S = src + img * src_img_stride;
+    const uint8_t* E = ep.base + img * ep.img_stride;
+    uint8_t* P = pyr + img * pyr_bytes;
+    const int x0 = ST_COLS * st + 8 * lane - 20;  // this lane's 16 source bytes
+    const bool own_lane = lane >= 2 && lane < 62;
+    const int w1 = L.w[0], h1 = L.h[0], p1 = L.pitch[0];
+    const int c1 = (ST_COLS / 2) * st;            // level-1 column of lane 2, byte 0
+    const bool fix1 = NL > 1 && c1 + 4 * 62 > w1;  // strip reaches past the right edge
+    int w2 = 0, h2 = 0, p2 = 0, c2 = 0, w3 = 0, h3 = 0, p3 = 0, c3 = 0;
+    bool fix2 = false;
+    if (NL > 1) {
+        w2 = L.w[1], h2 = L.h[1], p2 = L.pitch[1], c2 = (ST_COLS / 4) * st;
+        fix2 = NL > 2 && c2 + 2 * 62 > w2;
+    }
+    if (NL > 2) w3 = L.w[2], h3 = L.h[2], p3 = L.pitch[2], c3 = (ST_COLS / 8) * st;
+    // level-1 rows walked: everything the band's deepest owned rows depend on
+    const int r1s = 64 * bd - (NL == 3 ? 6 : NL == 2 ? 2 : 0);
+    const int n1 = 64 + (NL == 3 ? 9 : NL == 2 ? 3 : 0);  // rows r1s .. r1s+n1-1
+    const int o1lo = 64 * bd, o1hi = min(64 * bd + 64, h1);
+    const int o2lo = 32 * bd, o2hi = NL > 1 ? min(32 * bd + 32, h2) : 0;
+    const int o3lo = 16 * bd, o3hi = NL > 2 ? min(16 * bd + 16, h3) : 0;
+
+    // rolling state: horizontal sums of source rows 2r1-2 .. 2r1+2 (hr[0..4]),
+    // level-2 horizontal sums of level-1 rows (g2[0..4], newest last), level-3
+    // horizontal sums of level-2 rows (g3[0..4])
+    uint2 hr[5];
+    uint32_t g2[5] = {0, 0, 0, 0, 0}, g3[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * r1s - 2 + k));
+    // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % 4;
+    // they are fetched PF iterations ahead (6 rows x 1 KB in flight per wave)
+    constexpr int PF = 3;
+    uint4 pa[4], pb[4];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        pa[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 1);
+        pb[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 2);
+    }
+    int n2 = 0;  // level-2 rows produced so far
+    auto body = [&](int k, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
+        const int r1 = r1s + k;
+        hr[3] = hsum_row(pa[slot]);
+        hr[4] = hsum_row(pb[slot]);
+        if (k + PF < n1) {
+            pa[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 1);
+            pb[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 2);
+        }
+        // level-1 row r1
+        uint32_t l1 = hibytes(vsum2(hr[0].x, hr[1].x, hr[2].x, hr[3].x, hr[4].x),
+                              vsum2(hr[0].y, hr[1].y, hr[2].y, hr[3].y, hr[4].y));
+        hr[0] = hr[2];
+        hr[1] = hr[3];
+        hr[2] = hr[4];
+        if (fix1) l1 = fix_right<4>(l1, lane, c1, w1);
+        if (r1 >= o1lo && r1 < o1hi && own_lane && c1 + 4 * (lane - 2) < w1) {
+            uint8_t* q = P + L.off[0] + c1 + 4 * (lane - 2) + PAD;
+            *reinterpret_cast<uint32_t*>(q + (int64_t)(r1 + PAD) * p1) = l1;
+            const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
+            if (mr != r1) *reinterpret_cast<uint32_t*>(q + (int64_t)(mr + PAD) * p1) = l1;
+        }
+        if constexpr (NL > 1) {
+            // level-2 horizontal sums of level-1 row r1 (rows >= h1 mirror rows
+            // 2h1-2-r1, which are 2 / 4 rows back)
+            uint32_t g;
+            if (r1 < h1) {
+                const uint32_t pv = wave_shr1(l1), nx = wave_shl1(l1);
+                const uint32_t a = __builtin_amdgcn_perm(l1, pv, 0x05040302u);  // prev.b2 prev.b3 l1.b0 l1.b1
+                const uint32_t o0 = __builtin_amdgcn_udot4(a, 0x04060401u, (l1 >> 16) & 0xffu, false);
+                const uint32_t o1 = __builtin_amdgcn_udot4(l1, 0x04060401u, nx & 0xffu, false);
+                g = o0 | (o1 << 16);
+            } else {
+                g = r1 == h1 ? g2[3] : g2[1];
+            }
+            g2[0] = g2[1];
+            g2[1] = g2[2];
+            g2[2] = g2[3];
+            g2[3] = g2[4];
+            g2[4] = g;
+            // level-2 row r2 = (r1-2)/2 once level-1 rows r1-4 .. r1 are in
+            if (k >= 4 && ((slot & 1) == 0)) {
+                const int r2 = (r1 - 2) >> 1;
+                const uint32_t v = vsum2(g2[0], g2[1], g2[2], g2[3], g2[4]);
+                uint32_t l2 = __builtin_amdgcn_perm(0u, v, 0x0c0c0301u);  // (s+128)>>8 of both halves
+                if (fix2) l2 = fix_right<2>(l2, lane, c2, w2);
+                if (r2 >= o2lo && r2 < o2hi && own_lane && c2 + 2 * (lane - 2) < w2) {
+                    uint8_t* q = P + L.off[1] + c2 + 2 * (lane - 2) + PAD;
+                    *reinterpret_cast<uint16_t*>(q + (int64_t)(r2 + PAD) * p2) = (uint16_t)l2;
+                    const int mr = mirror_row(r2, h2);
+                    if (mr != r2) *reinterpret_cast<uint16_t*>(q + (int64_t)(mr + PAD) * p2) = (uint16_t)l2;
+                }
+                if constexpr (NL > 2) {
+                    uint32_t g;
+                    if (r2 < h2) {
+                        const uint32_t pv = wave_shr1(l2), nx = wave_shl1(l2);
+                        const uint32_t a = __builtin_amdgcn_perm(l2, pv, 0x05040100u);  // prev.b0 prev.b1 l2.b0 l2.b1
+                        g = __builtin_amdgcn_udot4(a, 0x04060401u, nx & 0xffu, false);
+                    } else {
+                        g = r2 == h2 ? g3[3] : g3[1];
+                    }
+                    g3[0] = g3[1];
+                    g3[1] = g3[2];
+                    g3[2] = g3[3];
+                    g3[3] = g3[4];
+                    g3[4] = g;
+                    // level-3 row r3 = (r2-2)/2 once level-2 rows r2-4 .. r2 are in
+                    ++n2;
+                    if (n2 >= 5 && ((n2 & 1) == 1)) {
+                        const int r3 = (r2 - 2) >> 1;
+                        const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
+                        if (r3 >= o3lo && r3 < o3hi && own_lane && c3 + (lane - 2) < w3) {
+                            uint8_t* q = P + L.off[2] + c3 + (lane - 2) + PAD;
+                            q[(int64_t)(r3 + PAD) * p3] = (uint8_t)(s3 >> 8);
+                            const int mr = mirror_row(r3, h3);
+                            if (mr != r3) q[(int64_t)(mr + PAD) * p3] = (uint8_t)(s3 >> 8);
+                        }
+                    }
+                }
+            }
+        }
+    };
+    // r1s is even and the slot tracks k % 4, so the level-2 parity is static
+    for (int k = 0; k < n1; k += 4) {
+        body(k, std::integral_constant<int, 0>{});
+        if (k + 1 < n1) body(k + 1, std::integral_constant<int, 1>{});
+        if (k + 2 < n1) body(k + 2, std::integral_constant<int, 2>{});
+        if (k + 3 < n1) body(k + 3, std::integral_constant<int, 3>{});
+    }
+}
+
+template <int NL>
+void launch_stream(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int src_pitch, int src_w, int src_h,
+                   const EdgePlane& ep, int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
+    DownLevels D{};
+    for (int k = 0; k < NL; ++k) {
+        D.off[k] = lay.off[l0 + 1 + k];
+        D.pitch[k] = lay.pitch[l0 + 1 + k];
+        D.w[k] = lay.w[l0 + 1 + k];
+        D.h[k] = lay.h[l0 + 1 + k];
+    }
+    const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
+    const int n_bands = (D.h[0] + 63) / 64;
+    const int n_units = n_strips * n_bands * n_img;
+    const int nblk = (n_units + 3) / 4;
+    hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, src_img_stride,
+                       src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units);
+}
+
+
 // ------------------------------------------------------------------ rings
 // REFLECT_101 rings of levels lo..hi of every image in one launch.  Item = one
 // dword of ring: the top / bottom PAD rows over the padded width, then per
@@ -340,9 +646,15 @@ struct RingLevels {
     int32_t dw[MAX_LEVELS];     // dwords per padded row (top/bottom bands)
     int32_t rd0[MAX_LEVELS];    // first dword (padded col / 4) of the right band
     int32_t rdn[MAX_LEVELS];    // dwords of the right band
+    int32_t sides[MAX_LEVELS];  // 1: top/bottom rows already written (side bands only)
     int32_t items[MAX_LEVELS];  // ring dwords of the level
 };
 
+// Item = one dword of ring.  Full ring: the top / bottom PAD rows over the
+// padded width, then the side bands of the interior rows.  Side-bands-only
+// levels: the left PAD columns and the right columns [w, w+PAD) of every padded
+// row (ring rows included: their sources are interior pixels).  Bytes of the
+// last interior dword of a row rewrite their own value.
 __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes, RingLevels R) {
     const int l = blockIdx.z;  // level slot (wave-uniform)
     int j = blockIdx.x * 256 + threadIdx.x;
@@ -350,7 +662,7 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
     const int w = R.w[l], h = R.h[l], pitch = R.pitch[l];
     uint8_t* base = pyr + (int64_t)blockIdx.y * pyr_bytes + R.off[l];
     int prow, pcol;  // padded row, padded byte column of the dword
-    const int nb = 2 * PAD * R.dw[l];
+    const int nb = R.sides[l] ? 0 : 2 * PAD * R.dw[l];
     if (j < nb) {
         const int r = j / R.dw[l];
         prow = r < PAD ? r : h + r;
@@ -359,7 +671,7 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
         j -= nb;
         const int per = PAD / 4 + R.rdn[l];
         const int r = j / per, c = j - r * per;
-        prow = PAD + r;
+        prow = R.sides[l] ? r : PAD + r;
         pcol = c < PAD / 4 ? 4 * c : 4 * (R.rd0[l] + c - PAD / 4);
     }
     const int sy = refl(prow - PAD, h) + PAD;
@@ -402,6 +714,30 @@ void launch_fused(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int sr
                        src_w, src_h, vec16, dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
 }
 
+// Rings of levels lo..hi.  sides_only: the streaming pass already wrote the
+// top / bottom ring rows of every level tall enough (RING_MIRROR_H).
+void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst, bool sides_only) {
+    RingLevels R{};
+    R.n = hi - lo + 1;
+    int most = 0;
+    for (int k = 0; k < R.n; ++k) {
+        const int lv = lo + k, w = lay.w[lv];
+        R.off[k] = lay.off[lv];
+        R.pitch[k] = lay.pitch[lv];
+        R.w[k] = w;
+        R.h[k] = lay.h[lv];
+        R.dw[k] = (w + 2 * PAD + 3) / 4;
+        R.rd0[k] = (w + PAD) / 4;
+        R.rdn[k] = (w + 2 * PAD + 3) / 4 - R.rd0[k];
+        R.sides[k] = sides_only && lay.h[lv] >= RING_MIRROR_H;
+        R.items[k] = R.sides[k] ? (lay.h[lv] + 2 * PAD) * (PAD / 4 + R.rdn[k])
+                                : 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
+        most = R.items[k] > most ? R.items[k] : most;
+    }
+    dim3 grid((most + 255) / 256, n_img, R.n);
+    hipLaunchKernelGGL(ring_kernel, grid, dim3(256), 0, c->stream, dst, lay.bytes, R);
+}
+
 }  // namespace
 
 PyrLayout make_layout(int w, int h, int max_level, int win) {
@@ -429,53 +765,45 @@ PyrLayout make_layout(int w, int h, int max_level, int win) {
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride, int n_img,
                                  const PyrLayout& lay, uint8_t* dst, bool write_l0) {
     if (n_img <= 0) return hipSuccess;
+    // level-0 slot of the pyramid: pixel (0,0) of image 0
+    uint8_t* slot0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
+    const bool aligned = stride % 4 == 0 && img_stride % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 4 == 0;
     const uint8_t* s0 = src;
     int64_t s0_img = img_stride;
     int s0_pitch = stride;
-    if (write_l0) {
+    if (write_l0 || !aligned) {
+        // full padded level-0 copy: the source of the build and its own edge plane
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
         const int items = groups * (lay.h[0] + 2 * PAD);
         dim3 grid((items + 255) / 256, n_img);
         hipLaunchKernelGGL(level0_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride, lay.w[0],
                            lay.h[0], lay.pitch[0], lay.bytes, dst);
-        // build the other levels from the aligned padded copy
-        s0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
+        s0 = slot0;
         s0_img = lay.bytes;
         s0_pitch = lay.pitch[0];
+    } else {
+        // read level 0 in place; only its edge bands go to the (otherwise unused) slot
+        dim3 grid((lay.h[0] * 12 + 255) / 256, n_img);
+        hipLaunchKernelGGL(edge_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride, lay.w[0], lay.h[0],
+                           slot0, lay.bytes, lay.pitch[0]);
     }
-    // levels 1.. in fused passes of up to 3 levels
+    // levels 1.. in streaming passes of up to 3 levels; a later pass reads the
+    // previous pass's deepest level (padded, its ring built first)
     int l = 0;
     while (l + 1 < lay.nlev) {
         const int nl = lay.nlev - 1 - l >= 3 ? 3 : lay.nlev - 1 - l;
         const uint8_t* s = l == 0 ? s0 : dst + lay.off[l] + (int64_t)PAD * lay.pitch[l] + PAD;
         const int64_t si = l == 0 ? s0_img : lay.bytes;
         const int sp = l == 0 ? s0_pitch : lay.pitch[l];
+        const EdgePlane ep = l == 0 ? EdgePlane{slot0, lay.bytes, lay.pitch[0]} : EdgePlane{s, lay.bytes, sp};
         if (nl == 3)
-            launch_fused<3>(c, s, si, sp, lay.w[l], lay.h[l], n_img, lay, l, dst);
+            launch_stream<3>(c, s, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
         else if (nl == 2)
-            launch_fused<2>(c, s, si, sp, lay.w[l], lay.h[l], n_img, lay, l, dst);
+            launch_stream<2>(c, s, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
         else
-            launch_fused<1>(c, s, si, sp, lay.w[l], lay.h[l], n_img, lay, l, dst);
+            launch_stream<1>(c, s, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
+        launch_rings(c, n_img, lay, l + 1, l + nl, dst, true);
         l += nl;
-    }
-    if (lay.nlev > 1) {
-        RingLevels R{};
-        R.n = lay.nlev - 1;
-        int most = 0;
-        for (int k = 0; k < R.n; ++k) {
-            const int lv = k + 1, w = lay.w[lv];
-            R.off[k] = lay.off[lv];
-            R.pitch[k] = lay.pitch[lv];
-            R.w[k] = w;
-            R.h[k] = lay.h[lv];
-            R.dw[k] = (w + 2 * PAD + 3) / 4;
-            R.rd0[k] = (w + PAD) / 4;
-            R.rdn[k] = (w + 2 * PAD + 3) / 4 - R.rd0[k];
-            R.items[k] = 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
-            most = R.items[k] > most ? R.items[k] : most;
-        }
-        dim3 grid((most + 255) / 256, n_img, R.n);
-        hipLaunchKernelGGL(ring_kernel, grid, dim3(256), 0, c->stream, dst, lay.bytes, R);
     }
     return hipGetLastError();
 }
