@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ 
 //   neighbours from lanes L-1 / L+1 with DPP wave shifts, so valid results
 //   shrink by one lane per level and lanes 2..61 own the strip (480 source
 //   columns per strip, 7 % overlap).
-// Band b owns level-1 rows [64b, 64b+64) (level k: [64b, 64b+64) >> (k-1)).
+// Band b owns level-1 rows [BAND*b, BAND*(b+1)) (level k: the same >> (k-1)).
 // Borders: source rows / columns are REFLECT_101-extended at load.  Because the
 // filter is symmetric, the extension of a level computed from an extended
 // source IS the REFLECT_101 extension of that level at the left / top edges;
@@ -347,6 +347,7 @@ __global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ 
 // columns >= w are re-gathered from their mirror lanes (ds_bpermute) and the
 // rows >= h are taken from their mirror rows in the rolling registers.
 constexpr int ST_COLS = 480;  // source columns owned per strip
+constexpr int BAND = 32;      // level-1 rows owned per band (level k: BAND >> (k-1))
 
 // Levels of at least RING_MIRROR_H rows get their top / bottom ring rows from
 // the streaming pass (each ring row is a single-bounce REFLECT_101 copy of one
@@ -366,9 +367,6 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane L <- lane L
 }
 __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane L <- lane L+1
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint32_t lane_fetch(uint32_t v, int src_lane) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
 
 // Edge bands: for every source row, the REFLECT_101-extended columns
@@ -455,30 +453,47 @@ __device__ __forceinline__ uint2 hsum_row(uint4 r) {
     const uint32_t w[4] = {r.x, r.y, r.z, r.w};
     return hsum4<2>(w, 0);
 }
-// Replace the bytes of `v` (NB bytes per lane, lane column base c0 + NB*(L-2))
-// whose columns are >= w by their REFLECT_101 mirrors 2w-2-c.
-template <int NB>
-__device__ __forceinline__ uint32_t fix_right(uint32_t v, int lane, int c0, int w) {
-    uint32_t out = v;
+// Right-edge fix-up.  The next level's taps read this level at most two
+// columns past its width w (columns w and w+1); their REFLECT_101 values are
+// columns w-2 and w-3, which lie in this lane or the one / two lanes to the
+// left.  The pass gathers them with DPP wave shifts and one v_perm whose
+// per-lane selector is fixed for the whole strip.  Columns further out are
+// never read and may hold anything.
+// Level 1 (4 bytes per lane, lane column base c1 + 4(L-2)): window = the lane
+// to the left (perm bytes 0..3) and this lane (4..7).
+__device__ __forceinline__ uint32_t fix_sel4(int lane, int c0, int w) {
+    const int base = c0 + 4 * (lane - 2);
+    uint32_t sel = 0;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int c = c0 + NB * (lane - 2) + b;
-        const int m = 2 * w - 2 - c;  // mirror column (valid when c >= w)
-        const int rel = m - c0;
-        const int sl = c >= w ? (rel >= 0 ? rel / NB : -((-rel + NB - 1) / NB)) + 2 : lane;
-        const int sb = c >= w ? rel - NB * (sl - 2) : b;
-        const uint32_t src = lane_fetch(v, sl < 0 ? 0 : (sl > 63 ? 63 : sl));
-        const uint32_t byte = (src >> (8 * sb)) & 0xffu;
-        out = c >= w ? ((out & ~(0xffu << (8 * b))) | (byte << (8 * b))) : out;
+    for (int b = 0; b < 4; ++b) {
+        const int c = base + b;
+        const int idx = c < w ? 4 + b : min(max(2 * w - 2 - c - base + 4, 0), 7);
+        sel |= (uint32_t)idx << (8 * b);
     }
-    return out;
+    return sel;
+}
+// Level 2 (2 bytes per lane in the low half): window = lanes L-2 (perm bytes
+// 0,1), L-1 (2,3) and this lane (4,5).
+__device__ __forceinline__ uint32_t fix_sel2(int lane, int c0, int w) {
+    const int base = c0 + 2 * (lane - 2);
+    uint32_t sel = 0x0c0c0000u;  // bytes 2,3 of the result: zero
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int c = base + b;
+        const int idx = c < w ? 4 + b : min(max(2 * w - 2 - c - base + 4, 0), 5);
+        sel |= (uint32_t)idx << (8 * b);
+    }
+    return sel;
 }
 
-template <int NL>
-__global__ void __launch_bounds__(256) stream_kernel(const uint8_t* __restrict__ src, int64_t src_img_stride,
+// SKIP (tools/pyr_micro.hip only): bit k-1 set = level-k outputs are folded
+// into a register instead of stored (to time the store traffic).
+template <int NL, int SKIP = 0>
+__global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restrict__ src, int64_t src_img_stride,
                                                      int src_pitch, int w0, int h0, EdgePlane ep,
                                                      uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
-                                                     int n_strips, int n_bands, int n_units) {
+                                                     int n_strips, int n_bands, int n_units,
+                                                     uint8_t* __restrict__ trash) {
     const int lane = threadIdx.x & 63;
     const int nblk = (n_units + 3) / 4;
     const int unit = xcd_swizzle(blockIdx.x, nblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -500,12 +515,14 @@ __global__ void __launch_bounds__(256) stream_kernel(const uint8_t* __restrict__
         fix2 = NL > 2 && c2 + 2 * 62 > w2;
     }
     if (NL > 2) w3 = L.w[2], h3 = L.h[2], p3 = L.pitch[2], c3 = (ST_COLS / 8) * st;
+    const uint32_t sel1 = fix1 ? fix_sel4(lane, c1, w1) : 0u;
+    const uint32_t sel2 = fix2 ? fix_sel2(lane, c2, w2) : 0u;
     // level-1 rows walked: everything the band's deepest owned rows depend on
-    const int r1s = 64 * bd - (NL == 3 ? 6 : NL == 2 ? 2 : 0);
-    const int n1 = 64 + (NL == 3 ? 9 : NL == 2 ? 3 : 0);  // rows r1s .. r1s+n1-1
-    const int o1lo = 64 * bd, o1hi = min(64 * bd + 64, h1);
-    const int o2lo = 32 * bd, o2hi = NL > 1 ? min(32 * bd + 32, h2) : 0;
-    const int o3lo = 16 * bd, o3hi = NL > 2 ? min(16 * bd + 16, h3) : 0;
+    const int r1s = BAND * bd - (NL == 3 ? 6 : NL == 2 ? 2 : 0);
+    const int n1 = BAND + (NL == 3 ? 9 : NL == 2 ? 3 : 0);  // rows r1s .. r1s+n1-1
+    const int o1lo = BAND * bd, o1hi = min(BAND * bd + BAND, h1);
+    const int o2lo = BAND / 2 * bd, o2hi = NL > 1 ? min(BAND / 2 * bd + BAND / 2, h2) : 0;
+    const int o3lo = BAND / 4 * bd, o3hi = NL > 2 ? min(BAND / 4 * bd + BAND / 4, h3) : 0;
 
     // rolling state: horizontal sums of source rows 2r1-2 .. 2r1+2 (hr[0..4]),
     // level-2 horizontal sums of level-1 rows (g2[0..4], newest last), level-3
@@ -515,36 +532,46 @@ __global__ void __launch_bounds__(256) stream_kernel(const uint8_t* __restrict__
 #pragma unroll
     for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * r1s - 2 + k));
     // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % 4;
-    // they are fetched PF iterations ahead (6 rows x 1 KB in flight per wave)
-    constexpr int PF = 3;
+    // they are fetched PF iterations ahead (4 rows x 1 KB in flight per wave; PF = 2
+    // keeps the kernel at 64 VGPRs, 8 waves per SIMD: every unit resident at once)
+    constexpr int PF = 2;
     uint4 pa[4], pb[4];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         pa[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 1);
         pb[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 2);
     }
-    int n2 = 0;  // level-2 rows produced so far
+    // Every load and store below is issued unconditionally: on gfx9 stores and
+    // loads share vmcnt, and a store skipped by a branch would make the compiler
+    // wait for all earlier stores before using a prefetched row.  Outputs that
+    // are not owned (rows outside the band, lanes 0/1/62/63, columns past the
+    // level, the schedule's warm-up rows) go to this lane's dword of a trash line.
+    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
+    uint32_t nsink = 0;
     auto body = [&](int k, auto slot_c) {
         constexpr int slot = decltype(slot_c)::value;
         const int r1 = r1s + k;
         hr[3] = hsum_row(pa[slot]);
         hr[4] = hsum_row(pb[slot]);
-        if (k + PF < n1) {
-            pa[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 1);
-            pb[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 2);
-        }
+        pa[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 1);
+        pb[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 2);
         // level-1 row r1
         uint32_t l1 = hibytes(vsum2(hr[0].x, hr[1].x, hr[2].x, hr[3].x, hr[4].x),
                               vsum2(hr[0].y, hr[1].y, hr[2].y, hr[3].y, hr[4].y));
         hr[0] = hr[2];
         hr[1] = hr[3];
         hr[2] = hr[4];
-        if (fix1) l1 = fix_right<4>(l1, lane, c1, w1);
-        if (r1 >= o1lo && r1 < o1hi && own_lane && c1 + 4 * (lane - 2) < w1) {
+        if (fix1) l1 = __builtin_amdgcn_perm(l1, wave_shr1(l1), sel1);
+        {
+            const bool ok = r1 >= o1lo && r1 < o1hi && own_lane && c1 + 4 * (lane - 2) < w1;
             uint8_t* q = P + L.off[0] + c1 + 4 * (lane - 2) + PAD;
-            *reinterpret_cast<uint32_t*>(q + (int64_t)(r1 + PAD) * p1) = l1;
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
-            if (mr != r1) *reinterpret_cast<uint32_t*>(q + (int64_t)(mr + PAD) * p1) = l1;
+            if constexpr ((SKIP & 1) != 0) {
+                nsink ^= l1;
+            } else {
+                *reinterpret_cast<uint32_t*>(ok ? q + (int64_t)(r1 + PAD) * p1 : tl) = l1;
+                *reinterpret_cast<uint32_t*>(ok && mr != r1 ? q + (int64_t)(mr + PAD) * p1 : tl) = l1;
+            }
         }
         if constexpr (NL > 1) {
             // level-2 horizontal sums of level-1 row r1 (rows >= h1 mirror rows
@@ -564,17 +591,26 @@ __global__ void __launch_bounds__(256) stream_kernel(const uint8_t* __restrict__
             g2[2] = g2[3];
             g2[3] = g2[4];
             g2[4] = g;
-            // level-2 row r2 = (r1-2)/2 once level-1 rows r1-4 .. r1 are in
-            if (k >= 4 && ((slot & 1) == 0)) {
+            // level-2 row r2 = (r1-2)/2 at every even k (rows before k = 4 are
+            // warm-up garbage and go to the trash line)
+            if constexpr ((slot & 1) == 0) {
                 const int r2 = (r1 - 2) >> 1;
                 const uint32_t v = vsum2(g2[0], g2[1], g2[2], g2[3], g2[4]);
                 uint32_t l2 = __builtin_amdgcn_perm(0u, v, 0x0c0c0301u);  // (s+128)>>8 of both halves
-                if (fix2) l2 = fix_right<2>(l2, lane, c2, w2);
-                if (r2 >= o2lo && r2 < o2hi && own_lane && c2 + 2 * (lane - 2) < w2) {
+                if (fix2) {
+                    const uint32_t a1 = wave_shr1(l2), a2 = wave_shr1(a1);
+                    l2 = __builtin_amdgcn_perm(l2, (a2 & 0xffffu) | (a1 << 16), sel2);
+                }
+                {
+                    const bool ok = k >= 4 && r2 >= o2lo && r2 < o2hi && own_lane && c2 + 2 * (lane - 2) < w2;
                     uint8_t* q = P + L.off[1] + c2 + 2 * (lane - 2) + PAD;
-                    *reinterpret_cast<uint16_t*>(q + (int64_t)(r2 + PAD) * p2) = (uint16_t)l2;
                     const int mr = mirror_row(r2, h2);
-                    if (mr != r2) *reinterpret_cast<uint16_t*>(q + (int64_t)(mr + PAD) * p2) = (uint16_t)l2;
+                    if constexpr ((SKIP & 2) != 0) {
+                        nsink ^= l2 << 7;
+                    } else {
+                        *reinterpret_cast<uint16_t*>(ok ? q + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
+                        *reinterpret_cast<uint16_t*>(ok && mr != r2 ? q + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
+                    }
                 }
                 if constexpr (NL > 2) {
                     uint32_t g;
@@ -590,29 +626,34 @@ __global__ void __launch_bounds__(256) stream_kernel(const uint8_t* __restrict__
                     g3[2] = g3[3];
                     g3[3] = g3[4];
                     g3[4] = g;
-                    // level-3 row r3 = (r2-2)/2 once level-2 rows r2-4 .. r2 are in
-                    ++n2;
-                    if (n2 >= 5 && ((n2 & 1) == 1)) {
+                    // level-3 row r3 = (r2-2)/2 at every k = 0 (mod 4); valid from
+                    // k = 12, when level-2 rows r2-4 .. r2 (k = 4..12) are in
+                    if constexpr (slot == 0) {
                         const int r3 = (r2 - 2) >> 1;
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
-                        if (r3 >= o3lo && r3 < o3hi && own_lane && c3 + (lane - 2) < w3) {
-                            uint8_t* q = P + L.off[2] + c3 + (lane - 2) + PAD;
-                            q[(int64_t)(r3 + PAD) * p3] = (uint8_t)(s3 >> 8);
-                            const int mr = mirror_row(r3, h3);
-                            if (mr != r3) q[(int64_t)(mr + PAD) * p3] = (uint8_t)(s3 >> 8);
+                        const bool ok = k >= 12 && r3 >= o3lo && r3 < o3hi && own_lane && c3 + (lane - 2) < w3;
+                        uint8_t* q = P + L.off[2] + c3 + (lane - 2) + PAD;
+                        const int mr = mirror_row(r3, h3);
+                        if constexpr ((SKIP & 4) != 0) {
+                            nsink ^= s3 << 13;
+                        } else {
+                            *(ok ? q + (int64_t)(r3 + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
+                            *(ok && mr != r3 ? q + (int64_t)(mr + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
                         }
                     }
                 }
             }
         }
     };
-    // r1s is even and the slot tracks k % 4, so the level-2 parity is static
+    // r1s is even and the slot tracks k % 4, so the level-2 / level-3 schedule
+    // is static; the trip count is rounded up to whole groups of four rows
     for (int k = 0; k < n1; k += 4) {
         body(k, std::integral_constant<int, 0>{});
-        if (k + 1 < n1) body(k + 1, std::integral_constant<int, 1>{});
-        if (k + 2 < n1) body(k + 2, std::integral_constant<int, 2>{});
-        if (k + 3 < n1) body(k + 3, std::integral_constant<int, 3>{});
+        body(k + 1, std::integral_constant<int, 1>{});
+        body(k + 2, std::integral_constant<int, 2>{});
+        body(k + 3, std::integral_constant<int, 3>{});
     }
+    if constexpr (SKIP != 0) *reinterpret_cast<uint32_t*>(tl) = nsink;
 }
 
 template <int NL>
@@ -626,11 +667,12 @@ void launch_stream(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int s
         D.h[k] = lay.h[l0 + 1 + k];
     }
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
-    const int n_bands = (D.h[0] + 63) / 64;
+    const int n_bands = (D.h[0] + BAND - 1) / BAND;
     const int n_units = n_strips * n_bands * n_img;
     const int nblk = (n_units + 3) / 4;
+    uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
     hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, src_img_stride,
-                       src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units);
+                       src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units, trash);
 }
 
 

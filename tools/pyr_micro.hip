@@ -1,5 +1,6 @@
-// Phase timing of the fused pyramid pass (diagnostics, not part of libgvx):
-// 256 random 1280x560 images, fused_kernel<3, STOP> for every truncation point.
+// Phase timing of the pyramid passes (diagnostics, not part of libgvx):
+// 256 random 1280x560 images; the streaming pass with and without its stores,
+// the edge-band and ring kernels, and a plain streaming read of the same bytes.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off
 //        -I include -I ic-gvins_amd/csrc tools/pyr_micro.hip -o tools/pyr_micro
 #include "../ic-gvins_amd/csrc/pyramid.hip"
@@ -8,6 +9,10 @@
 #include <vector>
 
 using namespace gvx;
+
+namespace gvx {
+void* scratch(gvx_ctx*, const std::string&, size_t) { return nullptr; }
+}
 
 __global__ void read_all(const uint4* __restrict__ p, size_t n16, uint32_t* sink) {
     uint32_t acc = 0;
@@ -18,42 +23,14 @@ __global__ void read_all(const uint4* __restrict__ p, size_t n16, uint32_t* sink
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
-float time_read(const uint8_t* src, size_t bytes, uint32_t* sink, int blocks, int reps) {
+template <class F>
+float timeit(F f, int reps) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    read_all<<<blocks, 256>>>((const uint4*)src, bytes / 16, sink);
+    for (int i = 0; i < 3; ++i) f();
     hipEventRecord(a);
-    for (int i = 0; i < reps; ++i) read_all<<<blocks, 256>>>((const uint4*)src, bytes / 16, sink);
-    hipEventRecord(b);
-    hipEventSynchronize(b);
-    float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
-    return 1000.f * ms / reps;
-}
-
-template <int STOP>
-float run(const uint8_t* src, uint8_t* dst, const PyrLayout& lay, int n_img, int n_cu, int reps) {
-    DownLevels D{};
-    for (int k = 0; k < 3; ++k) {
-        D.off[k] = lay.off[1 + k];
-        D.pitch[k] = lay.pitch[1 + k];
-        D.w[k] = lay.w[1 + k];
-        D.h[k] = lay.h[1 + k];
-    }
-    const int w = lay.w[0], h = lay.h[0];
-    const int tiles_x = (w + 127) / 128, tiles_y = (h + 63) / 64, n_tiles = tiles_x * tiles_y * n_img;
-    const int slots = n_cu * 5, per_wg = (n_tiles + slots - 1) / slots, n_wg = (n_tiles + per_wg - 1) / per_wg;
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    for (int i = 0; i < 3; ++i)
-        hipLaunchKernelGGL((fused_kernel<3, STOP>), dim3(N_XCD * xcd_per(n_wg)), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, 1,
-                           dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
-    hipEventRecord(a);
-    for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((fused_kernel<3, STOP>), dim3(N_XCD * xcd_per(n_wg)), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, 1,
-                           dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
+    for (int i = 0; i < reps; ++i) f();
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0;
@@ -69,21 +46,45 @@ int main() {
     std::vector<uint8_t> img((size_t)w * h * n);
     uint32_t x = 12345;
     for (auto& v : img) v = (uint8_t)((x = x * 1664525u + 1013904223u) >> 24);
-    uint8_t *src, *dst;
+    uint8_t *src, *dst, *trash;
     hipMalloc(&src, img.size());
     hipMalloc(&dst, (size_t)lay.bytes * n);
+    hipMalloc(&trash, 1 << 24);
     hipMemcpy(src, img.data(), img.size(), hipMemcpyHostToDevice);
+    DownLevels D{};
+    for (int k = 0; k < 3; ++k) {
+        D.off[k] = lay.off[1 + k];
+        D.pitch[k] = lay.pitch[1 + k];
+        D.w[k] = lay.w[1 + k];
+        D.h[k] = lay.h[1 + k];
+    }
+    uint8_t* slot0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
+    const EdgePlane ep{slot0, lay.bytes, lay.pitch[0]};
+    const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2), n_bands = (D.h[0] + BAND - 1) / BAND;
+    const int n_units = n_strips * n_bands * n;
+    const int nblk = (n_units + 3) / 4;
+    const dim3 grid(N_XCD * xcd_per(nblk));
     const int cu = prop.multiProcessorCount;
-    for (int blocks : {cu * 4, cu * 8, cu * 16, cu * 32}) {
-        const float us = time_read(src, img.size(), (uint32_t*)dst, blocks, reps);
+    for (int blocks : {cu * 8, cu * 32}) {
+        const float us = timeit([&] { read_all<<<blocks, 256>>>((const uint4*)src, img.size() / 16, (uint32_t*)trash); }, reps);
         printf("read_all %5d blocks  %8.1f us  %6.2f TB/s\n", blocks, us, img.size() / us / 1e6);
     }
-    printf("stage0 (staging)      %8.1f us\n", run<0>(src, dst, lay, n, cu, reps));
-    printf("stage1 (+h L1)        %8.1f us\n", run<1>(src, dst, lay, n, cu, reps));
-    printf("stage2 (+v L1)        %8.1f us\n", run<2>(src, dst, lay, n, cu, reps));
-    printf("stage3 (+own/fix L1)  %8.1f us\n", run<3>(src, dst, lay, n, cu, reps));
-    printf("stage6 (+L2)          %8.1f us\n", run<6>(src, dst, lay, n, cu, reps));
-    printf("full                  %8.1f us\n", run<99>(src, dst, lay, n, cu, reps));
-    printf("bytes in %.1f MB\n", img.size() / 1e6);
+    printf("edge_kernel            %8.1f us\n", timeit([&] {
+        hipLaunchKernelGGL(edge_kernel, dim3((h * 12 + 255) / 256, n), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h,
+                           slot0, lay.bytes, lay.pitch[0]);
+    }, reps));
+    auto run3 = [&](auto skip_c, const char* what) {
+        constexpr int SK = decltype(skip_c)::value;
+        printf("stream_kernel<3> %-28s %7.1f us\n", what, timeit([&] {
+            hipLaunchKernelGGL((stream_kernel<3, SK>), grid, dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, ep, dst,
+                               lay.bytes, D, n_strips, n_bands, n_units, trash);
+        }, reps));
+    };
+    run3(std::integral_constant<int, 0>{}, "all stores");
+    run3(std::integral_constant<int, 6>{}, "level-1 stores only");
+    run3(std::integral_constant<int, 5>{}, "level-2 stores only");
+    run3(std::integral_constant<int, 3>{}, "level-3 stores only");
+    run3(std::integral_constant<int, 7>{}, "no stores");
+    printf("units %d (waves), %d per SIMD\n", n_units, n_units / (cu * 4));
     return 0;
 }
