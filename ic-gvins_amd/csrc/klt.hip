@@ -18,6 +18,8 @@
 //    the CPU restatement (oracle/klt.c), whose LK outputs are matched bit-exactly.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gvx_internal.h"
 
 namespace gvx {
@@ -112,22 +114,24 @@ __device__ __forceinline__ int refl(int p, int len) {
     a = abs(a);
     return min(a, len - 1);
 }
-// Border windows of an unpadded plane (level 0 read in place): the wave gathers
-// its window -- rows y0 .. y0+rows-1, bytes x0 .. x0+31, REFLECT_101 outside
-// the image (the values the padded ring of OpenCV's pyramid level holds there)
-// -- into its own LDS tile once (byte buffer loads off the wave-uniform plane
-// base), then every lane reads its rows from LDS like the aligned global path.
+// Border windows of an unpadded plane (level 0 read in place): a point's lane
+// group gathers its window -- rows y0 .. y0+rows-1, bytes x0 .. x0+31,
+// REFLECT_101 outside the image (the values the padded ring of OpenCV's
+// pyramid level holds there) -- into its own LDS tile once (byte buffer loads
+// off the wave-uniform plane base), then every lane reads its rows from LDS
+// like the aligned global path.
 constexpr int WIN_DW = 8;  // dwords per LDS tile row
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+template <int G>
 __device__ __forceinline__ void fill_win(uint32_t* win, const Plane& P, int W, int H, int x0, int y0, int rows,
-                                         int lane) {
+                                         int gl) {
     wave_lds_sync();  // earlier reads of the tile are done
 #pragma unroll 1
-    for (int i = lane; i < rows * WIN_DW; i += 64) {
+    for (int i = gl; i < rows * WIN_DW; i += G) {
         const int r = i >> 3, q = i & 7;
         const int ro = P.o0 + refl(y0 + r, H) * P.pitch;
         uint32_t v = 0;
@@ -150,15 +154,21 @@ __device__ __forceinline__ void read_win(const uint32_t* win, int row, int byteo
 }
 
 // cvRound((1-a)(1-b) 2^14) ... in fp32 (LKTrackerInvoker), packed as int16 pairs
-// W0 = (w00, w01), W1 = (w10, w11).
+// W0 = (w00, w01), W1 = (w10, w11).  p*2^14 is exact, so fma(p, 2^14, 1.5*2^23)
+// is 1.5*2^23 + cvRound(p*2^14) (round to nearest even, 0 <= p*2^14 <= 2^14)
+// with the integer in the low mantissa bits; the packs read those bits and
+// w11 = 2^14 - w00 - w01 - w10 is taken on the raw bit patterns (mod 2^32).
 __device__ __forceinline__ void weights(float a, float b, uint32_t& W0, uint32_t& W1) {
-    const int w00 = __float2int_rn((1.f - a) * (1.f - b) * (float)(1 << W_BITS));
-    const int w01 = __float2int_rn(a * (1.f - b) * (float)(1 << W_BITS));
-    const int w10 = __float2int_rn((1.f - a) * b * (float)(1 << W_BITS));
-    const int w11 = (1 << W_BITS) - w00 - w01 - w10;
-    W0 = pack16(w00, w01);
-    W1 = pack16(w10, w11);
+    constexpr float M = 12582912.0f;  // 1.5 * 2^23, bit pattern 0x4B400000
+    const float ra = 1.f - a, rb = 1.f - b;
+    const uint32_t f00 = __float_as_uint(__builtin_fmaf(ra * rb, (float)(1 << W_BITS), M));
+    const uint32_t f01 = __float_as_uint(__builtin_fmaf(a * rb, (float)(1 << W_BITS), M));
+    const uint32_t f10 = __float_as_uint(__builtin_fmaf(ra * b, (float)(1 << W_BITS), M));
+    const uint32_t f11 = ((1u << W_BITS) + 3u * 0x4B400000u) - (f00 + f01 + f10);
+    W0 = __builtin_amdgcn_perm(f01, f00, 0x05040100u);
+    W1 = __builtin_amdgcn_perm(f11, f10, 0x05040100u);
 }
+
 
 struct LkCfg {
     int max_iter;
@@ -173,6 +183,23 @@ struct Unit {
     bool valid;
     uint32_t iv[4], ix[4], iy[4];  // packed int16 pairs (pixel 2k, 2k+1); pair 3 high = 0
 };
+// A lane's extracted window values live in LDS between the extraction and the
+// iterations (registers hold only the unit being matched): slot (s, q) of lane
+// `lane` at ust[(3*s + q)*64], ust = wave base + lane (16-B per lane, linear).
+__device__ __forceinline__ void unit_put(v4u* ust, int s, const Unit& u) {
+    ust[(3 * s + 0) * 64] = v4u{u.iv[0], u.iv[1], u.iv[2], u.iv[3]};
+    ust[(3 * s + 1) * 64] = v4u{u.ix[0], u.ix[1], u.ix[2], u.ix[3]};
+    ust[(3 * s + 2) * 64] = v4u{u.iy[0], u.iy[1], u.iy[2], u.iy[3]};
+}
+__device__ __forceinline__ void unit_get(const v4u* ust, int s, Unit& u) {
+    const v4u a = ust[(3 * s + 0) * 64], b = ust[(3 * s + 1) * 64], c = ust[(3 * s + 2) * 64];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        u.iv[k] = a[k];
+        u.ix[k] = b[k];
+        u.iy[k] = c[k];
+    }
+}
 
 // byte pair (T, T+1) of a 12-byte row in three dwords, as int16 halves (T <= 9;
 // T is a constant after unrolling)
@@ -273,7 +300,7 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
 // r0 / r1: bytes jx+7*seg .. +7 of rows jy+row and jy+row+1.
 template <bool ERR>
 __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
-                                           uint32_t W0, uint32_t W1, int& b1, int& b2, int& es) {
+                                           uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
     constexpr int RND = 1 << (W_BITS - 6);
     int jv[8];
     jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2k(byte_pair<0>(r0[0], r0[1]), W0, RND));
@@ -287,12 +314,14 @@ __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2
     for (int t = 0; t < 7; ++t) jv[t] >>= (W_BITS - 5);
     jv[7] = 0;
     if (ERR) {
+        int e = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);  // diff pair
             const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
-            es += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
+            e += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
         }
+        es += valid ? e : 0;
     } else {
         const uint32_t d0 = psub16(pack16(jv[0], jv[1]), u.iv[0]);
         int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
@@ -302,41 +331,57 @@ __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2
             s1 = dot2(d, u.ix[k], s1);
             s2 = dot2(d, u.iy[k], s2);
         }
-        b1 += s1;
-        b2 += s2;
+        b1 += valid ? s1 : 0;
+        b2 += valid ? s2 : 0;
     }
 }
 
-// Exact wave-wide sums of per-lane values |v| < 2^28 (one 7-pixel unit of
-// products per lane).  The DPP chain leaves the total in lane 63.
-__device__ __forceinline__ int wave_dpp(int v) {
+// Exact sums over a point's lane group (G = 16, 32 or 64 lanes, aligned):
+// a butterfly, so every lane of the group ends with the group total --
+// DPP quad / row mirrors inside 16-lane rows, then v_permlane16_swap /
+// v_permlane32_swap across rows (CDNA4).
+template <int G>
+__device__ __forceinline__ int group_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm 2,3,0,1
     v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
     v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);  // row_mirror
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1,3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2,3
+    if constexpr (G >= 32) {
+        const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+        v = (int)(r[0] + r[1]);
+    }
+    if constexpr (G >= 64) {
+        const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+        v = (int)(r[0] + r[1]);
+    }
     return v;
 }
-__device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_dpp(v), 63); }
-// (float) of the exact 64-bit sum, round-to-nearest-even: 14-bit halves keep
-// both DPP sums in int32; hi*2^14 + lo is exact in fp64 (|sum| < 2^35) and the
-// single fp64 -> fp32 conversion rounds once -- all on the VALU, one readlane.
-__device__ __forceinline__ float wave_sum_f32(int v) {
-    const int hi = wave_dpp(v >> 14), lo = wave_dpp(v & 0x3fff);
-    const double d = (double)hi * 16384.0 + (double)lo;
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, (float)d), 63));
+// (float) of the exact group sums of per-lane values |v| < 2^31, round to
+// nearest even: v = hi*2^10 + lo with lo in [0, 1024); the hi sums stay below
+// 2^27 and two lo sums (< 2^16 each) share one packed chain; hi*2^10 + lo is
+// exact in fp64 (|sum| < 2^37) and the fp64 -> fp32 conversion rounds once.
+template <int G>
+__device__ __forceinline__ void group_sums_f32(int v0, int v1, float& f0, float& f1) {
+    const int h0 = group_sum<G>(v0 >> 10), h1 = group_sum<G>(v1 >> 10);
+    const uint32_t l = (uint32_t)group_sum<G>((int)(((uint32_t)v0 & 1023u) | (((uint32_t)v1 & 1023u) << 16)));
+    f0 = (float)__builtin_fma((double)h0, 1024.0, (double)(l & 0xffffu));
+    f1 = (float)__builtin_fma((double)h1, 1024.0, (double)(l >> 16));
+}
+template <int G>
+__device__ __forceinline__ float group_sum_f32(int v) {
+    const int h = group_sum<G>(v >> 10), l = group_sum<G>(v & 1023);
+    return (float)__builtin_fma((double)h, 1024.0, (double)l);
 }
 
-// Window rows of one unit: 4 rows x 12 bytes of I for the extraction, 2 rows x
-// 8 bytes of J for a match.  `raw` planes (level 0 read in place from the
-// caller's image) take the aligned-load path only when every byte it touches is
-// inside the image, and gather with REFLECT_101 otherwise; padded levels always
-// take the aligned path (their PAD ring covers every window the LK loop admits).
-// lane_off = row*pitch + 7*seg of the unit at this level.
-__device__ __forceinline__ void load_i_rows(const Unit& u, const Plane& P, int lane_off, int W, int H, int ipx,
-                                            int ipy, bool raw, uint32_t* win, int lane, uint32_t (&d)[4][3]) {
-    if (!raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H)) {
+// Window rows of a point's units: 4 rows x 12 bytes of I per unit for the
+// extraction, 2 rows x 8 bytes of J for a match.  `raw` planes (level 0 read in
+// place from the caller's image) take the aligned-load path only when every
+// byte the window touches is inside the image, and gather with REFLECT_101
+// otherwise; padded levels always take the aligned path (their PAD ring covers
+// every window the LK loop admits).  lane_off[s] = row*pitch + 7*seg of unit s.
+__device__ __forceinline__ void load_i_unit(const Unit& u, const Plane& P, int lane_off, int ipx, int ipy, bool fast,
+                                            const uint32_t* win, uint32_t (&d)[4][3]) {
+    if (fast) {
         const int off = lane_off + (P.o0 + (ipy - 1) * P.pitch + ipx - 1);
         const int al = off & ~3;
         const uint32_t sh = (uint32_t)off & 3u;
@@ -346,15 +391,13 @@ __device__ __forceinline__ void load_i_rows(const Unit& u, const Plane& P, int l
         brow<3>(P, al, sh, 3 * P.pitch, d[3]);
     } else {
         // tile: rows ipy-1 .., bytes ipx-1 ..; the unit reads 4 rows x 12 bytes
-        fill_win(win, P, W, H, ipx - 1, ipy - 1, WIN + 3, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) read_win<3>(win, u.row + r, 7 * u.seg, d[r]);
     }
 }
-__device__ __forceinline__ void load_j_rows(const Unit& u, const Plane& P, int lane_off, int W, int H, int jx,
-                                            int jy, bool raw, uint32_t* win, int lane, uint32_t (&r0)[2],
-                                            uint32_t (&r1)[2]) {
-    if (!raw || (jx >= 3 && jx + 26 <= W && jy >= 0 && jy + 22 <= H)) {
+__device__ __forceinline__ void load_j_unit(const Unit& u, const Plane& P, int lane_off, int jx, int jy, bool fast,
+                                            const uint32_t* win, uint32_t (&r0)[2], uint32_t (&r1)[2]) {
+    if (fast) {
         const int off = lane_off + (P.o0 + jy * P.pitch + jx);
         const int al = off & ~3;
         const uint32_t sh = (uint32_t)off & 3u;
@@ -362,7 +405,6 @@ __device__ __forceinline__ void load_j_rows(const Unit& u, const Plane& P, int l
         brow<2>(P, al, sh, P.pitch, r1);
     } else {
         // tile: rows jy .., bytes jx ..; the unit reads 2 rows x 8 bytes
-        fill_win(win, P, W, H, jx, jy, WIN + 1, lane);
         read_win<2>(win, u.row, 7 * u.seg, r0);
         read_win<2>(win, u.row + 1, 7 * u.seg, r1);
     }
@@ -378,18 +420,28 @@ struct L0Planes {
 };
 
 // LKTrackerInvoker::operator() for one point across all levels (coarse to
-// fine), one wavefront per point, one 7-pixel window unit per lane (lane 63
-// idle).  I/J: padded pyramids of the prev / next image (levels >= 1); level 0
-// from `p0`.
-__device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
-                                        const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
-                                        float p0y, float& nx, float& ny, int& status, float& err, int lane,
-                                        uint32_t* win) {
-    Unit u;
-    u.valid = lane < 63;
-    const int uc = u.valid ? lane : 62;
-    u.row = uc / 3;
-    u.seg = uc - 3 * u.row;
+// fine).  PPW points share a wavefront: each point has a group of G = 64/PPW
+// lanes and lane gl of the group owns the PPW 7-pixel window units
+// gl, gl+G, .. (unit k = window row k/3, segment k%3; unit 63 does not exist).
+// The per-point scalar work (weights, sums, 2x2 solve, convergence) is thus
+// issued once for PPW points.  I/J: padded pyramids of the prev / next image
+// (levels >= 1); level 0 from `p0`.  Every per-point value below is uniform
+// over the point's group; control flow diverges only between groups.
+template <int PPW>
+__device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
+                                         const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
+                                         float p0y, float& nx, float& ny, int& status, float& err, int gl,
+                                         uint32_t* win, v4u* ust) {
+    constexpr int G = 64 / PPW, U = PPW;
+    Unit u[U];
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+        const int k = gl + s * G;
+        u[s].valid = k < 63;
+        const int kc = k < 63 ? k : 62;
+        u[s].row = kc / 3;
+        u[s].seg = kc - 3 * u[s].row;
+    }
     const float halfw = (float)((WIN - 1) * 0.5f);
     const int max_level = lay.nlev - 1;
     status = 1;
@@ -401,7 +453,9 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         const int o0 = l == 0 ? p0.o0 : PAD * pitch + PAD;
         const Plane PI = make_plane(l == 0 ? p0.i : I + lay.off[l], o0, pitch);
         const Plane PJ = make_plane(l == 0 ? p0.j : J + lay.off[l], o0, pitch);
-        const int lane_off = __mul24(u.row, pitch) + 7 * u.seg;
+        int lane_off[U];
+#pragma unroll
+        for (int s = 0; s < U; ++s) lane_off[s] = __mul24(u[s].row, pitch) + 7 * u[s].seg;
         const float sc = ldexpf(1.f, -l);  // == (float)(1./(1 << l)), exact
         float prevx = p0x * sc, prevy = p0y * sc;
         float nextx, nexty;
@@ -421,7 +475,8 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         ny = nexty;
         prevx -= halfw;
         prevy -= halfw;
-        const int ipx = (int)floorf(prevx), ipy = (int)floorf(prevy);
+        const float fpx = floorf(prevx), fpy = floorf(prevy);
+        const int ipx = (int)fpx, ipy = (int)fpy;
         if (ipx < -WIN || ipx >= W || ipy < -WIN || ipy >= H) {
             if (l == 0) {
                 status = 0;
@@ -430,18 +485,30 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
             continue;
         }
         uint32_t W0, W1;
-        weights(prevx - ipx, prevy - ipy, W0, W1);
+        weights(prevx - fpx, prevy - fpy, W0, W1);
         int a11 = 0, a12 = 0, a22 = 0;
         {
-            uint32_t d[4][3];
-            load_i_rows(u, PI, lane_off, W, H, ipx, ipy, raw, win, lane, d);
+            const bool fast = !raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H);
+            if (!fast) fill_win<G>(win, PI, W, H, ipx - 1, ipy - 1, WIN + 3, gl);
             // every unit's derivative columns / rows inside the image
             const bool interior = ipx >= 0 && ipx + WIN + 1 <= W && ipy >= 0 && ipy + WIN + 1 <= H;
-            extract_unit(u, d, W, H, ipx, ipy, interior, W0, W1, a11, a12, a22);
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                uint32_t d[4][3];
+                load_i_unit(u[s], PI, lane_off[s], ipx, ipy, fast, win, d);
+                int t11, t12, t22;
+                extract_unit(u[s], d, W, H, ipx, ipy, interior, W0, W1, t11, t12, t22);
+                a11 += t11;
+                a12 += t12;
+                a22 += t22;
+                unit_put(ust, s, u[s]);
+            }
         }
-        const float A11 = wave_sum_f32(a11) * FLT_SCALE;
-        const float A12 = wave_sum_f32(a12) * FLT_SCALE;
-        const float A22 = wave_sum_f32(a22) * FLT_SCALE;
+        float A11, A12;
+        group_sums_f32<G>(a11, a12, A11, A12);
+        A11 *= FLT_SCALE;
+        A12 *= FLT_SCALE;
+        const float A22 = group_sum_f32<G>(a22) * FLT_SCALE;
         float D = A11 * A22 - A12 * A12;
         const float minEig =
             __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12), (float)(2 * WIN * WIN));
@@ -458,29 +525,38 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < cfg.max_iter; ++j) {
-            const int inx = (int)floorf(nextx), iny = (int)floorf(nexty);
+            const float fnx = floorf(nextx), fny = floorf(nexty);
+            const int inx = (int)fnx, iny = (int)fny;
             if (inx < -WIN || inx >= W || iny < -WIN || iny >= H) {
                 if (l == 0) status = 0;
                 break;
             }
             uint32_t J0, J1;
-            weights(nextx - inx, nexty - iny, J0, J1);
+            weights(nextx - fnx, nexty - fny, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
             {
-                uint32_t r0[2], r1[2];
-                load_j_rows(u, PJ, lane_off, W, H, inx, iny, raw, win, lane, r0, r1);
-                match_unit<false>(u, r0, r1, J0, J1, b1, b2, es);
+                const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+                if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
+#pragma unroll
+                for (int s = 0; s < U; ++s) {
+                    uint32_t r0[2], r1[2];
+                    load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
+                    unit_get(ust, s, u[s]);
+                    match_unit<false>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                }
             }
-            if (!u.valid) b1 = b2 = 0;
-            const float fb1 = wave_sum_f32(b1) * FLT_SCALE;
-            const float fb2 = wave_sum_f32(b2) * FLT_SCALE;
+            float fb1, fb2;
+            group_sums_f32<G>(b1, b2, fb1, fb2);
+            fb1 *= FLT_SCALE;
+            fb2 *= FLT_SCALE;
             const float dx = (A12 * fb2 - A22 * fb1) * D;
             const float dy = (A12 * fb1 - A11 * fb2) * D;
             nextx += dx;
             nexty += dy;
             nx = nextx + halfw;
             ny = nexty + halfw;
-            if ((double)dx * (double)dx + (double)dy * (double)dy <= cfg.crit_eps) break;
+            // delta.ddot(delta) <= eps^2 in double: dx*dx is exact in fp64, so the fma rounds once like the sum
+            if (__builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps) break;
             if (j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f) {
                 nx -= dx * 0.5f;
                 ny -= dy * 0.5f;
@@ -492,40 +568,64 @@ __device__ __forceinline__ void lk_wave(const uint8_t* __restrict__ I, const uin
         if (status && l == 0) {
             // final error (OPTFLOW_LK_GET_MIN_EIGENVALS not set)
             const float exf = nx - halfw, eyf = ny - halfw;
-            const int inx = (int)floorf(exf), iny = (int)floorf(eyf);
+            const float fex = floorf(exf), fey = floorf(eyf);
+            const int inx = (int)fex, iny = (int)fey;
             if (inx < -WIN || inx >= W || iny < -WIN || iny >= H) {
                 status = 0;
                 continue;
             }
             uint32_t J0, J1;
-            weights(exf - inx, eyf - iny, J0, J1);
+            weights(exf - fex, eyf - fey, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
             {
-                uint32_t r0[2], r1[2];
-                load_j_rows(u, PJ, lane_off, W, H, inx, iny, raw, win, lane, r0, r1);
-                match_unit<true>(u, r0, r1, J0, J1, b1, b2, es);
+                const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+                if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
+#pragma unroll
+                for (int s = 0; s < U; ++s) {
+                    uint32_t r0[2], r1[2];
+                    load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
+                    unit_get(ust, s, u[s]);
+                    match_unit<true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                }
             }
-            if (!u.valid) es = 0;
-            err = __fdiv_rn((float)wave_total(es) * 1.f, (float)(32 * WIN * WIN));
+            err = __fdiv_rn((float)group_sum<G>(es) * 1.f, (float)(32 * WIN * WIN));
         }
     }
 }
 
-__global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
+// One launch for a batch of pairs: PPW points per wavefront, the points of a
+// wave always from one pair (wave-uniform plane bases); ceil(n_pts / PPW)
+// waves per pair, the spare groups of a pair's last wave recompute its last
+// point and store nothing.
+// minimum waves per SIMD the register allocation must allow
+template <int PPW>
+constexpr int klt_occupancy() {
+    return PPW == 1 ? 7 : PPW == 2 ? 5 : 3;
+}
+template <int PPW>
+__global__ void __launch_bounds__(256, klt_occupancy<PPW>()) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
                                                   const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
                                                   int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
                                                   float* __restrict__ next_xy, float* __restrict__ back_xy,
                                                   uint8_t* __restrict__ flags, float* __restrict__ err_out) {
-    __shared__ uint32_t wins[4][(WIN + 3) * WIN_DW];  // per-wave border tiles
+    constexpr int G = 64 / PPW;
+    __shared__ uint32_t wins[4 * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
+    __shared__ v4u units[4][3 * PPW * 64];                  // per-lane window values
     const int lane = threadIdx.x & 63;
-    uint32_t* win = wins[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-    const int64_t total = (int64_t)a.n_pairs * a.n_pts;
-    // wave-uniform point index in an SGPR: the per-point state, the level /
-    // iteration control and the 2x2 solve then stay scalar (uniform branches)
-    const int nb = (int)((total + 3) / 4);
-    const int64_t gp = (int64_t)xcd_swizzle(blockIdx.x, nb) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (gp >= total) return;
-    const int64_t pair = gp / a.n_pts;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = lane / G, gl = lane & (G - 1);
+    uint32_t* win = wins[wv * PPW + grp];
+    v4u* ust = &units[wv][lane];
+    const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair
+    const int n_waves = a.n_pairs * wpp;
+    const int nb = (n_waves + 3) / 4;
+    const int wg = xcd_swizzle(blockIdx.x, nb) * 4 + wv;
+    if (wg >= n_waves) return;
+    const int pair = wg / wpp;
+    const int pt_raw = (wg - pair * wpp) * PPW + grp;
+    const bool own = pt_raw < a.n_pts;
+    const int64_t gp = (int64_t)pair * a.n_pts + (own ? pt_raw : a.n_pts - 1);
+    const bool writer = own && gl == 0;
     const uint8_t* I = pyr_prev + pair * prev_stride;
     const uint8_t* J = pyr_next + pair * next_stride;
     const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.o0, l0.pitch,
@@ -536,9 +636,9 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
     float nx = next_xy[2 * gp], ny = next_xy[2 * gp + 1];
     int st = 1;
     float e = 0.f;
-    lk_wave(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, lane, win);
+    lk_group<PPW>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, gl, win, ust);
     if (a.mode == 0) {
-        if (lane == 0) {
+        if (writer) {
             next_xy[2 * gp] = nx;
             next_xy[2 * gp + 1] = ny;
             flags[gp] = (uint8_t)st;
@@ -551,8 +651,8 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
     int st2 = 1;
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
-    lk_wave(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, lane, win);
-    if (lane == 0) {
+    lk_group<PPW>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, gl, win, ust);
+    if (writer) {
         const double B = a.border;
         const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
         const double ddx = (double)(bx - p0x), ddy = (double)(by - p0y);
@@ -568,6 +668,7 @@ __global__ void __launch_bounds__(256) klt_kernel(KltArgs a, PyrLayout lay, cons
         if (err_out) err_out[gp] = e;
     }
 }
+
 
 // reduceVector (tracking.cc:831-839): order-preserving index compaction of the
 // keep bit, one workgroup per pair.
@@ -598,15 +699,48 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 
 }  // namespace
 
+// Points per wavefront of the LK launch (1, 2 or 4; GVX_KLT_PPW overrides the
+// default for measurements).
+static int klt_ppw() {
+    static const int v = [] {
+        const char* e = getenv("GVX_KLT_PPW");
+        const int p = e ? atoi(e) : 2;
+        return (p == 1 || p == 2 || p == 4) ? p : 2;
+    }();
+    return v;
+}
+
+template <int PPW>
+static void launch_klt_ppw(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                           const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                           const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                           float* err) {
+    const int n_waves = a.n_pairs * ((a.n_pts + PPW - 1) / PPW);
+    dim3 grid((unsigned)(N_XCD * xcd_per((n_waves + 3) / 4)));
+    hipLaunchKernelGGL(klt_kernel<PPW>, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
+                       next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
+}
+
 hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
                       const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
                       const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
                       float* err) {
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     if (total <= 0) return hipSuccess;
-    dim3 grid((unsigned)(N_XCD * xcd_per((int)((total + 3) / 4))));
-    hipLaunchKernelGGL(klt_kernel, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
-                       next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
+    if (total > (int64_t)1 << 30) return hipErrorInvalidValue;  // wave indices are int32
+    switch (klt_ppw()) {
+        case 1:
+            launch_klt_ppw<1>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+            break;
+        case 4:
+            launch_klt_ppw<4>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+            break;
+        default:
+            launch_klt_ppw<2>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+    }
     return hipGetLastError();
 }
 

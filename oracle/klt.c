@@ -18,6 +18,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifdef ORC_ITER_STATS
+/* LK iterations per (level, point) -- diagnostic builds (-DORC_ITER_STATS, one thread) */
+long orc_iter_hist[8][64];
+#endif
+
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
 void orc_klt_params_default(orc_klt_params* p) {
@@ -314,7 +319,13 @@ static void lk_level(const lk_job* jb) {
         nextx -= halfw;
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
+#ifdef ORC_ITER_STATS
+        int j_used = 0;
+#endif
         for (int j = 0; j < jb->p->max_iter; j++) {
+#ifdef ORC_ITER_STATS
+            j_used = j + 1;
+#endif
             int inx = cv_floor(nextx), iny = cv_floor(nexty);
             if (inx < -win || inx >= J->w || iny < -win || iny >= J->h) {
                 if (level == 0) jb->status[pt] = 0;
@@ -356,6 +367,9 @@ static void lk_level(const lk_job* jb) {
             pdx = dx;
             pdy = dy;
         }
+#ifdef ORC_ITER_STATS
+        orc_iter_hist[level][j_used]++;  /* single-threaded diagnostic build only */
+#endif
 
         if (jb->status[pt] && level == 0) {
             float nx = jb->next_pts[2 * pt] - halfw;
