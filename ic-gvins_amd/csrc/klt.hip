@@ -175,6 +175,7 @@ struct LkCfg {
     double crit_eps;
     float min_eig;
     int use_initial_flow;
+    int want_err;  // compute the level-0 error (the status checks run regardless)
 };
 
 // One window unit: 7 pixels (cols 7*seg .. 7*seg+6 of window row `row`).
@@ -574,6 +575,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 status = 0;
                 continue;
             }
+            if (!cfg.want_err) continue;
             uint32_t J0, J1;
             weights(exf - fex, eyf - fey, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
@@ -631,7 +633,7 @@ __global__ void __launch_bounds__(256, klt_occupancy<PPW>()) klt_kernel(KltArgs 
     const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.o0, l0.pitch,
                       l0.raw != 0};
     const L0Planes pb{pf.j, pf.i, pf.o0, pf.pitch, pf.raw};
-    LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow};
+    LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow, err_out != nullptr};
     const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
     float nx = next_xy[2 * gp], ny = next_xy[2 * gp + 1];
     int st = 1;
@@ -651,6 +653,7 @@ __global__ void __launch_bounds__(256, klt_occupancy<PPW>()) klt_kernel(KltArgs 
     int st2 = 1;
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
+    cfg.want_err = 0;  // the backward error is not reported
     lk_group<PPW>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, gl, win, ust);
     if (writer) {
         const double B = a.border;

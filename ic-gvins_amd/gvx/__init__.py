@@ -20,7 +20,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgvx.so")
+LIB_PATH = os.environ.get("GVX_LIB") or os.path.join(_HERE, "libgvx.so")  # GVX_LIB: A/B builds (tools/variant.sh)
 
 GVX_OK = 0
 GVX_PREINT_NORMAL = 0
