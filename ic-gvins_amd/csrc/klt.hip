@@ -599,20 +599,26 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 // wave always from one pair (wave-uniform plane bases); ceil(n_pts / PPW)
 // waves per pair, the spare groups of a pair's last wave recompute its last
 // point and store nothing.
+// Waves per workgroup.  One: a finished wave's slot (and its LDS) is refilled
+// at once instead of idling until the slowest wave of its workgroup is done
+// (per-point iteration counts differ).
+#ifndef KLT_WPB
+#define KLT_WPB 1
+#endif
 // minimum waves per SIMD the register allocation must allow
 template <int PPW>
 constexpr int klt_occupancy() {
-    return PPW == 1 ? 7 : PPW == 2 ? 5 : 3;
+    return PPW == 1 ? 7 : PPW == 2 ? 5 : 2;
 }
 template <int PPW>
-__global__ void __launch_bounds__(256, klt_occupancy<PPW>()) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
+__global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
                                                   const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
                                                   int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
                                                   float* __restrict__ next_xy, float* __restrict__ back_xy,
                                                   uint8_t* __restrict__ flags, float* __restrict__ err_out) {
     constexpr int G = 64 / PPW;
-    __shared__ uint32_t wins[4 * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
-    __shared__ v4u units[4][3 * PPW * 64];                  // per-lane window values
+    __shared__ uint32_t wins[KLT_WPB * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
+    __shared__ v4u units[KLT_WPB][3 * PPW * 64];                  // per-lane window values
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp = lane / G, gl = lane & (G - 1);
@@ -620,8 +626,8 @@ __global__ void __launch_bounds__(256, klt_occupancy<PPW>()) klt_kernel(KltArgs 
     v4u* ust = &units[wv][lane];
     const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair
     const int n_waves = a.n_pairs * wpp;
-    const int nb = (n_waves + 3) / 4;
-    const int wg = xcd_swizzle(blockIdx.x, nb) * 4 + wv;
+    const int nb = (n_waves + KLT_WPB - 1) / KLT_WPB;
+    const int wg = xcd_swizzle(blockIdx.x, nb) * KLT_WPB + wv;
     if (wg >= n_waves) return;
     const int pair = wg / wpp;
     const int pt_raw = (wg - pair * wpp) * PPW + grp;
@@ -719,8 +725,8 @@ static void launch_klt_ppw(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, c
                            const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
                            float* err) {
     const int n_waves = a.n_pairs * ((a.n_pts + PPW - 1) / PPW);
-    dim3 grid((unsigned)(N_XCD * xcd_per((n_waves + 3) / 4)));
-    hipLaunchKernelGGL(klt_kernel<PPW>, grid, dim3(256), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
+    dim3 grid((unsigned)(N_XCD * xcd_per((n_waves + KLT_WPB - 1) / KLT_WPB)));
+    hipLaunchKernelGGL(klt_kernel<PPW>, grid, dim3(64 * KLT_WPB), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
                        next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
 }
 

@@ -5,5 +5,5 @@ T=$1; shift
 mkdir -p gpurun_out/$T
 for p in "$@"; do
   GVX_KLT_PPW=$p timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/$T/t$p.log 2>&1
-  GVX_KLT_PPW=$p timeout -k 10 200 python bench.py --no-cpu --steps 20 --warmup 3 > gpurun_out/$T/b$p.json 2> gpurun_out/$T/b$p.err
+  GVX_KLT_PPW=$p timeout -k 10 200 python bench.py --no-cpu --steps 40 --warmup 30 > gpurun_out/$T/b$p.json 2> gpurun_out/$T/b$p.err
 done
