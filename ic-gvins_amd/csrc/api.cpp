@@ -292,6 +292,21 @@ gvx_status gvx_frame_level(gvx_ctx* c, uint64_t id, int32_t level, uint8_t* out,
     return hip_err(c, hipStreamSynchronize(c->stream), "copy level sync");
 }
 
+gvx_status gvx_frame_level_padded(gvx_ctx* c, uint64_t id, int32_t level, int32_t pad, uint8_t* out) {
+    static_assert(GVX_PYR_PAD == PAD, "ABI pad constant");
+    if (!c) return GVX_ERR_INVALID;
+    auto it = c->frames.find(id);
+    if (it == c->frames.end()) return set_err(c, GVX_ERR_NOT_FOUND, "frame %llu", (unsigned long long)id);
+    const PyrLayout& L = it->second.lay;
+    if (level < 0 || level >= L.nlev) return set_err(c, GVX_ERR_INVALID, "level %d", level);
+    if (pad < 0 || pad > PAD || !out) return set_err(c, GVX_ERR_INVALID, "pad %d", pad);
+    const uint8_t* src = it->second.pyr + L.off[level] + (int64_t)(PAD - pad) * L.pitch[level] + (PAD - pad);
+    const int w = L.w[level] + 2 * pad, h = L.h[level] + 2 * pad;
+    hipError_t e = hipMemcpy2DAsync(out, w, src, L.pitch[level], w, h, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "copy level");
+    return hip_err(c, hipStreamSynchronize(c->stream), "copy level sync");
+}
+
 // Shared single-pair path of gvx_klt / gvx_klt_fb.
 static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, const float* prev_xy,
                              float* next_xy, float* back_xy, uint8_t* flags_out, float* err,

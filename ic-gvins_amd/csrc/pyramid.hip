@@ -370,7 +370,7 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane L <- lane L
 }
 
 // Edge bands: for every source row, the REFLECT_101-extended columns
-// [-32, 64) and [w-64, w+32) are stored in a padded plane (the pyramid's unused
+// [-32, 16) and [w-16, w+32) are stored in a padded plane (the pyramid's unused
 // level-0 slot on the batched path, the padded level 0 itself in the frame
 // cache).  Lanes whose 16-byte window leaves [48, w-48) read the band instead
 // of the source, so the streaming loop never gathers bytes: every row is one
@@ -380,7 +380,7 @@ struct EdgePlane {
     int64_t img_stride;
     int pitch;
 };
-constexpr int EDGE_L = 64, EDGE_R = 64;  // band extents inside the image
+constexpr int EDGE_L = 16, EDGE_R = 16;  // band extents inside the image
 
 __device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pitch, const uint8_t* __restrict__ E,
                                            int epitch, int w, int h, int x, int y) {
@@ -393,33 +393,39 @@ __device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pi
 }
 
 // Fill the edge bands of n_img source images into the padded plane E: per row
-// six 16-byte chunks on each side.  Inside and outside chunks are separate item
-// ranges, so waves never mix paths: chunks inside the image are vector copies;
-// the two outside chunks per side are the byte-reversed
-// mirror ranges, built from aligned 16-byte loads and v_perm (w % 4 == 0; other
-// widths gather bytes).
+// three 16-byte chunks on each side.  Inside and outside chunks are separate
+// item ranges, so waves never mix paths: the chunk inside the image ([0, 16),
+// [w-16, w)) is a vector copy; the two outside chunks per side are the
+// byte-reversed mirror ranges, built from aligned dword loads and v_perm.
+// Requires w % 4 == 0 and 4-byte aligned rows (other inputs take the padded
+// level-0 copy instead); vec16: 16-byte aligned rows and w % 16 == 0.
 __global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ src, int64_t img_stride, int pitch,
                                                    int w, int h, uint8_t* __restrict__ E, int64_t e_img_stride,
-                                                   int epitch) {
+                                                   int epitch, int vec16) {
     const int img = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= h * 12) return;
-    // items [0, 8h): the 8 chunks per row inside the image (row-major, so a wave
-    // reads 8 rows x 64 contiguous bytes per side); [8h, 12h): the 4 mirrored chunks
+    if (i >= h * 6) return;
+    // items [0, 2h): the chunk inside the image on each side; [2h, 6h): the 4
+    // mirrored chunks of a row
     int q, y;
-    if (i < 8 * h) {
-        y = i >> 3;
-        q = (i & 7) < 4 ? (i & 7) + 2 : (i & 7) + 2;
+    if (i < 2 * h) {
+        y = i >> 1;
+        q = 2 + (i & 1);
     } else {
-        const int j = i - 8 * h;
+        const int j = i - 2 * h;
         y = j >> 2;
-        q = (j & 3) < 2 ? (j & 3) : (j & 3) + 8;
+        q = (j & 3) < 2 ? (j & 3) : (j & 3) + 2;
     }
-    const int x = q < 6 ? -32 + 16 * q : w - EDGE_R + 16 * (q - 6);
+    const int x = q < 3 ? -32 + 16 * q : w - EDGE_R + 16 * (q - 3);
     const uint8_t* row = src + img * img_stride + (int64_t)y * pitch;
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);  // 4-byte aligned rows
+    uint32_t* o = reinterpret_cast<uint32_t*>(E + img * e_img_stride + (int64_t)y * epitch + x);
     uint32_t d[4];
     if (x >= 0 && x + 16 <= w) {
+        if (vec16) {
+            *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(row + x);
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) d[k] = rw[(x >> 2) + k];
     } else if (x < 0 && w >= 40) {
@@ -442,7 +448,10 @@ __global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ s
             d[k] = t;
         }
     }
-    uint32_t* o = reinterpret_cast<uint32_t*>(E + img * e_img_stride + (int64_t)y * epitch + x);
+    if (vec16) {
+        *reinterpret_cast<uint4*>(o) = make_uint4(d[0], d[1], d[2], d[3]);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[k] = d[k];
 }
@@ -541,11 +550,13 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
         pa[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 1);
         pb[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 2);
     }
-    // Every load and store below is issued unconditionally: on gfx9 stores and
-    // loads share vmcnt, and a store skipped by a branch would make the compiler
-    // wait for all earlier stores before using a prefetched row.  Outputs that
-    // are not owned (rows outside the band, lanes 0/1/62/63, columns past the
-    // level, the schedule's warm-up rows) go to this lane's dword of a trash line.
+    // Loads are issued unconditionally and stores branch only on wave-uniform
+    // row conditions (rows of the band, mirrored ring rows): on gfx9 stores and
+    // loads share vmcnt, and a store under a lane-divergent branch would make the
+    // compiler wait for all earlier stores before using a prefetched row; a
+    // uniform branch costs at most one extra counted op at the join.  Lanes that
+    // own no output (lanes 0/1/62/63, columns past the level) store to this
+    // lane's dword of a trash line.
     uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
     uint32_t nsink = 0;
     auto body = [&](int k, auto slot_c) {
@@ -562,15 +573,15 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
         hr[1] = hr[3];
         hr[2] = hr[4];
         if (fix1) l1 = __builtin_amdgcn_perm(l1, wave_shr1(l1), sel1);
-        {
-            const bool ok = r1 >= o1lo && r1 < o1hi && own_lane && c1 + 4 * (lane - 2) < w1;
+        if (r1 >= o1lo && r1 < o1hi) {  // wave-uniform: rows of the band
+            const bool ok = own_lane && c1 + 4 * (lane - 2) < w1;
             uint8_t* q = P + L.off[0] + c1 + 4 * (lane - 2) + PAD;
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
             if constexpr ((SKIP & 1) != 0) {
                 nsink ^= l1;
             } else {
                 *reinterpret_cast<uint32_t*>(ok ? q + (int64_t)(r1 + PAD) * p1 : tl) = l1;
-                *reinterpret_cast<uint32_t*>(ok && mr != r1 ? q + (int64_t)(mr + PAD) * p1 : tl) = l1;
+                if (mr != r1) *reinterpret_cast<uint32_t*>(ok ? q + (int64_t)(mr + PAD) * p1 : tl) = l1;
             }
         }
         if constexpr (NL > 1) {
@@ -601,15 +612,16 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
                     const uint32_t a1 = wave_shr1(l2), a2 = wave_shr1(a1);
                     l2 = __builtin_amdgcn_perm(l2, (a2 & 0xffffu) | (a1 << 16), sel2);
                 }
-                {
-                    const bool ok = k >= 4 && r2 >= o2lo && r2 < o2hi && own_lane && c2 + 2 * (lane - 2) < w2;
+                if (k >= 4 && r2 >= o2lo && r2 < o2hi) {
+                    const bool ok = own_lane && c2 + 2 * (lane - 2) < w2;
                     uint8_t* q = P + L.off[1] + c2 + 2 * (lane - 2) + PAD;
                     const int mr = mirror_row(r2, h2);
                     if constexpr ((SKIP & 2) != 0) {
                         nsink ^= l2 << 7;
                     } else {
                         *reinterpret_cast<uint16_t*>(ok ? q + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
-                        *reinterpret_cast<uint16_t*>(ok && mr != r2 ? q + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
+                        if (mr != r2)
+                            *reinterpret_cast<uint16_t*>(ok ? q + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
                     }
                 }
                 if constexpr (NL > 2) {
@@ -631,14 +643,14 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
                     if constexpr (slot == 0) {
                         const int r3 = (r2 - 2) >> 1;
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
-                        const bool ok = k >= 12 && r3 >= o3lo && r3 < o3hi && own_lane && c3 + (lane - 2) < w3;
+                        const bool ok = own_lane && c3 + (lane - 2) < w3;
                         uint8_t* q = P + L.off[2] + c3 + (lane - 2) + PAD;
                         const int mr = mirror_row(r3, h3);
                         if constexpr ((SKIP & 4) != 0) {
                             nsink ^= s3 << 13;
-                        } else {
+                        } else if (k >= 12 && r3 >= o3lo && r3 < o3hi) {
                             *(ok ? q + (int64_t)(r3 + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
-                            *(ok && mr != r3 ? q + (int64_t)(mr + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
+                            if (mr != r3) *(ok ? q + (int64_t)(mr + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
                         }
                     }
                 }
@@ -692,7 +704,25 @@ struct RingLevels {
     int32_t items[MAX_LEVELS];  // ring dwords of the level
 };
 
-// Item = one dword of ring.  Full ring: the top / bottom PAD rows over the
+// One ring dword at padded byte column pcol of padded row prow.  Inside the
+// level it is a plain copy (last interior dword of a row: its own bytes); outside,
+// the four REFLECT_101 source columns span at most 4 consecutive bytes
+// (descending, or folded at the right edge), so two aligned dwords and one
+// v_perm with a computed selector build it.
+__device__ __forceinline__ uint32_t ring_dword(const uint32_t* rw, int pcol, int w) {
+    const int x0 = pcol - PAD;
+    if (x0 >= 0 && x0 + 4 <= w) return rw[pcol >> 2];
+    int sx[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) sx[b] = refl(min(x0 + b, w + PAD - 1), w) + PAD;
+    const int lo = min(min(sx[0], sx[1]), min(sx[2], sx[3])) & ~3;
+    uint32_t sel = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) sel |= (uint32_t)(sx[b] - lo) << (8 * b);
+    return __builtin_amdgcn_perm(rw[(lo >> 2) + 1], rw[lo >> 2], sel);
+}
+
+// Item = one ring dword.  Full ring: the top / bottom PAD rows over the
 // padded width, then the side bands of the interior rows.  Side-bands-only
 // levels: the left PAD columns and the right columns [w, w+PAD) of every padded
 // row (ring rows included: their sources are interior pixels).  Bytes of the
@@ -716,21 +746,8 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
         prow = R.sides[l] ? r : PAD + r;
         pcol = c < PAD / 4 ? 4 * c : 4 * (R.rd0[l] + c - PAD / 4);
     }
-    const int sy = refl(prow - PAD, h) + PAD;
-    const int x0 = pcol - PAD;
-    uint32_t v;
-    if (x0 >= 0 && x0 + 4 <= w) {
-        v = *reinterpret_cast<const uint32_t*>(base + (int64_t)sy * pitch + pcol);
-    } else {
-        v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int x = x0 + b;
-            if (x >= w + PAD) break;  // past the ring (pitch slack): leave 0
-            v |= (uint32_t)base[(int64_t)sy * pitch + refl(x, w) + PAD] << (8 * b);
-        }
-    }
-    *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = v;
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(base + (int64_t)(refl(prow - PAD, h) + PAD) * pitch);
+    *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = ring_dword(rw, pcol, w);
 }
 
 template <int NL>
@@ -809,7 +826,8 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
     if (n_img <= 0) return hipSuccess;
     // level-0 slot of the pyramid: pixel (0,0) of image 0
     uint8_t* slot0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
-    const bool aligned = stride % 4 == 0 && img_stride % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 4 == 0;
+    const bool aligned = stride % 4 == 0 && img_stride % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 4 == 0 &&
+                         lay.w[0] % 4 == 0;
     const uint8_t* s0 = src;
     int64_t s0_img = img_stride;
     int s0_pitch = stride;
@@ -825,9 +843,11 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         s0_pitch = lay.pitch[0];
     } else {
         // read level 0 in place; only its edge bands go to the (otherwise unused) slot
-        dim3 grid((lay.h[0] * 12 + 255) / 256, n_img);
+        const int vec16 = stride % 16 == 0 && img_stride % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                          lay.w[0] % 16 == 0 && reinterpret_cast<uintptr_t>(slot0) % 16 == 0 && lay.pitch[0] % 16 == 0;
+        dim3 grid((lay.h[0] * 6 + 255) / 256, n_img);
         hipLaunchKernelGGL(edge_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride, lay.w[0], lay.h[0],
-                           slot0, lay.bytes, lay.pitch[0]);
+                           slot0, lay.bytes, lay.pitch[0], vec16);
     }
     // levels 1.. in streaming passes of up to 3 levels; a later pass reads the
     // previous pass's deepest level (padded, its ring built first)

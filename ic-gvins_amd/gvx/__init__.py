@@ -104,6 +104,7 @@ def _declare(L):
         "gvx_frame_put": (i32, [P, u64, P, i32, i32, i32, C.POINTER(KltParams)]),
         "gvx_frame_drop": (i32, [P, u64]),
         "gvx_frame_level": (i32, [P, u64, i32, P, C.POINTER(i32), C.POINTER(i32)]),
+        "gvx_frame_level_padded": (i32, [P, u64, i32, i32, P]),
         "gvx_klt": (i32, [P, u64, u64, P, P, P, P, i32, C.POINTER(KltParams)]),
         "gvx_klt_fb": (i32, [P, u64, u64, P, P, P, P, P, P, P, P, i32, f64, f64, i32, i32,
                              C.POINTER(KltParams)]),
@@ -211,6 +212,15 @@ class Context:
                     "frame_level")
         out = np.empty((h.value, w.value), np.uint8)
         self._check(self._L.gvx_frame_level(self._h, fid, level, _ptr(out), None, None), "frame_level")
+        return out
+
+    def frame_level_padded(self, fid: int, level: int, pad: int = 32) -> np.ndarray:
+        """Level `level` with its REFLECT_101 border of `pad` pixels."""
+        w, h = C.c_int32(), C.c_int32()
+        self._check(self._L.gvx_frame_level(self._h, fid, level, None, C.byref(w), C.byref(h)),
+                    "frame_level")
+        out = np.empty((h.value + 2 * pad, w.value + 2 * pad), np.uint8)
+        self._check(self._L.gvx_frame_level_padded(self._h, fid, level, pad, _ptr(out)), "frame_level_padded")
         return out
 
     # ------------------------------------------------------------------ KLT

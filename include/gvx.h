@@ -117,6 +117,13 @@ gvx_status gvx_klt_fb_batch(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h,
 gvx_status gvx_frame_level(gvx_ctx* ctx, uint64_t id, int32_t level, uint8_t* out, int32_t* w,
                            int32_t* h);
 
+/* The same level with its BORDER_REFLECT_101 border of `pad` pixels
+   (0 <= pad <= GVX_PYR_PAD), (w_l + 2 pad) x (h_l + 2 pad) bytes, tightly packed:
+   the padded pyramid buildOpticalFlowPyramid(..., pyrBorder = BORDER_REFLECT_101)
+   hands to calcOpticalFlowPyrLK (the level plus its ring). */
+#define GVX_PYR_PAD 32
+gvx_status gvx_frame_level_padded(gvx_ctx* ctx, uint64_t id, int32_t level, int32_t pad, uint8_t* out);
+
 /* ------------------------------------------------------ feature detection */
 /* Tracking::featuresDetection (tracking/tracking.cc:576-688): block grid from
    the Tracking ctor (:65-85), FILLED circle mask of radius

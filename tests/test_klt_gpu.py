@@ -31,6 +31,18 @@ def test_pyramid_levels_bit_exact(ctx, orc, gvx_mod, w, h, L):
     ctx.frame_drop(7)
 
 
+@pytest.mark.parametrize("w,h,L", [(160, 70, 3), (161, 71, 3), (1280, 560, 3), (333, 97, 2), (130, 44, 1)])
+def test_pyramid_rings_reflect101(ctx, orc, gvx_mod, w, h, L):
+    """The padded levels LK reads: every level with its 32-pixel REFLECT_101 ring
+    (numpy "reflect" = BORDER_REFLECT_101) around the oracle's level."""
+    img = synth.make_image(w, h, np.random.default_rng(3 * w + h))
+    p = gvx_mod.KltParams.default(max_level=L)
+    ctx.frame_put(9, img, p)
+    for l, r in enumerate(orc.build_pyramid(img, L)):
+        _assert_same(ctx.frame_level_padded(9, l, 32), np.pad(r, 32, mode="reflect"), f"padded level {l}")
+    ctx.frame_drop(9)
+
+
 @pytest.mark.parametrize("w,h,n,L,seed", [(160, 70, 32, 3, 1), (320, 140, 64, 3, 2),
                                           (1280, 560, 150, 3, 20261015), (1920, 1200, 500, 4, 5)])
 def test_calc_optical_flow_bit_exact(ctx, orc, gvx_mod, w, h, n, L, seed):

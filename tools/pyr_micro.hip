@@ -2,7 +2,7 @@
 // 256 random 1280x560 images; the streaming pass with and without its stores,
 // the edge-band and ring kernels, and a plain streaming read of the same bytes.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off
-//        -I include -I ic-gvins_amd/csrc tools/pyr_micro.hip -o tools/pyr_micro
+//        -Wno-unused-result -I include -I ic-gvins_amd/csrc tools/pyr_micro.hip -o tools/pyr_micro
 #include "../ic-gvins_amd/csrc/pyramid.hip"
 
 #include <cstdio>
@@ -41,7 +41,7 @@ float timeit(F f, int reps) {
 int main() {
     const int w = 1280, h = 560, n = 256, reps = 20;
     hipDeviceProp_t prop;
-    hipGetDeviceProperties(&prop, 0);
+    (void)hipGetDeviceProperties(&prop, 0);
     PyrLayout lay = make_layout(w, h, 3, 21);
     std::vector<uint8_t> img((size_t)w * h * n);
     uint32_t x = 12345;
@@ -70,8 +70,8 @@ int main() {
         printf("read_all %5d blocks  %8.1f us  %6.2f TB/s\n", blocks, us, img.size() / us / 1e6);
     }
     printf("edge_kernel            %8.1f us\n", timeit([&] {
-        hipLaunchKernelGGL(edge_kernel, dim3((h * 12 + 255) / 256, n), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h,
-                           slot0, lay.bytes, lay.pitch[0]);
+        hipLaunchKernelGGL(edge_kernel, dim3((h * 6 + 255) / 256, n), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h,
+                           slot0, lay.bytes, lay.pitch[0], 1);
     }, reps));
     auto run3 = [&](auto skip_c, const char* what) {
         constexpr int SK = decltype(skip_c)::value;
