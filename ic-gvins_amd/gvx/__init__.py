@@ -118,6 +118,11 @@ def _declare(L):
         "gvx_preint_factor_eval": (i32, [P, i32, P, P, i32, P, P, i32, P, P, P]),
         "gvx_preint_factor_eval_dev": (i32, [P, i32, P, P, P, P, P, P, P]),
         "gvx_reproj_eval": (i32, [P, i32, P, P, i32, P, P, P]),
+        "gvx_factor_set_create": (i32, [P, i32, P, P, i32, P, P, i32, P, P, i32, P, P, P]),
+        "gvx_factor_set_destroy": (None, [P]),
+        "gvx_factors_prepare": (i32, [P, i32]),
+        "gvx_factor_read_reproj": (i32, [P, i32, P, P]),
+        "gvx_factor_read_preint": (i32, [P, i32, P, P]),
         "gvx_reproj_eval_dev": (i32, [P, i32, P, P, P, P, P]),
         "gvx_detect_params_default": (None, [C.POINTER(DetectParams)]),
         "gvx_detect": (i32, [P, u64, P, i32, P, i32, i32, i32, C.POINTER(DetectParams), P, P, C.POINTER(i32)]),
@@ -378,3 +383,76 @@ def earth_iewn(origin, local) -> np.ndarray:
     out = np.zeros(3)
     lib().gvx_earth_iewn(_ptr(o), _ptr(l_), _ptr(out))
     return out
+
+
+class FactorSet:
+    """Two-phase factor evaluation (gvx_factor_set_* / gvx_factors_prepare /
+    gvx_factor_read_*): the Ceres EvaluationCallback pattern.  `blocks` are the
+    caller's float64 parameter blocks; prepare() re-reads them in place, like
+    PrepareForEvaluation after Ceres has written a candidate point."""
+
+    RP_SIZES = (7, 7, 7, 1, 1)
+    PF_SIZES = (7, 9, 7, 9)
+
+    def __init__(self, ctx: "Context", blocks, reproj_consts=None, r_blocks=None, pre=None, pn=None,
+                 pn_off=None, p_blocks=None):
+        self._ctx = ctx
+        self._blocks = [b for b in blocks]
+        for b in self._blocks:
+            if not (isinstance(b, np.ndarray) and b.dtype == np.float64 and b.flags.c_contiguous):
+                raise GvxError("parameter blocks must be C-contiguous float64 arrays")
+        nb = len(self._blocks)
+        self._ptrs = (C.c_void_p * nb)(*[b.ctypes.data for b in self._blocks])
+        self._sizes = np.array([b.size for b in self._blocks], np.int32)
+        rc = np.ascontiguousarray(reproj_consts if reproj_consts is not None else np.zeros(0, REPROJ_DTYPE),
+                                  dtype=REPROJ_DTYPE)
+        self.n_reproj = rc.shape[0]
+        rb = np.ascontiguousarray(r_blocks if r_blocks is not None else np.zeros((0, 5)), np.int32).reshape(-1, 5)
+        pr = np.ascontiguousarray(pre if pre is not None else np.zeros(0, PREINT_DTYPE), dtype=PREINT_DTYPE)
+        self.n_preint = pr.shape[0]
+        pb = np.ascontiguousarray(p_blocks if p_blocks is not None else np.zeros((0, 4)), np.int32).reshape(-1, 4)
+        pnn = np.ascontiguousarray(pn if pn is not None else np.zeros((0, 4)), np.float64).reshape(-1, 4)
+        pno = np.ascontiguousarray(pn_off if pn_off is not None else np.zeros(self.n_preint), np.int32)
+        h = C.c_void_p()
+        ctx._check(ctx._L.gvx_factor_set_create(ctx._h, nb, self._ptrs, _ptr(self._sizes), self.n_reproj, _ptr(rc),
+                                                _ptr(rb), self.n_preint, _ptr(pr), _ptr(pnn), pnn.shape[0],
+                                                _ptr(pno), _ptr(pb), C.byref(h)), "gvx_factor_set_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._ctx._L.gvx_factor_set_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prepare(self, jacobians: bool = True):
+        self._ctx._check(self._ctx._L.gvx_factors_prepare(self._h, 1 if jacobians else 0), "gvx_factors_prepare")
+
+    def _read(self, fn, i, n_res, sizes, jacobians):
+        res = np.zeros(n_res)
+        if jacobians is False or jacobians is None:
+            s = fn(self._h, i, _ptr(res), None)
+            if s != GVX_OK:
+                raise GvxError(f"factor read {i}: {self._ctx._L.gvx_status_string(s).decode()}")
+            return res, None
+        want = [True] * len(sizes) if jacobians is True else list(jacobians)
+        J = [np.zeros((n_res, k)) if w else None for w, k in zip(want, sizes)]
+        arr = (C.c_void_p * len(sizes))(*[j.ctypes.data if j is not None else None for j in J])
+        s = fn(self._h, i, _ptr(res), arr)
+        if s != GVX_OK:
+            raise GvxError(f"factor read {i}: {self._ctx._L.gvx_status_string(s).decode()}")
+        return res, J
+
+    def read_reproj(self, i: int, jacobians=True):
+        """(residuals[2], [J_pose_ref 2x7, J_pose_obs 2x7, J_ext 2x7, J_invdepth 2x1, J_td 2x1]);
+        jacobians: True, False, or a per-block list of booleans (False -> null block)."""
+        return self._read(self._ctx._L.gvx_factor_read_reproj, i, 2, self.RP_SIZES, jacobians)
+
+    def read_preint(self, i: int, jacobians=True):
+        """(residuals[15], [J_pose0 15x7, J_mix0 15x9, J_pose1 15x7, J_mix1 15x9])."""
+        return self._read(self._ctx._L.gvx_factor_read_preint, i, 15, self.PF_SIZES, jacobians)

@@ -235,6 +235,42 @@ gvx_status gvx_reproj_eval_dev(gvx_ctx* ctx, int32_t n, const gvx_reproj_const* 
                                const double* d_params, const int32_t* d_offs,
                                double* d_residuals, double* d_jacobians);
 
+/* ------------------------------------------- two-phase factor evaluation */
+/* The Ceres EvaluationCallback pattern: a factor set holds one
+   sliding window's factors; gvx_factors_prepare (called from
+   ceres::EvaluationCallback::PrepareForEvaluation, after Ceres has written the
+   candidate point into the user's parameter blocks) gathers the parameter
+   blocks, evaluates every factor's residuals (and Jacobians) in one pass on the
+   device and keeps the results in host memory owned by the set; each
+   CostFunction::Evaluate then copies its slice with gvx_factor_read_*.
+
+   Parameter blocks are host arrays registered once: blocks[b] points at
+   block_sizes[b] doubles (the user's state / landmark storage, read at every
+   prepare).  Reprojection factor i uses blocks r_blocks[5i+k] (pose_ref 7,
+   pose_obs 7, ext 7, invdepth 1, td 1); preintegration factor i uses pre[i],
+   its pn list at pn[4*pn_off[i]] (Earth) and blocks p_blocks[4i+k] (pose0 7,
+   mix0 9, pose1 7, mix1 9).  The set keeps copies of the constants. */
+typedef struct gvx_factor_set gvx_factor_set;
+
+gvx_status gvx_factor_set_create(gvx_ctx* ctx, int32_t n_blocks, const double* const* blocks,
+                                 const int32_t* block_sizes, int32_t n_reproj, const gvx_reproj_const* rc,
+                                 const int32_t* r_blocks, int32_t n_preint, const gvx_preint_result* pre,
+                                 const double* pn, int32_t n_pn, const int32_t* pn_off,
+                                 const int32_t* p_blocks, gvx_factor_set** out);
+void gvx_factor_set_destroy(gvx_factor_set* set);
+
+/* Phase 1: evaluate every factor at the current block values (with_jacobians
+   0: residuals only).  Synchronous; not to be overlapped with reads. */
+gvx_status gvx_factors_prepare(gvx_factor_set* set, int32_t with_jacobians);
+
+/* Phase 2: factor i's residuals and Jacobian blocks in the Ceres layout
+   (row-major num_residuals x block_size); jacobians and any jacobians[k] may
+   be NULL.  Reads only the set's host buffers: reentrant and lock-free, safe
+   from concurrent Ceres worker threads.  GVX_ERR_INVALID if Jacobians are asked
+   for after a residual-only prepare, or for an index out of range. */
+gvx_status gvx_factor_read_reproj(const gvx_factor_set* set, int32_t i, double* residuals, double** jacobians);
+gvx_status gvx_factor_read_preint(const gvx_factor_set* set, int32_t i, double* residuals, double** jacobians);
+
 #ifdef __cplusplus
 }
 #endif

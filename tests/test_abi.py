@@ -46,8 +46,8 @@ def test_params_defaults_match_reference(gvx_mod):
 
 
 def test_no_cpu_fallback_without_device(gvx_mod):
-    import torch
-    if torch.cuda.is_available():
-        pytest.skip("device present")
+    import os
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("device present (the ROCm kernel driver is there)")
     with pytest.raises(gvx_mod.GvxError):
         gvx_mod.Context(0)
