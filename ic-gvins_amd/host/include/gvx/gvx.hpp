@@ -451,4 +451,60 @@ private:
     gvx_reproj_const c_{};
 };
 
+// ------------------------------------------------- two-phase factor set
+// The EvaluationCallback pattern: register the window's
+// parameter blocks and factors once; prepare() from
+// ceres::EvaluationCallback::PrepareForEvaluation evaluates everything on the
+// device; each CostFunction::Evaluate reads its slice (reentrant).
+class FactorSet {
+public:
+    struct ReprojFactor {
+        gvx_reproj_const c;
+        int32_t blocks[5];  // pose_ref, pose_obs, ext, invdepth, td (indices into the block table)
+    };
+    struct PreintFactor {
+        Preintegration* pre;  // integrated segment (its result and pn list are copied at construction)
+        int32_t blocks[4];    // pose0, mix0, pose1, mix1
+    };
+    FactorSet(Context& ctx, const std::vector<double*>& blocks, const std::vector<int32_t>& sizes,
+              const std::vector<ReprojFactor>& reproj, const std::vector<PreintFactor>& preint)
+        : ctx_(&ctx) {
+        std::vector<gvx_reproj_const> rc;
+        std::vector<int32_t> rb, pb, pn_off;
+        for (const auto& f : reproj) {
+            rc.push_back(f.c);
+            rb.insert(rb.end(), f.blocks, f.blocks + 5);
+        }
+        std::vector<gvx_preint_result> pre;
+        std::vector<double> pn;
+        for (const auto& f : preint) {
+            pre.push_back(f.pre->raw());
+            pn_off.push_back((int32_t)(pn.size() / 4));
+            const std::vector<double>& l = f.pre->pn();
+            pn.insert(pn.end(), l.begin(), l.end());
+            pb.insert(pb.end(), f.blocks, f.blocks + 4);
+        }
+        std::vector<const double*> cb(blocks.begin(), blocks.end());
+        check(gvx_factor_set_create(ctx.get(), (int32_t)cb.size(), cb.data(), sizes.data(), (int32_t)rc.size(),
+                                    rc.data(), rb.data(), (int32_t)pre.size(), pre.data(), pn.data(),
+                                    (int32_t)(pn.size() / 4), pn_off.data(), pb.data(), &set_),
+              ctx.get(), "gvx_factor_set_create");
+    }
+    ~FactorSet() { gvx_factor_set_destroy(set_); }
+    FactorSet(const FactorSet&) = delete;
+    FactorSet& operator=(const FactorSet&) = delete;
+
+    void prepare(bool jacobians) { check(gvx_factors_prepare(set_, jacobians ? 1 : 0), ctx_->get(), "prepare"); }
+    bool readReprojection(int i, double* residuals, double** jacobians) const {
+        return gvx_factor_read_reproj(set_, i, residuals, jacobians) == GVX_OK;
+    }
+    bool readPreintegration(int i, double* residuals, double** jacobians) const {
+        return gvx_factor_read_preint(set_, i, residuals, jacobians) == GVX_OK;
+    }
+
+private:
+    Context* ctx_;
+    gvx_factor_set* set_ = nullptr;
+};
+
 }  // namespace gvx

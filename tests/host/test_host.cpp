@@ -141,6 +141,36 @@ int main(int argc, char** argv) {
     double* rj[5] = {rr.data() + 2, rr.data() + 16, rr.data() + 30, rr.data() + 44, rr.data() + 46};
     rf.Evaluate(rb, rr.data(), rj);
     writef(d + "rf.bin", rr.data(), rr.size());
+
+    // two-phase FactorSet over the same blocks (EvaluationCallback pattern): the
+    // reprojection factor and the (reintegrated) preintegration factor; every
+    // slice must equal the single-factor Evaluate
+    std::vector<double> b_pose_ref(rp.begin(), rp.begin() + 7), b_pose_obs(rp.begin() + 7, rp.begin() + 14),
+        b_ext(rp.begin() + 14, rp.begin() + 21), b_inv(1, rp[21]), b_td(1, rp[22]);
+    std::vector<double> b_p0(fp.begin(), fp.begin() + 7), b_m0(fp.begin() + 7, fp.begin() + 16),
+        b_p1(fp.begin() + 16, fp.begin() + 23), b_m1(fp.begin() + 23, fp.begin() + 32);
+    std::vector<double*> tbl = {b_pose_ref.data(), b_pose_obs.data(), b_ext.data(), b_inv.data(), b_td.data(),
+                                b_p0.data(), b_m0.data(), b_p1.data(), b_m1.data()};
+    std::vector<int32_t> tsz = {7, 7, 7, 1, 1, 7, 9, 7, 9};
+    gvx::FactorSet::ReprojFactor frp{rf.constants(), {0, 1, 2, 3, 4}};
+    gvx::FactorSet::PreintFactor fpf{&pre, {5, 6, 7, 8}};
+    gvx::FactorSet fs(ctx, tbl, tsz, {frp}, {fpf});
+    fs.prepare(true);
+    std::vector<double> sr(2 + 46);
+    double* sj[5] = {sr.data() + 2, sr.data() + 16, sr.data() + 30, sr.data() + 44, sr.data() + 46};
+    if (!fs.readReprojection(0, sr.data(), sj) || sr != rr) {
+        std::printf("FAIL factor set reprojection\n");
+        return 1;
+    }
+    gvx::PreintegrationFactor pf2(pre);
+    std::vector<double> r2(15), k0(105), k1(135), k2(105), k3(135), q(15), q0(105), q1(135), q2(105), q3(135);
+    double* kj[4] = {k0.data(), k1.data(), k2.data(), k3.data()};
+    double* qj[4] = {q0.data(), nullptr, q2.data(), q3.data()};  // a null block is skipped
+    pf2.Evaluate(blocks, r2.data(), kj);
+    if (!fs.readPreintegration(0, q.data(), qj) || q != r2 || q0 != k0 || q2 != k2 || q3 != k3) {
+        std::printf("FAIL factor set preintegration\n");
+        return 1;
+    }
     std::printf("OK\n");
     return 0;
 }
