@@ -48,7 +48,7 @@ def algorithmic_bytes(w, h, levels, n):
     return 2 * a0 + 4 * ap + 16 * (a0 + ap) + 58 * n
 
 
-def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1):
+def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False):
     """Oracle (C restatement) on the reference's 4-call pattern (each
     calcOpticalFlowPyrLK rebuilds both pyramids; LK points split over `threads`
     like OpenCV's parallel_for_), bounded sample of about budget_s seconds."""
@@ -60,6 +60,10 @@ def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1):
     half = n // 2  # Tracking::trackMappoint / trackReferencePoint point sets
 
     def frame(I, J, P, Q):
+        if reuse:
+            # baseline (b): the same LK work with each image's pyramid built once
+            orc.klt_fb(I, J, P, Q, params=p, reuse_pyramids=True, nthreads=threads)
+            return
         # tracking.cc:385/390 (map points, fwd + bwd) and :487/493 (reference
         # points): four calcOpticalFlowPyrLK calls, each rebuilding both pyramids
         orc.klt_fb(I, J, P[:half], Q[:half], params=p, reuse_pyramids=False, nthreads=threads)
@@ -72,10 +76,35 @@ def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1):
         frame(I, J, P, Q)
         done += 1
     dt = time.perf_counter() - t0
+    what = ("fwd + bwd LK of all points, each pyramid built once (baseline b)" if reuse else
+            f"({half} map + {n - half} reference points), 4 LK calls each rebuilding both pyramids "
+            f"(tracking.cc:385,390,487,493)")
     return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{done} frame pairs {w}x{h}/{n} feat ({half} map + {n - half} reference points), "
-                      f"4 LK calls each rebuilding both pyramids (tracking.cc:385,390,487,493), "
-                      f"{threads} thread(s), {dt:.1f} s"}
+            "sample": f"{done} frame pairs {w}x{h}/{n} feat {what}, {threads} thread(s), {dt:.1f} s"}
+
+
+def cpu_factor_baseline(prob, segs, states, iewn, params, poffs, threads, budget_s=3.0):
+    """Oracle factor evaluation of one sliding window (every reprojection and
+    preintegration factor, residuals + Jacobians) on `threads` host threads,
+    bounded to about budget_s seconds -> factor evals/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # test-infrastructure import: cpu_baseline leg only
+    from gvx import synth_ba
+    prm = orc.imu_params(*synth_ba.imu_params())
+    osegs = [orc.PreintSeg(2, prm, segs[k], orc.make_state(float(st["time"]), st["p"], st["q"], st["v"],
+                                                           st["bg"], st["ba"]), iewn[k])
+             for k, st in enumerate(states)]
+    n = len(prob["consts"]) + len(osegs)
+    orc.reproj_eval_batch(prob["consts"], params, prob["offs"], nthreads=threads)  # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        orc.reproj_eval_batch(prob["consts"], params, prob["offs"], nthreads=threads)
+        orc.preint_factor_eval_batch(osegs, params, poffs, nthreads=threads)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done * n / dt, "unit": "factor evals/s", "cores": threads, "kind": "port",
+            "sample": f"{done} windows x {n} factors ({len(prob['consts'])} reprojection + {len(osegs)} Earth "
+                      f"preintegration, M=100, residuals + Jacobians), {threads} thread(s), {dt:.1f} s"}
 
 
 def traffic_for(workload):
@@ -213,6 +242,9 @@ def main():
         if world == 1 and not args.no_cpu:
             nt = host_threads()
             cpu = cpu_baseline(W, H, N, L, args.cpu_budget, threads=nt)
+            reuse = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=nt, reuse=True)
+            cpu["reuse_value"] = reuse["value"]
+            cpu["reuse_sample"] = reuse["sample"]
             if nt > 1:
                 one = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=1)
                 cpu["single_thread_value"] = one["value"]
@@ -359,6 +391,34 @@ def factors_main(args):
 
     el, fam = timed(step, args.steps)
     el_i, fam_i = timed(integ, max(1, args.steps // 4))
+
+    # one window at problem size (1800 + 9 factors, latency-bound): device-pointer
+    # launches, and the two-phase FactorSet prepare (block gather, H2D, both
+    # kernels, D2H) that a Ceres EvaluationCallback would call per LM iteration
+    n_w = n_rp + (n_kf - 1)
+
+    def window():
+        ctx.reproj_eval_dev(n_rp, d_consts.data_ptr(), d_params.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(),
+                            d_jac.data_ptr())
+        ctx.preint_factor_eval_dev(n_kf - 1, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
+                                   d_params.data_ptr(), d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr())
+
+    k_w = max(50, args.steps)
+    el_w, _ = timed(window, k_w)
+    # parameter blocks as views of the packed vector (the layout the offsets index)
+    starts = sorted({int(v) for v in prob["offs"].ravel()} | {int(v) for v in poffs.ravel()})
+    sizes = {}
+    for o, sz in zip(prob["offs"].T, (7, 7, 7, 1, 1)):
+        sizes.update({int(v): sz for v in o})
+    for o, sz in zip(poffs.T, (7, 9, 7, 9)):
+        sizes.update({int(v): sz for v in o})
+    bidx = {st: i for i, st in enumerate(starts)}
+    blocks = [params[st:st + sizes[st]] for st in starts]
+    fset = gvx.FactorSet(ctx, blocks, prob["consts"].astype(gvx.REPROJ_DTYPE),
+                         np.vectorize(bidx.get)(prob["offs"]).astype(np.int32), pre, pn, pn_off,
+                         np.vectorize(bidx.get)(poffs).astype(np.int32))
+    el_p, _ = timed(lambda: fset.prepare(True), k_w)
+    fset.close()
     k_i = max(1, args.steps // 4)
     evals = world * (n_r + n_p) * args.steps
     value = evals / el
@@ -381,8 +441,20 @@ def factors_main(args):
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
             "preint_steps_per_s": round(world * S * (M - 1) * k_i / el_i, 1),
             "preint_device_ms_per_launch": round(fam_i["preint"][0] / k_i, 4),
+            "problem_size": {"window_factors": n_w,
+                             "device_launch_evals_per_s": round(world * n_w * k_w / el_w, 1),
+                             "factor_set_prepare_evals_per_s": round(world * n_w * k_w / el_p, 1),
+                             "factor_set_prepare_ms": round(el_p / k_w * 1e3, 4)},
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu:
+            ref = cpu_factor_baseline(prob, segs, states, iewn, params, poffs, threads=4)
+            nt = host_threads()
+            if nt != 4:
+                allc = cpu_factor_baseline(prob, segs, states, iewn, params, poffs, threads=nt)
+                ref["all_cores_value"] = allc["value"]
+                ref["all_cores_sample"] = allc["sample"]
+            line["cpu_baseline"] = ref
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()

@@ -9,6 +9,7 @@
 
 #include "gvx_oracle.h"
 #include "orc_math.h"
+#include "orc_pool.h"
 
 /* C(2x3) = A(2x3) * B(3x3) */
 static void m23m33(const double* A, const double* B, double* C) {
@@ -157,4 +158,54 @@ void orc_pose_plus(const double* x, const double* delta, double* xp) {
     for (int i = 0; i < 3; i++) xp[i] = x[i] + delta[i];
     oq r = oq_normalized(oq_mul(q, dq));
     oq_to_xyzw(r, xp + 3);
+}
+
+/* ------------------------------------------------------------------ batches */
+typedef struct {
+    const orc_reproj_const* c;
+    const double* params;
+    const int* offs;
+    double *res, *jac;
+} reproj_job;
+
+static void reproj_range(void* ctx, int b, int e) {
+    const reproj_job* j = (const reproj_job*)ctx;
+    for (int i = b; i < e; ++i) {
+        const int* o = j->offs + 5 * i;
+        const double* prm[5] = {j->params + o[0], j->params + o[1], j->params + o[2], j->params + o[3],
+                                j->params + o[4]};
+        double* J = j->jac ? j->jac + 46 * (size_t)i : NULL;
+        double* jb[5] = {J, J ? J + 14 : NULL, J ? J + 28 : NULL, J ? J + 42 : NULL, J ? J + 44 : NULL};
+        orc_reproj_eval(j->c + i, prm, j->res + 2 * (size_t)i, J ? jb : NULL);
+    }
+}
+
+void orc_reproj_eval_batch(int n, const orc_reproj_const* c, const double* params, const int* offs,
+                           double* residuals, double* jacobians, int nthreads) {
+    reproj_job j = {c, params, offs, residuals, jacobians};
+    orc_parallel_for(n, nthreads, reproj_range, &j);
+}
+
+typedef struct {
+    const orc_preint* const* segs;
+    const double* params;
+    const int* offs;
+    double *res, *jac;
+} preint_job;
+
+static void preint_range(void* ctx, int b, int e) {
+    const preint_job* j = (const preint_job*)ctx;
+    for (int i = b; i < e; ++i) {
+        const int* o = j->offs + 4 * i;
+        const double* prm[4] = {j->params + o[0], j->params + o[1], j->params + o[2], j->params + o[3]};
+        double* J = j->jac ? j->jac + 480 * (size_t)i : NULL;
+        double* jb[4] = {J, J ? J + 105 : NULL, J ? J + 240 : NULL, J ? J + 345 : NULL};
+        orc_preint_factor_eval(j->segs[i], prm, j->res + 15 * (size_t)i, J ? jb : NULL);
+    }
+}
+
+void orc_preint_factor_eval_batch(int n, const orc_preint* const* segs, const double* params, const int* offs,
+                                  double* residuals, double* jacobians, int nthreads) {
+    preint_job j = {segs, params, offs, residuals, jacobians};
+    orc_parallel_for(n, nthreads, preint_range, &j);
 }

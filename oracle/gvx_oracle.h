@@ -239,6 +239,17 @@ typedef struct {
 void orc_reproj_eval(const orc_reproj_const* c, const double* const* params, double* residual,
                      double** jac);
 
+/* CPU baseline of a solve's factor evaluation (the reference evaluates with
+   Ceres num_threads = 4, ic_gvins.cc:1180): n reprojection factors over packed
+   parameters (factor i: blocks at params + offs[5i+k]); residuals n x 2,
+   jacobians (may be NULL) n x 46 = [J0 | J1 | J2 | J3 | J4]. */
+void orc_reproj_eval_batch(int n, const orc_reproj_const* c, const double* params, const int* offs,
+                           double* residuals, double* jacobians, int nthreads);
+/* n preintegration factors (segments segs[i], blocks at params + offs[4i+k]);
+   residuals n x 15, jacobians (may be NULL) n x 480. */
+void orc_preint_factor_eval_batch(int n, const orc_preint* const* segs, const double* params, const int* offs,
+                                  double* residuals, double* jacobians, int nthreads);
+
 /* PoseParameterization::Plus (pose_parameterization.h:34-49). */
 void orc_pose_plus(const double* x, const double* delta, double* x_plus_delta);
 

@@ -124,6 +124,8 @@ def lib():
                                              C.POINTER(C.c_void_p)]
         L.orc_earth_iewn.argtypes = [P, P, P]
         L.orc_reproj_eval.argtypes = [C.POINTER(ReprojConst), C.POINTER(C.c_void_p), P, C.POINTER(C.c_void_p)]
+        L.orc_reproj_eval_batch.argtypes = [C.c_int, P, P, P, P, P, C.c_int]
+        L.orc_preint_factor_eval_batch.argtypes = [C.c_int, P, P, P, P, P, C.c_int]
         L.orc_pose_plus.argtypes = [P, P, P]
         _lib = L
     return _lib
@@ -364,3 +366,28 @@ def features_detection(img, count_xy=None, mask_xy=None, ismask=True, n_existing
     if n < 0:
         return None, blk[:0]
     return out[:n].copy(), blk[:g.block_cnts]
+
+
+def reproj_eval_batch(consts: np.ndarray, params, offs, jacobians=True, nthreads=1):
+    """n reprojection factors (consts: structured array with the ReprojConst
+    fields) -> (residuals [n,2], jacobians [n,46] or None)."""
+    cs = np.ascontiguousarray(consts)
+    n = cs.shape[0]
+    prm = np.ascontiguousarray(params, np.float64)
+    o = np.ascontiguousarray(offs, np.int32).reshape(n, 5)
+    res = np.zeros((n, 2))
+    jac = np.zeros((n, 46)) if jacobians else None
+    lib().orc_reproj_eval_batch(n, _p(cs), _p(prm), _p(o), _p(res), _p(jac), nthreads)
+    return res, jac
+
+
+def preint_factor_eval_batch(segs, params, offs, jacobians=True, nthreads=1):
+    """n preintegration factors over PreintSeg objects -> (residuals [n,15], jacobians [n,480] or None)."""
+    n = len(segs)
+    ptrs = (C.c_void_p * n)(*[C.addressof(s.s) for s in segs])
+    prm = np.ascontiguousarray(params, np.float64)
+    o = np.ascontiguousarray(offs, np.int32).reshape(n, 4)
+    res = np.zeros((n, 15))
+    jac = np.zeros((n, 480)) if jacobians else None
+    lib().orc_preint_factor_eval_batch(n, C.cast(ptrs, C.c_void_p), _p(prm), _p(o), _p(res), _p(jac), nthreads)
+    return res, jac

@@ -233,3 +233,37 @@ def test_pose_plus_normalises(orc):
     y = orc.pose_plus(x, np.r_[0.1, 0.2, 0.3, 0.01, -0.02, 0.03])
     assert np.linalg.norm(y[3:]) == pytest.approx(1.0, abs=1e-15)
     np.testing.assert_allclose(y[:3], [1.1, 2.2, 3.3])
+
+
+def test_factor_batches_match_single_evaluations(orc):
+    """The threaded CPU-baseline batches (bench.py configs[3] cpu leg) return
+    exactly the single-factor evaluations, for any thread count."""
+    prob = synth_ba.make_ba_problem(n_kf=4, n_lm=12)
+    cs, prm, offs = prob["consts"], prob["params"], prob["offs"]
+    r1, j1 = orc.reproj_eval_batch(cs, prm, offs, nthreads=1)
+    r4, j4 = orc.reproj_eval_batch(cs, prm, offs, nthreads=4)
+    assert np.array_equal(r1, r4) and np.array_equal(j1, j4)
+    for i in (0, 5, len(cs) - 1):
+        c, o = cs[i], offs[i]
+        rc = orc.reproj_const(c["pts0"], c["pts1"], c["vel0"], c["vel1"], c["td0"], c["td1"], c["std"])
+        r, J = orc.reproj_eval(rc, prm[o[0]:o[0] + 7], prm[o[1]:o[1] + 7], prm[o[2]:o[2] + 7],
+                               prm[o[3]:o[3] + 1], prm[o[4]:o[4] + 1])
+        assert np.array_equal(r1[i], r)
+        assert np.array_equal(j1[i], np.concatenate([b.ravel() for b in J]))
+    rng = np.random.default_rng(3)
+    segs, blocks, poffs = [], [], []
+    for k in range(3):
+        st = synth_ba.random_state(rng)
+        s = orc.make_state(float(st["time"]), st["p"], st["q"], st["v"], st["bg"], st["ba"])
+        segs.append(orc.PreintSeg(EARTH, orc.imu_params(*synth_ba.imu_params()),
+                                  synth_ba.make_imu_segment(rng, 30), s, (7e-5, 0.0, -2e-5)))
+        b = [np.r_[st["p"], st["q"]], np.r_[st["v"], st["bg"], st["ba"]],
+             np.r_[st["p"] + 1.0, st["q"]], np.r_[st["v"], st["bg"], st["ba"]]]
+        poffs.append([32 * k, 32 * k + 7, 32 * k + 16, 32 * k + 23])
+        blocks += b
+    pp = np.concatenate(blocks)
+    pr, pj = orc.preint_factor_eval_batch(segs, pp, np.array(poffs), nthreads=2)
+    for k in range(3):
+        r, J = segs[k].evaluate(*blocks[4 * k:4 * k + 4])
+        assert np.array_equal(pr[k], r)
+        assert np.array_equal(pj[k], np.concatenate([b.ravel() for b in J]))
