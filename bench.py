@@ -143,13 +143,17 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
     ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
-    ap.add_argument("--config", type=int, default=1, choices=(1, 3, 4),
+    ap.add_argument("--config", type=int, default=1, choices=(1, 3, 4, 5),
                     help="BASELINE.json config: 1 = 1280x560/150 L3 (default, the metric), "
-                         "3 = 1920x1200/500 L4 batch, 4 = sliding-window BA factor batch")
+                         "3 = 1920x1200/500 L4 batch, 4 = sliding-window BA factor batch, "
+                         "5 = sequence replay (one sequence per GPU, RCCL gather of the tracks)")
+    ap.add_argument("--frames", type=int, default=2000, help="configs[4]: frames per sequence")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
     if args.mock:
         return mock_main(args)
+    if args.config == 5:
+        return sequence_main(args)
     if args.config == 3:
         args.width, args.height, args.features, args.levels = 1920, 1200, 500, 4
     if args.config == 4:
@@ -461,6 +465,146 @@ def factors_main(args):
     ctx.close()
 
 
+def gather_tracks(tracks, counts, dist, dev):
+    """configs[4]'s exchange: every rank's per-frame tracks ([F, N, 2] f32 and
+    [F] counts) to rank 0 in one collective (RCCL gather over xGMI on the GPU
+    box, gloo in the CPU test).  Returns the list of (tracks, counts) per rank
+    on rank 0, None elsewhere."""
+    import torch
+    packed = torch.cat([tracks.reshape(-1).to(torch.float32), counts.to(torch.float32)]).to(dev)
+    if not dist:
+        return [(tracks, counts)]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    bufs = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+    dist.gather(packed, bufs, dst=0)
+    if rank != 0:
+        return None
+    n = tracks.numel()
+    return [(b[:n].reshape(tracks.shape).cpu(), b[n:].to(torch.int32).cpu()) for b in bufs]
+
+
+def sequence_main(args):
+    """configs[4]: one synthetic sequence per GPU (a moving
+    camera over a textured plane, frames rendered into HBM before the timed
+    region).  Per frame, as Tracking::track does: the frame's pyramid once
+    (gvx_frame_put_dev), forward + backward LK of the tracked points from the
+    previous frame with a constant-velocity initial flow, FB + border +
+    compaction (gvx_klt_fb), and block-grid detection (gvx_detect) topping the
+    tracks up to N whenever they drop below it.  After the last frame every
+    rank's per-frame tracks go to rank 0 in one RCCL gather.  A step = one
+    frame per GPU; value = frames of all ranks / max-over-ranks time."""
+    import torch
+    import gvx
+    from gvx import synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    W, H, N, L = args.width, args.height, args.features, args.levels
+    F = max(args.frames, args.warmup + 2)
+    frames, _ = synth.make_sequence(W, H, F, dev, seed=synth.SEED + 7919 * rank)
+    torch.cuda.synchronize()
+    ctx = gvx.Context(local)
+    kp = gvx.KltParams.default(max_level=L)
+    dp = gvx.DetectParams.default(max_features=N)
+    tracks = np.zeros((F, N, 2), np.float32)
+    counts = np.zeros(F, np.int32)
+    stats = {"detect_frames": 0}
+
+    def frame(t, pts, vel):
+        ctx.frame_put_dev(t % 2, frames[t].data_ptr(), W, H, params=kp)
+        if t > 0 and pts.shape[0]:
+            r = ctx.track_fb((t - 1) % 2, t % 2, pts, pts + vel, W, H, params=kp)
+            k = r["kept_idx"]
+            nxt = r["next"][k]
+            vel = nxt - pts[k]
+            pts = nxt
+        if pts.shape[0] < N:
+            corners, _ = ctx.detect(t % 2, pts, pts, True, int(pts.shape[0]), dp)
+            if corners is not None and corners.shape[0]:
+                add = corners[:N - pts.shape[0]]
+                pts = np.concatenate([pts, add]).astype(np.float32)
+                vel = np.concatenate([vel, np.zeros_like(add)]).astype(np.float32)
+            stats["detect_frames"] += 1
+        tracks[t, :pts.shape[0]] = pts
+        counts[t] = pts.shape[0]
+        return pts, vel
+
+    pts, vel = np.zeros((0, 2), np.float32), np.zeros((0, 2), np.float32)
+    t = 0
+    for _ in range(args.warmup):
+        pts, vel = frame(t, pts, vel)
+        t += 1
+    ctx.sync()
+    if dist:
+        dist.barrier()
+    stats["detect_frames"] = 0
+    ctx.profile_reset()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    timed = 0
+    while t < F:
+        pts, vel = frame(t, pts, vel)
+        t += 1
+        timed += 1
+    ctx.sync()
+    gathered = gather_tracks(torch.from_numpy(tracks), torch.from_numpy(counts), dist, dev)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact", "detect")}
+    fam = {k: v for k, v in fam.items() if v[1] > 0}
+    ctx.profile(False)
+    elapsed = max_over_ranks(elapsed, dist, dev)
+    if rank == 0:
+        value = world * timed / elapsed
+        dev_ms = sum(v[0] for v in fam.values()) / timed
+        # the frame-pair unit (SURVEY 8d) with each frame read and its pyramid
+        # built once per sequence frame instead of twice
+        ap, sw, sh = 0, W, H
+        for _ in range(L):
+            sw, sh = (sw + 1) // 2, (sh + 1) // 2
+            ap += sw * sh
+        B = algorithmic_bytes(W, H, L, N) - W * H - 2 * ap
+        achieved = B / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=host_threads())
+            cpu["sample"] += " (per sequence frame, detection not included)"
+        tr = counts[F - timed:]
+        print(json.dumps({
+            "metric": f"KLT sequence frames/sec @{W}x{H},{N} feat (configs[4])", "value": round(value, 2),
+            "unit": "frames/s", "n_gpus": world, "steps": timed, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / timed * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8/i32 windows, f32 solve",
+            "data": "synthetic sequences (moving camera over a band-limited texture, seed 20261015 + 7919*rank)",
+            "config": {"workload": f"configs[4]: one {F}-frame sequence per GPU, {W}x{H} mono, {N} feat, maxLevel "
+                                   f"{L}: per frame pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
+                                   f"RCCL gather of all per-frame tracks to rank 0",
+                       "parallelism": f"sequences sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
+                         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": None, "algorithmic_bytes_per_frame": B,
+                         "device_ms_per_frame": {k: round(v[0] / timed, 4) for k, v in fam.items()}},
+            "cpu_baseline": cpu,
+            "tracks_per_frame_mean": round(float(tr.mean()), 1), "detect_frames": stats["detect_frames"],
+            "gathered_ranks": len(gathered) if gathered else 0,
+        }))
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
 def max_over_ranks(elapsed, dist, dev=None):
     if not dist:
         return elapsed
@@ -473,6 +617,7 @@ def max_over_ranks(elapsed, dist, dev=None):
 def mock_main(args):
     """The launcher contract without a GPU: same rank handling, barrier-bracketed
     timing, max over ranks and rank-0 JSON line; a step is a fixed host sleep.
+    With --config 5 the sequence replay's track gather runs too (gloo).
     Used by tests/test_bench_dist.py (gloo, world_size 2)."""
     import torch
     import torch.distributed as tdist
@@ -493,12 +638,22 @@ def mock_main(args):
         time.sleep(step_s)
     if dist:
         dist.barrier()
+    gathered_ok = None
+    if args.config == 5:
+        F, N = 6, 4
+        tr = torch.full((F, N, 2), float(rank)) + torch.arange(F, dtype=torch.float32)[:, None, None]
+        cn = torch.full((F,), 3 + rank, dtype=torch.int32)
+        g = gather_tracks(tr, cn, dist, torch.device("cpu"))
+        if rank == 0:
+            gathered_ok = len(g) == world and all(
+                bool((gt[:, :, 0] == r + torch.arange(F)[:, None]).all()) and bool((gc == 3 + r).all())
+                for r, (gt, gc) in enumerate(g))
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
     if rank == 0:
         print(json.dumps({"metric": "mock", "value": world * args.pairs * args.steps / elapsed, "unit": "frames/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-                          "scaling": "weak", "elapsed_s": elapsed}))
+                          "scaling": "weak", "elapsed_s": elapsed, "gathered_ok": gathered_ok}))
     if dist:
         dist.destroy_process_group()
 

@@ -266,6 +266,38 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
     return hip_err(c, hipStreamSynchronize(c->stream), "frame_put sync");
 }
 
+gvx_status gvx_frame_put_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_gray, int32_t w, int32_t h,
+                             int32_t stride, const gvx_klt_params* p) {
+    if (!c || !d_gray || w <= 0 || h <= 0 || stride < w) return set_err(c, GVX_ERR_INVALID, "bad frame");
+    gvx_status s = check_klt_params(c, p);
+    if (s) return s;
+    if (w <= WIN || h <= WIN) return set_err(c, GVX_ERR_INVALID, "frame smaller than the window");
+    hipSetDevice(c->device);
+    PyrLayout lay = make_layout(w, h, p->max_level, p->win);
+    Frame& f = c->frames[id];
+    if (!f.pyr || f.lay.bytes < lay.bytes) {
+        if (f.pyr) {
+            hipStreamSynchronize(c->stream);
+            hipFree(f.pyr);
+            f.pyr = nullptr;
+        }
+        hipError_t e = hipMalloc(&f.pyr, lay.bytes);
+        if (e != hipSuccess) {
+            c->frames.erase(id);
+            return hip_err(c, e, "hipMalloc(pyramid)");
+        }
+    }
+    f.lay = lay;
+    f.w = w;
+    f.h = h;
+    hipEvent_t ev{};
+    prof_begin(c, "pyramid", &ev);
+    // the padded level-0 copy reads the caller's device image in place (any stride)
+    hipError_t e = launch_build_pyramids(c, d_gray, (int64_t)h * stride, stride, 1, lay, f.pyr, true);
+    prof_end(c, "pyramid", ev);
+    return hip_err(c, e, "pyramid kernels");
+}
+
 gvx_status gvx_frame_drop(gvx_ctx* c, uint64_t id) {
     if (!c) return GVX_ERR_INVALID;
     auto it = c->frames.find(id);

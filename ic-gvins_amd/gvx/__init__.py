@@ -104,6 +104,7 @@ def _declare(L):
         "gvx_frame_put": (i32, [P, u64, P, i32, i32, i32, C.POINTER(KltParams)]),
         "gvx_frame_drop": (i32, [P, u64]),
         "gvx_frame_level": (i32, [P, u64, i32, P, C.POINTER(i32), C.POINTER(i32)]),
+        "gvx_frame_put_dev": (i32, [P, u64, P, i32, i32, i32, P]),
         "gvx_frame_level_padded": (i32, [P, u64, i32, i32, P]),
         "gvx_klt": (i32, [P, u64, u64, P, P, P, P, i32, C.POINTER(KltParams)]),
         "gvx_klt_fb": (i32, [P, u64, u64, P, P, P, P, P, P, P, P, i32, f64, f64, i32, i32,
@@ -207,6 +208,13 @@ class Context:
         p = params or KltParams.default()
         h, w = g.shape
         self._check(self._L.gvx_frame_put(self._h, fid, _ptr(g), w, h, w, C.byref(p)), "frame_put")
+
+    def frame_put_dev(self, fid: int, d_gray: int, w: int, h: int, stride: Optional[int] = None,
+                      params: Optional[KltParams] = None):
+        """Pyramid of a device-resident image (pointer as int), enqueued without waiting."""
+        p = params or KltParams.default()
+        self._check(self._L.gvx_frame_put_dev(self._h, fid, d_gray, w, h, stride or w, C.byref(p)),
+                    "frame_put_dev")
 
     def frame_drop(self, fid: int):
         self._check(self._L.gvx_frame_drop(self._h, fid), "frame_drop")

@@ -150,3 +150,47 @@ def make_batch(n_pairs: int, w: int, h: int, n: int, seed: int = SEED, distinct:
         idx = np.arange(n_pairs) % m
         I, J, P, Q = I[idx], J[idx], P[idx], Q[idx]
     return I, J, P, Q
+
+
+SEQ_VEL = (1.6, 0.5)  # px / frame
+
+
+def camera_path(t: int):
+    """Similarity of frame t of a synthetic sequence: the camera drifts over a
+    textured plane at SEQ_VEL px/frame with a slow roll (+-1.2 deg) and zoom
+    (+-2 %).  Returns (A, c): texture point = A @ (x - centre) + c."""
+    th = np.deg2rad(1.2) * np.sin(2 * np.pi * t / 700.0)
+    s = 1.0 + 0.02 * np.sin(2 * np.pi * t / 900.0 + 1.0)
+    A = s * np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    return A, np.array([SEQ_VEL[0] * t, SEQ_VEL[1] * t])
+
+
+def make_sequence(w: int, h: int, n_frames: int, device, seed: int = SEED, tex=None):
+    """configs[4]: n_frames u8 frames [F, h, w] of a moving camera
+    over one band-limited texture, rendered on `device` with bilinear resampling
+    (torch.nn.functional.grid_sample) plus +-2 LSB noise.  Returns the frame
+    tensor and the texture (numpy) it was rendered from."""
+    import torch
+    import torch.nn.functional as F
+    rng = np.random.default_rng(seed)
+    tw, th_ = int(w + SEQ_VEL[0] * n_frames) + 1000, int(h + SEQ_VEL[1] * n_frames) + 600
+    if tex is None:
+        tex = make_image(tw, th_, rng)
+    T = torch.from_numpy(tex).to(device=device, dtype=torch.float32)[None, None]
+    out = torch.empty((n_frames, h, w), dtype=torch.uint8, device=device)
+    ys, xs = torch.meshgrid(torch.arange(h, device=device, dtype=torch.float64),
+                            torch.arange(w, device=device, dtype=torch.float64), indexing="ij")
+    xc, yc = xs - (w - 1) / 2.0, ys - (h - 1) / 2.0
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    origin = np.array([(w - 1) / 2.0 + 500.0, (h - 1) / 2.0 + 300.0])
+    for t in range(n_frames):
+        A, c = camera_path(t)
+        c = c + origin
+        tx = A[0, 0] * xc + A[0, 1] * yc + c[0]
+        ty = A[1, 0] * xc + A[1, 1] * yc + c[1]
+        grid = torch.stack([2 * tx / (tw - 1) - 1, 2 * ty / (th_ - 1) - 1], dim=-1)[None].to(torch.float32)
+        v = F.grid_sample(T, grid, mode="bilinear", padding_mode="border", align_corners=True)[0, 0]
+        v = v + torch.randint(-2, 3, v.shape, device=device, generator=gen, dtype=torch.int32).to(v.dtype)
+        out[t] = v.round().clamp(0, 255).to(torch.uint8)
+    return out, tex

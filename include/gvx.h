@@ -71,6 +71,12 @@ void gvx_klt_params_default(gvx_klt_params* p);
    per frame (tracking/tracking.cc:385,390,487,493).  Re-putting an id replaces it. */
 gvx_status gvx_frame_put(gvx_ctx* ctx, uint64_t id, const uint8_t* gray, int32_t w, int32_t h,
                          int32_t stride, const gvx_klt_params* p);
+
+/* The same from an image already in device memory (d_gray, row stride in
+   bytes): the pyramid build is enqueued on the context stream and the call
+   returns without waiting (sequence replay with frames resident in HBM). */
+gvx_status gvx_frame_put_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_gray, int32_t w, int32_t h,
+                             int32_t stride, const gvx_klt_params* p);
 gvx_status gvx_frame_drop(gvx_ctx* ctx, uint64_t id);
 
 /* One cv::calcOpticalFlowPyrLK(prev, next, prevPts, nextPts, status, err, ...)

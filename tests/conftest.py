@@ -41,6 +41,11 @@ def orc():
 
 @pytest.fixture(scope="session")
 def ctx(gvx_mod):
+    # torch ships its own HIP runtime: bring it up before libgvx's (as bench.py
+    # does), so tests that stage device buffers with torch see the device
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     c = gvx_mod.Context(0)
     yield c
     c.close()

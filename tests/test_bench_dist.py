@@ -31,3 +31,16 @@ def test_bench_mock_two_ranks_gloo():
     # rank 1 sleeps 4 ms per step: the max over ranks must be >= 20 * 4 ms
     assert d["elapsed_s"] >= 0.08
     assert abs(d["value"] - 2 * 8 * 20 / d["elapsed_s"]) < 1e-6 * d["value"]
+
+
+def test_bench_mock_sequence_gather_gloo():
+    """configs[4]'s exchange: per-frame tracks of every rank reach rank 0 intact."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--mock", "--config", "5", "--backend", "gloo", "--gpus", "2", "--steps", "4", "--warmup", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    assert json.loads(lines[0])["gathered_ok"] is True

@@ -173,3 +173,22 @@ def test_batch_border_and_odd_sizes(ctx, orc, gvx_mod, w, h, L):
         flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
         _assert_same(g["flags"][i], flags, f"pair {i} flags")
         _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
+
+
+def test_frame_put_dev_matches_host_put(ctx, gvx_mod):
+    """gvx_frame_put_dev (image already in HBM, any row stride) builds the same
+    padded pyramid as gvx_frame_put."""
+    import torch
+    w, h, stride = 333, 150, 352
+    img = synth.make_image(w, h, np.random.default_rng(5))
+    buf = np.zeros((h, stride), np.uint8)
+    buf[:, :w] = img
+    d = torch.from_numpy(buf).cuda()
+    p = gvx_mod.KltParams.default(max_level=3)
+    ctx.frame_put(21, img, p)
+    ctx.frame_put_dev(22, d.data_ptr(), w, h, stride, p)
+    ctx.sync()
+    for l in range(3):
+        _assert_same(ctx.frame_level_padded(22, l, 32), ctx.frame_level_padded(21, l, 32), f"level {l}")
+    ctx.frame_drop(21)
+    ctx.frame_drop(22)
