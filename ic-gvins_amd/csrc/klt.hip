@@ -708,15 +708,18 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 
 }  // namespace
 
-// Points per wavefront of the LK launch (1, 2 or 4; GVX_KLT_PPW overrides the
-// default for measurements).
-static int klt_ppw() {
-    static const int v = [] {
+// Points per wavefront of the LK launch.  Batches that fill the chip take 2
+// (the per-point scalar work is shared; 0.47 vs 0.61 ms per 256 pairs); small
+// ones (one frame of a sequence: 150 points) take 1, which halves the work of
+// the slowest wave (41 vs 54 us per frame).  GVX_KLT_PPW (1, 2 or 4) forces it.
+static int klt_ppw(int64_t total_points) {
+    static const int forced = [] {
         const char* e = getenv("GVX_KLT_PPW");
-        const int p = e ? atoi(e) : 2;
-        return (p == 1 || p == 2 || p == 4) ? p : 2;
+        const int p = e ? atoi(e) : 0;
+        return (p == 1 || p == 2 || p == 4) ? p : 0;
     }();
-    return v;
+    if (forced) return forced;
+    return total_points < 8192 ? 1 : 2;
 }
 
 template <int PPW>
@@ -737,7 +740,7 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     if (total <= 0) return hipSuccess;
     if (total > (int64_t)1 << 30) return hipErrorInvalidValue;  // wave indices are int32
-    switch (klt_ppw()) {
+    switch (klt_ppw(total)) {
         case 1:
             launch_klt_ppw<1>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
                               back_xy, flags, err);
