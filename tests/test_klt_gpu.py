@@ -192,3 +192,26 @@ def test_frame_put_dev_matches_host_put(ctx, gvx_mod):
         _assert_same(ctx.frame_level_padded(22, l, 32), ctx.frame_level_padded(21, l, 32), f"level {l}")
     ctx.frame_drop(21)
     ctx.frame_drop(22)
+
+
+@pytest.mark.parametrize("n_pairs,n_pts", [(64, 149), (3, 2731)])
+def test_batch_two_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
+    """Launches of >= 8192 points take the two-points-per-wave LK; odd point
+    counts leave a spare lane group in each pair's last wave.  Border points
+    included (the LDS tile gather runs per lane group)."""
+    w, h = 320, 140
+    rng = np.random.default_rng(n_pairs + n_pts)
+    I = np.stack([synth.make_image(w, h, rng) for _ in range(n_pairs)])
+    J = np.stack([np.roll(I[i], (1, -1), axis=(0, 1)) for i in range(n_pairs)])
+    prev = np.stack([np.concatenate([_border_points(w, h, 20, rng),
+                                     rng.uniform([0, 0], [w, h], (n_pts - 20, 2)).astype(np.float32)])
+                     for _ in range(n_pairs)])
+    init = (prev + rng.uniform(-1.0, 1.0, prev.shape)).astype(np.float32)
+    g = ctx.klt_fb_batch(I, J, prev, init)
+    for i in range(0, n_pairs, max(1, n_pairs // 8)):
+        o = orc.klt_fb(I[i], J[i], prev[i], init[i], reuse_pyramids=True)
+        _assert_same(g["next"][i], o["next"], f"pair {i} next")
+        _assert_same(g["back"][i], o["back"], f"pair {i} back")
+        flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
+        _assert_same(g["flags"][i], flags, f"pair {i} flags")
+        _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
