@@ -143,13 +143,16 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
     ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
-    ap.add_argument("--config", type=int, default=1, choices=(1, 3, 4, 5),
-                    help="BASELINE.json config: 1 = 1280x560/150 L3 (default, the metric), "
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5),
+                    help="BASELINE.json config, 1-based as in SURVEY.md 8d: 2 = 1280x560/150 L3 on "
+                         "1 MI355X (default, the metric; 1 is accepted as an alias), "
                          "3 = 1920x1200/500 L4 batch, 4 = sliding-window BA factor batch, "
                          "5 = sequence replay (one sequence per GPU, RCCL gather of the tracks)")
     ap.add_argument("--frames", type=int, default=2000, help="configs[4]: frames per sequence")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
+    if args.config == 1:
+        args.config = 2  # configs[0] is the CPU-only reference case; its GPU twin is configs[1]
     if args.mock:
         return mock_main(args)
     if args.config == 5:
