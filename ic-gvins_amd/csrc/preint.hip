@@ -41,145 +41,71 @@ __device__ __forceinline__ Imu load_imu(const gvx_imu* p, const double* bg, cons
     return r;
 }
 
-// The non-zero structure of Phi for one step (updateJacobianAndCovariance).
+// Quantities of step k that depend only on the IMU samples, the (constant)
+// biases, iewn and the running delta_time -- not on the recursion.  They
+// carry all the transcendental work (rotvec2quaternion) and are computed for
+// CH steps at once, one step per lane, before the sequential part.
+struct StepPre {
+    double dt, time, dtime;    // dt, sample time, delta_time after this step
+    double dvfb[3];            // two-sample sculling (preintegration_base.cc:47-48)
+    double dv[3], dth[3];      // bias-compensated dvel / dtheta (Phi's C and M blocks)
+    double qd[4];              // rotvec2quaternion(dtheta + coning)
+    double qnn[4];             // Earth: rotvec2quaternion(-iewn dt)
+    double qa[4], qb[4];       // Earth: q0^-1 q(-(dtime - dt/2) iewn) q0, q0^-1 q(-dtime iewn) q0
+};
+constexpr int PRE_DW = sizeof(StepPre) / 8;
+
+// Sparse Phi (updateJacobianAndCovariance: preintegration_base.cc:94-125,
+// preintegration_earth.cc:266-303) applied to one column vector; terms in
+// ascending k like the dense product.
 struct Phi {
-    double dt, ndt, f;   // dt, -dt, 1 - dt/corr_time
+    double dt, f;        // Phi(0:3, 3:6) = dt I ; Phi(9:15, 9:15) = (1 - dt/T) I
     double C[9];         // Phi(3:6, 6:9) = cbb0 * skew(dvel)
     double D[9];         // Phi(3:6, 12:15) = cbb0 * dt
-    double M[9];         // Phi(6:9, 6:9) = I - skew(dtheta)
-    double gR[9];        // gt(3:6, 3:6)
-    double g60;          // gt(6:9, 0:3) diagonal
-    double N[12];        // noise diagonal
+    double M[9];         // Phi(6:9, 6:9) = I - skew(dtheta); Phi(6:9, 9:12) = -dt I
 };
 
-// (Phi * X)[i][j], X row-major 15x15 (k ascending over Phi's row i non-zeros)
-__device__ __forceinline__ double phi_left(const Phi& f, const double* X, int i, int j) {
-    if (i < 3) return X[i * NS + j] + f.dt * X[(3 + i) * NS + j];
-    if (i < 6) {
-        const int a = i - 3;
-        double s = X[i * NS + j];
-        s = s + f.C[3 * a] * X[6 * NS + j];
-        s = s + f.C[3 * a + 1] * X[7 * NS + j];
-        s = s + f.C[3 * a + 2] * X[8 * NS + j];
-        s = s + f.D[3 * a] * X[12 * NS + j];
-        s = s + f.D[3 * a + 1] * X[13 * NS + j];
-        s = s + f.D[3 * a + 2] * X[14 * NS + j];
-        return s;
+__device__ __forceinline__ void phi_mv(const Phi& f, const double* v, double* y) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = v[i] + f.dt * v[3 + i];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double s = v[3 + a];
+        s = s + f.C[3 * a] * v[6];
+        s = s + f.C[3 * a + 1] * v[7];
+        s = s + f.C[3 * a + 2] * v[8];
+        s = s + f.D[3 * a] * v[12];
+        s = s + f.D[3 * a + 1] * v[13];
+        s = s + f.D[3 * a + 2] * v[14];
+        y[3 + a] = s;
     }
-    if (i < 9) {
-        const int a = i - 6;
-        double s = f.M[3 * a] * X[6 * NS + j];
-        s = s + f.M[3 * a + 1] * X[7 * NS + j];
-        s = s + f.M[3 * a + 2] * X[8 * NS + j];
-        s = s + f.ndt * X[(9 + a) * NS + j];
-        return s;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double s = f.M[3 * a] * v[6];
+        s = s + f.M[3 * a + 1] * v[7];
+        s = s + f.M[3 * a + 2] * v[8];
+        s = s + (-f.dt) * v[9 + a];
+        y[6 + a] = s;
     }
-    return f.f * X[i * NS + j];
+#pragma unroll
+    for (int i = 9; i < NS; ++i) y[i] = f.f * v[i];
 }
 
-// (X * Phi^T)[i][j] = sum_k X[i][k] Phi[j][k]
-__device__ __forceinline__ double phi_right(const Phi& f, const double* X, int i, int j) {
-    const double* x = X + i * NS;
-    if (j < 3) return x[j] + x[3 + j] * f.dt;
-    if (j < 6) {
-        const int a = j - 3;
-        double s = x[j];
-        s = s + x[6] * f.C[3 * a];
-        s = s + x[7] * f.C[3 * a + 1];
-        s = s + x[8] * f.C[3 * a + 2];
-        s = s + x[12] * f.D[3 * a];
-        s = s + x[13] * f.D[3 * a + 1];
-        s = s + x[14] * f.D[3 * a + 2];
-        return s;
-    }
-    if (j < 9) {
-        const int a = j - 6;
-        double s = x[6] * f.M[3 * a];
-        s = s + x[7] * f.M[3 * a + 1];
-        s = s + x[8] * f.M[3 * a + 2];
-        s = s + x[9 + a] * f.ndt;
-        return s;
-    }
-    return x[j] * f.f;
-}
+constexpr int GL = 16;                  // lanes per segment: lane c owns column c of J and row c of P
+constexpr int SPW = 64 / GL;            // segments per (one-wave) workgroup
+constexpr int CH = GL;                  // steps per precompute chunk (one per lane)
+constexpr int MS = NS * NS;
 
-// Phi[i][k] (dense accessor used by Qk)
-__device__ __forceinline__ double phi_at(const Phi& f, int i, int k) {
-    if (i < 3) return k == i ? 1.0 : (k == 3 + i ? f.dt : 0.0);
-    if (i < 6) {
-        const int a = i - 3;
-        if (k == i) return 1.0;
-        if (k >= 6 && k < 9) return f.C[3 * a + k - 6];
-        if (k >= 12) return f.D[3 * a + k - 12];
-        return 0.0;
-    }
-    if (i < 9) {
-        const int a = i - 6;
-        if (k >= 6 && k < 9) return f.M[3 * a + k - 6];
-        if (k == 9 + a) return f.ndt;
-        return 0.0;
-    }
-    return k == i ? f.f : 0.0;
-}
-
-// t2[i][c] = (Phi * gt)[i][c] * N[c]
-__device__ __forceinline__ double t2_at(const Phi& f, int i, int c) {
-    double t1;
-    if (c < 3)
-        t1 = phi_at(f, i, 6 + c) * f.g60;
-    else if (c < 6) {
-        const int b = c - 3;
-        t1 = phi_at(f, i, 3) * f.gR[b];
-        t1 = t1 + phi_at(f, i, 4) * f.gR[3 + b];
-        t1 = t1 + phi_at(f, i, 5) * f.gR[6 + b];
-    } else if (c < 9)
-        t1 = phi_at(f, i, 9 + c - 6) * 1.0;
-    else
-        t1 = phi_at(f, i, 12 + c - 9) * 1.0;
-    return t1 * f.N[c];
-}
-
-// Qk[i][j] = 0.5 dt (Phi G N G^T + G N G^T Phi^T)[i][j]
-__device__ double qk_at(const Phi& f, int i, int j) {
-    // A = ((Phi gt) N) gt^T
-    double A;
-    if (j < 3)
-        A = 0.0;
-    else if (j < 6) {
-        const int a = j - 3;
-        A = t2_at(f, i, 3) * f.gR[3 * a];
-        A = A + t2_at(f, i, 4) * f.gR[3 * a + 1];
-        A = A + t2_at(f, i, 5) * f.gR[3 * a + 2];
-    } else if (j < 9)
-        A = t2_at(f, i, j - 6) * f.g60;
-    else
-        A = t2_at(f, i, j - 3) * 1.0;
-    // B = ((gt N) gt^T) Phi^T ; G = (gt N) gt^T is block diagonal
-    double B;
-    if (i < 3)
-        B = 0.0;
-    else if (i < 6) {
-        const int a = i - 3;
-        double Gr[3];
-        for (int b = 0; b < 3; ++b) {
-            double g = (f.gR[3 * a] * f.N[3]) * f.gR[3 * b];
-            g = g + (f.gR[3 * a + 1] * f.N[4]) * f.gR[3 * b + 1];
-            g = g + (f.gR[3 * a + 2] * f.N[5]) * f.gR[3 * b + 2];
-            Gr[b] = g;
-        }
-        B = Gr[0] * phi_at(f, j, 3);
-        B = B + Gr[1] * phi_at(f, j, 4);
-        B = B + Gr[2] * phi_at(f, j, 5);
-    } else if (i < 9) {
-        const double g = (f.g60 * f.N[i - 6]) * f.g60;
-        B = g * phi_at(f, j, i);
-    } else {
-        const double g = (1.0 * f.N[i - 3]) * 1.0;
-        B = g * phi_at(f, j, i);
-    }
-    return 0.5 * f.dt * (A + B);
-}
-
+// One wavefront = 4 segments x 16 lanes.  Per IMU step:
+//   * the state recursion (cheap once the StepPre terms exist) runs redundantly
+//     on the 16 lanes of a segment, so Phi's blocks are in every lane's registers;
+//   * J <- Phi J: lane c updates column c (sparse mat-vec, 45 MAC);
+//   * P <- Phi P Phi^T + Qk, Qk = a (Phi W + W Phi^T), a = dt/2, W = gt N gt^T
+//     (block diagonal): lane c writes G(:,c) = Phi P(:,c) to LDS and reads row
+//     c back; with P symmetric, P Phi^T = G^T, so
+//     P'(:,c) = Phi (G(c,:)^T + a W(:,c)) + a W Phi(c,:)^T.
+// Sums are reassociated against the dense Eigen products (relative 1e-16 per
+// step); the parity bound is 1e-10 of each block's magnitude (tests/test_ba_gpu.py).
 __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params prm, int n_seg,
                                                     const gvx_imu* __restrict__ imu,
                                                     const int32_t* __restrict__ seg_off,
@@ -187,19 +113,24 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
                                                     const double* __restrict__ iewn_in,
                                                     gvx_preint_result* __restrict__ out,
                                                     double* __restrict__ pn) {
-    __shared__ double sJ[2][NS * NS];
-    __shared__ double sP[NS * NS];
-    __shared__ double sG[NS * NS];
-    const int seg = blockIdx.x;
-    if (seg >= n_seg) return;
+    __shared__ double sPre[SPW][CH][PRE_DW];
+    __shared__ double sG[SPW][MS];
     const int lane = threadIdx.x;
-    const int b0 = seg_off[seg], m = seg_off[seg + 1] - b0;
+    const int grp = lane / GL, c = lane % GL;
+    const int seg = blockIdx.x * SPW + grp;
+    const bool live = seg < n_seg;
+    const int b0 = live ? seg_off[seg] : 0;
+    const int m = live ? seg_off[seg + 1] - b0 : 0;
+    // wave-uniform trip count over the 4 segments (ragged m)
+    int mmax = m;
+#pragma unroll
+    for (int o = GL; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
     const gvx_imu* im = imu + b0;
-    double* pns = pn ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    double* pns = (pn && live) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
     const bool earth = variant == GVX_PREINT_EARTH;
 
     // ---- constructor: resetState(state, NUM_STATE) + setNoiseMatrix ----
-    gvx_state cur = state0[seg];
+    gvx_state cur = live ? state0[seg] : gvx_state{};
     double dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
     dq dqt = dq_make(1, 0, 0, 0);
     double bg[3], ba[3];
@@ -208,138 +139,213 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
         ba[i] = cur.ba[i];
     }
     const dq q0 = dq_load(cur.q);
+    const dq q0i = dq_inv(q0);
     double iewn[3] = {0, 0, 0};
-    if (earth)
+    if (earth && live)
         for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
     const double g3[3] = {0, 0, prm.gravity};
+    const double ngyr = prm.gyr_arw * prm.gyr_arw, nacc = prm.acc_vrw * prm.acc_vrw;
+    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
+    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
+    const double g60 = earth ? -1.0 : 1.0;
+    const double wg = (g60 * ngyr) * g60;
+    // W's constant diagonal from row 6 on: (g60 N_g g60, N_bg, N_ba)
+    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    double Jc[NS], Pc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        Jc[i] = i == c ? 1.0 : 0.0;
+        Pc[i] = 0.0;
+    }
     double delta_time = 0.0;
-    Phi f;
-    {
-        const double nv[4] = {prm.gyr_arw * prm.gyr_arw, prm.acc_vrw * prm.acc_vrw,
-                              2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time,
-                              2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time};
-        for (int b = 0; b < 4; ++b)
-            for (int i = 0; i < 3; ++i) f.N[3 * b + i] = nv[b];
-    }
-    for (int e = lane; e < NS * NS; e += 64) {
-        const int i = e / NS, j = e - i * NS;
-        sJ[0][e] = i == j ? 1.0 : 0.0;
-        sP[e] = 0.0;
-    }
-    int jb = 0;
-    __syncthreads();
+    double* pre_base = &sPre[grp][0][0];
 
-    for (int k = 1; k < m; ++k) {
-        const Imu pre = load_imu(im + k - 1, bg, ba);
-        const Imu ic = load_imu(im + k, bg, ba);
-        const double dt = ic.dt;
-        delta_time += dt;
-        // dvfb: two-sample sculling (preintegration_base.cc:47-48)
-        double c1[3], c2[3], c3[3], dvfb[3], dth[3];
-        cross3(ic.dth, ic.dv, c1);
-        cross3(pre.dth, ic.dv, c2);
-        cross3(pre.dv, ic.dth, c3);
-        for (int i = 0; i < 3; ++i) dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
-        cross3(pre.dth, ic.dth, c1);
-        for (int i = 0; i < 3; ++i) dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
-        const dq qd = dq_from_rotvec(dth);
-        double R[9], dvel[3];
-        double cbb0[9];
-        if (!earth) {
-            dq_rot(dq_load(cur.q), R);
-            mv3(R, dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + g3[i] * dt;
-            for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
-            dq_store(dq_normalized(dq_mul(dq_load(cur.q), qd)), cur.q);
-            dq_rot(dqt, R);
-            mv3(R, dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
-            dqt = dq_normalized(dq_mul(dqt, qd));
-            dq_rot(dqt, R);
-            for (int i = 0; i < 9; ++i) {
-                cbb0[i] = -R[i];
-                f.gR[i] = R[i];
+    for (int kc = 1; kc < mmax; kc += CH) {
+        // ---- precompute StepPre for steps kc .. kc+CH-1, one per lane ----
+        {
+            const int k = kc + c;
+            StepPre sp;
+            if (k < m) {
+                const Imu pr = load_imu(im + k - 1, bg, ba);
+                const Imu ic = load_imu(im + k, bg, ba);
+                double dtime = delta_time;
+                for (int i = kc; i <= k; ++i) dtime += im[i].dt;  // sequential, as delta_time_ += dt
+                sp.dt = ic.dt;
+                sp.time = ic.time;
+                sp.dtime = dtime;
+                double c1[3], c2[3], c3[3], dth[3];
+                cross3(ic.dth, ic.dv, c1);
+                cross3(pr.dth, ic.dv, c2);
+                cross3(pr.dv, ic.dth, c3);
+                for (int i = 0; i < 3; ++i) sp.dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
+                cross3(pr.dth, ic.dth, c1);
+                for (int i = 0; i < 3; ++i) {
+                    dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
+                    sp.dv[i] = ic.dv[i];
+                    sp.dth[i] = ic.dth[i];
+                }
+                dq_store(dq_from_rotvec(dth), sp.qd);
+                if (earth) {
+                    const double dt = ic.dt;
+                    const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
+                    dq_store(dq_from_rotvec(dnn), sp.qnn);
+                    const double sc = -(dtime - 0.5 * dt);
+                    const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
+                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), sp.qa);
+                    const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
+                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), sp.qb);
+                }
+                const double* w = reinterpret_cast<const double*>(&sp);
+                double* dst = pre_base + c * PRE_DW;
+                for (int i = 0; i < PRE_DW; ++i) dst[i] = w[i];
             }
-            f.g60 = 1.0;
-        } else {
-            double c[3], dvcg[3];
-            cross3(iewn, cur.v, c);
-            for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * c[i]) * dt;
-            const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
-            const dq qnn = dq_from_rotvec(dnn);
-            double Rnn[9], M1[9];
-            dq_rot(qnn, Rnn);
-            for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + Rnn[i]);
-            dq_rot(dq_load(cur.q), R);
-            mm3(M1, R, M1);
-            mv3(M1, dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + dvcg[i];
-            for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
-            if (pns && lane == 0) {
-                pns[4 * (k - 1)] = dt;
-                pns[4 * (k - 1) + 1] = cur.p[0];
-                pns[4 * (k - 1) + 2] = cur.p[1];
-                pns[4 * (k - 1) + 3] = cur.p[2];
-            }
-            dq_store(dq_normalized(dq_mul(dq_mul(qnn, dq_load(cur.q)), qd)), cur.q);
-            const double sc = -(delta_time - 0.5 * dt);
-            const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
-            const dq q0i = dq_inv(q0);
-            dq qm = dq_mul(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), dqt);
-            dq_rot(qm, R);
-            mv3(R, dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
-            dqt = dq_normalized(dq_mul(dqt, qd));
-            // updateJacobianAndCovariance (preintegration_earth.cc:266-303)
-            const double dnn3[3] = {-iewn[0] * delta_time, -iewn[1] * delta_time, -iewn[2] * delta_time};
-            qm = dq_mul(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), dqt);
-            dq_rot(qm, R);
-            for (int i = 0; i < 9; ++i) {
-                cbb0[i] = -R[i];
-                f.gR[i] = cbb0[i];
-            }
-            f.g60 = -1.0;
-        }
-        cur.time = ic.time;
-        // Phi blocks
-        double S[9];
-        skew(ic.dv, S);
-        mm3(cbb0, S, f.C);
-        for (int i = 0; i < 9; ++i) f.D[i] = cbb0[i] * dt;
-        skew(ic.dth, S);
-        for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
-        f.dt = dt;
-        f.ndt = -dt;
-        f.f = 1 - dt / prm.corr_time;
-
-        // J <- Phi J (into the other buffer); G <- Phi P
-        const double* Jc = sJ[jb];
-        double* Jn = sJ[jb ^ 1];
-        for (int e = lane; e < NS * NS; e += 64) {
-            const int i = e / NS, j = e - i * NS;
-            Jn[e] = phi_left(f, Jc, i, j);
-            sG[e] = phi_left(f, sP, i, j);
         }
         __syncthreads();
-        for (int e = lane; e < NS * NS; e += 64) {
-            const int i = e / NS, j = e - i * NS;
-            sP[e] = phi_right(f, sG, i, j) + qk_at(f, i, j);
+        const int kend = min(kc + CH, mmax);
+        for (int k = kc; k < kend; ++k) {
+            const bool act = k < m;
+            Phi f;
+            double Wv[9];
+            if (act) {
+                const StepPre& sp = *reinterpret_cast<const StepPre*>(pre_base + (k - kc) * PRE_DW);
+                const double dt = sp.dt;
+                delta_time = sp.dtime;
+                const dq qd = dq_load(sp.qd);
+                double R[9], dvel[3], cbb0[9];
+                if (!earth) {
+                    // PreintegrationNormal::integrationProcess (preintegration_normal.cc:183-214)
+                    dq_rot(dq_load(cur.q), R);
+                    mv3(R, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + g3[i] * dt;
+                    for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
+                    dq_store(dq_normalized(dq_mul(dq_load(cur.q), qd)), cur.q);
+                    dq_rot(dqt, R);
+                    mv3(R, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
+                    dqt = dq_normalized(dq_mul(dqt, qd));
+                    dq_rot(dqt, R);
+                    for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
+                } else {
+                    // PreintegrationEarth::integrationProcess (preintegration_earth.cc:205-260)
+                    double cc[3], dvcg[3], T[9], M1[9];
+                    cross3(iewn, cur.v, cc);
+                    for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc[i]) * dt;
+                    dq_rot(dq_load(sp.qnn), T);
+                    for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
+                    dq_rot(dq_load(cur.q), R);
+                    mm3(M1, R, T);
+                    mv3(T, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + dvcg[i];
+                    for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
+                    if (pns && c == 0) {
+                        pns[4 * (k - 1)] = dt;
+                        pns[4 * (k - 1) + 1] = cur.p[0];
+                        pns[4 * (k - 1) + 2] = cur.p[1];
+                        pns[4 * (k - 1) + 3] = cur.p[2];
+                    }
+                    dq_store(dq_normalized(dq_mul(dq_mul(dq_load(sp.qnn), dq_load(cur.q)), qd)), cur.q);
+                    dq_rot(dq_mul(dq_load(sp.qa), dqt), R);
+                    mv3(R, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
+                    dqt = dq_normalized(dq_mul(dqt, qd));
+                    dq_rot(dq_mul(dq_load(sp.qb), dqt), R);
+                    for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
+                }
+                cur.time = sp.time;
+                // gt(3:6, 3:6) = R (Normal) or cbb0 (Earth); W(3:6, 3:6) = gR N_v gR^T
+                const double sg = earth ? 1.0 : -1.0;  // gR = sg * cbb0
+                double gR[9];
+                for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) {
+                        double g = (gR[3 * a] * nacc) * gR[3 * b];
+                        g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+                        g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+                        Wv[3 * a + b] = g;
+                    }
+                double S[9];
+                skew(sp.dv, S);
+                mm3(cbb0, S, f.C);
+                for (int i = 0; i < 9; ++i) f.D[i] = cbb0[i] * dt;
+                skew(sp.dth, S);
+                for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+                f.dt = dt;
+                f.f = 1 - dt / prm.corr_time;
+
+                // G(:,c) = Phi P(:,c) to LDS; J <- Phi J
+                double y[NS];
+                phi_mv(f, Pc, y);
+                if (c < NS) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
+                }
+                phi_mv(f, Jc, y);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            }
+            __syncthreads();
+            if (act) {
+                const double a = 0.5 * f.dt;
+                const int cl = c < NS ? c : 0;
+                // K(:,c) = G(c,:)^T + a W(:,c)   (P symmetric: P Phi^T = (Phi P)^T)
+                double K[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
+                if (c >= 3 && c < 6) {
+                    K[3] = K[3] + a * Wv[c - 3];
+                    K[4] = K[4] + a * Wv[3 + c - 3];
+                    K[5] = K[5] + a * Wv[6 + c - 3];
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i)
+                    if (i == c) K[i] = K[i] + a * wd(i);
+                // phi_c = row c of Phi (lane-dependent selects)
+                const int r3 = c - 3, r6 = c - 6;
+                double ph[NS];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    ph[3 + b] = (c == b) ? f.dt : (c == 3 + b ? 1.0 : 0.0);
+                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
+                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
+                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
+                    ph[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
+                    ph[9 + b] = (c == 6 + b) ? -f.dt : (c == 9 + b ? f.f : 0.0);
+                    ph[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (c == 12 + b ? f.f : 0.0);
+                }
+                // P'(:,c) = Phi K(:,c) + a W phi_c
+                double y[NS];
+                phi_mv(f, K, y);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[i] = y[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    double u = Wv[3 * i] * ph[3];
+                    u = u + Wv[3 * i + 1] * ph[4];
+                    u = u + Wv[3 * i + 2] * ph[5];
+                    Pc[3 + i] = y[3 + i] + a * u;
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i) Pc[i] = y[i] + a * (wd(i) * ph[i]);
+            }
+            __syncthreads();
         }
-        jb ^= 1;
-        __syncthreads();
     }
 
     // ---- outputs ----
+    if (!live) return;
     gvx_preint_result* o = out + seg;
-    for (int e = lane; e < NS * NS; e += 64) {
-        o->jacobian[e] = sJ[jb][e];
-        o->covariance[e] = sP[e];
+    if (c < NS) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            o->jacobian[i * NS + c] = Jc[i];
+            o->covariance[c * NS + i] = Pc[i];
+        }
     }
-    if (lane == 0) {
+    if (c == 0) {
         o->variant = variant;
         o->m = m;
         o->delta_time = delta_time;
@@ -368,7 +374,7 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
                          const double* iewn, gvx_preint_result* out, double* pn) {
     if (n_seg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(preint_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, prm, n_seg, imu,
+    hipLaunchKernelGGL(preint_kernel, dim3((n_seg + SPW - 1) / SPW), dim3(64), 0, c->stream, variant, prm, n_seg, imu,
                        seg_off, state0, iewn, out, pn);
     return hipGetLastError();
 }
