@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <map>
@@ -131,6 +132,21 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
                       float* err);
 hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
                           int32_t* n_kept);
+
+// ---- clahe.hip ----
+// CLAHE_Impl::apply geometry for an h x w 8-bit image (oracle/clahe.c).
+struct ClaheGeom {
+    int32_t w, h, tiles_x, tiles_y;
+    int32_t tw, th;      // tile size (of the REFLECT_101-extended LUT source)
+    int32_t clip;        // clipLimit in pixels (0: no clipping)
+    float lut_scale;     // 255.f / (tw*th)
+};
+ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles_y);
+// n images; lut: n*tiles*256 bytes scratch; hist_img (nullable): n*256 u32
+// scratch for the histogram check, whose means go to hist_mean (device).
+hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
+                        int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
+                        uint32_t* hist_img, double* hist_mean);
 
 // ---- preint.hip / factors.hip ----
 hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,

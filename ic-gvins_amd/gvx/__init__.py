@@ -72,6 +72,18 @@ class DetectParams(C.Structure):
         return p
 
 
+class ClaheParams(C.Structure):
+    """cv::createCLAHE(clipLimit, tileGridSize) -- tracking.cc:63 uses (3.0, (21, 21))."""
+    _fields_ = [("clip_limit", C.c_double), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32)]
+
+    @classmethod
+    def default(cls, **kw) -> "ClaheParams":
+        p = cls(3.0, 21, 21)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+
 _lib = None
 
 
@@ -127,6 +139,13 @@ def _declare(L):
         "gvx_reproj_eval_dev": (i32, [P, i32, P, P, P, P, P]),
         "gvx_detect_params_default": (None, [C.POINTER(DetectParams)]),
         "gvx_detect": (i32, [P, u64, P, i32, P, i32, i32, i32, C.POINTER(DetectParams), P, P, C.POINTER(i32)]),
+        "gvx_clahe_params_default": (None, [C.POINTER(ClaheParams)]),
+        "gvx_clahe_batch_dev": (i32, [P, i32, i32, i32, P, i64, i32, P, i64, i32, C.POINTER(ClaheParams), P]),
+        "gvx_clahe": (i32, [P, i32, i32, P, i32, P, i32, C.POINTER(ClaheParams), P]),
+        "gvx_frame_preprocess": (i32, [P, u64, P, i32, i32, i32, C.POINTER(ClaheParams), C.POINTER(KltParams),
+                                       P, P]),
+        "gvx_frame_preprocess_dev": (i32, [P, u64, P, i32, i32, i32, C.POINTER(ClaheParams),
+                                           C.POINTER(KltParams), P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -215,6 +234,51 @@ class Context:
         p = params or KltParams.default()
         self._check(self._L.gvx_frame_put_dev(self._h, fid, d_gray, w, h, stride or w, C.byref(p)),
                     "frame_put_dev")
+
+    # -------------------------------------------------------- preprocessing
+    def clahe(self, gray: np.ndarray, params: Optional[ClaheParams] = None, hist_mean: bool = False):
+        """clahe_->apply(image, image) (tracking.cc:139); with hist_mean also
+        calculateHistigram of the input (tracking.cc:88-105) -> (image, mean)."""
+        g = np.ascontiguousarray(gray, dtype=np.uint8)
+        if g.ndim != 2:
+            raise ValueError("gray image must be 2-D u8")
+        h, w = g.shape
+        out = np.empty_like(g)
+        m = C.c_double()
+        self._check(self._L.gvx_clahe(self._h, w, h, _ptr(g), w, _ptr(out), w, C.byref(params or ClaheParams.default()),
+                                      C.byref(m) if hist_mean else None), "clahe")
+        return (out, m.value) if hist_mean else out
+
+    def clahe_batch_dev(self, n, w, h, d_src, d_dst, params: Optional[ClaheParams] = None, d_hist_mean=None,
+                        src_img_stride=None, src_stride=None, dst_img_stride=None, dst_stride=None):
+        self._check(self._L.gvx_clahe_batch_dev(self._h, n, w, h, d_src, src_img_stride or w * h, src_stride or w,
+                                                d_dst, dst_img_stride or w * h, dst_stride or w,
+                                                C.byref(params or ClaheParams.default()), d_hist_mean),
+                    "clahe_batch_dev")
+
+    def frame_preprocess(self, fid: int, gray: np.ndarray, clahe: Optional[ClaheParams] = None,
+                         params: Optional[KltParams] = None, hist_mean: bool = False):
+        """Tracking::preprocessing (tracking.cc:107-141) into the frame cache:
+        -> (equalised image, histogram mean or None)."""
+        g = np.ascontiguousarray(gray, dtype=np.uint8)
+        if g.ndim != 2:
+            raise ValueError("gray image must be 2-D u8")
+        h, w = g.shape
+        out = np.empty_like(g)
+        m = C.c_double()
+        self._check(self._L.gvx_frame_preprocess(self._h, fid, _ptr(g), w, h, w,
+                                                 C.byref(clahe or ClaheParams.default()),
+                                                 C.byref(params or KltParams.default()),
+                                                 C.byref(m) if hist_mean else None, _ptr(out)), "frame_preprocess")
+        return out, (m.value if hist_mean else None)
+
+    def frame_preprocess_dev(self, fid: int, d_gray: int, w: int, h: int, stride: Optional[int] = None,
+                             clahe: Optional[ClaheParams] = None, params: Optional[KltParams] = None,
+                             d_hist_mean=None, d_clahe_out=None):
+        self._check(self._L.gvx_frame_preprocess_dev(self._h, fid, d_gray, w, h, stride or w,
+                                                     C.byref(clahe or ClaheParams.default()),
+                                                     C.byref(params or KltParams.default()), d_hist_mean,
+                                                     d_clahe_out), "frame_preprocess_dev")
 
     def frame_drop(self, fid: int):
         self._check(self._L.gvx_frame_drop(self._h, fid), "frame_drop")

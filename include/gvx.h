@@ -130,6 +130,43 @@ gvx_status gvx_frame_level(gvx_ctx* ctx, uint64_t id, int32_t level, uint8_t* ou
 #define GVX_PYR_PAD 32
 gvx_status gvx_frame_level_padded(gvx_ctx* ctx, uint64_t id, int32_t level, int32_t pad, uint8_t* out);
 
+/* --------------------------------------------------------- preprocessing */
+/* Tracking::preprocessing (tracking/tracking.cc:107-141): CLAHE with
+   clahe_ = cv::createCLAHE(3.0, cv::Size(21, 21)) (:63) applied in place (:139),
+   and the optional histogram check calculateHistigram (:88-105, used when
+   track_check_histogram). */
+#define GVX_CLAHE_MAX_TILES 64
+typedef struct {
+    double clip_limit;         /* 3.0 */
+    int32_t tiles_x, tiles_y;  /* tileGridSize = (21, 21), each in [1, GVX_CLAHE_MAX_TILES] */
+} gvx_clahe_params;
+void gvx_clahe_params_default(gvx_clahe_params* p);
+
+/* clahe_->apply on n images in device memory, async on the context stream.
+   Image i is h x w u8 at d_src + i*src_img_stride with rows src_stride bytes
+   apart (likewise d_dst); d_dst may equal d_src (in place, like the reference).
+   d_hist_mean (nullable): n doubles, calculateHistigram of each SOURCE image. */
+gvx_status gvx_clahe_batch_dev(gvx_ctx* ctx, int32_t n, int32_t w, int32_t h, const uint8_t* d_src,
+                               int64_t src_img_stride, int32_t src_stride, uint8_t* d_dst,
+                               int64_t dst_img_stride, int32_t dst_stride, const gvx_clahe_params* cp,
+                               double* d_hist_mean);
+/* One host image, synchronous.  hist_mean (nullable) as above. */
+gvx_status gvx_clahe(gvx_ctx* ctx, int32_t w, int32_t h, const uint8_t* src, int32_t src_stride, uint8_t* dst,
+                     int32_t dst_stride, const gvx_clahe_params* cp, double* hist_mean);
+
+/* The whole per-frame preprocessing into the frame cache: calculateHistigram
+   of the raw frame (when hist_mean != NULL), CLAHE, then gvx_frame_put of the
+   equalised image (its pyramid).  clahe_out (nullable, w*h bytes, tightly
+   packed) receives frame->image() after :139.  Synchronous. */
+gvx_status gvx_frame_preprocess(gvx_ctx* ctx, uint64_t id, const uint8_t* gray, int32_t w, int32_t h,
+                                int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
+                                double* hist_mean, uint8_t* clahe_out);
+/* The same from a device image, async on the context stream; d_hist_mean and
+   d_clahe_out (w*h, tightly packed) are device pointers and may be NULL. */
+gvx_status gvx_frame_preprocess_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_gray, int32_t w, int32_t h,
+                                    int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
+                                    double* d_hist_mean, uint8_t* d_clahe_out);
+
 /* ------------------------------------------------------ feature detection */
 /* Tracking::featuresDetection (tracking/tracking.cc:576-688): block grid from
    the Tracking ctor (:65-85), FILLED circle mask of radius

@@ -28,6 +28,9 @@
  *   orc_preint_*           preintegration/preintegration_{base,earth,normal}.cc
  *   orc_preint_factor_eval preintegration/preintegration_factor.h:45-69
  *   orc_reproj_eval        factors/reprojection_factor.h:61-161
+ *   orc_clahe / orc_hist_mean  Tracking::preprocessing (tracking.cc:107-141):
+ *                          cv::createCLAHE(3.0, Size(21,21))->apply and
+ *                          calculateHistigram (clahe.c)
  *
  * Documented choices where the upstream arithmetic is build-dependent:
  *   - LK window sums (A11/A12/A22, b1/b2) are exact int64 sums converted to
@@ -252,6 +255,16 @@ void orc_preint_factor_eval_batch(int n, const orc_preint* const* segs, const do
 
 /* PoseParameterization::Plus (pose_parameterization.h:34-49). */
 void orc_pose_plus(const double* x, const double* delta, double* x_plus_delta);
+
+/* ------------------------------------------------------------------------- */
+/* Preprocessing: CLAHE and the histogram check (clahe.c)                     */
+/* ------------------------------------------------------------------------- */
+void orc_clahe_geometry(int w, int h, int tiles_x, int tiles_y, int* tw, int* th, int* ext_w, int* ext_h);
+void orc_clahe_luts(const uint8_t* src, int w, int h, int stride, double clip_limit, int tiles_x,
+                    int tiles_y, uint8_t* lut);
+void orc_clahe(const uint8_t* src, int w, int h, int stride, double clip_limit, int tiles_x, int tiles_y,
+               uint8_t* dst, int dst_stride);
+double orc_hist_mean(const uint8_t* src, int w, int h, int stride);
 
 #ifdef __cplusplus
 }

@@ -127,6 +127,10 @@ def lib():
         L.orc_reproj_eval_batch.argtypes = [C.c_int, P, P, P, P, P, C.c_int]
         L.orc_preint_factor_eval_batch.argtypes = [C.c_int, P, P, P, P, P, C.c_int]
         L.orc_pose_plus.argtypes = [P, P, P]
+        L.orc_clahe_luts.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, P]
+        L.orc_clahe.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, P, C.c_int]
+        L.orc_hist_mean.argtypes = [P, C.c_int, C.c_int, C.c_int]
+        L.orc_hist_mean.restype = C.c_double
         _lib = L
     return _lib
 
@@ -391,3 +395,29 @@ def preint_factor_eval_batch(segs, params, offs, jacobians=True, nthreads=1):
     jac = np.zeros((n, 480)) if jacobians else None
     lib().orc_preint_factor_eval_batch(n, C.cast(ptrs, C.c_void_p), _p(prm), _p(o), _p(res), _p(jac), nthreads)
     return res, jac
+
+
+# ------------------------------------------------------------------ preprocessing
+def clahe(img: np.ndarray, clip_limit=3.0, tiles=(21, 21)) -> np.ndarray:
+    """cv::createCLAHE(clip_limit, Size(tiles))->apply(img) (tracking.cc:63, :139)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.empty_like(img)
+    lib().orc_clahe(_p(img), w, h, w, clip_limit, tiles[0], tiles[1], _p(out), w)
+    return out
+
+
+def clahe_luts(img: np.ndarray, clip_limit=3.0, tiles=(21, 21)) -> np.ndarray:
+    """The per-tile LUTs (tiles_y*tiles_x x 256) of CLAHE_CalcLut_Body."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.empty((tiles[1] * tiles[0], 256), np.uint8)
+    lib().orc_clahe_luts(_p(img), w, h, w, clip_limit, tiles[0], tiles[1], _p(out))
+    return out
+
+
+def hist_mean(img: np.ndarray) -> float:
+    """Tracking::calculateHistigram (tracking.cc:88-105)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    return float(lib().orc_hist_mean(_p(img), w, h, w))

@@ -1,0 +1,96 @@
+"""GPU parity of the preprocessing step (CLAHE + histogram check, libgvx.so via
+the C ABI) against the CPU restatement (oracle/clahe.c): equalised images are
+required to be BIT-EXACT (integer histograms/LUTs, fp32 interpolation without
+FMA on both sides), histogram means equal to the last bit."""
+import numpy as np
+import pytest
+
+from gvx import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _img(w, h, seed):
+    return synth.make_image(w, h, np.random.default_rng(seed))
+
+
+def _same(a, b, what):
+    if not np.array_equal(a, b):
+        d = np.argwhere(a != b)
+        raise AssertionError(f"{what}: {len(d)} mismatches, first at {d[:5].tolist()}: "
+                             f"gpu={a[tuple(d[0])]} oracle={b[tuple(d[0])]}")
+
+
+@pytest.mark.parametrize("w,h,tiles,clip", [
+    (1280, 560, (21, 21), 3.0),    # the reference: both sides padded (61 x 27 tiles)
+    (1920, 1200, (21, 21), 3.0),
+    (210, 147, (21, 21), 3.0),     # divisible: no border
+    (215, 147, (21, 21), 3.0),     # width only indivisible: a whole extra tile row
+    (100, 100, (8, 8), 40.0),
+    (96, 64, (6, 4), 0.0),         # no clipping
+    (47, 33, (5, 3), 1.0),
+    (161, 71, (64, 1), 3.0),       # widest grid
+])
+def test_clahe_bit_exact(ctx, orc, gvx_mod, w, h, tiles, clip):
+    img = _img(w, h, w * 7 + h)
+    p = gvx_mod.ClaheParams.default(clip_limit=clip, tiles_x=tiles[0], tiles_y=tiles[1])
+    out, m = ctx.clahe(img, p, hist_mean=True)
+    _same(out, orc.clahe(img, clip, tiles), "clahe")
+    assert m == orc.hist_mean(img)
+
+
+def test_clahe_constant_and_extremes(ctx, orc, gvx_mod):
+    for v in (0, 255):
+        img = np.full((140, 320), v, np.uint8)
+        _same(ctx.clahe(img), orc.clahe(img), f"constant {v}")
+    img = (np.indices((140, 320)).sum(0) % 2 * 255).astype(np.uint8)  # checkerboard of 0/255
+    _same(ctx.clahe(img), orc.clahe(img), "checkerboard")
+
+
+def test_clahe_batch_dev_strided_and_in_place(ctx, orc, gvx_mod):
+    import torch
+    w, h, n, pitch = 333, 97, 5, 340        # odd width: byte path; rows 340 bytes apart
+    imgs = [_img(w, h, 100 + i) for i in range(n)]
+    host = np.zeros((n, h, pitch), np.uint8)
+    for i in range(n):
+        host[i, :, :w] = imgs[i]
+    src = torch.from_numpy(host).cuda()
+    dst = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
+    means = torch.zeros(n, dtype=torch.float64, device="cuda")
+    ctx.clahe_batch_dev(n, w, h, src.data_ptr(), dst.data_ptr(), d_hist_mean=means.data_ptr(),
+                        src_img_stride=h * pitch, src_stride=pitch)
+    ctx.sync()
+    out, mv = dst.cpu().numpy(), means.cpu().numpy()
+    for i in range(n):
+        _same(out[i], orc.clahe(imgs[i]), f"image {i}")
+        assert mv[i] == orc.hist_mean(imgs[i])
+    # in place (the reference's clahe_->apply(image, image)), aligned dword path
+    w2, h2 = 1280, 560
+    b = [_img(w2, h2, 7 + i) for i in range(3)]
+    t = torch.from_numpy(np.stack(b)).cuda()
+    ctx.clahe_batch_dev(3, w2, h2, t.data_ptr(), t.data_ptr())
+    ctx.sync()
+    tt = t.cpu().numpy()
+    for i in range(3):
+        _same(tt[i], orc.clahe(b[i]), f"in-place image {i}")
+
+
+def test_frame_preprocess_feeds_pyramid(ctx, orc, gvx_mod):
+    """Tracking::preprocessing then the frame's pyramid: level 0 is the CLAHE
+    output and every level is the oracle pyramid of it."""
+    img = _img(1280, 560, 42)
+    eq, m = ctx.frame_preprocess(11, img, hist_mean=True)
+    ref = orc.clahe(img)
+    _same(eq, ref, "equalised frame")
+    assert m == orc.hist_mean(img)
+    for l, r in enumerate(orc.build_pyramid(ref, 3)):
+        _same(ctx.frame_level(11, l), r, f"level {l}")
+    ctx.frame_drop(11)
+
+
+def test_clahe_rejects_bad_grids(ctx, gvx_mod):
+    img = _img(64, 40, 1)
+    for p in (gvx_mod.ClaheParams.default(tiles_x=0), gvx_mod.ClaheParams.default(tiles_y=65),
+              gvx_mod.ClaheParams.default(tiles_x=65), gvx_mod.ClaheParams.default(tiles_x=21, tiles_y=41)):
+        with pytest.raises(gvx_mod.GvxError):
+            ctx.clahe(img, p)
