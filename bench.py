@@ -48,7 +48,7 @@ def algorithmic_bytes(w, h, levels, n):
     return 2 * a0 + 4 * ap + 16 * (a0 + ap) + 58 * n
 
 
-def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False):
+def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False, clahe=False):
     """Oracle (C restatement) on the reference's 4-call pattern (each
     calcOpticalFlowPyrLK rebuilds both pyramids; LK points split over `threads`
     like OpenCV's parallel_for_), bounded sample of about budget_s seconds."""
@@ -60,6 +60,8 @@ def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False):
     half = n // 2  # Tracking::trackMappoint / trackReferencePoint point sets
 
     def frame(I, J, P, Q):
+        if clahe:
+            orc.clahe(J)  # Tracking::preprocessing of the new frame (tracking.cc:139)
         if reuse:
             # baseline (b): the same LK work with each image's pyramid built once
             orc.klt_fb(I, J, P, Q, params=p, reuse_pyramids=True, nthreads=threads)
@@ -79,6 +81,8 @@ def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False):
     what = ("fwd + bwd LK of all points, each pyramid built once (baseline b)" if reuse else
             f"({half} map + {n - half} reference points), 4 LK calls each rebuilding both pyramids "
             f"(tracking.cc:385,390,487,493)")
+    if clahe:
+        what += " + CLAHE of the new frame (1 thread)"
     return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{done} frame pairs {w}x{h}/{n} feat {what}, {threads} thread(s), {dt:.1f} s"}
 
@@ -140,6 +144,7 @@ def main():
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic pairs (tiled)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pre", action="store_true", help="skip the CLAHE preprocessing leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
     ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
@@ -230,6 +235,7 @@ def main():
     fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact")}
     ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
+    pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if not args.no_pre else None
     if world > 1 and not args.gather:
         collect_once = [torch.empty_like(dNK) for _ in range(world)]
         dist.all_gather(collect_once, dNK)  # results check, outside the timed region
@@ -283,11 +289,46 @@ def main():
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
+            "preprocess": pre,
         }
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
     ctx.close()
+
+
+def preprocess_leg(ctx, dI, dJ, Pn, W, H, steps):
+    """Tracking::preprocessing (CLAHE, tracking.cc:139) over the step's 2*Pn
+    frames resident in HBM, timed on its own (not part of `value`, whose
+    frame-pair unit in SURVEY 8d starts after CLAHE).  Algorithmic bytes: each
+    pixel read once and written once (2 B/px); the design reads it twice (LUT
+    pass + apply pass)."""
+    import torch
+    out = torch.empty_like(dI)
+
+    def run():
+        ctx.clahe_batch_dev(Pn, W, H, dI.data_ptr(), out.data_ptr())
+        ctx.clahe_batch_dev(Pn, W, H, dJ.data_ptr(), out.data_ptr())
+
+    for _ in range(5):
+        run()
+    ctx.sync()
+    ctx.profile_reset()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    ctx.sync()
+    el = time.perf_counter() - t0
+    ms, _ = ctx.profile_read("clahe")
+    ctx.profile(False)
+    imgs = 2 * Pn * steps
+    gbs = 2.0 * W * H * imgs / (ms * 1e-3) / 1e9 if ms > 0 else None
+    return {"what": "CLAHE createCLAHE(3.0, 21x21)->apply on the 2*pairs frames of a step (tracking.cc:139)",
+            "images_per_s": round(imgs / el, 1), "device_ms_per_image": round(ms / imgs, 5),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                         "algorithmic_bytes_per_image": 2 * W * H}}
 
 
 def factors_main(args):
@@ -523,7 +564,8 @@ def sequence_main(args):
     stats = {"detect_frames": 0}
 
     def frame(t, pts, vel):
-        ctx.frame_put_dev(t % 2, frames[t].data_ptr(), W, H, params=kp)
+        # Tracking::preprocessing (CLAHE, tracking.cc:139) + the frame's pyramid
+        ctx.frame_preprocess_dev(t % 2, frames[t].data_ptr(), W, H, params=kp)
         if t > 0 and pts.shape[0]:
             r = ctx.track_fb((t - 1) % 2, t % 2, pts, pts + vel, W, H, params=kp)
             k = r["kept_idx"]
@@ -564,7 +606,7 @@ def sequence_main(args):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact", "detect")}
+    fam = {f: ctx.profile_read(f) for f in ("clahe", "pyramid", "klt", "compact", "detect")}
     fam = {k: v for k, v in fam.items() if v[1] > 0}
     ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
@@ -577,11 +619,11 @@ def sequence_main(args):
         for _ in range(L):
             sw, sh = (sw + 1) // 2, (sh + 1) // 2
             ap += sw * sh
-        B = algorithmic_bytes(W, H, L, N) - W * H - 2 * ap
+        B = algorithmic_bytes(W, H, L, N) - W * H - 2 * ap + 2 * W * H  # + CLAHE: read + write the frame
         achieved = B / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=host_threads())
+            cpu = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=host_threads(), clahe=True)
             cpu["sample"] += " (per sequence frame, detection not included)"
         tr = counts[F - timed:]
         print(json.dumps({
@@ -591,7 +633,7 @@ def sequence_main(args):
             "vs_baseline": None, "dtype": "u8/i32 windows, f32 solve",
             "data": "synthetic sequences (moving camera over a band-limited texture, seed 20261015 + 7919*rank)",
             "config": {"workload": f"configs[4]: one {F}-frame sequence per GPU, {W}x{H} mono, {N} feat, maxLevel "
-                                   f"{L}: per frame pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
+                                   f"{L}: per frame CLAHE + pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
                                    f"RCCL gather of all per-frame tracks to rank 0",
                        "parallelism": f"sequences sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
