@@ -5,18 +5,24 @@
 // CLAHE_Impl::apply, 8-bit) are written down in oracle/clahe.c.
 //
 // Kernels:
-//  lut_kernel    one 256-thread workgroup per (image, tile): LDS histogram of
-//                the tile (REFLECT_101 source for the bottom/right pad tiles),
-//                clip, redistribute, cumulative sum and the 256-byte LUT by
-//                wave 0 (4 bins per lane, shuffle scan).  When the histogram
-//                check is on, the in-image part of each tile's histogram is
-//                added to the image histogram first (global atomics, non-zero
-//                bins only).
-//  apply_kernel  one workgroup per (image, band of rows): the <= 3 LUT rows of
-//                tiles the band touches are staged in LDS, then every pixel is
-//                the bilinear blend of 4 LUT entries in fp32 (OpenCV's scalar
-//                CLAHE_Interpolation_Body order, no FMA) rounded half to even.
-//                4 pixels per thread and step, dword loads/stores when aligned.
+//  lut_kernel    one 256-thread workgroup per (image, row of tiles): every
+//                pixel of the tile row is read once (8 bytes per load, 8 loads
+//                in flight per thread) into per-tile LDS histograms, the
+//                REFLECT_101 pad pixels (copyMakeBorder of the LUT source)
+//                are added, and each wave then turns tiles into LUTs: clip,
+//                redistribute, cumulative sum (4 bins per lane, shuffle scan)
+//                and the 256-byte LUT.  When the histogram check is on, the
+//                in-image counts of the tile row go to the image histogram
+//                (one global atomic per non-zero bin) before the pads are added.
+//  apply_kernel  one workgroup per (image, band of rows with the same upper
+//                tile row, part of the band): the band's two LUT rows are
+//                interleaved in LDS so one ds_read_b32 returns a pixel's four
+//                LUT values; each thread owns 8 columns for the whole band --
+//                their table offsets and fp32 weights are computed once -- and
+//                walks the band 8 rows at a time, loads first.  Every pixel is
+//                the bilinear blend of the 4 LUT values in fp32 (OpenCV's
+//                scalar CLAHE_Interpolation_Body order, no FMA), rounded half
+//                to even.
 //  mean_kernel   Tracking::calculateHistigram from the image histogram.
 #include <hip/hip_runtime.h>
 
@@ -40,42 +46,22 @@ __device__ __forceinline__ uint32_t sat_round_u8(float v) {
     return (uint32_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
 }
 
-__global__ void __launch_bounds__(256) lut_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
-                                                  int stride, ClaheGeom g, uint8_t* __restrict__ lut,
-                                                  uint32_t* __restrict__ hist_img) {
-    __shared__ uint32_t hist[256];
-    const int ntiles = g.tiles_x * g.tiles_y;
-    const int img = blockIdx.x / ntiles, k = blockIdx.x - img * ntiles;
-    const int ty = k / g.tiles_x, tx = k - ty * g.tiles_x;
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    hist[t] = 0;
-    __syncthreads();
-    const uint8_t* s = src + img * img_stride;
-    const int x0 = tx * g.tw, y0 = ty * g.th;
-    const int xe = min(x0 + g.tw, g.w), ye = min(y0 + g.th, g.h);
-    for (int y = y0 + wave; y < ye; y += 4) {
-        const uint8_t* row = s + (int64_t)y * stride;
-        for (int x = x0 + lane; x < xe; x += 64) atomicAdd(&hist[row[x]], 1u);
-    }
-    if (hist_img) {
-        __syncthreads();
-        const uint32_t v = hist[t];
-        if (v) atomicAdd(&hist_img[img * 256 + t], v);
-    }
-    if (x0 + g.tw > g.w || y0 + g.th > g.h) {
-        // the copyMakeBorder(..., BORDER_REFLECT_101) part of the LUT source
-        for (int y = y0 + wave; y < y0 + g.th; y += 4) {
-            const uint8_t* row = s + (int64_t)refl101(y, g.h) * stride;
-            const bool yin = y < g.h;
-            for (int x = x0 + lane; x < x0 + g.tw; x += 64)
-                if (!yin || x >= g.w) atomicAdd(&hist[row[refl101(x, g.w)]], 1u);
-        }
-    }
-    __syncthreads();
-    if (wave != 0) return;
+// x / d for 0 <= x < 2^20, d >= 1 (fp32 estimate, corrected to exact)
+__device__ __forceinline__ int div_small(int x, int d, float inv_d) {
+    int q = (int)((float)x * inv_d);
+    q += (q + 1) * d <= x ? 1 : 0;
+    q -= q * d > x ? 1 : 0;
+    return q;
+}
+
+constexpr int LUT_THREADS = 256;
+constexpr int LUT_UNROLL = 8;
+
+// CLAHE_CalcLut_Body for one tile, by one wavefront: h = the tile's 256 bins.
+__device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, int lane, uint8_t* out) {
     uint32_t h4[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) h4[i] = hist[4 * lane + i];
+    for (int i = 0; i < 4; ++i) h4[i] = h[4 * lane + i];
     if (g.clip > 0) {
         const uint32_t clip = (uint32_t)g.clip;
         uint32_t cl = 0;
@@ -109,70 +95,221 @@ __global__ void __launch_bounds__(256) lut_kernel(const uint8_t* __restrict__ sr
     uint32_t packed = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) packed |= sat_round_u8((float)(base + c4[i]) * g.lut_scale) << (8 * i);
-    reinterpret_cast<uint32_t*>(lut + ((int64_t)img * ntiles + k) * 256)[lane] = packed;
+    reinterpret_cast<uint32_t*>(out)[lane] = packed;
 }
 
-constexpr int MAX_LUT_ROWS = 3;
+__global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
+                                                          int stride, ClaheGeom g, int vec8,
+                                                          uint8_t* __restrict__ lut,
+                                                          uint32_t* __restrict__ hist_img) {
+    extern __shared__ uint32_t hs[];  // tiles_x * 256 bins
+    const int img = blockIdx.x / g.tiles_y, ty = blockIdx.x - img * g.tiles_y;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const int nbins = g.tiles_x * 256;
+    for (int i = t; i < nbins; i += LUT_THREADS) hs[i] = 0;
+    __syncthreads();
+    const uint8_t* s = src + img * img_stride;
+    const int y0 = ty * g.th;
+    const int rows_in = max(0, min(y0 + g.th, g.h) - y0);
+    const float inv_tw = 1.0f / g.tw;
+    // ---- in-image pixels of the tile row (every tile: x in [0, w)) ----
+    if (vec8) {
+        const int n8 = g.w >> 3;  // w % 8 == 0
+        const int total = rows_in * n8;
+        for (int base = t; base < total; base += LUT_UNROLL * LUT_THREADS) {
+            uint2 v[LUT_UNROLL];
+            int x0[LUT_UNROLL];
+#pragma unroll
+            for (int k = 0; k < LUT_UNROLL; ++k) {
+                const int i = base + k * LUT_THREADS;
+                const int r = i / n8, c8 = i - r * n8;
+                x0[k] = 8 * c8;
+                v[k] = i < total ? *reinterpret_cast<const uint2*>(s + (int64_t)(y0 + r) * stride + 8 * c8)
+                                 : uint2{0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < LUT_UNROLL; ++k) {
+                if (base + k * LUT_THREADS >= total) break;
+                const int txa = div_small(x0[k], g.tw, inv_tw);
+                const int xb = (txa + 1) * g.tw;  // first column of the next tile
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t b = ((j < 4 ? v[k].x : v[k].y) >> (8 * (j & 3))) & 255u;
+                    const int x = x0[k] + j;
+                    const int tx = x < xb ? txa : (x < xb + g.tw ? txa + 1 : div_small(x, g.tw, inv_tw));
+                    atomicAdd(&hs[tx * 256 + b], 1u);
+                }
+            }
+        }
+    } else {
+        const int total = rows_in * g.w;
+        for (int i = t; i < total; i += LUT_THREADS) {
+            const int r = i / g.w, x = i - r * g.w;
+            atomicAdd(&hs[div_small(x, g.tw, inv_tw) * 256 + s[(int64_t)(y0 + r) * stride + x]], 1u);
+        }
+    }
+    if (hist_img) {
+        __syncthreads();
+        for (int b = t; b < 256; b += LUT_THREADS) {
+            uint32_t sum = 0;
+            for (int tx = 0; tx < g.tiles_x; ++tx) sum += hs[tx * 256 + b];
+            if (sum) atomicAdd(&hist_img[img * 256 + b], sum);
+        }
+    }
+    // ---- the copyMakeBorder(..., BORDER_REFLECT_101) part of the LUT source ----
+    const int ew = g.tiles_x * g.tw;
+    if (ew > g.w) {  // pad columns of the in-image rows
+        const int pc = ew - g.w;
+        for (int i = t; i < rows_in * pc; i += LUT_THREADS) {
+            const int r = i / pc, x = g.w + (i - r * pc);
+            atomicAdd(&hs[div_small(x, g.tw, inv_tw) * 256 + s[(int64_t)(y0 + r) * stride + refl101(x, g.w)]], 1u);
+        }
+    }
+    const int pr = g.th - rows_in;  // pad rows (reflected source rows), every ext column
+    for (int i = t; i < pr * ew; i += LUT_THREADS) {
+        const int r = i / ew, x = i - r * ew;
+        const int sy = refl101(y0 + rows_in + r, g.h);
+        atomicAdd(&hs[div_small(x, g.tw, inv_tw) * 256 + s[(int64_t)sy * stride + refl101(x, g.w)]], 1u);
+    }
+    __syncthreads();
+    for (int tx = wave; tx < g.tiles_x; tx += LUT_THREADS / 64)
+        tile_lut(hs + tx * 256, g, lane, lut + ((int64_t)img * g.tiles_x * g.tiles_y + ty * g.tiles_x + tx) * 256);
+}
+
+constexpr int TROW = 257;  // LDS dwords per table row (bank skew between tiles)
+constexpr int PPT = 8;     // pixels (columns) per thread
+constexpr int ROWS_UNROLL = 8;
+constexpr int TAB_UNROLL = 8;
+
+// First row y with floor(y/th - 0.5) >= k in fp32 (CLAHE_Interpolation_Body's
+// row mapping), y in [0, h].
+__device__ __forceinline__ int first_row(int k, const ClaheGeom& g, float inv_th) {
+    int y = max(0, min(g.h, (int)((k + 0.5f) * g.th)));
+    while (y > 0 && (int)floorf((float)(y - 1) * inv_th - 0.5f) >= k) --y;
+    while (y < g.h && (int)floorf((float)y * inv_th - 0.5f) < k) ++y;
+    return y;
+}
 
 // src may equal dst (in place, like the reference's apply(image, image)): each
-// thread reads its 4 pixels before it writes them, and no other thread reads them.
-__global__ void __launch_bounds__(256) apply_kernel(const uint8_t* src, int64_t img_stride,
-                                                    int stride, uint8_t* dst, int64_t dst_img_stride,
-                                                    int dst_stride, ClaheGeom g, const uint8_t* __restrict__ lut,
-                                                    int band_rows, int nbands, int aligned) {
-    extern __shared__ uint4 sl4[];  // MAX_LUT_ROWS * tiles_x * 256 bytes
-    uint8_t* sl = reinterpret_cast<uint8_t*>(sl4);
-    const int img = blockIdx.x / nbands, band = blockIdx.x - img * nbands;
-    const int y0 = band * band_rows, y1 = min(y0 + band_rows, g.h);
+// thread reads its pixels before it writes them, and no other thread reads them.
+//
+// Band b = the rows whose upper tile row is ty1 = b - 1 (b = 0 .. tiles_y), so a
+// band blends one pair of LUT rows (ty1, ty2 clamped); the band is split over
+// `nsplit` workgroups.  LDS table: entry (k, v), k = tx1 + 1 in [0, tiles_x],
+// is one dword {L[ty1][tx1c][v], L[ty1][tx2c][v], L[ty2][tx1c][v],
+// L[ty2][tx2c][v]} (tile indices clamped as the reference does), so each pixel
+// takes one ds_read_b32 for its four LUT values.
+__global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t img_stride, int stride,
+                                                     uint8_t* dst, int64_t dst_img_stride, int dst_stride,
+                                                     ClaheGeom g, const uint8_t* __restrict__ lut, int nsplit,
+                                                     int vec8) {
+    extern __shared__ uint32_t tab[];  // (tiles_x + 1) * TROW dwords
+    const int nb = g.tiles_y + 1;
+    const int img = blockIdx.x / (nb * nsplit);
+    const int rem = blockIdx.x - img * nb * nsplit;
+    const int b = rem / nsplit, part = rem - b * nsplit;
     const float inv_th = 1.0f / g.th, inv_tw = 1.0f / g.tw;
-    const int tyA = max((int)floorf((float)y0 * inv_th - 0.5f), 0);
-    const int tyB = min((int)floorf((float)(y1 - 1) * inv_th - 0.5f) + 1, g.tiles_y - 1);
-    const int ntiles = g.tiles_x * g.tiles_y;
+    const int ys = b == 0 ? 0 : first_row(b - 1, g, inv_th);
+    const int ye = b == g.tiles_y ? g.h : first_row(b, g, inv_th);
+    const int per = (ye - ys + nsplit - 1) / nsplit;
+    const int y0 = ys + part * per, y1 = min(ye, y0 + per);
+    if (y0 >= y1) return;  // whole workgroup: no barrier below is skipped by part of it
+    const int ty1 = max(b - 1, 0), ty2 = min(b, g.tiles_y - 1);
     {
-        const uint4* lsrc = reinterpret_cast<const uint4*>(lut + ((int64_t)img * ntiles + tyA * g.tiles_x) * 256);
-        const int n16 = (tyB - tyA + 1) * g.tiles_x * 16;
-        for (int i = threadIdx.x; i < n16; i += 256) sl4[i] = lsrc[i];
+        // all loads of a thread's table entries first (L2 hits; one round trip)
+        const uint32_t* L = reinterpret_cast<const uint32_t*>(lut + (int64_t)img * g.tiles_x * g.tiles_y * 256);
+        const int items = (g.tiles_x + 1) * 64;
+        for (int i0 = threadIdx.x; i0 < items; i0 += TAB_UNROLL * blockDim.x) {
+            uint32_t a[TAB_UNROLL], bb[TAB_UNROLL], c[TAB_UNROLL], d[TAB_UNROLL];
+#pragma unroll
+            for (int u = 0; u < TAB_UNROLL; ++u) {
+                const int i = min(i0 + u * (int)blockDim.x, items - 1);
+                const int k = i >> 6, q = i & 63;
+                const int ta = max(k - 1, 0), tb = min(k, g.tiles_x - 1);
+                a[u] = L[(ty1 * g.tiles_x + ta) * 64 + q];
+                bb[u] = L[(ty1 * g.tiles_x + tb) * 64 + q];
+                c[u] = L[(ty2 * g.tiles_x + ta) * 64 + q];
+                d[u] = L[(ty2 * g.tiles_x + tb) * 64 + q];
+            }
+#pragma unroll
+            for (int u = 0; u < TAB_UNROLL; ++u) {
+                const int i = i0 + u * (int)blockDim.x;
+                if (i >= items) break;
+                const int k = i >> 6, q = i & 63;
+                // byte j of (a, bb, c, d) -> dword for value 4q + j
+                const uint32_t ab_lo = __builtin_amdgcn_perm(bb[u], a[u], 0x05010400u);  // a0 b0 a1 b1
+                const uint32_t ab_hi = __builtin_amdgcn_perm(bb[u], a[u], 0x07030602u);  // a2 b2 a3 b3
+                const uint32_t cd_lo = __builtin_amdgcn_perm(d[u], c[u], 0x05010400u);
+                const uint32_t cd_hi = __builtin_amdgcn_perm(d[u], c[u], 0x07030602u);
+                uint32_t* o = tab + k * TROW + 4 * q;
+                o[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);  // a0 b0 c0 d0
+                o[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);  // a1 b1 c1 d1
+                o[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+                o[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+            }
+        }
     }
     __syncthreads();
     const uint8_t* s = src + img * img_stride;
-    uint8_t* d = dst + img * dst_img_stride;
-    const int nq = (g.w + 3) >> 2;
-    const int total = (y1 - y0) * nq;
-    const int lrow = g.tiles_x * 256;
-    for (int idx = threadIdx.x; idx < total; idx += 256) {
-        const int r = idx / nq, q = idx - r * nq;
-        const int y = y0 + r, x = 4 * q;
-        const float tyf = (float)y * inv_th - 0.5f;
-        const int ty1r = (int)floorf(tyf);
-        const float ya = tyf - (float)ty1r, ya1 = 1.0f - ya;
-        const uint8_t* p1 = sl + (max(ty1r, 0) - tyA) * lrow;
-        const uint8_t* p2 = sl + (min(ty1r + 1, g.tiles_y - 1) - tyA) * lrow;
-        const uint8_t* srow = s + (int64_t)y * stride;
-        uint8_t* drow = d + (int64_t)y * dst_stride;
-        const int nv = min(4, g.w - x);
-        uint32_t pix;
-        if (aligned && nv == 4)
-            pix = *reinterpret_cast<const uint32_t*>(srow + x);
-        else {
-            pix = 0;
-            for (int j = 0; j < nv; ++j) pix |= (uint32_t)srow[x + j] << (8 * j);
-        }
-        uint32_t out = 0;
+    uint8_t* dd = dst + img * dst_img_stride;
+    for (int x0 = PPT * threadIdx.x; x0 < g.w; x0 += PPT * blockDim.x) {
+        // column terms of CLAHE_Interpolation_Body's constructor, once per thread
+        int ko[PPT];
+        float xa[PPT], xa1[PPT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float txf = (float)(x + j) * inv_tw - 0.5f;
-            const int tx1r = (int)floorf(txf);
-            const float xa = txf - (float)tx1r, xa1 = 1.0f - xa;
-            const int v = (pix >> (8 * j)) & 255;
-            const int i1 = max(tx1r, 0) * 256 + v, i2 = min(tx1r + 1, g.tiles_x - 1) * 256 + v;
-            const float res = ((float)p1[i1] * xa1 + (float)p1[i2] * xa) * ya1 +
-                              ((float)p2[i1] * xa1 + (float)p2[i2] * xa) * ya;
-            out |= sat_round_u8(res) << (8 * j);
+        for (int j = 0; j < PPT; ++j) {
+            const float txf = (float)(x0 + j) * inv_tw - 0.5f;
+            const int tx1 = (int)floorf(txf);
+            xa[j] = txf - (float)tx1;
+            xa1[j] = 1.0f - xa[j];
+            ko[j] = (min(tx1, g.tiles_x - 1) + 1) * TROW;
         }
-        if (aligned && nv == 4)
-            *reinterpret_cast<uint32_t*>(drow + x) = out;
-        else
-            for (int j = 0; j < nv; ++j) drow[x + j] = (uint8_t)(out >> (8 * j));
+        const int nv = min(PPT, g.w - x0);
+        const bool fast = vec8 && nv == PPT;
+        for (int yb = y0; yb < y1; yb += ROWS_UNROLL) {
+            uint2 pix[ROWS_UNROLL];
+#pragma unroll
+            for (int k = 0; k < ROWS_UNROLL; ++k) {
+                const int y = min(yb + k, y1 - 1);
+                const uint8_t* srow = s + (int64_t)y * stride + x0;
+                if (fast) {
+                    pix[k] = *reinterpret_cast<const uint2*>(srow);
+                } else {
+                    uint32_t lo = 0, hi = 0;
+                    for (int j = 0; j < nv; ++j) {
+                        const uint32_t bv = srow[j];
+                        if (j < 4)
+                            lo |= bv << (8 * j);
+                        else
+                            hi |= bv << (8 * (j - 4));
+                    }
+                    pix[k] = uint2{lo, hi};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < ROWS_UNROLL; ++k) {
+                const int y = yb + k;
+                if (y >= y1) break;
+                const float tyf = (float)y * inv_th - 0.5f;
+                const float ya = tyf - floorf(tyf), ya1 = 1.0f - ya;
+                uint32_t out[2] = {0, 0};
+#pragma unroll
+                for (int j = 0; j < PPT; ++j) {
+                    const uint32_t v = ((j < 4 ? pix[k].x : pix[k].y) >> (8 * (j & 3))) & 255u;
+                    const uint32_t e = tab[ko[j] + v];
+                    const float l11 = (float)(e & 255u), l12 = (float)((e >> 8) & 255u);
+                    const float l21 = (float)((e >> 16) & 255u), l22 = (float)(e >> 24);
+                    const float res = (l11 * xa1[j] + l12 * xa[j]) * ya1 + (l21 * xa1[j] + l22 * xa[j]) * ya;
+                    out[j >> 2] |= sat_round_u8(res) << (8 * (j & 3));
+                }
+                uint8_t* drow = dd + (int64_t)y * dst_stride + x0;
+                if (fast) {
+                    *reinterpret_cast<uint2*>(drow) = uint2{out[0], out[1]};
+                } else {
+                    for (int j = 0; j < nv; ++j) drow[j] = (uint8_t)(out[j >> 2] >> (8 * (j & 3)));
+                }
+            }
+        }
     }
 }
 
@@ -212,23 +349,24 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean) {
     if (n <= 0) return hipSuccess;
-    const int ntiles = g.tiles_x * g.tiles_y;
     if (hist_img) {
         hipError_t e = hipMemsetAsync(hist_img, 0, (size_t)n * 256 * sizeof(uint32_t), c->stream);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(lut_kernel, dim3(n * ntiles), dim3(256), 0, c->stream, src, img_stride, stride, g, lut,
-                       hist_img);
-    // bands: <= th rows (so <= 3 LUT rows), and enough workgroups to fill the chip
-    int band = (int)std::min<int64_t>(g.th, 32);
-    const int64_t want = 4LL * c->n_cu;
-    while (band > 1 && (int64_t)n * ((g.h + band - 1) / band) < want) band = (band + 1) / 2;
-    const int nbands = (g.h + band - 1) / band;
-    const int aligned = ((uintptr_t)src % 4 == 0) && ((uintptr_t)dst % 4 == 0) && stride % 4 == 0 &&
-                        dst_stride % 4 == 0 && img_stride % 4 == 0 && dst_img_stride % 4 == 0;
-    const size_t lds = (size_t)MAX_LUT_ROWS * g.tiles_x * 256;
-    hipLaunchKernelGGL(apply_kernel, dim3(n * nbands), dim3(256), lds, c->stream, src, img_stride, stride, dst,
-                       dst_img_stride, dst_stride, g, (const uint8_t*)lut, band, nbands, aligned);
+    const bool src8 = (uintptr_t)src % 8 == 0 && stride % 8 == 0 && img_stride % 8 == 0;
+    const bool dst8 = (uintptr_t)dst % 8 == 0 && dst_stride % 8 == 0 && dst_img_stride % 8 == 0;
+    const int lut_vec8 = src8 && g.w % 8 == 0;
+    hipLaunchKernelGGL(lut_kernel, dim3(n * g.tiles_y), dim3(LUT_THREADS), (size_t)g.tiles_x * 256 * 4, c->stream,
+                       src, img_stride, stride, g, lut_vec8, lut, hist_img);
+    // bands of rows sharing one pair of LUT rows, split to fill the chip
+    const int nb = g.tiles_y + 1;
+    int nsplit = 1;
+    while ((int64_t)n * nb * nsplit < 4LL * c->n_cu && nsplit < g.th) nsplit *= 2;
+    const int cols = (g.w + PPT - 1) / PPT;
+    const int threads = std::min(1024, (cols + 63) / 64 * 64);
+    const size_t lds = (size_t)(g.tiles_x + 1) * TROW * 4;
+    hipLaunchKernelGGL(apply_kernel, dim3(n * nb * nsplit), dim3(threads), lds, c->stream, src, img_stride, stride,
+                       dst, dst_img_stride, dst_stride, g, (const uint8_t*)lut, nsplit, (int)(src8 && dst8));
     if (hist_img && hist_mean)
         hipLaunchKernelGGL(mean_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, (const uint32_t*)hist_img, n,
                            g.w, g.h, hist_mean);

@@ -148,6 +148,16 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean);
 
+// ---- camera.hip ----
+struct CamArgs {
+    gvx_camera cam;
+    double M[9];  // r_cur_pre (PREDICT), pose R (PROJECT), R1^T R0 (PARALLAX)
+    double t[3];  // pose t (PROJECT)
+    double dt;    // VELOCITY
+    int32_t n;
+};
+hipError_t launch_camera(gvx_ctx* c, int op, const CamArgs& a, const void* in0, const void* in1, void* out);
+
 // ---- preint.hip / factors.hip ----
 hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,

@@ -84,6 +84,13 @@ class ClaheParams(C.Structure):
         return p
 
 
+class Camera(C.Structure):
+    """gvx_camera: Camera (tracking/camera.cc:25-46), K = [fx skew cx; 0 fy cy; 0 0 1],
+    distortion (k1, k2, p1, p2, k3)."""
+    _fields_ = [(k, C.c_double) for k in ("fx", "fy", "cx", "cy", "skew", "k1", "k2", "p1", "p2", "k3")] + \
+               [("width", C.c_int32), ("height", C.c_int32)]
+
+
 _lib = None
 
 
@@ -140,6 +147,18 @@ def _declare(L):
         "gvx_detect_params_default": (None, [C.POINTER(DetectParams)]),
         "gvx_detect": (i32, [P, u64, P, i32, P, i32, i32, i32, C.POINTER(DetectParams), P, P, C.POINTER(i32)]),
         "gvx_clahe_params_default": (None, [C.POINTER(ClaheParams)]),
+        "gvx_undistort_points": (i32, [P, C.POINTER(Camera), i32, P, P]),
+        "gvx_undistort_points_dev": (i32, [P, C.POINTER(Camera), i32, P, P]),
+        "gvx_distort_points": (i32, [P, C.POINTER(Camera), i32, P, P]),
+        "gvx_distort_points_dev": (i32, [P, C.POINTER(Camera), i32, P, P]),
+        "gvx_predict_rotated": (i32, [P, C.POINTER(Camera), P, i32, P, P]),
+        "gvx_predict_rotated_dev": (i32, [P, C.POINTER(Camera), P, i32, P, P]),
+        "gvx_project_points": (i32, [P, C.POINTER(Camera), P, P, i32, P, P]),
+        "gvx_project_points_dev": (i32, [P, C.POINTER(Camera), P, P, i32, P, P]),
+        "gvx_point_velocity": (i32, [P, C.POINTER(Camera), i32, P, P, f64, P]),
+        "gvx_point_velocity_dev": (i32, [P, C.POINTER(Camera), i32, P, P, f64, P]),
+        "gvx_keypoint_parallax": (i32, [P, C.POINTER(Camera), P, P, i32, P, P, P]),
+        "gvx_keypoint_parallax_dev": (i32, [P, C.POINTER(Camera), P, P, i32, P, P, P]),
         "gvx_clahe_batch_dev": (i32, [P, i32, i32, i32, P, i64, i32, P, i64, i32, C.POINTER(ClaheParams), P]),
         "gvx_clahe": (i32, [P, i32, i32, P, i32, P, i32, C.POINTER(ClaheParams), P]),
         "gvx_frame_preprocess": (i32, [P, u64, P, i32, i32, i32, C.POINTER(ClaheParams), C.POINTER(KltParams),
@@ -279,6 +298,58 @@ class Context:
                                                      C.byref(clahe or ClaheParams.default()),
                                                      C.byref(params or KltParams.default()), d_hist_mean,
                                                      d_clahe_out), "frame_preprocess_dev")
+
+    # ----------------------------------------------------------- camera ops
+    def undistort_points(self, cam: Camera, pts):
+        """Camera::undistortPoints (camera.cc:72-74)."""
+        p = _f32xy(pts)
+        out = np.empty_like(p)
+        self._check(self._L.gvx_undistort_points(self._h, C.byref(cam), len(p), _ptr(p), _ptr(out)), "undistort")
+        return out
+
+    def distort_points(self, cam: Camera, pts):
+        """Camera::distortPoints (camera.cc:76-89)."""
+        p = _f32xy(pts)
+        out = np.empty_like(p)
+        self._check(self._L.gvx_distort_points(self._h, C.byref(cam), len(p), _ptr(p), _ptr(out)), "distort")
+        return out
+
+    def predict_rotated(self, cam: Camera, r_cur_pre, pts):
+        """trackReferenceFrame's rotation-compensated initial flow (tracking.cc:465-478)."""
+        p = _f32xy(pts)
+        R = np.ascontiguousarray(r_cur_pre, np.float64).reshape(9)
+        out = np.empty_like(p)
+        self._check(self._L.gvx_predict_rotated(self._h, C.byref(cam), _ptr(R), len(p), _ptr(p), _ptr(out)),
+                    "predict_rotated")
+        return out
+
+    def project_points(self, cam: Camera, R, t, pw):
+        """trackMappoint's prediction: world2pixel + distortPoints (tracking.cc:366-377)."""
+        R = np.ascontiguousarray(R, np.float64).reshape(9)
+        t = np.ascontiguousarray(t, np.float64).reshape(3)
+        pw = np.ascontiguousarray(pw, np.float64).reshape(-1, 3)
+        out = np.empty((len(pw), 2), np.float32)
+        self._check(self._L.gvx_project_points(self._h, C.byref(cam), _ptr(R), _ptr(t), len(pw), _ptr(pw),
+                                               _ptr(out)), "project_points")
+        return out
+
+    def point_velocity(self, cam: Camera, pre, cur, dt: float):
+        """(pixel2cam(cur) - pixel2cam(pre)) / dt (tracking.cc:433, :530)."""
+        a, b = _f32xy(pre), _f32xy(cur)
+        out = np.empty((len(a), 2), np.float64)
+        self._check(self._L.gvx_point_velocity(self._h, C.byref(cam), len(a), _ptr(a), _ptr(b), dt, _ptr(out)),
+                    "point_velocity")
+        return out
+
+    def keypoint_parallax(self, cam: Camera, R0, R1, ref, cur):
+        """Tracking::keyPointParallax (tracking.cc:861-871) per point pair."""
+        a, b = _f32xy(ref), _f32xy(cur)
+        R0 = np.ascontiguousarray(R0, np.float64).reshape(9)
+        R1 = np.ascontiguousarray(R1, np.float64).reshape(9)
+        out = np.empty(len(a), np.float64)
+        self._check(self._L.gvx_keypoint_parallax(self._h, C.byref(cam), _ptr(R0), _ptr(R1), len(a), _ptr(a),
+                                                  _ptr(b), _ptr(out)), "keypoint_parallax")
+        return out
 
     def frame_drop(self, fid: int):
         self._check(self._L.gvx_frame_drop(self._h, fid), "frame_drop")

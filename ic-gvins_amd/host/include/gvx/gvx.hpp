@@ -89,6 +89,16 @@ public:
         p.max_level = maxLevel;
         check(gvx_frame_put(ctx.get(), id_, gray, w, h, stride, &p), ctx.get(), "gvx_frame_put");
     }
+    // The raw frame through Tracking::preprocessing's CLAHE first (see preprocessFrame).
+    GpuFrame(Context& ctx, const uint8_t* gray, int w, int h, int stride, int maxLevel, const gvx_clahe_params* cp,
+             uint8_t* equalized, double* histMean)
+        : ctx_(&ctx), id_(next_id()), w_(w), h_(h), max_level_(maxLevel) {
+        gvx_klt_params p;
+        gvx_klt_params_default(&p);
+        p.max_level = maxLevel;
+        check(gvx_frame_preprocess(ctx.get(), id_, gray, w, h, stride, cp, &p, histMean, equalized), ctx.get(),
+              "gvx_frame_preprocess");
+    }
     ~GpuFrame() {
         if (ctx_) gvx_frame_drop(ctx_->get(), id_);
     }
@@ -231,6 +241,96 @@ inline bool featuresDetection(const GpuFrame& frame, const std::vector<Point2f>&
     if (blockCounts) *blockCounts = blk;
     return true;
 }
+
+// ------------------------------------------------------- preprocessing
+// cv::CLAHE stand-in: createCLAHE(clipLimit, tileGridSize) then apply (in place
+// allowed), as Tracking builds it at tracking.cc:63 and applies it at :139.
+class CLAHE {
+public:
+    CLAHE(Context& ctx, double clipLimit = 40.0, Size tileGridSize = Size{8, 8}) : ctx_(&ctx) {
+        p_.clip_limit = clipLimit;
+        p_.tiles_x = tileGridSize.width;
+        p_.tiles_y = tileGridSize.height;
+    }
+    void apply(const uint8_t* src, int w, int h, int srcStride, uint8_t* dst, int dstStride) const {
+        check(gvx_clahe(ctx_->get(), w, h, src, srcStride, dst, dstStride, &p_, nullptr), ctx_->get(), "gvx_clahe");
+    }
+    const gvx_clahe_params& params() const { return p_; }
+    Context& context() const { return *ctx_; }
+
+private:
+    Context* ctx_;
+    gvx_clahe_params p_;
+};
+inline CLAHE createCLAHE(Context& ctx, double clipLimit = 40.0, Size tileGridSize = Size{8, 8}) {
+    return CLAHE(ctx, clipLimit, tileGridSize);
+}
+
+// Tracking::preprocessing (tracking.cc:107-141) + the frame upload in one call:
+// CLAHE of the raw gray frame on the device, then its pyramid (a GpuFrame of the
+// equalised image).  equalized (nullable, w*h bytes) receives frame->image()
+// after :139; histMean (nullable) calculateHistigram of the raw frame (:88-105).
+inline GpuFrame preprocessFrame(const CLAHE& clahe, const uint8_t* gray, int w, int h, int stride,
+                                uint8_t* equalized = nullptr, double* histMean = nullptr, int maxLevel = 3) {
+    return GpuFrame(clahe.context(), gray, w, h, stride, maxLevel, &clahe.params(), equalized, histMean);
+}
+
+// ---------------------------------------------------------- camera ops
+// Camera (tracking/camera.h) point operations on the device; vectors in/out like
+// the reference's std::vector<cv::Point2f> calls.
+class Camera {
+public:
+    Camera(Context& ctx, const gvx_camera& c) : ctx_(&ctx), c_(c) {}
+    // Camera::undistortPoints / distortPoints (camera.cc:72-89), in place
+    void undistortPoints(std::vector<Point2f>& pts) const { run(gvx_undistort_points, pts); }
+    void distortPoints(std::vector<Point2f>& pts) const { run(gvx_distort_points, pts); }
+    // trackReferenceFrame's initial flow (tracking.cc:465-478)
+    std::vector<Point2f> predictRotated(const std::array<double, 9>& r_cur_pre, const std::vector<Point2f>& pts) const {
+        std::vector<Point2f> out(pts.size());
+        check(gvx_predict_rotated(ctx_->get(), &c_, r_cur_pre.data(), (int32_t)pts.size(), fp(pts), fp(out)),
+              ctx_->get(), "gvx_predict_rotated");
+        return out;
+    }
+    // trackMappoint's prediction: world2pixel + distortPoints (tracking.cc:366-377); pw n x 3
+    std::vector<Point2f> projectPoints(const std::array<double, 9>& R, const std::array<double, 3>& t,
+                                       const std::vector<double>& pw) const {
+        std::vector<Point2f> out(pw.size() / 3);
+        check(gvx_project_points(ctx_->get(), &c_, R.data(), t.data(), (int32_t)out.size(), pw.data(), fp(out)),
+              ctx_->get(), "gvx_project_points");
+        return out;
+    }
+    // (pixel2cam(cur) - pixel2cam(pre)) / dt (tracking.cc:433, :530), n x 2
+    std::vector<double> velocity(const std::vector<Point2f>& pre, const std::vector<Point2f>& cur, double dt) const {
+        if (pre.size() != cur.size()) throw Error(GVX_ERR_INVALID, "velocity: size mismatch");
+        std::vector<double> v(2 * pre.size());
+        check(gvx_point_velocity(ctx_->get(), &c_, (int32_t)pre.size(), fp(pre), fp(cur), dt, v.data()),
+              ctx_->get(), "gvx_point_velocity");
+        return v;
+    }
+    // Tracking::keyPointParallax (tracking.cc:861-871) per pair
+    std::vector<double> keyPointParallax(const std::array<double, 9>& R0, const std::array<double, 9>& R1,
+                                         const std::vector<Point2f>& ref, const std::vector<Point2f>& cur) const {
+        if (ref.size() != cur.size()) throw Error(GVX_ERR_INVALID, "keyPointParallax: size mismatch");
+        std::vector<double> out(ref.size());
+        check(gvx_keypoint_parallax(ctx_->get(), &c_, R0.data(), R1.data(), (int32_t)ref.size(), fp(ref), fp(cur),
+                                    out.data()),
+              ctx_->get(), "gvx_keypoint_parallax");
+        return out;
+    }
+    double focalLength() const { return (c_.fx + c_.fy) * 0.5; }  // camera.h:82-84
+
+private:
+    static const float* fp(const std::vector<Point2f>& v) { return reinterpret_cast<const float*>(v.data()); }
+    static float* fp(std::vector<Point2f>& v) { return reinterpret_cast<float*>(v.data()); }
+    template <class F>
+    void run(F f, std::vector<Point2f>& pts) const {
+        std::vector<Point2f> out(pts.size());
+        check(f(ctx_->get(), &c_, (int32_t)pts.size(), fp(pts), fp(out)), ctx_->get(), "camera op");
+        pts.swap(out);
+    }
+    Context* ctx_;
+    gvx_camera c_;
+};
 
 // ------------------------------------------------------ preintegration
 using IMU = gvx_imu;  // common/types.h:50-58 {time, dt, dtheta[3], dvel[3], odovel}

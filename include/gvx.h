@@ -167,6 +167,54 @@ gvx_status gvx_frame_preprocess_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_
                                     int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
                                     double* d_hist_mean, uint8_t* d_clahe_out);
 
+/* ------------------------------------------------------------ camera ops */
+/* Camera (tracking/camera.cc:25-46): K = [fx skew cx; 0 fy cy; 0 0 1] and the
+   distortion (k1, k2, p1, p2, k3); k3 = 0 for a 4-term config (:62-64). */
+typedef struct {
+    double fx, fy, cx, cy, skew;
+    double k1, k2, p1, p2, k3;
+    int32_t width, height;
+} gvx_camera;
+enum {
+    GVX_CAM_UNDISTORT = 0, GVX_CAM_DISTORT = 1, GVX_CAM_PREDICT = 2,
+    GVX_CAM_PROJECT = 3, GVX_CAM_VELOCITY = 4, GVX_CAM_PARALLAX = 5
+};
+
+/* Per-point camera operations around the KLT calls on n points (xy: n x 2
+   float pixels).  Host pointers, synchronous; each *_dev twin takes device
+   pointers and is async on the context stream.  Rotations are row-major 3x3
+   doubles.  Outputs may not alias inputs. */
+/* Camera::undistortPoints = cv::undistortPoints(pts, pts, K, D, Mat(), K) (camera.cc:72-74) */
+gvx_status gvx_undistort_points(gvx_ctx* ctx, const gvx_camera* cam, int32_t n, const float* xy, float* out);
+gvx_status gvx_undistort_points_dev(gvx_ctx* ctx, const gvx_camera* cam, int32_t n, const float* d_xy, float* d_out);
+/* Camera::distortPoints (camera.cc:76-89) */
+gvx_status gvx_distort_points(gvx_ctx* ctx, const gvx_camera* cam, int32_t n, const float* xy, float* out);
+gvx_status gvx_distort_points_dev(gvx_ctx* ctx, const gvx_camera* cam, int32_t n, const float* d_xy, float* d_out);
+/* Tracking::trackReferenceFrame's initial flow (tracking.cc:465-478): undistort,
+   pixel2cam, r_cur_pre * pc, distortCameraPoint (camera.cc:105-118). */
+gvx_status gvx_predict_rotated(gvx_ctx* ctx, const gvx_camera* cam, const double* r_cur_pre, int32_t n,
+                               const float* xy, float* out);
+gvx_status gvx_predict_rotated_dev(gvx_ctx* ctx, const gvx_camera* cam, const double* r_cur_pre, int32_t n,
+                                   const float* d_xy, float* d_out);
+/* Tracking::trackMappoint's prediction (tracking.cc:366-377): world2pixel(pw,
+   pose) (camera.cc:137-143, R/t = pose.R, pose.t) then distortPoints; pw n x 3. */
+gvx_status gvx_project_points(gvx_ctx* ctx, const gvx_camera* cam, const double* R, const double* t, int32_t n,
+                              const double* pw, float* out);
+gvx_status gvx_project_points_dev(gvx_ctx* ctx, const gvx_camera* cam, const double* R, const double* t,
+                                  int32_t n, const double* d_pw, float* d_out);
+/* (pixel2cam(cur) - pixel2cam(pre)) / dt on undistorted points (tracking.cc:433,
+   :530); vel n x 2 doubles. */
+gvx_status gvx_point_velocity(gvx_ctx* ctx, const gvx_camera* cam, int32_t n, const float* pre, const float* cur,
+                              double dt, double* vel);
+gvx_status gvx_point_velocity_dev(gvx_ctx* ctx, const gvx_camera* cam, int32_t n, const float* d_pre,
+                                  const float* d_cur, double dt, double* d_vel);
+/* Tracking::keyPointParallax (tracking.cc:861-871) per undistorted point pair,
+   R0/R1 = pose0.R / pose1.R; out n doubles (pixels). */
+gvx_status gvx_keypoint_parallax(gvx_ctx* ctx, const gvx_camera* cam, const double* R0, const double* R1,
+                                 int32_t n, const float* ref, const float* cur, double* out);
+gvx_status gvx_keypoint_parallax_dev(gvx_ctx* ctx, const gvx_camera* cam, const double* R0, const double* R1,
+                                     int32_t n, const float* d_ref, const float* d_cur, double* d_out);
+
 /* ------------------------------------------------------ feature detection */
 /* Tracking::featuresDetection (tracking/tracking.cc:576-688): block grid from
    the Tracking ctor (:65-85), FILLED circle mask of radius

@@ -28,6 +28,9 @@
  *   orc_preint_*           preintegration/preintegration_{base,earth,normal}.cc
  *   orc_preint_factor_eval preintegration/preintegration_factor.h:45-69
  *   orc_reproj_eval        factors/reprojection_factor.h:61-161
+ *   orc_undistort_points .. orc_keypoint_parallax  per-point camera operations
+ *                          around the KLT calls (camera.c; tracking/camera.cc:72-143,
+ *                          tracking.cc:366-377, :419-437, :462-478, :514-544, :861-871)
  *   orc_clahe / orc_hist_mean  Tracking::preprocessing (tracking.cc:107-141):
  *                          cv::createCLAHE(3.0, Size(21,21))->apply and
  *                          calculateHistigram (clahe.c)
@@ -265,6 +268,24 @@ void orc_clahe_luts(const uint8_t* src, int w, int h, int stride, double clip_li
 void orc_clahe(const uint8_t* src, int w, int h, int stride, double clip_limit, int tiles_x, int tiles_y,
                uint8_t* dst, int dst_stride);
 double orc_hist_mean(const uint8_t* src, int w, int h, int stride);
+
+/* ------------------------------------------------------------------------- */
+/* Camera operations (camera.c)                                               */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    double fx, fy, cx, cy, skew;  /* intrinsic [fx skew cx; 0 fy cy; 0 0 1] (camera.cc:29-33) */
+    double k1, k2, p1, p2, k3;    /* distortion (camera.cc:35-39) */
+    int width, height;
+} orc_camera;
+void orc_undistort_points(const orc_camera* c, int n, const float* in, float* out);
+void orc_distort_points(const orc_camera* c, int n, const float* in, float* out);
+void orc_predict_rotated(const orc_camera* c, const double* r_cur_pre, int n, const float* in, float* out);
+void orc_project_points(const orc_camera* c, const double* R, const double* t, int n, const double* pw,
+                        float* out);
+void orc_point_velocity(const orc_camera* c, int n, const float* pre, const float* cur, double dt, double* vel);
+void orc_r1t_r0(const double* R0, const double* R1, double* M);
+void orc_keypoint_parallax(const orc_camera* c, const double* R0, const double* R1, int n, const float* ref,
+                           const float* cur, double* out);
 
 #ifdef __cplusplus
 }

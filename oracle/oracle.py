@@ -80,6 +80,12 @@ class ReprojConst(C.Structure):
                 ("std", C.c_double)]
 
 
+class Camera(C.Structure):
+    """Camera intrinsics + distortion (tracking/camera.cc:25-46)."""
+    _fields_ = [(k, C.c_double) for k in ("fx", "fy", "cx", "cy", "skew", "k1", "k2", "p1", "p2", "k3")] + \
+               [("width", C.c_int), ("height", C.c_int)]
+
+
 _lib = None
 
 
@@ -131,6 +137,13 @@ def lib():
         L.orc_clahe.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, P, C.c_int]
         L.orc_hist_mean.argtypes = [P, C.c_int, C.c_int, C.c_int]
         L.orc_hist_mean.restype = C.c_double
+        CP = C.POINTER(Camera)
+        L.orc_undistort_points.argtypes = [CP, C.c_int, P, P]
+        L.orc_distort_points.argtypes = [CP, C.c_int, P, P]
+        L.orc_predict_rotated.argtypes = [CP, P, C.c_int, P, P]
+        L.orc_project_points.argtypes = [CP, P, P, C.c_int, P, P]
+        L.orc_point_velocity.argtypes = [CP, C.c_int, P, P, C.c_double, P]
+        L.orc_keypoint_parallax.argtypes = [CP, P, P, C.c_int, P, P, P]
         _lib = L
     return _lib
 
@@ -421,3 +434,55 @@ def hist_mean(img: np.ndarray) -> float:
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape
     return float(lib().orc_hist_mean(_p(img), w, h, w))
+
+
+# ------------------------------------------------------------------ camera ops
+def _xy(a):
+    return np.ascontiguousarray(a, np.float32).reshape(-1, 2)
+
+
+def undistort_points(cam: Camera, pts):
+    p = _xy(pts)
+    out = np.empty_like(p)
+    lib().orc_undistort_points(C.byref(cam), len(p), _p(p), _p(out))
+    return out
+
+
+def distort_points(cam: Camera, pts):
+    p = _xy(pts)
+    out = np.empty_like(p)
+    lib().orc_distort_points(C.byref(cam), len(p), _p(p), _p(out))
+    return out
+
+
+def predict_rotated(cam: Camera, r_cur_pre, pts):
+    p = _xy(pts)
+    R = np.ascontiguousarray(r_cur_pre, np.float64).reshape(9)
+    out = np.empty_like(p)
+    lib().orc_predict_rotated(C.byref(cam), _p(R), len(p), _p(p), _p(out))
+    return out
+
+
+def project_points(cam: Camera, R, t, pw):
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    t = np.ascontiguousarray(t, np.float64).reshape(3)
+    pw = np.ascontiguousarray(pw, np.float64).reshape(-1, 3)
+    out = np.empty((len(pw), 2), np.float32)
+    lib().orc_project_points(C.byref(cam), _p(R), _p(t), len(pw), _p(pw), _p(out))
+    return out
+
+
+def point_velocity(cam: Camera, pre, cur, dt):
+    a, b = _xy(pre), _xy(cur)
+    out = np.empty((len(a), 2), np.float64)
+    lib().orc_point_velocity(C.byref(cam), len(a), _p(a), _p(b), dt, _p(out))
+    return out
+
+
+def keypoint_parallax(cam: Camera, R0, R1, ref, cur):
+    a, b = _xy(ref), _xy(cur)
+    R0 = np.ascontiguousarray(R0, np.float64).reshape(9)
+    R1 = np.ascontiguousarray(R1, np.float64).reshape(9)
+    out = np.empty(len(a), np.float64)
+    lib().orc_keypoint_parallax(C.byref(cam), _p(R0), _p(R1), len(a), _p(a), _p(b), _p(out))
+    return out

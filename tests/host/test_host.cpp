@@ -94,6 +94,39 @@ int main(int argc, char** argv) {
     if (!ran) corners.clear();
     writef(d + "det.bin", corners.data(), corners.size());
 
+    // Tracking::preprocessing: clahe_ = cv::createCLAHE(3.0, Size(21, 21)) (tracking.cc:63),
+    // apply (:139); the one-call form must give the same equalised frame
+    gvx::CLAHE clahe = gvx::createCLAHE(ctx, 3.0, gvx::Size{21, 21});
+    std::vector<uint8_t> eq(I.size()), eq2(I.size());
+    clahe.apply(I.data(), w, h, w, eq.data(), w);
+    double hmean = 0;
+    gvx::GpuFrame fP = gvx::preprocessFrame(clahe, I.data(), w, h, w, eq2.data(), &hmean);
+    if (eq != eq2 || fP.width() != w) {
+        std::printf("FAIL preprocessFrame\n");
+        return 1;
+    }
+    writef(d + "clahe.bin", eq.data(), eq.size());
+    writef(d + "hist_mean.bin", &hmean, 1);
+
+    // Camera point operations (camera.cc, tracking.cc:366-544, :861-871)
+    const auto cv = readf<double>(d + "cam.bin");  // fx fy cx cy skew k1 k2 p1 p2 k3
+    const gvx_camera gc{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7], cv[8], cv[9], w, h};
+    gvx::Camera cam(ctx, gc);
+    std::vector<gvx::Point2f> und = prev, dis = prev;
+    cam.undistortPoints(und);
+    cam.distortPoints(dis);
+    const auto rot = readf<double>(d + "rot.bin");  // r_cur_pre, R0, R1
+    std::array<double, 9> Rc, R0, R1;
+    for (int k = 0; k < 9; ++k) Rc[k] = rot[k], R0[k] = rot[9 + k], R1[k] = rot[18 + k];
+    const auto pred = cam.predictRotated(Rc, prev);
+    const auto vel = cam.velocity(prev, init, 0.05);
+    const auto par = cam.keyPointParallax(R0, R1, prev, init);
+    writef(d + "cam_undist.bin", und.data(), und.size());
+    writef(d + "cam_dist.bin", dis.data(), dis.size());
+    writef(d + "cam_pred.bin", pred.data(), pred.size());
+    writef(d + "cam_vel.bin", vel.data(), vel.size());
+    writef(d + "cam_par.bin", par.data(), par.size());
+
     // preintegration: constructor(imu0) + addNewImu per sample, then reintegration
     const auto imu = readf<gvx::IMU>(d + "imu.bin");
     const auto st = readf<double>(d + "state.bin");

@@ -73,6 +73,14 @@ def test_host_mirror_matches_oracle(host_bin, orc, tmp_path, variant):
     rblocks = [pr[o[0]:o[0] + 7], pr[o[1]:o[1] + 7], pr[o[2]:o[2] + 7], pr[o[3]:o[3] + 1], pr[o[4]:o[4] + 1]]
     np.concatenate(rblocks).tofile(f"{d}/rparams.bin")
 
+    cam = (787.1611861559479, 787.3928431375225, 664.4061078354368, 519.5129292754456, 0.0,
+           -0.0917403092279957, 0.08134715036932794, 0.00017620136958692255, 0.00016737385248865412, 0.0)
+    np.array(cam, np.float64).tofile(f"{d}/cam.bin")
+    a, b = 0.02 + 0.01 * variant, 0.3
+    Rc = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+    R0 = np.array([[np.cos(b), -np.sin(b), 0], [np.sin(b), np.cos(b), 0], [0, 0, 1]])
+    np.concatenate([Rc.ravel(), R0.ravel(), (Rc @ R0).ravel()]).tofile(f"{d}/rot.bin")
+
     r = subprocess.run([host_bin, "run", d], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
@@ -89,6 +97,14 @@ def test_host_mirror_matches_oracle(host_bin, orc, tmp_path, variant):
     assert np.array_equal(rd("fb_reduced.bin", np.float32).reshape(-1, 2), fb["next"][fb["kept_idx"]])
     det, _ = orc.features_detection(I, None, None, False, 0, orc.DetectParams.default())
     assert np.array_equal(rd("det.bin", np.float32).reshape(-1, 2), det)
+    assert np.array_equal(rd("clahe.bin", np.uint8).reshape(h, w), orc.clahe(I))
+    assert rd("hist_mean.bin", np.float64)[0] == orc.hist_mean(I)
+    oc = orc.Camera(*cam, w, h)
+    assert np.array_equal(rd("cam_undist.bin", np.float32).reshape(-1, 2), orc.undistort_points(oc, prev))
+    assert np.array_equal(rd("cam_dist.bin", np.float32).reshape(-1, 2), orc.distort_points(oc, prev))
+    assert np.array_equal(rd("cam_pred.bin", np.float32).reshape(-1, 2), orc.predict_rotated(oc, Rc, prev))
+    assert np.array_equal(rd("cam_vel.bin", np.float64).reshape(-1, 2), orc.point_velocity(oc, prev, init, 0.05))
+    assert np.array_equal(rd("cam_par.bin", np.float64), orc.keypoint_parallax(oc, R0, Rc @ R0, prev, init))
 
     ps = rd("pre_state.bin", np.float64)
     dlt, cur = seg.delta(), seg.current()
