@@ -5,8 +5,9 @@
 // CLAHE_Impl::apply, 8-bit) are written down in oracle/clahe.c.
 //
 // Kernels:
-//  lut_kernel    one 256-thread workgroup per (image, row of tiles): every
-//                pixel of the tile row is read once (8 bytes per load, 8 loads
+//  lut_kernel    one 256-thread workgroup per (image, row of tiles, group of
+//                tiles -- the whole row for batches, a few tiles for a single
+//                frame): every pixel of the group is read once (8 bytes per load, 8 loads
 //                in flight per thread) into per-tile LDS histograms, the
 //                REFLECT_101 pad pixels (copyMakeBorder of the LUT source)
 //                are added, and each wave then turns tiles into LUTs: clip,
@@ -55,6 +56,7 @@ __device__ __forceinline__ int div_small(int x, int d, float inv_d) {
 }
 
 constexpr int LUT_THREADS = 256;
+constexpr int HROW = 257;  // histogram stride: one value in neighbouring tiles -> different banks
 constexpr int LUT_UNROLL = 8;
 
 // CLAHE_CalcLut_Body for one tile, by one wavefront: h = the tile's 256 bins.
@@ -99,30 +101,35 @@ __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, 
 }
 
 __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
-                                                          int stride, ClaheGeom g, int vec8,
+                                                          int stride, ClaheGeom g, int vec8, int tpw,
                                                           uint8_t* __restrict__ lut,
                                                           uint32_t* __restrict__ hist_img) {
-    extern __shared__ uint32_t hs[];  // tiles_x * 256 bins
-    const int img = blockIdx.x / g.tiles_y, ty = blockIdx.x - img * g.tiles_y;
+    extern __shared__ uint32_t hs[];  // tpw histograms of 256 bins, HROW dwords apart
+    const int ngrp = (g.tiles_x + tpw - 1) / tpw;
+    const int img = blockIdx.x / (g.tiles_y * ngrp);
+    const int rem = blockIdx.x - img * g.tiles_y * ngrp;
+    const int ty = rem / ngrp, grp = rem - ty * ngrp;
+    const int txa0 = grp * tpw, txa1 = min(txa0 + tpw, g.tiles_x);  // this workgroup's tiles
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    const int nbins = g.tiles_x * 256;
+    const int nbins = (txa1 - txa0) * HROW;
     for (int i = t; i < nbins; i += LUT_THREADS) hs[i] = 0;
     __syncthreads();
     const uint8_t* s = src + img * img_stride;
     const int y0 = ty * g.th;
     const int rows_in = max(0, min(y0 + g.th, g.h) - y0);
     const float inv_tw = 1.0f / g.tw;
-    // ---- in-image pixels of the tile row (every tile: x in [0, w)) ----
+    const int xlo = txa0 * g.tw, xhi_ext = txa1 * g.tw, xhi = min(xhi_ext, g.w);  // in-image columns [xlo, xhi)
+    // ---- in-image pixels ----
     if (vec8) {
-        const int n8 = g.w >> 3;  // w % 8 == 0
-        const int total = rows_in * n8;
+        const int c8lo = xlo >> 3, n8 = ((xhi + 7) >> 3) - c8lo;  // w % 8 == 0: chunks stay in the row
+        const int total = rows_in * max(n8, 0);
         for (int base = t; base < total; base += LUT_UNROLL * LUT_THREADS) {
             uint2 v[LUT_UNROLL];
             int x0[LUT_UNROLL];
 #pragma unroll
             for (int k = 0; k < LUT_UNROLL; ++k) {
                 const int i = base + k * LUT_THREADS;
-                const int r = i / n8, c8 = i - r * n8;
+                const int r = i / n8, c8 = c8lo + (i - r * n8);
                 x0[k] = 8 * c8;
                 v[k] = i < total ? *reinterpret_cast<const uint2*>(s + (int64_t)(y0 + r) * stride + 8 * c8)
                                  : uint2{0, 0};
@@ -130,50 +137,52 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
 #pragma unroll
             for (int k = 0; k < LUT_UNROLL; ++k) {
                 if (base + k * LUT_THREADS >= total) break;
-                const int txa = div_small(x0[k], g.tw, inv_tw);
+                const int txa = div_small(max(x0[k], xlo), g.tw, inv_tw);
                 const int xb = (txa + 1) * g.tw;  // first column of the next tile
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const uint32_t b = ((j < 4 ? v[k].x : v[k].y) >> (8 * (j & 3))) & 255u;
                     const int x = x0[k] + j;
                     const int tx = x < xb ? txa : (x < xb + g.tw ? txa + 1 : div_small(x, g.tw, inv_tw));
-                    atomicAdd(&hs[tx * 256 + b], 1u);
+                    if (x >= xlo && x < xhi) atomicAdd(&hs[(tx - txa0) * HROW + b], 1u);
                 }
             }
         }
     } else {
-        const int total = rows_in * g.w;
+        const int cw = xhi - xlo;
+        const int total = rows_in * max(cw, 0);
         for (int i = t; i < total; i += LUT_THREADS) {
-            const int r = i / g.w, x = i - r * g.w;
-            atomicAdd(&hs[div_small(x, g.tw, inv_tw) * 256 + s[(int64_t)(y0 + r) * stride + x]], 1u);
+            const int r = i / cw, x = xlo + (i - r * cw);
+            atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + s[(int64_t)(y0 + r) * stride + x]], 1u);
         }
     }
     if (hist_img) {
         __syncthreads();
         for (int b = t; b < 256; b += LUT_THREADS) {
             uint32_t sum = 0;
-            for (int tx = 0; tx < g.tiles_x; ++tx) sum += hs[tx * 256 + b];
+            for (int tx = 0; tx < txa1 - txa0; ++tx) sum += hs[tx * HROW + b];
             if (sum) atomicAdd(&hist_img[img * 256 + b], sum);
         }
     }
     // ---- the copyMakeBorder(..., BORDER_REFLECT_101) part of the LUT source ----
-    const int ew = g.tiles_x * g.tw;
-    if (ew > g.w) {  // pad columns of the in-image rows
-        const int pc = ew - g.w;
+    if (xhi_ext > g.w) {  // pad columns of the in-image rows (this group's share)
+        const int pxlo = max(g.w, xlo), pc = xhi_ext - pxlo;
         for (int i = t; i < rows_in * pc; i += LUT_THREADS) {
-            const int r = i / pc, x = g.w + (i - r * pc);
-            atomicAdd(&hs[div_small(x, g.tw, inv_tw) * 256 + s[(int64_t)(y0 + r) * stride + refl101(x, g.w)]], 1u);
+            const int r = i / pc, x = pxlo + (i - r * pc);
+            atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + s[(int64_t)(y0 + r) * stride + refl101(x, g.w)]],
+                      1u);
         }
     }
-    const int pr = g.th - rows_in;  // pad rows (reflected source rows), every ext column
-    for (int i = t; i < pr * ew; i += LUT_THREADS) {
-        const int r = i / ew, x = i - r * ew;
+    const int pr = g.th - rows_in, ecw = xhi_ext - xlo;  // pad rows (reflected source rows), this group's columns
+    for (int i = t; i < pr * ecw; i += LUT_THREADS) {
+        const int r = i / ecw, x = xlo + (i - r * ecw);
         const int sy = refl101(y0 + rows_in + r, g.h);
-        atomicAdd(&hs[div_small(x, g.tw, inv_tw) * 256 + s[(int64_t)sy * stride + refl101(x, g.w)]], 1u);
+        atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + s[(int64_t)sy * stride + refl101(x, g.w)]], 1u);
     }
     __syncthreads();
-    for (int tx = wave; tx < g.tiles_x; tx += LUT_THREADS / 64)
-        tile_lut(hs + tx * 256, g, lane, lut + ((int64_t)img * g.tiles_x * g.tiles_y + ty * g.tiles_x + tx) * 256);
+    for (int tx = txa0 + wave; tx < txa1; tx += LUT_THREADS / 64)
+        tile_lut(hs + (tx - txa0) * HROW, g, lane,
+                 lut + ((int64_t)img * g.tiles_x * g.tiles_y + ty * g.tiles_x + tx) * 256);
 }
 
 constexpr int TROW = 257;  // LDS dwords per table row (bank skew between tiles)
@@ -356,8 +365,13 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const bool src8 = (uintptr_t)src % 8 == 0 && stride % 8 == 0 && img_stride % 8 == 0;
     const bool dst8 = (uintptr_t)dst % 8 == 0 && dst_stride % 8 == 0 && dst_img_stride % 8 == 0;
     const int lut_vec8 = src8 && g.w % 8 == 0;
-    hipLaunchKernelGGL(lut_kernel, dim3(n * g.tiles_y), dim3(LUT_THREADS), (size_t)g.tiles_x * 256 * 4, c->stream,
-                       src, img_stride, stride, g, lut_vec8, lut, hist_img);
+    // tiles per workgroup: a whole tile row for batches, fewer for single frames
+    int ngrp = 1;
+    while ((int64_t)n * g.tiles_y * ngrp < 2LL * c->n_cu && ngrp < g.tiles_x) ++ngrp;
+    const int tpw = (g.tiles_x + ngrp - 1) / ngrp;
+    ngrp = (g.tiles_x + tpw - 1) / tpw;
+    hipLaunchKernelGGL(lut_kernel, dim3(n * g.tiles_y * ngrp), dim3(LUT_THREADS), (size_t)tpw * HROW * 4, c->stream,
+                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img);
     // bands of rows sharing one pair of LUT rows, split to fill the chip
     const int nb = g.tiles_y + 1;
     int nsplit = 1;
