@@ -9,7 +9,7 @@ unpinned against OpenCV itself).  They are small (about
 200 KB total), numeric-only .npz files (np.load(..., allow_pickle=False)), and
 tests/test_golden.py checks both the oracle (CPU) and libgvx (GPU) against them.
 
-    python tests/golden/make_golden.py      # rewrites tests/golden/*.npz
+    python tests/golden/make_golden.py [name.npz ...]   # rewrites tests/golden/*.npz
 """
 import os
 import sys
@@ -88,15 +88,54 @@ def reproj_case(name, n_kf, n_lm):
                         residuals=np.array(res), jacobians=np.array(jac))
 
 
+def clahe_case(name, w, h, tiles, clip, seed):
+    img = synth.make_image(w, h, np.random.default_rng(seed))
+    np.savez_compressed(os.path.join(HERE, name), img=img, tiles=np.int32(tiles), clip=np.float64(clip),
+                        luts=orc.clahe_luts(img, clip, tiles), out=orc.clahe(img, clip, tiles),
+                        hist_mean=np.float64(orc.hist_mean(img)))
+
+
+# config/gvins.yaml:65-73 (k3 = 0 for the 4-term distortion, camera.cc:62-64)
+KAIST_CAM = (787.1611861559479, 787.3928431375225, 664.4061078354368, 519.5129292754456, 0.0,
+             -0.0917403092279957, 0.08134715036932794, 0.00017620136958692255, 0.00016737385248865412, 0.0)
+
+
+def camera_case(name, n, seed):
+    rng = np.random.default_rng(seed)
+    cam = orc.Camera(*KAIST_CAM, 1278, 1022)
+    p = np.c_[rng.uniform(-20, 1298, n), rng.uniform(-20, 1042, n)].astype(np.float32)
+    q = (p + rng.uniform(-4, 4, (n, 2))).astype(np.float32)
+    a = 0.03
+    R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+    R0 = np.array([[np.cos(0.4), -np.sin(0.4), 0], [np.sin(0.4), np.cos(0.4), 0], [0, 0, 1]])
+    R1 = R @ R0
+    t = np.array([0.3, -1.2, 2.0])
+    pc = np.c_[rng.uniform(-8, 8, n), rng.uniform(-4, 4, n), rng.uniform(3, 60, n)]
+    pw = pc @ R0.T + t
+    np.savez_compressed(os.path.join(HERE, name), cam=np.array(KAIST_CAM), p=p, q=q, R=R, R0=R0, R1=R1, t=t, pw=pw,
+                        undist=orc.undistort_points(cam, p), dist=orc.distort_points(cam, p),
+                        pred=orc.predict_rotated(cam, R, p), proj=orc.project_points(cam, R0, t, pw),
+                        vel=orc.point_velocity(cam, p, q, 0.05), parallax=orc.keypoint_parallax(cam, R0, R1, p, q))
+
+
+CASES = {
+    "klt_160x70_n32_L3.npz": lambda n: klt_case(n, 160, 70, 32, 3, 1),
+    "klt_320x140_n64_L3.npz": lambda n: klt_case(n, 320, 140, 64, 3, 2),
+    "klt_333x97_n40_L2.npz": lambda n: klt_case(n, 333, 97, 40, 2, 3),
+    "detect_320x140.npz": lambda n: detect_case(n, 320, 140, 11, 12),
+    "preint_normal_m20.npz": lambda n: preint_case(n, NORMAL, 20, 41),
+    "preint_earth_m20.npz": lambda n: preint_case(n, EARTH, 20, 42),
+    "preint_earth_m100.npz": lambda n: preint_case(n, EARTH, 100, 43),
+    "reproj_3kf_16lm.npz": lambda n: reproj_case(n, 3, 16),
+    "clahe_320x140_t21.npz": lambda n: clahe_case(n, 320, 140, (21, 21), 3.0, 51),
+    "clahe_215x147_t8x6.npz": lambda n: clahe_case(n, 215, 147, (8, 6), 2.0, 52),
+    "camera_kaist_n200.npz": lambda n: camera_case(n, 200, 61),
+}
+
 if __name__ == "__main__":
-    klt_case("klt_160x70_n32_L3.npz", 160, 70, 32, 3, 1)
-    klt_case("klt_320x140_n64_L3.npz", 320, 140, 64, 3, 2)
-    klt_case("klt_333x97_n40_L2.npz", 333, 97, 40, 2, 3)
-    detect_case("detect_320x140.npz", 320, 140, 11, 12)
-    preint_case("preint_normal_m20.npz", NORMAL, 20, 41)
-    preint_case("preint_earth_m20.npz", EARTH, 20, 42)
-    preint_case("preint_earth_m100.npz", EARTH, 100, 43)
-    reproj_case("reproj_3kf_16lm.npz", 3, 16)
+    # python make_golden.py [case ...]: only the named fixtures (default: all)
+    for name in (sys.argv[1:] or list(CASES)):
+        CASES[name](name)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

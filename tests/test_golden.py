@@ -163,3 +163,50 @@ def test_gpu_reproj_golden(ctx, gvx_mod):
     consts = np.ascontiguousarray(z["consts"]).view(gvx_mod.REPROJ_DTYPE).reshape(-1)
     res, jac = ctx.reproj_eval(consts, z["params"], z["offs"])
     assert np.array_equal(res, z["residuals"]) and np.array_equal(jac, z["jacobians"])
+
+
+# ------------------------------------------------- preprocessing and camera ops
+def _cam(mod, z):
+    return mod.Camera(*[float(v) for v in z["cam"]], 1278, 1022)
+
+
+@pytest.mark.parametrize("name", cases("clahe_"))
+def test_oracle_clahe_golden(orc, name):
+    z = load(name)
+    tiles, clip = tuple(int(t) for t in z["tiles"]), float(z["clip"])
+    assert np.array_equal(orc.clahe_luts(z["img"], clip, tiles), z["luts"])
+    assert np.array_equal(orc.clahe(z["img"], clip, tiles), z["out"])
+    assert orc.hist_mean(z["img"]) == float(z["hist_mean"])
+
+
+def test_oracle_camera_golden(orc):
+    z = load("camera_kaist_n200.npz")
+    c = _cam(orc, z)
+    assert np.array_equal(orc.undistort_points(c, z["p"]), z["undist"])
+    assert np.array_equal(orc.distort_points(c, z["p"]), z["dist"])
+    assert np.array_equal(orc.predict_rotated(c, z["R"], z["p"]), z["pred"])
+    assert np.array_equal(orc.project_points(c, z["R0"], z["t"], z["pw"]), z["proj"])
+    assert np.array_equal(orc.point_velocity(c, z["p"], z["q"], 0.05), z["vel"])
+    assert np.array_equal(orc.keypoint_parallax(c, z["R0"], z["R1"], z["p"], z["q"]), z["parallax"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", cases("clahe_"))
+def test_gpu_clahe_golden(ctx, gvx_mod, name):
+    z = load(name)
+    tiles = tuple(int(t) for t in z["tiles"])
+    p = gvx_mod.ClaheParams.default(clip_limit=float(z["clip"]), tiles_x=tiles[0], tiles_y=tiles[1])
+    out, m = ctx.clahe(z["img"], p, hist_mean=True)
+    assert np.array_equal(out, z["out"]) and m == float(z["hist_mean"])
+
+
+@pytest.mark.gpu
+def test_gpu_camera_golden(ctx, gvx_mod):
+    z = load("camera_kaist_n200.npz")
+    c = _cam(gvx_mod, z)
+    assert np.array_equal(ctx.undistort_points(c, z["p"]), z["undist"])
+    assert np.array_equal(ctx.distort_points(c, z["p"]), z["dist"])
+    assert np.array_equal(ctx.predict_rotated(c, z["R"], z["p"]), z["pred"])
+    assert np.array_equal(ctx.project_points(c, z["R0"], z["t"], z["pw"]), z["proj"])
+    assert np.array_equal(ctx.point_velocity(c, z["p"], z["q"], 0.05), z["vel"])
+    assert np.array_equal(ctx.keypoint_parallax(c, z["R0"], z["R1"], z["p"], z["q"]), z["parallax"])
