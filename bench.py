@@ -236,6 +236,18 @@ def main():
     ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if not args.no_pre else None
+    pcie = None
+    if world == 1 and not args.no_pre:
+        # host-buffer rate (gvx_klt_fb_batch: images and points copied in and out per
+        # call, PCIe-inclusive) -- reported beside `value`, never as it
+        ctx.klt_fb_batch(I, J, P, Q, params=params)
+        hs = max(3, args.steps // 8)
+        t1 = time.perf_counter()
+        for _ in range(hs):
+            ctx.klt_fb_batch(I, J, P, Q, params=params)
+        pcie = {"pairs_per_s": round(Pn * hs / (time.perf_counter() - t1), 1), "steps": hs,
+                "what": "gvx_klt_fb_batch on host buffers (2 x %.0f MB image upload + points per step)"
+                        % (I.nbytes / 1e6)}
     if world > 1 and not args.gather:
         collect_once = [torch.empty_like(dNK) for _ in range(world)]
         dist.all_gather(collect_once, dNK)  # results check, outside the timed region
@@ -290,6 +302,7 @@ def main():
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
             "preprocess": pre,
+            "host_buffers": pcie,
         }
         print(json.dumps(line))
     if dist:
