@@ -486,8 +486,9 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
     hipEvent_t ev{};
     prof_begin(c, "pyramid", &ev);
     // level 0 stays in the caller's images; levels >= 1 go to the pyramid slots
-    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, n_pairs, lay, pyr_prev, false);
-    if (e == hipSuccess) e = launch_build_pyramids(c, d_next, (int64_t)w * h, w, n_pairs, lay, pyr_next, false);
+    // one launch per kernel for both frames of every pair (pyr_next follows pyr_prev)
+    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, 2 * n_pairs, lay, pyr_prev, false, d_next,
+                                         n_pairs);
     prof_end(c, "pyramid", ev);
     if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
     if (n_pts == 0) {

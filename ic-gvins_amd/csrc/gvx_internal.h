@@ -90,8 +90,11 @@ void prof_drain(gvx_ctx* c);
 // Build pyramids for n_img images (h x w, row stride `stride` bytes, image i at
 // src + i*img_stride) into dst + i*lay.bytes: levels >= 1 always; the padded
 // level-0 copy only when write_l0 (otherwise level 0 stays the caller's image).
+// src_b (optional): images n_a .. n_img-1 come from src_b + (i - n_a)*img_stride
+// instead (the prev and next frames of a batch built in one launch per kernel).
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride,
-                                 int n_img, const PyrLayout& lay, uint8_t* dst, bool write_l0);
+                                 int n_img, const PyrLayout& lay, uint8_t* dst, bool write_l0,
+                                 const uint8_t* src_b = nullptr, int n_a = 0);
 
 // Workgroups are dispatched to the 8 XCDs round-robin by id (each XCD has its
 // own L2).  xcd_swizzle maps the dispatch id to a logical id so that XCD k runs

@@ -347,7 +347,10 @@ __global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ 
 // columns >= w are re-gathered from their mirror lanes (ds_bpermute) and the
 // rows >= h are taken from their mirror rows in the rolling registers.
 constexpr int ST_COLS = 480;  // source columns owned per strip
-constexpr int BAND = 32;      // level-1 rows owned per band (level k: BAND >> (k-1))
+#ifndef STREAM_BAND
+#define STREAM_BAND 32
+#endif
+constexpr int BAND = STREAM_BAND;  // level-1 rows owned per band (level k: BAND >> (k-1))
 
 // Levels of at least RING_MIRROR_H rows get their top / bottom ring rows from
 // the streaming pass (each ring row is a single-bounce REFLECT_101 copy of one
@@ -399,9 +402,10 @@ __device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pi
 // byte-reversed mirror ranges, built from aligned dword loads and v_perm.
 // Requires w % 4 == 0 and 4-byte aligned rows (other inputs take the padded
 // level-0 copy instead); vec16: 16-byte aligned rows and w % 16 == 0.
-__global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ src, int64_t img_stride, int pitch,
-                                                   int w, int h, uint8_t* __restrict__ E, int64_t e_img_stride,
-                                                   int epitch, int vec16) {
+__global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ src, const uint8_t* __restrict__ src_b,
+                                                   int n_a, int64_t img_stride, int pitch, int w, int h,
+                                                   uint8_t* __restrict__ E, int64_t e_img_stride, int epitch,
+                                                   int vec16) {
     const int img = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= h * 6) return;
@@ -417,7 +421,7 @@ __global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ s
         q = (j & 3) < 2 ? (j & 3) : (j & 3) + 2;
     }
     const int x = q < 3 ? -32 + 16 * q : w - EDGE_R + 16 * (q - 3);
-    const uint8_t* row = src + img * img_stride + (int64_t)y * pitch;
+    const uint8_t* row = (img < n_a ? src + img * img_stride : src_b + (img - n_a) * img_stride) + (int64_t)y * pitch;
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);  // 4-byte aligned rows
     uint32_t* o = reinterpret_cast<uint32_t*>(E + img * e_img_stride + (int64_t)y * epitch + x);
     uint32_t d[4];
@@ -497,8 +501,12 @@ __device__ __forceinline__ uint32_t fix_sel2(int lane, int c0, int w) {
 
 // SKIP (tools/pyr_micro.hip only): bit k-1 set = level-k outputs are folded
 // into a register instead of stored (to time the store traffic).
+#ifndef STREAM_OCC
+#define STREAM_OCC 4
+#endif
 template <int NL, int SKIP = 0>
-__global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restrict__ src, int64_t src_img_stride,
+__global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* __restrict__ src,
+                                                     const uint8_t* __restrict__ src_b, int n_a, int64_t src_img_stride,
                                                      int src_pitch, int w0, int h0, EdgePlane ep,
                                                      uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
                                                      int n_strips, int n_bands, int n_units,
@@ -509,7 +517,9 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
     if (unit >= n_units) return;
     const int st = unit % n_strips, rest = unit / n_strips;
     const int bd = rest % n_bands, img = rest / n_bands;
-    const uint8_t* S = src + img * src_img_stride;
+    // images [0, n_a) from src, the rest from src_b (prev and next frames of a
+    // batch in one launch); the edge plane and the pyramids are contiguous
+    const uint8_t* S = img < n_a ? src + img * src_img_stride : src_b + (img - n_a) * src_img_stride;
     const uint8_t* E = ep.base + img * ep.img_stride;
     uint8_t* P = pyr + img * pyr_bytes;
     const int x0 = ST_COLS * st + 8 * lane - 20;  // this lane's 16 source bytes
@@ -540,11 +550,18 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
     uint32_t g2[5] = {0, 0, 0, 0, 0}, g3[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * r1s - 2 + k));
-    // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % 4;
-    // they are fetched PF iterations ahead (4 rows x 1 KB in flight per wave; PF = 2
-    // keeps the kernel at 64 VGPRs, 8 waves per SIMD: every unit resident at once)
-    constexpr int PF = 2;
-    uint4 pa[4], pb[4];
+    // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % RS;
+    // they are fetched PF iterations ahead (2*PF rows x 1 KB in flight per wave).
+    // PF = 4 at 4 waves per SIMD (99 VGPRs) measured 0.230 ms per 512 images
+    // against 0.244 for PF = 2 at 8 (63 VGPRs) and 0.234 / 0.231 for PF = 3 / 5
+    // (tools/ab.sh, r01 v21); 5 waves per SIMD spill.
+#ifndef STREAM_PF
+#define STREAM_PF 4
+#endif
+    constexpr int PF = STREAM_PF;
+    constexpr int RS = PF <= 2 ? 4 : 8;  // ring slots (a multiple of 4: the level-3 schedule)
+    static_assert(PF >= 1 && PF <= 6, "prefetch depth must fit the 8-slot ring");
+    uint4 pa[RS], pb[RS];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         pa[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 1);
@@ -564,8 +581,8 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
         const int r1 = r1s + k;
         hr[3] = hsum_row(pa[slot]);
         hr[4] = hsum_row(pb[slot]);
-        pa[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 1);
-        pb[(slot + PF) & 3] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 2);
+        pa[(slot + PF) % RS] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 1);
+        pb[(slot + PF) % RS] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 2);
         // level-1 row r1
         uint32_t l1 = hibytes(vsum2(hr[0].x, hr[1].x, hr[2].x, hr[3].x, hr[4].x),
                               vsum2(hr[0].y, hr[1].y, hr[2].y, hr[3].y, hr[4].y));
@@ -640,7 +657,7 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
                     g3[4] = g;
                     // level-3 row r3 = (r2-2)/2 at every k = 0 (mod 4); valid from
                     // k = 12, when level-2 rows r2-4 .. r2 (k = 4..12) are in
-                    if constexpr (slot == 0) {
+                    if constexpr ((slot & 3) == 0) {
                         const int r3 = (r2 - 2) >> 1;
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
                         const bool ok = own_lane && c3 + (lane - 2) < w3;
@@ -657,20 +674,29 @@ __global__ void __launch_bounds__(256, 8) stream_kernel(const uint8_t* __restric
             }
         }
     };
-    // r1s is even and the slot tracks k % 4, so the level-2 / level-3 schedule
-    // is static; the trip count is rounded up to whole groups of four rows
-    for (int k = 0; k < n1; k += 4) {
+    // r1s is even and the slot tracks k % RS, so the level-2 / level-3 schedule
+    // (k % 2, k % 4) is static; the trip count is rounded up to whole groups of
+    // four rows
+    for (int k = 0; k < n1; k += RS) {
         body(k, std::integral_constant<int, 0>{});
         body(k + 1, std::integral_constant<int, 1>{});
         body(k + 2, std::integral_constant<int, 2>{});
         body(k + 3, std::integral_constant<int, 3>{});
+        if constexpr (RS == 8) {
+            if (k + 4 >= n1) break;  // wave-uniform
+            body(k + 4, std::integral_constant<int, 4 % RS>{});
+            body(k + 5, std::integral_constant<int, 5 % RS>{});
+            body(k + 6, std::integral_constant<int, 6 % RS>{});
+            body(k + 7, std::integral_constant<int, 7 % RS>{});
+        }
     }
     if constexpr (SKIP != 0) *reinterpret_cast<uint32_t*>(tl) = nsink;
 }
 
 template <int NL>
-void launch_stream(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int src_pitch, int src_w, int src_h,
-                   const EdgePlane& ep, int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
+void launch_stream(gvx_ctx* c, const uint8_t* src, const uint8_t* src_b, int n_a, int64_t src_img_stride,
+                   int src_pitch, int src_w, int src_h, const EdgePlane& ep, int n_img, const PyrLayout& lay, int l0,
+                   uint8_t* dst) {
     DownLevels D{};
     for (int k = 0; k < NL; ++k) {
         D.off[k] = lay.off[l0 + 1 + k];
@@ -683,8 +709,9 @@ void launch_stream(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int s
     const int n_units = n_strips * n_bands * n_img;
     const int nblk = (n_units + 3) / 4;
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
-    hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, src_img_stride,
-                       src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units, trash);
+    hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, src_b, n_a,
+                       src_img_stride, src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units,
+                       trash);
 }
 
 
@@ -822,8 +849,9 @@ PyrLayout make_layout(int w, int h, int max_level, int win) {
 }
 
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride, int n_img,
-                                 const PyrLayout& lay, uint8_t* dst, bool write_l0) {
+                                 const PyrLayout& lay, uint8_t* dst, bool write_l0, const uint8_t* src_b, int n_a) {
     if (n_img <= 0) return hipSuccess;
+    if (!src_b) n_a = n_img;
     // level-0 slot of the pyramid: pixel (0,0) of image 0
     uint8_t* slot0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
     const bool aligned = stride % 4 == 0 && img_stride % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 4 == 0 &&
@@ -831,6 +859,13 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
     const uint8_t* s0 = src;
     int64_t s0_img = img_stride;
     int s0_pitch = stride;
+    if (n_a < n_img && (write_l0 || !aligned || reinterpret_cast<uintptr_t>(src_b) % 4 != 0)) {
+        // two sources on the level-0-copy path: one build per source
+        hipError_t e = launch_build_pyramids(c, src, img_stride, stride, n_a, lay, dst, write_l0, nullptr, 0);
+        if (e != hipSuccess) return e;
+        return launch_build_pyramids(c, src_b, img_stride, stride, n_img - n_a, lay, dst + (int64_t)n_a * lay.bytes,
+                                     write_l0, nullptr, 0);
+    }
     if (write_l0 || !aligned) {
         // full padded level-0 copy: the source of the build and its own edge plane
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
@@ -844,10 +879,11 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
     } else {
         // read level 0 in place; only its edge bands go to the (otherwise unused) slot
         const int vec16 = stride % 16 == 0 && img_stride % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                          (n_a == n_img || reinterpret_cast<uintptr_t>(src_b) % 16 == 0) &&
                           lay.w[0] % 16 == 0 && reinterpret_cast<uintptr_t>(slot0) % 16 == 0 && lay.pitch[0] % 16 == 0;
         dim3 grid((lay.h[0] * 6 + 255) / 256, n_img);
-        hipLaunchKernelGGL(edge_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride, lay.w[0], lay.h[0],
-                           slot0, lay.bytes, lay.pitch[0], vec16);
+        hipLaunchKernelGGL(edge_kernel, grid, dim3(256), 0, c->stream, src, src_b, n_a, img_stride, stride, lay.w[0],
+                           lay.h[0], slot0, lay.bytes, lay.pitch[0], vec16);
     }
     // levels 1.. in streaming passes of up to 3 levels; a later pass reads the
     // previous pass's deepest level (padded, its ring built first)
@@ -855,15 +891,17 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
     while (l + 1 < lay.nlev) {
         const int nl = lay.nlev - 1 - l >= 3 ? 3 : lay.nlev - 1 - l;
         const uint8_t* s = l == 0 ? s0 : dst + lay.off[l] + (int64_t)PAD * lay.pitch[l] + PAD;
+        const uint8_t* sb = l == 0 ? src_b : nullptr;  // the level-0 copy path never has two sources here
+        const int na = l == 0 ? n_a : n_img;
         const int64_t si = l == 0 ? s0_img : lay.bytes;
         const int sp = l == 0 ? s0_pitch : lay.pitch[l];
         const EdgePlane ep = l == 0 ? EdgePlane{slot0, lay.bytes, lay.pitch[0]} : EdgePlane{s, lay.bytes, sp};
         if (nl == 3)
-            launch_stream<3>(c, s, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
+            launch_stream<3>(c, s, sb, na, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
         else if (nl == 2)
-            launch_stream<2>(c, s, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
+            launch_stream<2>(c, s, sb, na, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
         else
-            launch_stream<1>(c, s, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
+            launch_stream<1>(c, s, sb, na, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
         launch_rings(c, n_img, lay, l + 1, l + nl, dst, true);
         l += nl;
     }

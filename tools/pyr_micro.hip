@@ -70,13 +70,13 @@ int main() {
         printf("read_all %5d blocks  %8.1f us  %6.2f TB/s\n", blocks, us, img.size() / us / 1e6);
     }
     printf("edge_kernel            %8.1f us\n", timeit([&] {
-        hipLaunchKernelGGL(edge_kernel, dim3((h * 6 + 255) / 256, n), dim3(256), 0, 0, src, (int64_t)w * h, w, w, h,
+        hipLaunchKernelGGL(edge_kernel, dim3((h * 6 + 255) / 256, n), dim3(256), 0, 0, src, src, n, (int64_t)w * h, w, w, h,
                            slot0, lay.bytes, lay.pitch[0], 1);
     }, reps));
     auto run3 = [&](auto skip_c, const char* what) {
         constexpr int SK = decltype(skip_c)::value;
         printf("stream_kernel<3> %-28s %7.1f us\n", what, timeit([&] {
-            hipLaunchKernelGGL((stream_kernel<3, SK>), grid, dim3(256), 0, 0, src, (int64_t)w * h, w, w, h, ep, dst,
+            hipLaunchKernelGGL((stream_kernel<3, SK>), grid, dim3(256), 0, 0, src, src, n, (int64_t)w * h, w, w, h, ep, dst,
                                lay.bytes, D, n_strips, n_bands, n_units, trash);
         }, reps));
     };

@@ -13,10 +13,11 @@ import sys
 sys.path.insert(0, os.path.dirname(__file__))
 from pmc_summary import load  # noqa: E402
 
-# launches per bench step of the KLT pipeline: per pyramid (prev + next) one
-# edge-band pass, one 3-level streaming pass and one ring pass; one LK launch
-# for fwd+bwd; one compaction
-PER_STEP = {"edge_kernel": 2, "stream_kernel": 2, "ring_kernel": 2, "klt_kernel": 1, "compact_kernel": 1}
+# launches per bench step of the KLT pipeline: one edge-band pass, one 3-level
+# streaming pass and one ring pass over the prev and next images together; one
+# LK launch for fwd+bwd; one compaction.  (Profiles before r01 v21 built prev
+# and next in separate launches: 2 of each pyramid kernel per step.)
+PER_STEP = {"edge_kernel": 1, "stream_kernel": 1, "ring_kernel": 1, "klt_kernel": 1, "compact_kernel": 1}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
