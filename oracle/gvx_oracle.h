@@ -31,6 +31,8 @@
  *   orc_undistort_points .. orc_keypoint_parallax  per-point camera operations
  *                          around the KLT calls (camera.c; tracking/camera.cc:72-143,
  *                          tracking.cc:366-377, :419-437, :462-478, :514-544, :861-871)
+ *   orc_ins_* / orc_imu_series_from_to  INS mechanization and IMU-series
+ *                          extraction (ins.c; misc.cc:40-83, :174-384)
  *   orc_clahe / orc_hist_mean  Tracking::preprocessing (tracking.cc:107-141):
  *                          cv::createCLAHE(3.0, Size(21,21))->apply and
  *                          calculateHistigram (clahe.c)
@@ -268,6 +270,28 @@ void orc_clahe_luts(const uint8_t* src, int w, int h, int stride, double clip_li
 void orc_clahe(const uint8_t* src, int w, int h, int stride, double clip_limit, int tiles_x, int tiles_y,
                uint8_t* dst, int dst_stride);
 double orc_hist_mean(const uint8_t* src, int w, int h, int stride);
+
+/* ------------------------------------------------------------------------- */
+/* INS mechanization (ins.c)                                                  */
+/* ------------------------------------------------------------------------- */
+/* IntegrationConfiguration (integration_state.h:91-99) as the mechanization
+   reads it; iswithscale is false in the reference (ic_gvins.cc:116). */
+typedef struct {
+    int iswithearth;
+    double gravity[3];  /* (0, 0, g) */
+    double iewn[3];     /* Earth::iewn(origin, p), ic_gvins.cc:709-711 */
+} orc_ins_config;
+void orc_ins_mechanization(const orc_ins_config* cfg, const orc_imu* pre, const orc_imu* cur, orc_state* s);
+void orc_ins_propagate(const orc_ins_config* cfg, const orc_imu* imu, int m, const orc_state* state0,
+                       orc_state* states);
+int orc_ins_window_index(const orc_imu* imu, int n, double t);
+int orc_need_interpolation(const orc_imu* imu0, const orc_imu* imu1, double mid);
+void orc_imu_interpolation(const orc_imu* imu01, orc_imu* imu00, orc_imu* imu11, double mid);
+/* returns the window index (0: not found, nothing written) */
+int orc_redo_ins_mechanization(const orc_ins_config* cfg, const orc_state* updated, const orc_imu* imu, int n,
+                               orc_state* states);
+/* returns the series length (<= n + 2), -1 when the window does not cover it */
+int orc_imu_series_from_to(const orc_imu* imu, int n, double start, double end, orc_imu* series);
 
 /* ------------------------------------------------------------------------- */
 /* Camera operations (camera.c)                                               */

@@ -66,6 +66,20 @@ class State(C.Structure):
                 ("v", C.c_double * 3), ("bg", C.c_double * 3), ("ba", C.c_double * 3)]
 
 
+class InsConfig(C.Structure):
+    """IntegrationConfiguration as insMechanization reads it (integration_state.h:91-99)."""
+    _fields_ = [("iswithearth", C.c_int), ("gravity", C.c_double * 3), ("iewn", C.c_double * 3)]
+
+    @classmethod
+    def make(cls, iswithearth, gravity, iewn=(0.0, 0.0, 0.0)):
+        c = cls()
+        c.iswithearth = int(bool(iswithearth))
+        for i in range(3):
+            c.gravity[i] = float(gravity[i])
+            c.iewn[i] = float(iewn[i])
+        return c
+
+
 class Preint(C.Structure):
     _fields_ = [("variant", C.c_int), ("m", C.c_int), ("delta_time", C.c_double),
                 ("start_time", C.c_double), ("end_time", C.c_double), ("current", State),
@@ -137,6 +151,17 @@ def lib():
         L.orc_clahe.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, P, C.c_int]
         L.orc_hist_mean.argtypes = [P, C.c_int, C.c_int, C.c_int]
         L.orc_hist_mean.restype = C.c_double
+        IC = C.POINTER(InsConfig)
+        L.orc_ins_mechanization.argtypes = [IC, P, P, C.POINTER(State)]
+        L.orc_ins_propagate.argtypes = [IC, P, C.c_int, C.POINTER(State), P]
+        L.orc_redo_ins_mechanization.argtypes = [IC, C.POINTER(State), P, C.c_int, P]
+        L.orc_redo_ins_mechanization.restype = C.c_int
+        L.orc_imu_series_from_to.argtypes = [P, C.c_int, C.c_double, C.c_double, P]
+        L.orc_imu_series_from_to.restype = C.c_int
+        L.orc_ins_window_index.argtypes = [P, C.c_int, C.c_double]
+        L.orc_ins_window_index.restype = C.c_int
+        L.orc_need_interpolation.argtypes = [P, P, C.c_double]
+        L.orc_need_interpolation.restype = C.c_int
         CP = C.POINTER(Camera)
         L.orc_undistort_points.argtypes = [CP, C.c_int, P, P]
         L.orc_distort_points.argtypes = [CP, C.c_int, P, P]
@@ -486,3 +511,40 @@ def keypoint_parallax(cam: Camera, R0, R1, ref, cur):
     out = np.empty(len(a), np.float64)
     lib().orc_keypoint_parallax(C.byref(cam), _p(R0), _p(R1), len(a), _p(a), _p(b), _p(out))
     return out
+
+
+# ------------------------------------------------------------------ INS mechanization
+STATE_DTYPE = np.dtype([("time", "f8"), ("p", "f8", 3), ("q", "f8", 4), ("v", "f8", 3), ("bg", "f8", 3),
+                        ("ba", "f8", 3)])
+
+
+def _state_array(n):
+    return np.zeros(n, STATE_DTYPE)
+
+
+def ins_propagate(cfg: InsConfig, imu, state0: State):
+    """insMechanization chained over imu[0..m) from state0 (at imu[0].time) -> m states."""
+    imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+    out = _state_array(len(imu))
+    lib().orc_ins_propagate(C.byref(cfg), _p(imu), len(imu), C.byref(state0), _p(out))
+    return out
+
+
+def redo_ins_mechanization(cfg: InsConfig, updated: State, imu, states):
+    """MISC::redoInsMechanization on a window (imu[n], states[n], updated in place) -> index."""
+    imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+    assert states.dtype == STATE_DTYPE and states.flags.c_contiguous
+    return int(lib().orc_redo_ins_mechanization(C.byref(cfg), C.byref(updated), _p(imu), len(imu), _p(states)))
+
+
+def imu_series_from_to(imu, start, end):
+    imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+    out = np.zeros(len(imu) + 2, IMU_DTYPE)
+    m = lib().orc_imu_series_from_to(_p(imu), len(imu), start, end, _p(out))
+    return None if m < 0 else out[:m]
+
+
+def ins_window_index(imu, n, t):
+    """MISC::getInsWindowIndex (misc.cc:40-83): first index with time > t, 0 = none."""
+    imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+    return int(lib().orc_ins_window_index(_p(imu), n, t))
