@@ -236,6 +236,8 @@ def main():
     ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if not args.no_pre else None
+    single = single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps=max(200, 5 * args.steps)) \
+        if world == 1 and not args.no_pre else None
     pcie = None
     if world == 1 and not args.no_pre:
         # host-buffer rate (gvx_klt_fb_batch: images and points copied in and out per
@@ -302,12 +304,60 @@ def main():
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
             "preprocess": pre,
+            "single_pair": single,
             "host_buffers": pcie,
         }
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
     ctx.close()
+
+
+def single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps):
+    """configs[1] as the live tracker runs it: ONE frame pair per launch (the
+    initial-flow copy, the pyramid kernels, LK, compaction), back to back on the
+    context stream -- eager host calls against the same work captured once into
+    a hipGraph and replayed.  Latency, not `value`."""
+    import torch
+    dev = dI.device
+    I1, J1, P1, Q1 = dI[0:1], dJ[0:1], dP[0:1], dQ[0:1]
+    outs = [dict(N=torch.empty_like(Q1), B=torch.empty_like(Q1),
+                 F=torch.empty((1, N), dtype=torch.uint8, device=dev),
+                 K=torch.empty((1, N), dtype=torch.int32, device=dev),
+                 NK=torch.empty((1,), dtype=torch.int32, device=dev)) for _ in range(2)]
+    nbytes = Q1.numel() * Q1.element_size()
+
+    def enqueue(o):
+        ctx.copy_dev(o["N"].data_ptr(), Q1.data_ptr(), nbytes)
+        ctx.klt_fb_batch_dev(1, W, H, I1.data_ptr(), J1.data_ptr(), N, P1.data_ptr(), o["N"].data_ptr(),
+                             o["B"].data_ptr(), o["F"].data_ptr(), o["K"].data_ptr(), o["NK"].data_ptr(),
+                             params=params)
+
+    torch.cuda.synchronize()
+    for _ in range(20):
+        enqueue(outs[0])
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enqueue(outs[0])
+    ctx.sync()
+    eager = (time.perf_counter() - t0) / reps
+    ctx.capture_begin()
+    enqueue(outs[1])
+    g = ctx.capture_end()
+    for _ in range(20):
+        ctx.graph_launch(g)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.graph_launch(g)
+    ctx.sync()
+    graph = (time.perf_counter() - t0) / reps
+    same = all(torch.equal(outs[0][k], outs[1][k]) for k in outs[0])
+    g.destroy()
+    return {"what": "one frame pair per launch, back to back: initial-flow copy + pyramids + LK + compaction",
+            "us_per_pair_eager": round(eager * 1e6, 2), "us_per_pair_graph": round(graph * 1e6, 2),
+            "pairs_per_s_graph": round(1.0 / graph, 1), "graph_matches_eager": same, "reps": reps}
 
 
 def preprocess_leg(ctx, dI, dJ, Pn, W, H, steps):

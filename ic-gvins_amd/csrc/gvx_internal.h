@@ -151,6 +151,10 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean);
 
+// ---- ins.hip ----
+hipError_t launch_ins(gvx_ctx* c, const gvx_ins_config& cfg, int n_chain, const gvx_imu* imu, const int32_t* off,
+                      const gvx_state* state0, gvx_state* states);
+
 // ---- camera.hip ----
 struct CamArgs {
     gvx_camera cam;

@@ -91,6 +91,21 @@ class Camera(C.Structure):
                [("width", C.c_int32), ("height", C.c_int32)]
 
 
+class InsConfig(C.Structure):
+    """gvx_ins_config: IntegrationConfiguration as insMechanization reads it
+    (integration_state.h:91-99)."""
+    _fields_ = [("iswithearth", C.c_int32), ("gravity", C.c_double * 3), ("iewn", C.c_double * 3)]
+
+    @classmethod
+    def make(cls, iswithearth, gravity, iewn=(0.0, 0.0, 0.0)) -> "InsConfig":
+        c = cls()
+        c.iswithearth = 1 if iswithearth else 0
+        for i in range(3):
+            c.gravity[i] = float(gravity[i])
+            c.iewn[i] = float(iewn[i])
+        return c
+
+
 _lib = None
 
 
@@ -165,6 +180,15 @@ def _declare(L):
                                        P, P]),
         "gvx_frame_preprocess_dev": (i32, [P, u64, P, i32, i32, i32, C.POINTER(ClaheParams),
                                            C.POINTER(KltParams), P, P]),
+        "gvx_ins_propagate": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
+        "gvx_ins_propagate_dev": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
+        "gvx_redo_ins_mechanization": (i32, [P, C.POINTER(InsConfig), P, i32, P, P, C.POINTER(i32)]),
+        "gvx_imu_series_from_to": (i32, [P, i32, f64, f64, P, C.POINTER(i32)]),
+        "gvx_capture_begin": (i32, [P]),
+        "gvx_capture_end": (i32, [P, C.POINTER(P)]),
+        "gvx_graph_launch": (i32, [P, P]),
+        "gvx_graph_destroy": (None, [P]),
+        "gvx_copy_dev": (i32, [P, P, P, C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -517,6 +541,97 @@ class Context:
         """Device-pointer ReprojectionFactor batch, async on the context stream."""
         self._check(self._L.gvx_reproj_eval_dev(self._h, n, d_consts, d_params, d_offs, d_res, d_jac),
                     "gvx_reproj_eval_dev")
+
+    # ---------------------------------------------------- INS mechanization
+    def ins_propagate(self, cfg: InsConfig, chains, states0):
+        """insMechanization chained over each IMU series (misc.cc:174-229): chain i
+        starts from states0[i] at chains[i][0] -> list of STATE_DTYPE arrays."""
+        segs = [np.ascontiguousarray(s, dtype=IMU_DTYPE) for s in chains]
+        n = len(segs)
+        if n == 0:
+            return []
+        off = np.zeros(n + 1, np.int32)
+        off[1:] = np.cumsum([len(s) for s in segs])
+        imu = np.concatenate(segs)
+        st0 = np.ascontiguousarray(states0, dtype=STATE_DTYPE).reshape(n)
+        out = np.zeros(max(int(off[-1]), 1), STATE_DTYPE)
+        self._check(self._L.gvx_ins_propagate(self._h, C.byref(cfg), n, _ptr(imu), _ptr(off), _ptr(st0),
+                                              _ptr(out)), "gvx_ins_propagate")
+        return [out[off[i]:off[i + 1]].copy() for i in range(n)]
+
+    def ins_propagate_dev(self, cfg: InsConfig, n_chain, d_imu, d_off, d_state0, d_states):
+        """Device-pointer INS chains (pointers as ints), async on the context stream."""
+        self._check(self._L.gvx_ins_propagate_dev(self._h, C.byref(cfg), n_chain, d_imu, d_off, d_state0,
+                                                  d_states), "gvx_ins_propagate_dev")
+
+    def redo_ins_mechanization(self, cfg: InsConfig, updated, imu, states) -> int:
+        """MISC::redoInsMechanization (misc.cc:231-284): states (STATE_DTYPE, len(imu))
+        updated in place -> window index (0 = nothing done)."""
+        imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+        if states.dtype != STATE_DTYPE or not states.flags.c_contiguous or len(states) != len(imu):
+            raise ValueError("states must be a contiguous STATE_DTYPE array of len(imu)")
+        u = np.ascontiguousarray(updated, dtype=STATE_DTYPE).reshape(1)
+        idx = C.c_int32()
+        self._check(self._L.gvx_redo_ins_mechanization(self._h, C.byref(cfg), _ptr(u), len(imu), _ptr(imu),
+                                                       _ptr(states), C.byref(idx)), "gvx_redo_ins_mechanization")
+        return idx.value
+
+    # ------------------------------------------------------------ hipGraphs
+    def capture_begin(self):
+        """Start capturing this context's stream (gvx_capture_begin)."""
+        self._check(self._L.gvx_capture_begin(self._h), "gvx_capture_begin")
+
+    def capture_end(self) -> "Graph":
+        g = C.c_void_p()
+        self._check(self._L.gvx_capture_end(self._h, C.byref(g)), "gvx_capture_end")
+        return Graph(self, g)
+
+    def graph_launch(self, g: "Graph"):
+        self._check(self._L.gvx_graph_launch(self._h, g.handle), "gvx_graph_launch")
+
+    def copy_dev(self, d_dst: int, d_src: int, nbytes: int):
+        """Device-to-device copy on the context stream (capturable)."""
+        self._check(self._L.gvx_copy_dev(self._h, d_dst, d_src, nbytes), "gvx_copy_dev")
+
+
+class Graph:
+    """A captured hipGraph of a context's stream; replay with launch()."""
+
+    def __init__(self, ctx: Context, handle):
+        self._ctx = ctx
+        self._h = handle
+
+    @property
+    def handle(self):
+        return self._h
+
+    def launch(self):
+        self._ctx.graph_launch(self)
+
+    def destroy(self):
+        if self._h:
+            lib().gvx_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def imu_series_from_to(imu, start, end):
+    """MISC::getImuSeriesFromTo (misc.cc:330-384), host logic of the C ABI ->
+    IMU_DTYPE array, or None when start or end is outside the window."""
+    imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+    out = np.zeros(len(imu) + 2, IMU_DTYPE)
+    n = C.c_int32()
+    s = lib().gvx_imu_series_from_to(_ptr(imu), len(imu), float(start), float(end), _ptr(out), C.byref(n))
+    if s == -5:  # GVX_ERR_NOT_FOUND
+        return None
+    if s != GVX_OK:
+        raise GvxError(f"gvx_imu_series_from_to: {lib().gvx_status_string(s).decode()}")
+    return out[:n.value]
 
 
 def earth_iewn(origin, local) -> np.ndarray:

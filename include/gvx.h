@@ -51,6 +51,22 @@ gvx_status gvx_profile_enable(gvx_ctx* ctx, int32_t on);
 gvx_status gvx_profile_read(gvx_ctx* ctx, const char* family, double* total_ms, int64_t* launches);
 gvx_status gvx_profile_reset(gvx_ctx* ctx);
 
+/* ---------------------------------------------------------------- hipGraphs */
+/* Capture what this context enqueues between gvx_capture_begin and
+   gvx_capture_end (stream capture of the context stream) into a graph that
+   gvx_graph_launch replays with one launch: one frame pair per graph launch
+   (BASELINE configs[1]) instead of one host call per kernel.
+   Only *_dev entry points may be captured, after one uncaptured call with the
+   same sizes (so no scratch buffer grows during capture), with profiling off. */
+typedef struct gvx_graph gvx_graph;
+gvx_status gvx_capture_begin(gvx_ctx* ctx);
+gvx_status gvx_capture_end(gvx_ctx* ctx, gvx_graph** out);
+gvx_status gvx_graph_launch(gvx_ctx* ctx, const gvx_graph* g);
+void gvx_graph_destroy(gvx_graph* g);
+/* Device-to-device copy on the context stream (capturable: e.g. the initial
+   flow copied into next_xy before each replay). */
+gvx_status gvx_copy_dev(gvx_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
+
 /* ------------------------------------------------------------------ KLT  */
 /* cv::calcOpticalFlowPyrLK arguments as used at tracking/tracking.cc:385-393:
    Size(21,21), maxLevel TRACK_PYRAMID_LEVEL=3 (tracking/tracking.h:113),
@@ -291,6 +307,39 @@ gvx_status gvx_preint_integrate_dev(gvx_ctx* ctx, int32_t variant, const gvx_imu
 /* Earth::iewn(station, p) (common/earth.h:233-237), host-side helper used by
    resetState (preintegration_earth.cc:320). */
 void gvx_earth_iewn(const double origin[3], const double local[3], double iewn[3]);
+
+/* ------------------------------------------------------ INS mechanization */
+/* IntegrationConfiguration as MISC::insMechanization reads it
+   (integration_state.h:91-99): iswithearth selects the Earth-rotation variant
+   (Coriolis term, qnn = q(-iewn dt)); gravity is the navigation-frame vector. */
+typedef struct {
+    int32_t iswithearth;
+    double gravity[3];
+    double iewn[3];
+} gvx_ins_config;
+
+/* The chain insMechanization(imu[k-1], imu[k], state), k = 1 .. m-1
+   (misc.cc:174-229; the loop of redoInsMechanization misc.cc:269-275 and the
+   per-sample call of ic_gvins.cc:304-310), batched over chains: chain i uses
+   imu[off[i] .. off[i+1]) and starts from state0[i]; states[off[i]] = state0[i]
+   and states[off[i]+k] is the state after sample k.  One wavefront per chain. */
+gvx_status gvx_ins_propagate(gvx_ctx* ctx, const gvx_ins_config* cfg, int32_t n_chain, const gvx_imu* imu,
+                             const int32_t* off, const gvx_state* state0, gvx_state* states);
+gvx_status gvx_ins_propagate_dev(gvx_ctx* ctx, const gvx_ins_config* cfg, int32_t n_chain, const gvx_imu* d_imu,
+                                 const int32_t* d_off, const gvx_state* d_state0, gvx_state* d_states);
+
+/* MISC::redoInsMechanization (misc.cc:231-284) on a window of n samples and
+   their states, updated in place from the sample after updated->time on (the
+   caller trims the window, as the reference's pop_front does).  *index =
+   getInsWindowIndex (0: updated->time outside the window, nothing changes). */
+gvx_status gvx_redo_ins_mechanization(gvx_ctx* ctx, const gvx_ins_config* cfg, const gvx_state* updated,
+                                      int32_t n, const gvx_imu* imu, gvx_state* states, int32_t* index);
+
+/* MISC::getImuSeriesFromTo (misc.cc:330-384), host logic (no device): the IMU
+   series over [start, end] with the boundary samples split; series must hold
+   n + 2 records.  GVX_ERR_NOT_FOUND when start or end is outside the window. */
+gvx_status gvx_imu_series_from_to(const gvx_imu* imu, int32_t n, double start, double end, gvx_imu* series,
+                                  int32_t* n_series);
 
 /* ------------------------------------------------------ factor batches */
 /* PreintegrationFactor::Evaluate (preintegration/preintegration_factor.h:45-69)
