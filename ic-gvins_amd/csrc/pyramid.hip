@@ -509,7 +509,7 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
                                                      const uint8_t* __restrict__ src_b, int n_a, int64_t src_img_stride,
                                                      int src_pitch, int w0, int h0, EdgePlane ep,
                                                      uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
-                                                     int n_strips, int n_bands, int n_units,
+                                                     int n_strips, int n_bands, int n_units, int band,
                                                      uint8_t* __restrict__ trash) {
     const int lane = threadIdx.x & 63;
     const int nblk = (n_units + 3) / 4;
@@ -537,11 +537,12 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
     const uint32_t sel1 = fix1 ? fix_sel4(lane, c1, w1) : 0u;
     const uint32_t sel2 = fix2 ? fix_sel2(lane, c2, w2) : 0u;
     // level-1 rows walked: everything the band's deepest owned rows depend on
-    const int r1s = BAND * bd - (NL == 3 ? 6 : NL == 2 ? 2 : 0);
-    const int n1 = BAND + (NL == 3 ? 9 : NL == 2 ? 3 : 0);  // rows r1s .. r1s+n1-1
-    const int o1lo = BAND * bd, o1hi = min(BAND * bd + BAND, h1);
-    const int o2lo = BAND / 2 * bd, o2hi = NL > 1 ? min(BAND / 2 * bd + BAND / 2, h2) : 0;
-    const int o3lo = BAND / 4 * bd, o3hi = NL > 2 ? min(BAND / 4 * bd + BAND / 4, h3) : 0;
+    // (band: a multiple of 4, so r1s = 2 mod 4 and the level-2 / level-3 schedule below holds)
+    const int r1s = band * bd - (NL == 3 ? 6 : NL == 2 ? 2 : 0);
+    const int n1 = band + (NL == 3 ? 9 : NL == 2 ? 3 : 0);  // rows r1s .. r1s+n1-1
+    const int o1lo = band * bd, o1hi = min(band * bd + band, h1);
+    const int o2lo = (band >> 1) * bd, o2hi = NL > 1 ? min((band >> 1) * (bd + 1), h2) : 0;
+    const int o3lo = (band >> 2) * bd, o3hi = NL > 2 ? min((band >> 2) * (bd + 1), h3) : 0;
 
     // rolling state: horizontal sums of source rows 2r1-2 .. 2r1+2 (hr[0..4]),
     // level-2 horizontal sums of level-1 rows (g2[0..4], newest last), level-3
@@ -705,13 +706,19 @@ void launch_stream(gvx_ctx* c, const uint8_t* src, const uint8_t* src_b, int n_a
         D.h[k] = lay.h[l0 + 1 + k];
     }
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
-    const int n_bands = (D.h[0] + BAND - 1) / BAND;
+    // BAND level-1 rows per wave when the batch fills the chip; a small batch
+    // (the live tracker's single frame or pair) takes narrower bands down to 4
+    // rows: more waves, each walking band + 9 rows instead of BAND + 9 -- less
+    // latency for more halo work on an otherwise idle GPU
+    int band = BAND;
+    while (band > 4 && n_strips * ((D.h[0] + band - 1) / band) * n_img < 4 * c->n_cu) band >>= 1;
+    const int n_bands = (D.h[0] + band - 1) / band;
     const int n_units = n_strips * n_bands * n_img;
     const int nblk = (n_units + 3) / 4;
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
     hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, src_b, n_a,
                        src_img_stride, src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units,
-                       trash);
+                       band, trash);
 }
 
 

@@ -77,7 +77,7 @@ int main() {
         constexpr int SK = decltype(skip_c)::value;
         printf("stream_kernel<3> %-28s %7.1f us\n", what, timeit([&] {
             hipLaunchKernelGGL((stream_kernel<3, SK>), grid, dim3(256), 0, 0, src, src, n, (int64_t)w * h, w, w, h, ep, dst,
-                               lay.bytes, D, n_strips, n_bands, n_units, trash);
+                               lay.bytes, D, n_strips, n_bands, n_units, BAND, trash);
         }, reps));
     };
     run3(std::integral_constant<int, 0>{}, "all stores");
