@@ -1,0 +1,122 @@
+// api_aux.cpp -- C ABI of the remaining window factors (include/gvx.h):
+// GnssFactor, ImuErrorFactor, ImuPosePriorFactor, ImuMixPriorFactor and
+// MarginalizationFactor evaluation (kernels in aux_factors.hip).
+#include <hip/hip_runtime.h>
+
+#include "gvx_internal.h"
+
+using namespace gvx;
+
+namespace {
+
+constexpr int MARG_MAX_R = 8192;  // dx staged in LDS (64 KB)
+
+}  // namespace
+
+gvx_status gvx_small_factor_eval_dev(gvx_ctx* c, int32_t kind, int32_t n, const double* d_consts,
+                                     const double* d_params, const int32_t* d_offs, double* d_residuals,
+                                     double* d_jacobians) {
+    if (!c) return GVX_ERR_INVALID;
+    int P = 0, NC = 0;
+    if (small_factor_dims(kind, &P, &NC) == 0) return set_err(c, GVX_ERR_INVALID, "unknown factor kind %d", kind);
+    if (n < 0) return set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (n == 0) return GVX_OK;
+    if ((NC && !d_consts) || !d_params || !d_offs || !d_residuals)
+        return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    hipEvent_t ev{};
+    prof_begin(c, "aux_factor", &ev);
+    hipError_t e = launch_small_factor(c, kind, n, d_consts, d_params, d_offs, d_residuals, d_jacobians);
+    prof_end(c, "aux_factor", ev);
+    return hip_err(c, e, "small factor kernel");
+}
+
+gvx_status gvx_small_factor_eval(gvx_ctx* c, int32_t kind, int32_t n, const double* consts, const double* params,
+                                 int32_t n_params, const int32_t* offs, double* residuals, double* jacobians) {
+    if (!c) return GVX_ERR_INVALID;
+    int P = 0, NC = 0;
+    const int R = small_factor_dims(kind, &P, &NC);
+    if (R == 0) return set_err(c, GVX_ERR_INVALID, "unknown factor kind %d", kind);
+    if (n < 0 || n_params < 0) return set_err(c, GVX_ERR_INVALID, "negative size");
+    if (n == 0) return GVX_OK;
+    if ((NC && !consts) || !params || !offs || !residuals) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    for (int i = 0; i < n; ++i)
+        if (offs[i] < 0 || offs[i] + P > n_params)
+            return set_err(c, GVX_ERR_INVALID, "factor %d: parameter block [%d, %d) outside %d values", i, offs[i],
+                           offs[i] + P, n_params);
+    hipSetDevice(c->device);
+    const size_t nc = (size_t)n * NC, nr = (size_t)n * R, nj = jacobians ? (size_t)n * R * P : 0;
+    size_t need = arena_size({sizeof(double) * (nc ? nc : 1), sizeof(double) * n_params, sizeof(int32_t) * n,
+                              sizeof(double) * nr, sizeof(double) * (nj ? nj : 1)});
+    Arena a{(char*)scratch(c, "aux_factor", need), need, 0};
+    if (!a.base) return set_err(c, GVX_ERR_OOM, "factor staging");
+    double* d_c = a.take<double>(nc ? nc : 1);
+    double* d_p = a.take<double>(n_params);
+    int32_t* d_o = a.take<int32_t>(n);
+    double* d_r = a.take<double>(nr);
+    double* d_j = a.take<double>(nj ? nj : 1);
+    hipError_t e = hipSuccess;
+    if (nc) e = hipMemcpyAsync(d_c, consts, sizeof(double) * nc, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_o, offs, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "factor upload");
+    gvx_status s = gvx_small_factor_eval_dev(c, kind, n, d_c, d_p, d_o, d_r, nj ? d_j : nullptr);
+    if (s) return s;
+    e = hipMemcpyAsync(residuals, d_r, sizeof(double) * nr, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && nj) e = hipMemcpyAsync(jacobians, d_j, sizeof(double) * nj, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_err(c, e, "factor download");
+}
+
+gvx_status gvx_marg_factor_eval(gvx_ctx* c, int32_t r, int32_t nb, const int32_t* size, const int32_t* index,
+                                const int32_t* xoff, int32_t n_x, const double* x0, const double* params,
+                                const double* J0, const double* e0, double* residuals, double* jacobians) {
+    if (!c) return GVX_ERR_INVALID;
+    if (r < 0 || nb < 0 || n_x < 0) return set_err(c, GVX_ERR_INVALID, "negative size");
+    if (r > MARG_MAX_R) return set_err(c, GVX_ERR_UNSUPPORTED, "remained size %d > %d", r, MARG_MAX_R);
+    if (r == 0) return GVX_OK;
+    if (!size || !index || !xoff || !x0 || !params || !J0 || !e0 || !residuals)
+        return set_err(c, GVX_ERR_INVALID, "null pointer");
+    // every block inside dx and inside the parameter vectors (the kernel trusts them)
+    int64_t jac_total = 0;
+    for (int b = 0; b < nb; ++b) {
+        const int local = size[b] == 7 ? 6 : size[b];
+        if (size[b] <= 0 || index[b] < 0 || index[b] + local > r || xoff[b] < 0 || xoff[b] + size[b] > n_x)
+            return set_err(c, GVX_ERR_INVALID, "remained block %d out of range", b);
+        jac_total = std::max<int64_t>(jac_total, (int64_t)r * (xoff[b] + size[b]));
+    }
+    hipSetDevice(c->device);
+    const size_t nj = jacobians ? (size_t)jac_total : 0;
+    size_t need = arena_size({sizeof(int32_t) * 3 * (nb ? nb : 1), sizeof(double) * 2 * (n_x ? n_x : 1),
+                              sizeof(double) * (size_t)r * r, sizeof(double) * 2 * r, sizeof(double) * (nj ? nj : 1)});
+    Arena a{(char*)scratch(c, "marg_factor", need), need, 0};
+    if (!a.base) return set_err(c, GVX_ERR_OOM, "marginalisation staging");
+    int32_t* d_blk = a.take<int32_t>(3 * (nb ? nb : 1));
+    double* d_x0 = a.take<double>(n_x ? n_x : 1);
+    double* d_x = a.take<double>(n_x ? n_x : 1);
+    double* d_J = a.take<double>((size_t)r * r);
+    double* d_e = a.take<double>(r);
+    double* d_r = a.take<double>(r);
+    double* d_j = a.take<double>(nj ? nj : 1);
+    hipError_t e = hipSuccess;
+    if (nb) {
+        e = hipMemcpyAsync(d_blk, size, sizeof(int32_t) * nb, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_blk + nb, index, sizeof(int32_t) * nb, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_blk + 2 * nb, xoff, sizeof(int32_t) * nb, hipMemcpyHostToDevice, c->stream);
+    }
+    if (e == hipSuccess && n_x) e = hipMemcpyAsync(d_x0, x0, sizeof(double) * n_x, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && n_x) e = hipMemcpyAsync(d_x, params, sizeof(double) * n_x, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_J, J0, sizeof(double) * r * r, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_e, e0, sizeof(double) * r, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "marginalisation upload");
+    hipEvent_t ev{};
+    prof_begin(c, "marg_factor", &ev);
+    e = launch_marg_factor(c, r, nb, d_blk, d_x0, d_x, d_J, d_e, d_r, nj ? d_j : nullptr);
+    prof_end(c, "marg_factor", ev);
+    if (e != hipSuccess) return hip_err(c, e, "marginalisation kernel");
+    e = hipMemcpyAsync(residuals, d_r, sizeof(double) * r, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && nj) e = hipMemcpyAsync(jacobians, d_j, sizeof(double) * nj, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_err(c, e, "marginalisation download");
+}

@@ -151,6 +151,15 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean);
 
+// ---- aux_factors.hip ----
+// residuals of a small factor kind (0: unknown kind); *P block size, *NC constants per factor
+int small_factor_dims(int kind, int* P, int* NC);
+hipError_t launch_small_factor(gvx_ctx* c, int kind, int n, const double* consts, const double* params,
+                               const int32_t* offs, double* residuals, double* jacobians);
+// blk = {size[nb], index[nb], xoff[nb]}
+hipError_t launch_marg_factor(gvx_ctx* c, int r, int nb, const int32_t* blk, const double* x0, const double* x,
+                              const double* J0, const double* e0, double* residuals, double* jacobians);
+
 // ---- ins.hip ----
 hipError_t launch_ins(gvx_ctx* c, const gvx_ins_config& cfg, int n_chain, const gvx_imu* imu, const int32_t* off,
                       const gvx_state* state0, gvx_state* states);

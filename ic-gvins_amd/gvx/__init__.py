@@ -106,6 +106,10 @@ class InsConfig(C.Structure):
         return c
 
 
+# GVX_FACTOR_* kind -> (residuals, parameter block size, constants per factor)
+SMALL_FACTOR_DIMS = {0: (3, 7, 9), 1: (6, 9, 0), 2: (6, 7, 13), 3: (9, 9, 18)}
+FACTOR_GNSS, FACTOR_IMU_ERROR, FACTOR_POSE_PRIOR, FACTOR_MIX_PRIOR = 0, 1, 2, 3
+
 _lib = None
 
 
@@ -184,6 +188,9 @@ def _declare(L):
         "gvx_ins_propagate_dev": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
         "gvx_redo_ins_mechanization": (i32, [P, C.POINTER(InsConfig), P, i32, P, P, C.POINTER(i32)]),
         "gvx_imu_series_from_to": (i32, [P, i32, f64, f64, P, C.POINTER(i32)]),
+        "gvx_small_factor_eval": (i32, [P, i32, i32, P, P, i32, P, P, P]),
+        "gvx_small_factor_eval_dev": (i32, [P, i32, i32, P, P, P, P, P]),
+        "gvx_marg_factor_eval": (i32, [P, i32, i32, P, P, P, i32, P, P, P, P, P, P]),
         "gvx_capture_begin": (i32, [P]),
         "gvx_capture_end": (i32, [P, C.POINTER(P)]),
         "gvx_graph_launch": (i32, [P, P]),
@@ -541,6 +548,44 @@ class Context:
         """Device-pointer ReprojectionFactor batch, async on the context stream."""
         self._check(self._L.gvx_reproj_eval_dev(self._h, n, d_consts, d_params, d_offs, d_res, d_jac),
                     "gvx_reproj_eval_dev")
+
+    # ---------------------------------------------- remaining window factors
+    def small_factor_eval(self, kind: int, consts, params, offs, jacobians=True):
+        """GnssFactor / ImuErrorFactor / ImuPosePriorFactor / ImuMixPriorFactor
+        batch (GVX_FACTOR_*) -> (residuals [n, R], jacobians [n, R*P] or None)."""
+        if kind not in SMALL_FACTOR_DIMS:
+            raise GvxError(f"small_factor_eval: unknown factor kind {kind}")
+        R, P, NC = SMALL_FACTOR_DIMS[kind]
+        o = np.ascontiguousarray(offs, np.int32).reshape(-1)
+        n = o.size
+        cs = np.ascontiguousarray(consts, np.float64).reshape(-1) if NC else None
+        prm = np.ascontiguousarray(params, np.float64).reshape(-1)
+        res = np.zeros((n, R))
+        jac = np.zeros((n, R * P)) if jacobians else None
+        self._check(self._L.gvx_small_factor_eval(self._h, kind, n, _ptr(cs), _ptr(prm), prm.size, _ptr(o),
+                                                  _ptr(res), _ptr(jac)), "gvx_small_factor_eval")
+        return res, jac
+
+    def small_factor_eval_dev(self, kind, n, d_consts, d_params, d_offs, d_res, d_jac):
+        """Device-pointer small-factor batch, async on the context stream."""
+        self._check(self._L.gvx_small_factor_eval_dev(self._h, kind, n, d_consts, d_params, d_offs, d_res, d_jac),
+                    "gvx_small_factor_eval_dev")
+
+    def marg_factor_eval(self, size, index, xoff, x0, params, J0, e0, jacobians=True):
+        """MarginalizationFactor::Evaluate; J0 as an (r, r) array -> (residuals [r],
+        jacobians [r * len(params)] (block b at r * xoff[b]) or None)."""
+        sz, ix, xo = (np.ascontiguousarray(a, np.int32) for a in (size, index, xoff))
+        J = np.ascontiguousarray(np.asarray(J0, np.float64).T)  # column-major data, as Eigen stores it
+        r = J.shape[0]
+        e = np.ascontiguousarray(e0, np.float64)
+        z = np.ascontiguousarray(x0, np.float64)
+        x = np.ascontiguousarray(params, np.float64)
+        res = np.zeros(r)
+        jac = np.zeros(r * x.size) if jacobians else None
+        self._check(self._L.gvx_marg_factor_eval(self._h, r, sz.size, _ptr(sz), _ptr(ix), _ptr(xo), x.size, _ptr(z),
+                                                 _ptr(x), _ptr(J), _ptr(e), _ptr(res), _ptr(jac)),
+                    "gvx_marg_factor_eval")
+        return res, jac
 
     # ---------------------------------------------------- INS mechanization
     def ins_propagate(self, cfg: InsConfig, chains, states0):

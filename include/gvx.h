@@ -308,6 +308,39 @@ gvx_status gvx_preint_integrate_dev(gvx_ctx* ctx, int32_t variant, const gvx_imu
    resetState (preintegration_earth.cc:320). */
 void gvx_earth_iewn(const double origin[3], const double local[3], double iewn[3]);
 
+/* ------------------------------------------------ remaining window factors */
+/* The other cost functions of the sliding window (ic_gvins.cc:1193, :1959-1990),
+   batched: factor i reads its parameter block at params + offs[i] (params holds
+   n_params doubles) and its constants at consts + i * NC; R residuals and an
+   R x P row-major Jacobian (like Ceres) per factor, jacobians may be NULL.
+     GVX_FACTOR_GNSS        GnssFactor::Evaluate (factors/gnss_factor.h:52-95):
+                            pose[7]; consts {blh[3], std[3], lever[3]}; R 3, P 7, NC 9
+     GVX_FACTOR_IMU_ERROR   ImuErrorFactor::Evaluate, NORMAL / EARTH options
+                            (preintegration/imu_error_factor.h:45-66): mix[9]; R 6, P 9, NC 0
+     GVX_FACTOR_POSE_PRIOR  ImuPosePriorFactor::Evaluate (imu_pose_prior_factor.h:42-68):
+                            pose[7]; consts {prior pose[7], std[6]}; R 6, P 7, NC 13
+     GVX_FACTOR_MIX_PRIOR   ImuMixPriorFactor::Evaluate, NORMAL / EARTH options
+                            (imu_mix_prior_factor.h:40-56): mix[9]; consts {prior mix[9],
+                            std[9]}; R 9, P 9, NC 18 */
+enum { GVX_FACTOR_GNSS = 0, GVX_FACTOR_IMU_ERROR = 1, GVX_FACTOR_POSE_PRIOR = 2, GVX_FACTOR_MIX_PRIOR = 3 };
+gvx_status gvx_small_factor_eval(gvx_ctx* ctx, int32_t kind, int32_t n, const double* consts, const double* params,
+                                 int32_t n_params, const int32_t* offs, double* residuals, double* jacobians);
+gvx_status gvx_small_factor_eval_dev(gvx_ctx* ctx, int32_t kind, int32_t n, const double* d_consts,
+                                     const double* d_params, const int32_t* d_offs, double* d_residuals,
+                                     double* d_jacobians);
+
+/* MarginalizationFactor::Evaluate (factors/marginalization_factor.h:54-110),
+   r = remainedSize() (<= 8192).  Remained block b: size[b] (7 = pose, local
+   size 6), index[b] = remainedBlockIndex()[b] - marginalizedSize(), values at
+   params + xoff[b] (current; n_x doubles in all) and x0 + xoff[b]
+   (remainedBlockData(), the linearisation point).  J0 = linearizedJacobians()
+   (r x r, column-major as Eigen stores it), e0 = linearizedResiduals().
+   residuals r; jacobians (may be NULL): block b at jacobians + r * xoff[b],
+   row-major r x size[b]. */
+gvx_status gvx_marg_factor_eval(gvx_ctx* ctx, int32_t r, int32_t nb, const int32_t* size, const int32_t* index,
+                                const int32_t* xoff, int32_t n_x, const double* x0, const double* params,
+                                const double* J0, const double* e0, double* residuals, double* jacobians);
+
 /* ------------------------------------------------------ INS mechanization */
 /* IntegrationConfiguration as MISC::insMechanization reads it
    (integration_state.h:91-99): iswithearth selects the Earth-rotation variant

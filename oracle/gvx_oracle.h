@@ -33,6 +33,11 @@
  *                          tracking.cc:366-377, :419-437, :462-478, :514-544, :861-871)
  *   orc_ins_* / orc_imu_series_from_to  INS mechanization and IMU-series
  *                          extraction (ins.c; misc.cc:40-83, :174-384)
+ *   orc_small_factor_eval / orc_marg_factor_eval  GNSS, ImuError, pose / mix
+ *                          prior and marginalisation factors (aux_factors.c;
+ *                          factors/gnss_factor.h:52-95, preintegration/
+ *                          imu_error_factor.h:45-66, imu_pose_prior_factor.h:42-68,
+ *                          imu_mix_prior_factor.h:40-56, factors/marginalization_factor.h:54-110)
  *   orc_clahe / orc_hist_mean  Tracking::preprocessing (tracking.cc:107-141):
  *                          cv::createCLAHE(3.0, Size(21,21))->apply and
  *                          calculateHistigram (clahe.c)
@@ -292,6 +297,20 @@ int orc_redo_ins_mechanization(const orc_ins_config* cfg, const orc_state* updat
                                orc_state* states);
 /* returns the series length (<= n + 2), -1 when the window does not cover it */
 int orc_imu_series_from_to(const orc_imu* imu, int n, double start, double end, orc_imu* series);
+
+/* ------------------------------------------------------------------------- */
+/* Remaining window factors (aux_factors.c)                                   */
+/* ------------------------------------------------------------------------- */
+/* kind 0 GNSS, 1 IMU_ERROR, 2 POSE_PRIOR, 3 MIX_PRIOR; dims = {residuals,
+   parameter block size, constants per factor}.  Returns -1 for a bad kind. */
+extern const int orc_small_factor_dims[4][3];
+int orc_small_factor_eval(int kind, int n, const double* consts, const double* params, const int* offs,
+                          double* residuals, double* jacobians);
+/* J0 column-major r x r; block b: size[b] (7 = pose), index[b] (dx offset),
+   xoff[b] (offset of its values in x0 / params and of its Jacobian, r * xoff[b]) */
+void orc_marg_factor_eval(int r, int nb, const int* size, const int* index, const int* xoff, const double* x0,
+                          const double* params, const double* J0, const double* e0, double* residuals,
+                          double* jacobians);
 
 /* ------------------------------------------------------------------------- */
 /* Camera operations (camera.c)                                               */

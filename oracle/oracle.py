@@ -162,6 +162,9 @@ def lib():
         L.orc_ins_window_index.restype = C.c_int
         L.orc_need_interpolation.argtypes = [P, P, C.c_double]
         L.orc_need_interpolation.restype = C.c_int
+        L.orc_small_factor_eval.argtypes = [C.c_int, C.c_int, P, P, P, P, P]
+        L.orc_small_factor_eval.restype = C.c_int
+        L.orc_marg_factor_eval.argtypes = [C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]
         CP = C.POINTER(Camera)
         L.orc_undistort_points.argtypes = [CP, C.c_int, P, P]
         L.orc_distort_points.argtypes = [CP, C.c_int, P, P]
@@ -548,3 +551,38 @@ def ins_window_index(imu, n, t):
     """MISC::getInsWindowIndex (misc.cc:40-83): first index with time > t, 0 = none."""
     imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
     return int(lib().orc_ins_window_index(_p(imu), n, t))
+
+
+# ------------------------------------------------ remaining window factors
+SMALL_FACTOR_DIMS = {0: (3, 7, 9), 1: (6, 9, 0), 2: (6, 7, 13), 3: (9, 9, 18)}  # GNSS, IMU_ERROR, POSE/MIX_PRIOR
+
+
+def small_factor_eval(kind, consts, params, offs, jacobians=True):
+    """GnssFactor / ImuErrorFactor / ImuPosePriorFactor / ImuMixPriorFactor batch
+    (aux_factors.c) -> (residuals [n, R], jacobians [n, R*P] or None)."""
+    R, P, NC = SMALL_FACTOR_DIMS[kind]
+    o = np.ascontiguousarray(offs, np.int32).reshape(-1)
+    n = o.size
+    cs = np.ascontiguousarray(consts, np.float64).reshape(-1) if NC else np.zeros(1)
+    prm = np.ascontiguousarray(params, np.float64).reshape(-1)
+    res = np.zeros((n, R))
+    jac = np.zeros((n, R * P)) if jacobians else None
+    assert lib().orc_small_factor_eval(kind, n, _p(cs), _p(prm), _p(o), _p(res), _p(jac)) == 0
+    return res, jac
+
+
+def marg_factor_eval(size, index, xoff, x0, params, J0, e0, jacobians=True):
+    """MarginalizationFactor::Evaluate (aux_factors.c); J0 given as an (r, r)
+    array -> (residuals [r], jacobians [r * sum(size)] or None)."""
+    sz = np.ascontiguousarray(size, np.int32)
+    ix = np.ascontiguousarray(index, np.int32)
+    xo = np.ascontiguousarray(xoff, np.int32)
+    J = np.ascontiguousarray(np.asarray(J0, np.float64).T)  # column-major data, as Eigen stores it
+    r = J.shape[0]
+    e = np.ascontiguousarray(e0, np.float64)
+    z = np.ascontiguousarray(x0, np.float64)
+    x = np.ascontiguousarray(params, np.float64)
+    res = np.zeros(r)
+    jac = np.zeros(r * int(sz.sum())) if jacobians else None
+    lib().orc_marg_factor_eval(r, sz.size, _p(sz), _p(ix), _p(xo), _p(z), _p(x), _p(J), _p(e), _p(res), _p(jac))
+    return res, jac
