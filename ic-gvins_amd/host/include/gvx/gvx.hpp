@@ -22,6 +22,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -492,6 +493,104 @@ private:
 // ceres::CostFunction-shaped wrappers: Evaluate(parameters, residuals,
 // jacobians) with the reference's block sizes.  A ceres::CostFunction subclass
 // forwarding to these is all the integration needs.
+// ------------------------------------------------------- INS mechanization
+// The fields of IntegrationConfiguration that MISC::insMechanization reads
+// (integration_state.h:91-99).
+struct IntegrationConfiguration {
+    bool iswithearth = false;
+    std::array<double, 3> gravity{0, 0, 9.8}, iewn{0, 0, 0};
+};
+
+namespace MISC {
+namespace detail {
+inline gvx_ins_config to_c(const IntegrationConfiguration& c) {
+    gvx_ins_config o;
+    o.iswithearth = c.iswithearth ? 1 : 0;
+    std::memcpy(o.gravity, c.gravity.data(), sizeof o.gravity);
+    std::memcpy(o.iewn, c.iewn.data(), sizeof o.iewn);
+    return o;
+}
+}  // namespace detail
+
+// MISC::insMechanization(config, imu_pre, imu_cur, state) (misc.cc:174-229)
+inline void insMechanization(Context& ctx, const IntegrationConfiguration& config, const IMU& imu_pre,
+                             const IMU& imu_cur, IntegrationState& state) {
+    const gvx_ins_config cfg = detail::to_c(config);
+    const gvx_imu imu[2] = {imu_pre, imu_cur};
+    const int32_t off[2] = {0, 2};
+    const gvx_state s0 = gvx::detail::to_c(state);
+    gvx_state out[2];
+    check(gvx_ins_propagate(ctx.get(), &cfg, 1, imu, off, &s0, out), ctx.get(), "insMechanization");
+    state = gvx::detail::from_c(out[1]);
+}
+
+// MISC::redoInsMechanization (misc.cc:231-284): same arguments and effect on the
+// window, including the pop_front of the expired epochs.
+inline void redoInsMechanization(Context& ctx, const IntegrationConfiguration& config,
+                                 const IntegrationState& updated_state, size_t reserved_ins_num,
+                                 std::deque<std::pair<IMU, IntegrationState>>& ins_windows) {
+    std::vector<gvx_imu> imu;
+    std::vector<gvx_state> st;
+    imu.reserve(ins_windows.size());
+    st.reserve(ins_windows.size());
+    for (const auto& w : ins_windows) {
+        imu.push_back(w.first);
+        st.push_back(gvx::detail::to_c(w.second));
+    }
+    const gvx_ins_config cfg = detail::to_c(config);
+    const gvx_state u = gvx::detail::to_c(updated_state);
+    int32_t index = 0;
+    check(gvx_redo_ins_mechanization(ctx.get(), &cfg, &u, (int32_t)imu.size(), imu.data(), st.data(), &index),
+          ctx.get(), "redoInsMechanization");
+    if (index == 0) return;  // "Failed to get right index in mechanization"
+    for (size_t k = (size_t)index; k < ins_windows.size(); ++k) ins_windows[k].second = gvx::detail::from_c(st[k]);
+    if ((size_t)index < reserved_ins_num) return;
+    for (size_t k = 0; k < (size_t)index - reserved_ins_num; ++k) ins_windows.pop_front();
+}
+
+// MISC::getImuSeriesFromTo (misc.cc:330-384)
+inline bool getImuSeriesFromTo(const std::deque<std::pair<IMU, IntegrationState>>& ins_windows, double start,
+                               double end, std::vector<IMU>& series) {
+    std::vector<gvx_imu> imu;
+    imu.reserve(ins_windows.size());
+    for (const auto& w : ins_windows) imu.push_back(w.first);
+    series.assign(imu.size() + 2, IMU{});
+    int32_t n = 0;
+    const gvx_status s = gvx_imu_series_from_to(imu.data(), (int32_t)imu.size(), start, end, series.data(), &n);
+    if (s == GVX_ERR_NOT_FOUND) {
+        series.clear();
+        return false;
+    }
+    check(s, nullptr, "getImuSeriesFromTo");
+    series.resize((size_t)n);
+    return true;
+}
+}  // namespace MISC
+
+// GnssFactor (factors/gnss_factor.h:36-100): Evaluate with Ceres' signature;
+// one factor per call here, gvx_small_factor_eval batches many.
+class GnssFactor {
+public:
+    GnssFactor(Context& ctx, const std::array<double, 3>& blh, const std::array<double, 3>& std,
+               const std::array<double, 3>& lever)
+        : ctx_(ctx) {
+        std::memcpy(c_, blh.data(), sizeof(double) * 3);
+        std::memcpy(c_ + 3, std.data(), sizeof(double) * 3);
+        std::memcpy(c_ + 6, lever.data(), sizeof(double) * 3);
+    }
+    bool Evaluate(double const* const* parameters, double* residuals, double** jacobians) const {
+        const int32_t off = 0;
+        double* jac = jacobians ? jacobians[0] : nullptr;
+        check(gvx_small_factor_eval(ctx_.get(), GVX_FACTOR_GNSS, 1, c_, parameters[0], 7, &off, residuals, jac),
+              ctx_.get(), "GnssFactor::Evaluate");
+        return true;
+    }
+
+private:
+    Context& ctx_;
+    double c_[9];
+};
+
 class PreintegrationFactor {
 public:
     explicit PreintegrationFactor(Preintegration& pre) : pre_(&pre) {}

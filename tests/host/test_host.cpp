@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <fstream>
 #include <string>
+#include <deque>
 #include <vector>
 
 template <class T>
@@ -203,6 +204,40 @@ int main(int argc, char** argv) {
     if (!fs.readPreintegration(0, q.data(), qj) || q != r2 || q0 != k0 || q2 != k2 || q3 != k3) {
         std::printf("FAIL factor set preintegration\n");
         return 1;
+    }
+    // MISC::redoInsMechanization on a window of the IMU records with the state as
+    // its states, updated at imu[20].time + 0.0021 (interpolation split)
+    {
+        gvx::IntegrationConfiguration cfg;
+        cfg.iswithearth = meta[3] == GVX_PREINT_EARTH;
+        cfg.gravity = {0, 0, prm[5]};
+        cfg.iewn = {1e-5, 2e-5, 6e-5};
+        std::deque<std::pair<gvx::IMU, gvx::IntegrationState>> win;
+        for (const auto& m : imu) win.emplace_back(m, state_from(st.data()));
+        gvx::IntegrationState upd = state_from(st.data());
+        upd.time = imu[20].time + 0.0021;
+        gvx::MISC::redoInsMechanization(ctx, cfg, upd, 8, win);
+        std::vector<double> o;
+        o.push_back((double)win.size());
+        for (const auto& w : win) {
+            double t[17];
+            state_to(w.second, t);
+            o.insert(o.end(), t, t + 17);
+        }
+        writef(d + "ins_redo.bin", o.data(), o.size());
+        std::vector<gvx::IMU> series;
+        if (!gvx::MISC::getImuSeriesFromTo(win, imu[25].time + 0.001, imu[40].time + 0.003, series)) {
+            std::printf("FAIL getImuSeriesFromTo\n");
+            return 1;
+        }
+        writef(d + "ins_series.bin", series.data(), series.size());
+        gvx::GnssFactor gf(ctx, {1.0, 2.0, 3.0}, {0.02, 0.03, 0.05}, {0.1, -0.2, 0.3});
+        const double* pp[1] = {fp.data()};
+        double gres[3], gjac[21];
+        double* gj[1] = {gjac};
+        gf.Evaluate(pp, gres, gj);
+        writef(d + "gnss.bin", gres, 3);
+        writef(d + "gnss_jac.bin", gjac, 21);
     }
     std::printf("OK\n");
     return 0;

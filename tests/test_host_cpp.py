@@ -128,6 +128,26 @@ def test_host_mirror_matches_oracle(host_bin, orc, tmp_path, variant):
     ps2 = rd("pre_state2.bin", np.float64)
     for k, (lo, hi) in (("p", (1, 4)), ("q", (4, 8)), ("v", (8, 11))):
         _close(ps2[lo:hi], seg2.delta()[k], f"reintegrated delta.{k}", 1e-10)
+    # MISC::redoInsMechanization on the deque window + pop_front, getImuSeriesFromTo, GnssFactor
+    g = prm[5]
+    iewn_ins = (1e-5, 2e-5, 6e-5) if variant == EARTH else (0.0, 0.0, 0.0)
+    ocfg = orc.InsConfig.make(variant == EARTH, (0, 0, g), iewn_ins)
+    states = np.array([s] * len(imu))
+    upd = orc.make_state(float(imu[20]["time"]) + 0.0021, s["p"], s["q"], s["v"], s["bg"], s["ba"])
+    idx = orc.redo_ins_mechanization(ocfg, upd, imu, states)
+    assert idx == 21
+    kept = states[idx - 8:]
+    got = rd("ins_redo.bin", np.float64)
+    assert int(got[0]) == len(kept)
+    got = got[1:].reshape(-1, 17)
+    ref = np.stack([np.r_[k["time"], k["p"], k["q"], k["v"], k["bg"], k["ba"]] for k in kept])
+    assert np.array_equal(got[:, 0], ref[:, 0]) and np.array_equal(got[:, 11:], ref[:, 11:])
+    _close(got[:, 1:11], ref[:, 1:11], "redoInsMechanization p/q/v", 1e-10)
+    ser = orc.imu_series_from_to(imu[idx - 8:], float(imu[25]["time"]) + 0.001, float(imu[40]["time"]) + 0.003)
+    assert np.array_equal(rd("ins_series.bin", np.float64), ser.view(np.float64).ravel())
+    gr, gj = orc.small_factor_eval(0, np.r_[1.0, 2.0, 3.0, 0.02, 0.03, 0.05, 0.1, -0.2, 0.3], blocks[0], [0])
+    _close(rd("gnss.bin", np.float64), gr[0], "GnssFactor residual", 1e-12)
+    _close(rd("gnss_jac.bin", np.float64), gj[0], "GnssFactor jacobian", 1e-12)
     rf = rd("rf.bin", np.float64)
     rcc = orc.reproj_const(rc["pts0"], rc["pts1"], rc["vel0"], rc["vel1"], rc["td0"], rc["td1"], rc["std"])
     rr, rj = orc.reproj_eval(rcc, *rblocks)
