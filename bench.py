@@ -537,6 +537,7 @@ def factors_main(args):
     B_rp = 15 * 8 + 5 * 4 + 48 * 8  # consts + offsets in, residual + 5 Jacobian blocks out
     achieved = B_rp * n_r / (rp_ms * 1e-3) / 1e9 if rp_ms > 0 else None
     if rank == 0:
+        wf = window_factor_leg(ctx, dev)
         line = {
             "metric": "BA factor-Jacobian evaluations/s (configs[3])",
             "value": round(value, 1), "unit": "factor evals/s", "n_gpus": world, "steps": args.steps,
@@ -556,6 +557,7 @@ def factors_main(args):
                              "device_launch_evals_per_s": round(world * n_w * k_w / el_w, 1),
                              "factor_set_prepare_evals_per_s": round(world * n_w * k_w / el_p, 1),
                              "factor_set_prepare_ms": round(el_p / k_w * 1e3, 4)},
+            "window_factors": wf,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu:
@@ -570,6 +572,67 @@ def factors_main(args):
     if dist:
         dist.destroy_process_group()
     ctx.close()
+
+
+def window_factor_leg(ctx, dev, reps=20):
+    """SURVEY 8f rank 3 (partial), beside configs[3]: GnssFactor as a device batch
+    (2^20 factors per launch for a throughput figure; the live system has one per
+    GNSS epoch) and one MarginalizationFactor of an IC-GVINS-shaped window (9
+    keyframes' pose + mix, extrinsic, td: r = 142) through the host entry, PCIe
+    included.  Not part of `value`."""
+    import torch
+    import gvx
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    poses = np.zeros((n, 7))
+    poses[:, :3] = rng.normal(0, 5, (n, 3))
+    q = rng.normal(0, 1, (n, 4))
+    poses[:, 3:] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    consts = np.concatenate([rng.normal(0, 5, (n, 3)), rng.uniform(0.01, 0.1, (n, 3)),
+                             np.tile([0.1, -0.2, 0.3], (n, 1))], 1)
+    d_p = torch.from_numpy(poses.ravel()).to(dev)
+    d_c = torch.from_numpy(consts.ravel()).to(dev)
+    d_o = torch.arange(0, 7 * n, 7, dtype=torch.int32, device=dev)
+    d_r = torch.empty(n * 3, dtype=torch.float64, device=dev)
+    d_j = torch.empty(n * 21, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def run():
+        ctx.small_factor_eval_dev(gvx.FACTOR_GNSS, n, d_c.data_ptr(), d_p.data_ptr(), d_o.data_ptr(), d_r.data_ptr(),
+                                  d_j.data_ptr())
+
+    for _ in range(3):
+        run()
+    ctx.sync()
+    ctx.profile_reset()
+    ctx.profile(True)
+    for _ in range(reps):
+        run()
+    ctx.sync()
+    ms, _ = ctx.profile_read("aux_factor")
+    ctx.profile(False)
+    per = ms / reps
+    bytes_per = (9 + 7 + 3 + 21) * 8 + 4  # constants, pose, residuals, Jacobian, offset
+    size = [7, 9] * 9 + [7, 1]
+    local = [6 if s == 7 else s for s in size]
+    index = np.concatenate([[0], np.cumsum(local)[:-1]]).astype(np.int32)
+    xoff = np.concatenate([[0], np.cumsum(size)[:-1]]).astype(np.int32)
+    r = int(sum(local))
+    x0 = rng.normal(0, 1, int(sum(size)))
+    for b, s in enumerate(size):
+        if s == 7:
+            x0[xoff[b] + 3:xoff[b] + 7] = (0, 0, 0, 1)
+    J0, e0 = rng.normal(0, 1, (r, r)), rng.normal(0, 1, r)
+    ctx.marg_factor_eval(size, index, xoff, x0, x0, J0, e0)
+    t0 = time.perf_counter()
+    for _ in range(50):
+        ctx.marg_factor_eval(size, index, xoff, x0, x0, J0, e0)
+    marg_us = (time.perf_counter() - t0) / 50 * 1e6
+    return {"gnss_factors_per_launch": n, "gnss_device_ms_per_launch": round(per, 4),
+            "gnss_factor_evals_per_s": round(n / (per * 1e-3)),
+            "gnss_roofline": {"bound": "hbm", "achieved": round(n * bytes_per / (per * 1e-3) / 1e9, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "algorithmic_bytes_per_factor": bytes_per},
+            "marg_factor_r": r, "marg_factor_host_call_us": round(marg_us, 1)}
 
 
 def gather_tracks(tracks, counts, dist, dev):

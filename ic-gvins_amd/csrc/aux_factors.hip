@@ -53,14 +53,21 @@ __global__ void __launch_bounds__(64) small_kernel(int n, const double* __restri
                                                    const double* __restrict__ params, const int32_t* __restrict__ offs,
                                                    double* __restrict__ residuals, double* __restrict__ jacobians) {
     constexpr int R = Dims<KIND>::R, P = Dims<KIND>::P, NC = Dims<KIND>::NC;
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= n) return;
-    const double* c = consts + (int64_t)i * NC;
-    const double* p = params + offs[i];
+    // outputs staged through LDS so the block's residual and Jacobian ranges
+    // are stored contiguously (a thread's own 21-81 doubles would be strided)
+    __shared__ double sres[64 * R], sjac[64 * R * P];
+    const int lane = threadIdx.x, i0 = blockIdx.x * 64, i = i0 + lane;
+    const int cnt = min(64, n - i0);
     double res[R], jac[R * P];
 #pragma unroll
+    for (int k = 0; k < R; ++k) res[k] = 0.0;
+#pragma unroll
     for (int k = 0; k < R * P; ++k) jac[k] = 0.0;
-    if constexpr (KIND == GVX_FACTOR_GNSS) {
+    const double* c = consts + (int64_t)min(i, n - 1) * NC;
+    const double* p = params + offs[min(i, n - 1)];
+    if (i >= n) {
+        // no factor: the stores below skip this lane's slots
+    } else if constexpr (KIND == GVX_FACTOR_GNSS) {
         const double *blh = c, *stdv = c + 3, *lever = c + 6;
         const dq q = dq_make(p[6], p[3], p[4], p[5]);
         double Rm[9], Rl[3], s[3];
@@ -107,13 +114,18 @@ __global__ void __launch_bounds__(64) small_kernel(int n, const double* __restri
             jac[k * 9 + k] = 1.0 / stdv[k];
         }
     }
-    double* ro = residuals + (int64_t)i * R;
 #pragma unroll
-    for (int k = 0; k < R; ++k) ro[k] = res[k];
+    for (int k = 0; k < R; ++k) sres[lane * R + k] = res[k];
     if (jacobians) {
-        double* jo = jacobians + (int64_t)i * R * P;
 #pragma unroll
-        for (int k = 0; k < R * P; ++k) jo[k] = jac[k];
+        for (int k = 0; k < R * P; ++k) sjac[lane * R * P + k] = jac[k];
+    }
+    __syncthreads();
+    double* ro = residuals + (int64_t)i0 * R;
+    for (int k = lane; k < cnt * R; k += 64) ro[k] = sres[k];
+    if (jacobians) {
+        double* jo = jacobians + (int64_t)i0 * R * P;
+        for (int k = lane; k < cnt * R * P; k += 64) jo[k] = sjac[k];
     }
 }
 
