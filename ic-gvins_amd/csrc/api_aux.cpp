@@ -3,6 +3,8 @@
 // MarginalizationFactor evaluation (kernels in aux_factors.hip).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "gvx_internal.h"
 
 using namespace gvx;
@@ -89,34 +91,48 @@ gvx_status gvx_marg_factor_eval(gvx_ctx* c, int32_t r, int32_t nb, const int32_t
     const size_t nj = jacobians ? (size_t)jac_total : 0;
     size_t need = arena_size({sizeof(int32_t) * 3 * (nb ? nb : 1), sizeof(double) * 2 * (n_x ? n_x : 1),
                               sizeof(double) * (size_t)r * r, sizeof(double) * 2 * r, sizeof(double) * (nj ? nj : 1)});
+    // one pinned staging arena laid out like the device one: the inputs are its
+    // prefix (one upload), the outputs its suffix (one download)
     Arena a{(char*)scratch(c, "marg_factor", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "marginalisation staging");
+    Arena h{(char*)pinned(c, "marg_factor", need), need, 0};
+    if (!a.base || !h.base) return set_err(c, GVX_ERR_OOM, "marginalisation staging");
     int32_t* d_blk = a.take<int32_t>(3 * (nb ? nb : 1));
+    int32_t* h_blk = h.take<int32_t>(3 * (nb ? nb : 1));
     double* d_x0 = a.take<double>(n_x ? n_x : 1);
+    double* h_x0 = h.take<double>(n_x ? n_x : 1);
     double* d_x = a.take<double>(n_x ? n_x : 1);
+    double* h_x = h.take<double>(n_x ? n_x : 1);
     double* d_J = a.take<double>((size_t)r * r);
+    double* h_J = h.take<double>((size_t)r * r);
     double* d_e = a.take<double>(r);
+    double* h_e = h.take<double>(r);
     double* d_r = a.take<double>(r);
+    double* h_r = h.take<double>(r);
     double* d_j = a.take<double>(nj ? nj : 1);
-    hipError_t e = hipSuccess;
+    double* h_j = h.take<double>(nj ? nj : 1);
     if (nb) {
-        e = hipMemcpyAsync(d_blk, size, sizeof(int32_t) * nb, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(d_blk + nb, index, sizeof(int32_t) * nb, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(d_blk + 2 * nb, xoff, sizeof(int32_t) * nb, hipMemcpyHostToDevice, c->stream);
+        std::memcpy(h_blk, size, sizeof(int32_t) * nb);
+        std::memcpy(h_blk + nb, index, sizeof(int32_t) * nb);
+        std::memcpy(h_blk + 2 * nb, xoff, sizeof(int32_t) * nb);
     }
-    if (e == hipSuccess && n_x) e = hipMemcpyAsync(d_x0, x0, sizeof(double) * n_x, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess && n_x) e = hipMemcpyAsync(d_x, params, sizeof(double) * n_x, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_J, J0, sizeof(double) * r * r, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_e, e0, sizeof(double) * r, hipMemcpyHostToDevice, c->stream);
+    if (n_x) {
+        std::memcpy(h_x0, x0, sizeof(double) * n_x);
+        std::memcpy(h_x, params, sizeof(double) * n_x);
+    }
+    std::memcpy(h_J, J0, sizeof(double) * r * r);
+    std::memcpy(h_e, e0, sizeof(double) * r);
+    hipError_t e = hipMemcpyAsync(d_blk, h_blk, (size_t)((char*)d_r - (char*)d_blk), hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "marginalisation upload");
     hipEvent_t ev{};
     prof_begin(c, "marg_factor", &ev);
     e = launch_marg_factor(c, r, nb, d_blk, d_x0, d_x, d_J, d_e, d_r, nj ? d_j : nullptr);
     prof_end(c, "marg_factor", ev);
     if (e != hipSuccess) return hip_err(c, e, "marginalisation kernel");
-    e = hipMemcpyAsync(residuals, d_r, sizeof(double) * r, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess && nj) e = hipMemcpyAsync(jacobians, d_j, sizeof(double) * nj, hipMemcpyDeviceToHost, c->stream);
+    const size_t out = (size_t)((char*)d_j - (char*)d_r) + sizeof(double) * (nj ? nj : 0);
+    e = hipMemcpyAsync(h_r, d_r, out, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    return hip_err(c, e, "marginalisation download");
+    if (e != hipSuccess) return hip_err(c, e, "marginalisation download");
+    std::memcpy(residuals, h_r, sizeof(double) * r);
+    if (nj) std::memcpy(jacobians, h_j, sizeof(double) * nj);
+    return GVX_OK;
 }

@@ -73,24 +73,35 @@ gvx_status run_chains(gvx_ctx* c, const gvx_ins_config* cfg, int n_chain, const 
     const size_t n_imu = (size_t)off[n_chain];
     size_t need = arena_size({n_imu * sizeof(gvx_imu), sizeof(int32_t) * (n_chain + 1),
                               sizeof(gvx_state) * n_chain, sizeof(gvx_state) * n_imu});
+    // a pinned arena laid out like the device one: one upload of the inputs
+    // (its prefix), one download of the states
     Arena a{(char*)scratch(c, "ins", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "INS staging");
+    Arena h{(char*)pinned(c, "ins", need), need, 0};
+    if (!a.base || !h.base) return set_err(c, GVX_ERR_OOM, "INS staging");
     gvx_imu* d_imu = a.take<gvx_imu>(n_imu);
+    gvx_imu* h_imu = h.take<gvx_imu>(n_imu);
     int32_t* d_off = a.take<int32_t>(n_chain + 1);
+    int32_t* h_off = h.take<int32_t>(n_chain + 1);
     gvx_state* d_s0 = a.take<gvx_state>(n_chain);
+    gvx_state* h_s0 = h.take<gvx_state>(n_chain);
     gvx_state* d_st = a.take<gvx_state>(n_imu);
-    hipError_t e = hipMemcpyAsync(d_imu, imu, n_imu * sizeof(gvx_imu), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_off, off, sizeof(int32_t) * (n_chain + 1), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_s0, state0, sizeof(gvx_state) * n_chain, hipMemcpyHostToDevice, c->stream);
+    gvx_state* h_st = h.take<gvx_state>(n_imu);
+    std::memcpy(h_imu, imu, n_imu * sizeof(gvx_imu));
+    std::memcpy(h_off, off, sizeof(int32_t) * (n_chain + 1));
+    std::memcpy(h_s0, state0, sizeof(gvx_state) * n_chain);
+    hipError_t e = hipMemcpyAsync(d_imu, h_imu, (size_t)((char*)d_st - (char*)d_imu), hipMemcpyHostToDevice,
+                                  c->stream);
     if (e != hipSuccess) return hip_err(c, e, "INS upload");
     hipEvent_t ev{};
     prof_begin(c, "ins", &ev);
     e = launch_ins(c, *cfg, n_chain, d_imu, d_off, d_s0, d_st);
     prof_end(c, "ins", ev);
     if (e != hipSuccess) return hip_err(c, e, "INS kernel");
-    e = hipMemcpyAsync(states, d_st, sizeof(gvx_state) * n_imu, hipMemcpyDeviceToHost, c->stream);
+    e = hipMemcpyAsync(h_st, d_st, sizeof(gvx_state) * n_imu, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    return hip_err(c, e, "INS download");
+    if (e != hipSuccess) return hip_err(c, e, "INS download");
+    std::memcpy(states, h_st, sizeof(gvx_state) * n_imu);
+    return GVX_OK;
 }
 
 }  // namespace
