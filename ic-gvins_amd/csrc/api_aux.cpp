@@ -50,24 +50,34 @@ gvx_status gvx_small_factor_eval(gvx_ctx* c, int32_t kind, int32_t n, const doub
     const size_t nc = (size_t)n * NC, nr = (size_t)n * R, nj = jacobians ? (size_t)n * R * P : 0;
     size_t need = arena_size({sizeof(double) * (nc ? nc : 1), sizeof(double) * n_params, sizeof(int32_t) * n,
                               sizeof(double) * nr, sizeof(double) * (nj ? nj : 1)});
+    // pinned arena laid out like the device one: one upload, one download
     Arena a{(char*)scratch(c, "aux_factor", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "factor staging");
+    Arena h{(char*)pinned(c, "aux_factor", need), need, 0};
+    if (!a.base || !h.base) return set_err(c, GVX_ERR_OOM, "factor staging");
     double* d_c = a.take<double>(nc ? nc : 1);
+    double* h_c = h.take<double>(nc ? nc : 1);
     double* d_p = a.take<double>(n_params);
+    double* h_p = h.take<double>(n_params);
     int32_t* d_o = a.take<int32_t>(n);
+    int32_t* h_o = h.take<int32_t>(n);
     double* d_r = a.take<double>(nr);
+    double* h_r = h.take<double>(nr);
     double* d_j = a.take<double>(nj ? nj : 1);
-    hipError_t e = hipSuccess;
-    if (nc) e = hipMemcpyAsync(d_c, consts, sizeof(double) * nc, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_o, offs, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
+    double* h_j = h.take<double>(nj ? nj : 1);
+    if (nc) std::memcpy(h_c, consts, sizeof(double) * nc);
+    std::memcpy(h_p, params, sizeof(double) * n_params);
+    std::memcpy(h_o, offs, sizeof(int32_t) * n);
+    hipError_t e = hipMemcpyAsync(d_c, h_c, (size_t)((char*)d_r - (char*)d_c), hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "factor upload");
     gvx_status s = gvx_small_factor_eval_dev(c, kind, n, d_c, d_p, d_o, d_r, nj ? d_j : nullptr);
     if (s) return s;
-    e = hipMemcpyAsync(residuals, d_r, sizeof(double) * nr, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess && nj) e = hipMemcpyAsync(jacobians, d_j, sizeof(double) * nj, hipMemcpyDeviceToHost, c->stream);
+    const size_t out = (size_t)((char*)d_j - (char*)d_r) + sizeof(double) * nj;
+    e = hipMemcpyAsync(h_r, d_r, out, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    return hip_err(c, e, "factor download");
+    if (e != hipSuccess) return hip_err(c, e, "factor download");
+    std::memcpy(residuals, h_r, sizeof(double) * nr);
+    if (nj) std::memcpy(jacobians, h_j, sizeof(double) * nj);
+    return GVX_OK;
 }
 
 gvx_status gvx_marg_factor_eval(gvx_ctx* c, int32_t r, int32_t nb, const int32_t* size, const int32_t* index,
