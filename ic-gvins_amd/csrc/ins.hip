@@ -26,6 +26,7 @@ struct InsStep {
     double dvfb[3];
     double qd[4];   // rotvec2quaternion(dtheta + coning)
     double qnn[4];  // Earth: rotvec2quaternion(-iewn dt)
+    double m1[9];   // Earth: 0.5 (I + R(qnn)), also independent of the recursion
 };
 constexpr int STEP_DW = sizeof(InsStep) / 8;
 constexpr int CHUNK = 64;
@@ -81,7 +82,11 @@ __global__ void __launch_bounds__(64) ins_kernel(gvx_ins_config cfg, int n_chain
                 dq_store(dq_from_rotvec(dth), st.qd);
                 if (earth) {
                     const double dnn[3] = {-cfg.iewn[0] * st.dt, -cfg.iewn[1] * st.dt, -cfg.iewn[2] * st.dt};
-                    dq_store(dq_from_rotvec(dnn), st.qnn);
+                    const dq qnn = dq_from_rotvec(dnn);
+                    dq_store(qnn, st.qnn);
+                    double Rnn[9];
+                    dq_rot(qnn, Rnn);
+                    for (int i = 0; i < 9; ++i) st.m1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + Rnn[i]);
                 }
                 const double* w = reinterpret_cast<const double*>(&st);
                 for (int i = 0; i < STEP_DW; ++i) sst[lane][i] = w[i];
@@ -96,14 +101,12 @@ __global__ void __launch_bounds__(64) ins_kernel(gvx_ins_config cfg, int n_chain
             double dvel[3], Rq[9];
             dq q = dq_load(s.q);
             if (earth) {
-                double cr[3], dvcg[3], Rnn[9], M1[9];
+                double cr[3], dvcg[3], M1[9];
                 cross3(cfg.iewn, s.v, cr);
                 for (int i = 0; i < 3; ++i) dvcg[i] = (cfg.gravity[i] - 2.0 * cr[i]) * dt;
                 const dq qnn = dq_load(st.qnn);
-                dq_rot(qnn, Rnn);
-                for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + Rnn[i]);
                 dq_rot(q, Rq);
-                mm3(M1, Rq, M1);
+                mm3(st.m1, Rq, M1);
                 mv3(M1, st.dvfb, dvel);
                 for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + dvcg[i];
                 q = dq_normalized(dq_mul(dq_mul(qnn, q), dq_load(st.qd)));
