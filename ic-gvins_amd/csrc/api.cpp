@@ -363,7 +363,9 @@ static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, con
     char* h = (char*)pinned(c, "klt", need);
     char* d = (char*)scratch(c, "klt", need);
     if (!h || !d) return set_err(c, GVX_ERR_OOM, "klt staging");
-    hipStreamSynchronize(c->stream);
+    // no wait here: the staging buffers are only in flight inside this call (it
+    // ends with a synchronisation), so the points are staged and the upload and
+    // launch queue up behind the frames' preprocessing already on the stream
     float* h_prev = (float*)h;
     float* h_next = (float*)(h + fb_bytes);
     float* h_back = (float*)(h + 2 * fb_bytes);
