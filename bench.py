@@ -156,6 +156,11 @@ def main():
     ap.add_argument("--frames", type=int, default=2000, help="configs[4]: frames per sequence")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return sys.exit(spawn_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; launch one rank per GPU")
     if args.config == 1:
         args.config = 2  # configs[0] is the CPU-only reference case; its GPU twin is configs[1]
     if args.mock:
@@ -774,6 +779,22 @@ def sequence_main(args):
     if dist:
         dist.destroy_process_group()
     ctx.close()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per
+    GPU) through torch.distributed.run as CHILD processes, before this process
+    touches the GPU, and return their exit status.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def max_over_ranks(elapsed, dist, dev=None):

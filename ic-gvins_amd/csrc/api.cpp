@@ -33,6 +33,8 @@ gvx_status hip_err(gvx_ctx* c, hipError_t e, const char* what) {
 void* scratch(gvx_ctx* c, const std::string& name, size_t bytes) {
     DevBuf& b = c->dev[name];
     if (b.bytes >= bytes && b.p) return b.p;
+    if (c->capturing) return nullptr;  // growing would synchronise the captured stream
+    ++c->mem_gen;
     if (b.p) {
         hipStreamSynchronize(c->stream);
         hipFree(b.p);
@@ -51,6 +53,8 @@ void* scratch(gvx_ctx* c, const std::string& name, size_t bytes) {
 void* pinned(gvx_ctx* c, const std::string& name, size_t bytes) {
     DevBuf& b = c->pinned[name];
     if (b.bytes >= bytes && b.p) return b.p;
+    if (c->capturing) return nullptr;
+    ++c->mem_gen;
     if (b.p) {
         hipStreamSynchronize(c->stream);
         hipHostFree(b.p);
@@ -236,6 +240,12 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
     PyrLayout lay = make_layout(w, h, p->max_level, p->win);
     Frame& f = c->frames[id];
     if (!f.pyr || f.lay.bytes < lay.bytes) {
+        if (c->capturing) {
+            if (!f.pyr) c->frames.erase(id);
+            return set_err(c, GVX_ERR_INVALID, "frame %llu needs a (re)allocation during a graph capture",
+                           (unsigned long long)id);
+        }
+        ++c->mem_gen;
         if (f.pyr) {
             hipStreamSynchronize(c->stream);
             hipFree(f.pyr);
@@ -276,6 +286,12 @@ gvx_status gvx_frame_put_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_gray, int
     PyrLayout lay = make_layout(w, h, p->max_level, p->win);
     Frame& f = c->frames[id];
     if (!f.pyr || f.lay.bytes < lay.bytes) {
+        if (c->capturing) {
+            if (!f.pyr) c->frames.erase(id);
+            return set_err(c, GVX_ERR_INVALID, "frame %llu needs a (re)allocation during a graph capture",
+                           (unsigned long long)id);
+        }
+        ++c->mem_gen;
         if (f.pyr) {
             hipStreamSynchronize(c->stream);
             hipFree(f.pyr);
@@ -302,6 +318,8 @@ gvx_status gvx_frame_drop(gvx_ctx* c, uint64_t id) {
     if (!c) return GVX_ERR_INVALID;
     auto it = c->frames.find(id);
     if (it == c->frames.end()) return set_err(c, GVX_ERR_NOT_FOUND, "frame %llu", (unsigned long long)id);
+    if (c->capturing) return set_err(c, GVX_ERR_INVALID, "gvx_frame_drop during a graph capture");
+    ++c->mem_gen;
     hipStreamSynchronize(c->stream);
     hipFree(it->second.pyr);
     c->frames.erase(it);

@@ -48,22 +48,19 @@ gvx_status gvx_small_factor_eval(gvx_ctx* c, int32_t kind, int32_t n, const doub
                            offs[i] + P, n_params);
     hipSetDevice(c->device);
     const size_t nc = (size_t)n * NC, nr = (size_t)n * R, nj = jacobians ? (size_t)n * R * P : 0;
-    size_t need = arena_size({sizeof(double) * (nc ? nc : 1), sizeof(double) * n_params, sizeof(int32_t) * n,
-                              sizeof(double) * nr, sizeof(double) * (nj ? nj : 1)});
     // pinned arena laid out like the device one: one upload, one download
-    Arena a{(char*)scratch(c, "aux_factor", need), need, 0};
-    Arena h{(char*)pinned(c, "aux_factor", need), need, 0};
-    if (!a.base || !h.base) return set_err(c, GVX_ERR_OOM, "factor staging");
-    double* d_c = a.take<double>(nc ? nc : 1);
-    double* h_c = h.take<double>(nc ? nc : 1);
-    double* d_p = a.take<double>(n_params);
-    double* h_p = h.take<double>(n_params);
-    int32_t* d_o = a.take<int32_t>(n);
-    int32_t* h_o = h.take<int32_t>(n);
-    double* d_r = a.take<double>(nr);
-    double* h_r = h.take<double>(nr);
-    double* d_j = a.take<double>(nj ? nj : 1);
-    double* h_j = h.take<double>(nj ? nj : 1);
+    double *d_c, *h_c, *d_p, *h_p, *d_r, *h_r, *d_j, *h_j;
+    int32_t *d_o, *h_o;
+    Staging st;
+    st.add(nc, &d_c, &h_c);
+    st.add((size_t)n_params, &d_p, &h_p);
+    st.add((size_t)n, &d_o, &h_o);
+    st.add(nr, &d_r, &h_r);
+    st.add(nj, &d_j, &h_j);
+    void* db = scratch(c, "aux_factor", st.bytes());
+    void* hb = pinned(c, "aux_factor", st.bytes());
+    if (!db || !hb) return set_err(c, GVX_ERR_OOM, "factor staging");
+    st.bind(db, hb);
     if (nc) std::memcpy(h_c, consts, sizeof(double) * nc);
     std::memcpy(h_p, params, sizeof(double) * n_params);
     std::memcpy(h_o, offs, sizeof(int32_t) * n);
@@ -99,27 +96,22 @@ gvx_status gvx_marg_factor_eval(gvx_ctx* c, int32_t r, int32_t nb, const int32_t
     }
     hipSetDevice(c->device);
     const size_t nj = jacobians ? (size_t)jac_total : 0;
-    size_t need = arena_size({sizeof(int32_t) * 3 * (nb ? nb : 1), sizeof(double) * 2 * (n_x ? n_x : 1),
-                              sizeof(double) * (size_t)r * r, sizeof(double) * 2 * r, sizeof(double) * (nj ? nj : 1)});
     // one pinned staging arena laid out like the device one: the inputs are its
     // prefix (one upload), the outputs its suffix (one download)
-    Arena a{(char*)scratch(c, "marg_factor", need), need, 0};
-    Arena h{(char*)pinned(c, "marg_factor", need), need, 0};
-    if (!a.base || !h.base) return set_err(c, GVX_ERR_OOM, "marginalisation staging");
-    int32_t* d_blk = a.take<int32_t>(3 * (nb ? nb : 1));
-    int32_t* h_blk = h.take<int32_t>(3 * (nb ? nb : 1));
-    double* d_x0 = a.take<double>(n_x ? n_x : 1);
-    double* h_x0 = h.take<double>(n_x ? n_x : 1);
-    double* d_x = a.take<double>(n_x ? n_x : 1);
-    double* h_x = h.take<double>(n_x ? n_x : 1);
-    double* d_J = a.take<double>((size_t)r * r);
-    double* h_J = h.take<double>((size_t)r * r);
-    double* d_e = a.take<double>(r);
-    double* h_e = h.take<double>(r);
-    double* d_r = a.take<double>(r);
-    double* h_r = h.take<double>(r);
-    double* d_j = a.take<double>(nj ? nj : 1);
-    double* h_j = h.take<double>(nj ? nj : 1);
+    int32_t *d_blk, *h_blk;
+    double *d_x0, *h_x0, *d_x, *h_x, *d_J, *h_J, *d_e, *h_e, *d_r, *h_r, *d_j, *h_j;
+    Staging st;
+    st.add(3 * (size_t)nb, &d_blk, &h_blk);
+    st.add((size_t)n_x, &d_x0, &h_x0);
+    st.add((size_t)n_x, &d_x, &h_x);
+    st.add((size_t)r * r, &d_J, &h_J);
+    st.add((size_t)r, &d_e, &h_e);
+    st.add((size_t)r, &d_r, &h_r);
+    st.add(nj, &d_j, &h_j);
+    void* db = scratch(c, "marg_factor", st.bytes());
+    void* hb = pinned(c, "marg_factor", st.bytes());
+    if (!db || !hb) return set_err(c, GVX_ERR_OOM, "marginalisation staging");
+    st.bind(db, hb);
     if (nb) {
         std::memcpy(h_blk, size, sizeof(int32_t) * nb);
         std::memcpy(h_blk + nb, index, sizeof(int32_t) * nb);

@@ -93,17 +93,21 @@ gvx_status gvx_preint_integrate(gvx_ctx* c, int32_t variant, const gvx_imu_param
     const size_t n_imu = (size_t)seg_off[n_seg];
     const size_t n_pn = n_imu - (size_t)n_seg;
     hipSetDevice(c->device);
-    size_t need = arena_size({n_imu * sizeof(gvx_imu), sizeof(int32_t) * (n_seg + 1), sizeof(gvx_state) * n_seg,
-                              sizeof(double) * 3 * n_seg, sizeof(gvx_preint_result) * n_seg,
-                              sizeof(double) * 4 * (n_pn + 1)});
-    Arena a{(char*)scratch(c, "preint", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "preint staging");
-    gvx_imu* d_imu = a.take<gvx_imu>(n_imu);
-    int32_t* d_off = a.take<int32_t>(n_seg + 1);
-    gvx_state* d_s0 = a.take<gvx_state>(n_seg);
-    double* d_iewn = a.take<double>(3 * n_seg);
-    gvx_preint_result* d_out = a.take<gvx_preint_result>(n_seg);
-    double* d_pn = a.take<double>(4 * (n_pn + 1));
+    gvx_imu* d_imu;
+    int32_t* d_off;
+    gvx_state* d_s0;
+    double *d_iewn, *d_pn;
+    gvx_preint_result* d_out;
+    Staging st;
+    st.add(n_imu, &d_imu);
+    st.add((size_t)n_seg + 1, &d_off);
+    st.add((size_t)n_seg, &d_s0);
+    st.add(3 * (size_t)n_seg, &d_iewn);
+    st.add((size_t)n_seg, &d_out);
+    st.add(4 * (n_pn + 1), &d_pn);
+    void* db = scratch(c, "preint", st.bytes());
+    if (!db) return set_err(c, GVX_ERR_OOM, "preint staging");
+    st.bind(db);
     hipError_t e = hipMemcpyAsync(d_imu, imu, n_imu * sizeof(gvx_imu), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_off, seg_off, sizeof(int32_t) * (n_seg + 1), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_s0, state0, sizeof(gvx_state) * n_seg, hipMemcpyHostToDevice, c->stream);
@@ -145,15 +149,19 @@ gvx_status gvx_reproj_eval(gvx_ctx* c, int32_t n, const gvx_reproj_const* cs, co
                            (long long)(i / 5), (int)(i % 5), offs[i]);
     }
     hipSetDevice(c->device);
-    size_t need = arena_size({sizeof(gvx_reproj_const) * n, sizeof(double) * n_params, sizeof(int32_t) * 5 * n,
-                              sizeof(double) * 2 * n, jac ? sizeof(double) * 46 * n : 0});
-    Arena a{(char*)scratch(c, "reproj", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "reproj staging");
-    gvx_reproj_const* d_c = a.take<gvx_reproj_const>(n);
-    double* d_p = a.take<double>(n_params);
-    int32_t* d_o = a.take<int32_t>(5 * (size_t)n);
-    double* d_r = a.take<double>(2 * (size_t)n);
-    double* d_j = jac ? a.take<double>(46 * (size_t)n) : nullptr;
+    gvx_reproj_const* d_c;
+    double *d_p, *d_r, *d_j;
+    int32_t* d_o;
+    Staging st;
+    st.add((size_t)n, &d_c);
+    st.add((size_t)n_params, &d_p);
+    st.add(5 * (size_t)n, &d_o);
+    st.add(2 * (size_t)n, &d_r);
+    st.add(jac ? 46 * (size_t)n : 0, &d_j);
+    void* db = scratch(c, "reproj", st.bytes());
+    if (!db) return set_err(c, GVX_ERR_OOM, "reproj staging");
+    st.bind(db);
+    if (!jac) d_j = nullptr;
     hipError_t e = hipMemcpyAsync(d_c, cs, sizeof(gvx_reproj_const) * n, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_p, params, sizeof(double) * n_params, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_o, offs, sizeof(int32_t) * 5 * n, hipMemcpyHostToDevice, c->stream);
@@ -203,18 +211,21 @@ gvx_status gvx_preint_factor_eval(gvx_ctx* c, int32_t n, const gvx_preint_result
     }
     hipSetDevice(c->device);
     const size_t npn = any_earth ? (size_t)n_pn : 0;
-    size_t need = arena_size({sizeof(gvx_preint_result) * n, sizeof(double) * 4 * (npn + 1), sizeof(int32_t) * n,
-                              sizeof(double) * n_params, sizeof(int32_t) * 4 * n, sizeof(double) * 15 * n,
-                              jac ? sizeof(double) * 480 * n : 0});
-    Arena a{(char*)scratch(c, "pfactor", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "preint factor staging");
-    gvx_preint_result* d_pre = a.take<gvx_preint_result>(n);
-    double* d_pn = a.take<double>(4 * (npn + 1));
-    int32_t* d_pno = a.take<int32_t>(n);
-    double* d_p = a.take<double>(n_params);
-    int32_t* d_o = a.take<int32_t>(4 * (size_t)n);
-    double* d_r = a.take<double>(15 * (size_t)n);
-    double* d_j = jac ? a.take<double>(480 * (size_t)n) : nullptr;
+    gvx_preint_result* d_pre;
+    double *d_pn, *d_p, *d_r, *d_j;
+    int32_t *d_pno, *d_o;
+    Staging st;
+    st.add((size_t)n, &d_pre);
+    st.add(4 * (npn + 1), &d_pn);
+    st.add((size_t)n, &d_pno);
+    st.add((size_t)n_params, &d_p);
+    st.add(4 * (size_t)n, &d_o);
+    st.add(15 * (size_t)n, &d_r);
+    st.add(jac ? 480 * (size_t)n : 0, &d_j);
+    void* db = scratch(c, "pfactor", st.bytes());
+    if (!db) return set_err(c, GVX_ERR_OOM, "preint factor staging");
+    st.bind(db);
+    if (!jac) d_j = nullptr;
     hipError_t e = hipMemcpyAsync(d_pre, pre, sizeof(gvx_preint_result) * n, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess && any_earth) {
         e = hipMemcpyAsync(d_pn, pn, sizeof(double) * 4 * npn, hipMemcpyHostToDevice, c->stream);

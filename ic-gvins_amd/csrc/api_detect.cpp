@@ -111,25 +111,29 @@ gvx_status gvx_detect(gvx_ctx* c, uint64_t frame_id, const float* count_xy, int3
     }
     const int64_t stride = (int64_t)col * row;
     hipSetDevice(c->device);
-    size_t need = arena_size({sizeof(int2) * (centers.size() + 1), sizeof(int) * (mindist + 1), sizeof(int4) * bcnt,
-                              sizeof(int) * (active.size() + 1), sizeof(int) * bcnt, (size_t)W * H,
-                              sizeof(float) * stride * bcnt, sizeof(unsigned long long) * stride * bcnt,
-                              sizeof(int2) * maxpb * bcnt, sizeof(int) * bcnt, sizeof(float2) * maxpb * bcnt,
-                              sizeof(float) * 121});
-    Arena a{(char*)scratch(c, "detect", need), need, 0};
-    if (!a.base) return set_err(c, GVX_ERR_OOM, "detect staging");
-    int2* d_cent = a.take<int2>(centers.size() + 1);
-    int* d_hw = a.take<int>(mindist + 1);
-    int4* d_rois = a.take<int4>(bcnt);
-    int* d_ids = a.take<int>(active.size() + 1);
-    int* d_want = a.take<int>(bcnt);
-    uint8_t* d_mask = a.take<uint8_t>((size_t)W * H);
-    float* d_eig = a.take<float>(stride * bcnt);
-    unsigned long long* d_cand = a.take<unsigned long long>(stride * bcnt);
-    int2* d_corn = a.take<int2>((size_t)maxpb * bcnt);
-    int* d_nc = a.take<int>(bcnt);
-    float2* d_out = a.take<float2>((size_t)maxpb * bcnt);
-    float* d_gm = a.take<float>(121);
+    int2 *d_cent, *d_corn;
+    int *d_hw, *d_ids, *d_want, *d_nc;
+    int4* d_rois;
+    uint8_t* d_mask;
+    float *d_eig, *d_gm;
+    unsigned long long* d_cand;
+    float2* d_out;
+    Staging st;
+    st.add(centers.size() + 1, &d_cent);
+    st.add((size_t)mindist + 1, &d_hw);
+    st.add((size_t)bcnt, &d_rois);
+    st.add(active.size() + 1, &d_ids);
+    st.add((size_t)bcnt, &d_want);
+    st.add((size_t)W * H, &d_mask);
+    st.add((size_t)stride * bcnt, &d_eig);
+    st.add((size_t)stride * bcnt, &d_cand);
+    st.add((size_t)maxpb * bcnt, &d_corn);
+    st.add((size_t)bcnt, &d_nc);
+    st.add((size_t)maxpb * bcnt, &d_out);
+    st.add(121, &d_gm);
+    void* db = scratch(c, "detect", st.bytes());
+    if (!db) return set_err(c, GVX_ERR_OOM, "detect staging");
+    st.bind(db);
     hipError_t e = hipSuccess;
     auto up = [&](void* d, const void* h, size_t b) {
         if (e == hipSuccess && b) e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, c->stream);

@@ -14,23 +14,37 @@ using namespace gvx;
 struct gvx_graph {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    const gvx_ctx* ctx = nullptr;
+    uint64_t mem_gen = 0;  // the context's memory generation the graph's pointers belong to
 };
 
 gvx_status gvx_capture_begin(gvx_ctx* c) {
     if (!c) return GVX_ERR_INVALID;
     // the profiling brackets record and query events on the host: not capturable
     if (c->prof) return set_err(c, GVX_ERR_INVALID, "disable profiling before capturing a graph");
+    if (c->capturing) return set_err(c, GVX_ERR_INVALID, "a capture is already open");
     hipSetDevice(c->device);
-    return hip_err(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    gvx_status s = hip_err(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    if (s == GVX_OK) {
+        c->capturing = true;
+        c->capture_gen = c->mem_gen;
+    }
+    return s;
 }
 
 gvx_status gvx_capture_end(gvx_ctx* c, gvx_graph** out) {
     if (!c || !out) return GVX_ERR_INVALID;
     *out = nullptr;
     hipSetDevice(c->device);
+    if (!c->capturing) return set_err(c, GVX_ERR_INVALID, "no capture is open");
+    c->capturing = false;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (e != hipSuccess) return hip_err(c, e, "hipStreamEndCapture");
+    if (c->mem_gen != c->capture_gen) {
+        hipGraphDestroy(g);
+        return set_err(c, GVX_ERR_INVALID, "device buffers moved during the capture");
+    }
     hipGraphExec_t x = nullptr;
     e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
@@ -45,12 +59,17 @@ gvx_status gvx_capture_end(gvx_ctx* c, gvx_graph** out) {
     }
     h->graph = g;
     h->exec = x;
+    h->ctx = c;
+    h->mem_gen = c->mem_gen;
     *out = h;
     return GVX_OK;
 }
 
 gvx_status gvx_graph_launch(gvx_ctx* c, const gvx_graph* g) {
     if (!c || !g || !g->exec) return GVX_ERR_INVALID;
+    if (g->ctx != c) return set_err(c, GVX_ERR_INVALID, "graph captured on another context");
+    if (g->mem_gen != c->mem_gen)
+        return set_err(c, GVX_ERR_INVALID, "stale graph: scratch or frame memory was reallocated after capture");
     hipSetDevice(c->device);
     return hip_err(c, hipGraphLaunch(g->exec, c->stream), "hipGraphLaunch");
 }

@@ -71,21 +71,20 @@ gvx_status check_cfg(gvx_ctx* c, const gvx_ins_config* cfg) {
 gvx_status run_chains(gvx_ctx* c, const gvx_ins_config* cfg, int n_chain, const gvx_imu* imu, const int32_t* off,
                       const gvx_state* state0, gvx_state* states) {
     const size_t n_imu = (size_t)off[n_chain];
-    size_t need = arena_size({n_imu * sizeof(gvx_imu), sizeof(int32_t) * (n_chain + 1),
-                              sizeof(gvx_state) * n_chain, sizeof(gvx_state) * n_imu});
     // a pinned arena laid out like the device one: one upload of the inputs
     // (its prefix), one download of the states
-    Arena a{(char*)scratch(c, "ins", need), need, 0};
-    Arena h{(char*)pinned(c, "ins", need), need, 0};
-    if (!a.base || !h.base) return set_err(c, GVX_ERR_OOM, "INS staging");
-    gvx_imu* d_imu = a.take<gvx_imu>(n_imu);
-    gvx_imu* h_imu = h.take<gvx_imu>(n_imu);
-    int32_t* d_off = a.take<int32_t>(n_chain + 1);
-    int32_t* h_off = h.take<int32_t>(n_chain + 1);
-    gvx_state* d_s0 = a.take<gvx_state>(n_chain);
-    gvx_state* h_s0 = h.take<gvx_state>(n_chain);
-    gvx_state* d_st = a.take<gvx_state>(n_imu);
-    gvx_state* h_st = h.take<gvx_state>(n_imu);
+    gvx_imu *d_imu, *h_imu;
+    int32_t *d_off, *h_off;
+    gvx_state *d_s0, *h_s0, *d_st, *h_st;
+    Staging st;
+    st.add(n_imu, &d_imu, &h_imu);
+    st.add((size_t)n_chain + 1, &d_off, &h_off);
+    st.add((size_t)n_chain, &d_s0, &h_s0);
+    st.add(n_imu, &d_st, &h_st);
+    void* db = scratch(c, "ins", st.bytes());
+    void* hb = pinned(c, "ins", st.bytes());
+    if (!db || !hb) return set_err(c, GVX_ERR_OOM, "INS staging");
+    st.bind(db, hb);
     std::memcpy(h_imu, imu, n_imu * sizeof(gvx_imu));
     std::memcpy(h_off, off, sizeof(int32_t) * (n_chain + 1));
     std::memcpy(h_s0, state0, sizeof(gvx_state) * n_chain);

@@ -63,6 +63,12 @@ struct gvx_ctx {
     // scratch (grown on demand, never shrunk)
     std::map<std::string, gvx::DevBuf> dev;
     std::map<std::string, gvx::DevBuf> pinned;
+    // bumped whenever device memory a captured graph may reference is freed or
+    // moved (scratch growth, a frame pyramid reallocated or dropped): a graph
+    // captured under another generation refuses to launch
+    uint64_t mem_gen = 0;
+    bool capturing = false;
+    uint64_t capture_gen = 0;
     // profiling
     bool prof = false;
     std::map<std::string, gvx::ProfEntry> prof_acc;
@@ -215,24 +221,36 @@ struct DetectLaunch {
 };
 hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d);
 
-// Device staging arena: bump-allocates 256-byte aligned slices of one scratch
-// buffer (named) for host-pointer API calls.
-struct Arena {
-    char* base = nullptr;
-    size_t cap = 0, used = 0;
+// Staging layout for host-pointer API calls: ONE list of slices both sizes the
+// buffer and carves it (256-byte aligned, in declaration order), so the two can
+// never disagree.  add() registers the device pointer (and, optionally, the
+// pinned-host twin at the same offset); bind() assigns every registered pointer
+// once the buffers exist.  A zero count still takes one aligned slot, so the
+// slices stay distinct and in order (callers size contiguous ranges with
+// pointer differences).
+class Staging {
+  public:
     template <class T>
-    T* take(size_t count) {
-        size_t b = (count * sizeof(T) + 255) & ~size_t(255);
-        if (used + b > cap) return nullptr;
-        T* p = reinterpret_cast<T*>(base + used);
-        used += b;
-        return p;
+    void add(size_t count, T** dev, T** host = nullptr) {
+        items_.push_back({total_, reinterpret_cast<void**>(dev), reinterpret_cast<void**>(host)});
+        total_ += (std::max<size_t>(count, 1) * sizeof(T) + 255) & ~size_t(255);
     }
+    size_t bytes() const { return total_ ? total_ : 256; }
+    void bind(void* dev_base, void* host_base = nullptr) const {
+        for (const Item& it : items_) {
+            *it.dev = static_cast<char*>(dev_base) + it.off;
+            if (it.host) *it.host = host_base ? static_cast<char*>(host_base) + it.off : nullptr;
+        }
+    }
+
+  private:
+    struct Item {
+        size_t off;
+        void** dev;
+        void** host;
+    };
+    std::vector<Item> items_;
+    size_t total_ = 0;
 };
-inline size_t arena_size(std::initializer_list<size_t> bytes) {
-    size_t s = 0;
-    for (size_t b : bytes) s += (b + 255) & ~size_t(255);
-    return s + 256;
-}
 
 }  // namespace gvx

@@ -12,11 +12,8 @@
 // reads across ROI edges).
 //
 //   level0_kernel   padded copy of level 0 (frame cache only)
-//   fused_kernel<NL> NL pyrDown levels in one pass: a 128x64 tile of the source
-//                   level (+ the 5-tap halo of every level below it) is staged in
-//                   LDS with 16-byte loads, each level is filtered in LDS
-//                   (horizontal taps on v_dot4_u32_u8, vertical taps as packed u16)
-//                   and written once; intermediate levels never round-trip HBM
+//   edge_kernel     REFLECT_101 edge bands of level 0 (batched path)
+//   stream_kernel<NL> NL pyrDown levels in one streaming pass per band
 //   ring_kernel     the PAD rings of all built levels >= 1, one launch
 #include <hip/hip_runtime.h>
 
@@ -75,33 +72,7 @@ __global__ void __launch_bounds__(256) level0_kernel(const uint8_t* __restrict__
     *reinterpret_cast<uint4*>(d) = v;
 }
 
-// Workgroup barrier ordering LDS only: __syncthreads() also waits for every
-// outstanding global load (vmcnt(0)), which would serialise the next tile's
-// prefetch with this tile's filtering.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// ------------------------------------------------------------ fused pyrDown
-// Tile geometry: the deepest of the NL output levels owns a (128>>NL) x (64>>NL)
-// tile; level k (k = 0 source .. NL) is computed over a region that starts
-// REG_OFF(k) pixels before the tile's owned origin at that level and spans
-// REG_N(k) x REG_M(k) pixels -- exactly the 5-tap dependency cone of the deepest
-// tile (region(k) = 2*region(k+1) + 3, starting 2*off(k+1)+2 earlier).
-template <int NL>
-struct Geo {
-    static constexpr int TXD = 128 >> NL, TYD = 64 >> NL;
-    static constexpr int n(int k) { return k >= NL ? TXD : 2 * n(k + 1) + 3; }
-    static constexpr int m(int k) { return k >= NL ? TYD : 2 * m(k + 1) + 3; }
-    static constexpr int off(int k) { return k >= NL ? 0 : 2 * off(k + 1) + 2; }
-    // groups of 4 outputs per row at level k >= 1
-    static constexpr int g(int k) { return (n(k) + 3) / 4; }
-    // LDS byte row stride of level k (k = 0: the 160-byte staged source rows)
-    static constexpr int rs(int k) { return k == 0 ? 160 : (4 * g(k) + 7) / 8 * 8; }
-};
-
+// ------------------------------------------------------------ pyrDown helpers
 struct DownLevels {
     int64_t off[3];  // padded-level offsets (bytes) inside one pyramid
     int32_t pitch[3], w[3], h[3];
@@ -149,184 +120,6 @@ __device__ __forceinline__ uint32_t hibytes(uint32_t lo, uint32_t hi) {
     return __builtin_amdgcn_perm(hi, lo, 0x07050301u);
 }
 
-// Persistent: workgroup w builds tiles [w*per_wg, (w+1)*per_wg) of the
-// (image, tile row, tile column)-ordered tile list.  Consecutive tiles are
-// horizontal neighbours, so their shared halo lines stay in this CU's XCD L2,
-// and the next tile's source rows are fetched into registers while the
-// current tile is filtered (global latency off the critical path).
-// STOP < 99 truncates the pass after a phase (tools/pyr_micro.hip timing only):
-// 0 staging, then per level k: 3k-2 horizontal, 3k-1 vertical, 3k owned/fix-up.
-template <int NL, int STOP = 99>
-__global__ void __launch_bounds__(256) fused_kernel(const uint8_t* __restrict__ src, int64_t src_img_stride,
-                                                    int src_pitch, int src_w, int src_h, int vec16,
-                                                    uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
-                                                    int tiles_x, int tiles_y, int n_tiles, int per_wg) {
-    using G = Geo<NL>;
-    constexpr int M0 = G::m(0);
-    constexpr int OFF0 = G::off(0);
-    constexpr int NITEM = M0 * 10;                // 16-byte chunks of the staged source region
-    constexpr int NST = (NITEM + 255) / 256;      // per thread
-    // LDS: staged source rows, reused for the byte planes of levels 1..NL-1; the
-    // u16 horizontal sums of the level being built.
-    constexpr int BYTES_A = (M0 * G::rs(0) > G::m(1) * G::rs(1) ? M0 * G::rs(0) : G::m(1) * G::rs(1)) + 64;
-    constexpr int HS_A = (M0 + 2) * 4 * G::g(1);  // u16 entries (largest level)
-    __shared__ __attribute__((aligned(16))) uint8_t bufA[BYTES_A];
-    __shared__ __attribute__((aligned(16))) uint16_t hs[HS_A];
-    __shared__ __attribute__((aligned(16))) uint8_t bufB[NL > 1 ? G::m(2) * G::rs(2) + 64 : 16];
-
-    const int tid = threadIdx.x;
-    const int t_begin = xcd_swizzle(blockIdx.x, (n_tiles + per_wg - 1) / per_wg) * per_wg;
-    const int t_end = min(t_begin + per_wg, n_tiles);
-    if (t_begin >= t_end) return;
-
-    // source region of tile t: rows [64*by - OFF0, +M0), bytes [128*bx - 16, +160).
-    // Rows are reflected per chunk (cheap); a 16-byte chunk whose columns are
-    // all inside the image is one vector load even in border tiles, only chunks
-    // straddling the left / right edge gather bytes.
-    uint4 pre[NST];
-    uint32_t sink = 0;
-    auto stage_load = [&](int t) {
-        const int bx = t % tiles_x, rest = t / tiles_x;
-        const int by = rest % tiles_y, img = rest / tiles_y;
-        const uint8_t* S = src + img * src_img_stride;
-        const int A = 128 * bx - 16, Y0 = 64 * by - OFF0;
-#pragma unroll
-        for (int j = 0; j < NST; ++j) {
-            const int i = tid + 256 * j;
-            if (i >= NITEM) break;
-            const int r = i / 10, c = i - r * 10;
-            const uint8_t* row = S + (int64_t)refl(Y0 + r, src_h) * src_pitch;
-            const int x = A + 16 * c;
-            if (vec16 && x >= 0 && x + 16 <= src_w) {
-                pre[j] = *reinterpret_cast<const uint4*>(row + x);
-            } else {
-                uint32_t q[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    uint32_t d = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) d |= (uint32_t)row[refl(x + 4 * k + b, src_w)] << (8 * b);
-                    q[k] = d;
-                }
-                pre[j] = make_uint4(q[0], q[1], q[2], q[3]);
-            }
-        }
-    };
-    stage_load(t_begin);
-
-    for (int t = t_begin; t < t_end; ++t) {
-        const int bx = t % tiles_x, rest = t / tiles_x;
-        const int by = rest % tiles_y, img = rest / tiles_y;
-        uint8_t* P = pyr + img * pyr_bytes;
-        const int X0 = 128 * bx, Yo = 64 * by;  // owned origin at the source level
-#pragma unroll
-        for (int j = 0; j < NST; ++j) {
-            const int i = tid + 256 * j;
-            if (i < NITEM) *reinterpret_cast<uint4*>(&bufA[16 * i]) = pre[j];  // row r = i/10, chunk c
-        }
-        lds_barrier();
-        if (t + 1 < t_end) stage_load(t + 1);
-
-        // ---- levels 1..NL ----
-        auto build = [&](auto kc, const uint8_t* in, int in_rs, uint8_t* out) {
-            constexpr int k = decltype(kc)::value;  // output level 1..NL
-            constexpr int NG = G::g(k), MO = G::m(k), MI = G::m(k - 1), RSO = G::rs(k);
-            constexpr int SH = k == 1 ? 2 : 0;
-            constexpr int DW0 = k == 1 ? (16 - OFF0 - 2) / 4 : 0;  // first dword of the row's taps
-            constexpr int OFFK = G::off(k);
-            const int lw = L.w[k - 1], lh = L.h[k - 1], lp = L.pitch[k - 1];
-            if constexpr (STOP < 3 * k - 2) return;
-            // horizontal pass
-            for (int i = tid; i < MI * NG; i += 256) {
-                const int r = i / NG, g = i - r * NG;
-                const uint2 o = hsum4<SH>(reinterpret_cast<const uint32_t*>(in + r * in_rs) + DW0, g);
-                *reinterpret_cast<uint2*>(&hs[r * 4 * NG + 4 * g]) = o;
-            }
-            lds_barrier();
-            if constexpr (STOP < 3 * k - 1) return;
-            // vertical pass: item = (output row pair, group)
-            const int ox = (X0 >> k) - OFFK, oy = (Yo >> k) - OFFK;  // region origin
-            for (int i = tid; i < ((MO + 1) / 2) * NG; i += 256) {
-                const int rp = i / NG, g = i - rp * NG;
-                uint2 h[7];
-#pragma unroll
-                for (int q = 0; q < 7; ++q) h[q] = *reinterpret_cast<const uint2*>(&hs[(4 * rp + q) * 4 * NG + 4 * g]);
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr) {
-                    const int row = 2 * rp + rr;
-                    if (row >= MO) continue;
-                    const uint32_t lo =
-                        vsum2(h[2 * rr].x, h[2 * rr + 1].x, h[2 * rr + 2].x, h[2 * rr + 3].x, h[2 * rr + 4].x);
-                    const uint32_t hi =
-                        vsum2(h[2 * rr].y, h[2 * rr + 1].y, h[2 * rr + 2].y, h[2 * rr + 3].y, h[2 * rr + 4].y);
-                    const uint32_t q = hibytes(lo, hi);
-                    if (k < NL) {
-                        *reinterpret_cast<uint32_t*>(&out[row * RSO + 4 * g]) = q;
-                    } else {
-                        // deepest level: region == owned tile, store in place
-                        const int gx = ox + 4 * g, gy = oy + row;
-                        if (gx < lw && gy < lh)
-                            *reinterpret_cast<uint32_t*>(P + L.off[k - 1] + (int64_t)(gy + PAD) * lp + gx + PAD) = q;
-                    }
-                }
-            }
-            lds_barrier();
-            if constexpr (STOP < 3 * k) return;
-            if (k < NL) {
-                // owned tile of this level -> global (owned columns start at region
-                // offset OFF = 2 (mod 4): realign pairs of LDS dwords)
-                constexpr int OFF = OFFK, OW = 128 >> k, OH = 64 >> k;
-                const int gx0 = X0 >> k, gy0 = Yo >> k;
-                for (int i = tid; i < OH * (OW / 4); i += 256) {
-                    const int r = i / (OW / 4), q = i - r * (OW / 4);
-                    const int gx = gx0 + 4 * q, gy = gy0 + r;
-                    if (gx >= lw || gy >= lh) continue;
-                    const uint32_t* p = reinterpret_cast<const uint32_t*>(&out[(OFF + r) * RSO + OFF + 4 * q - 2]);
-                    const uint32_t v = __builtin_amdgcn_alignbyte(p[1], p[0], 2);
-                    *reinterpret_cast<uint32_t*>(P + L.off[k - 1] + (int64_t)(gy + PAD) * lp + gx + PAD) = v;
-                }
-                // region entries outside the level's image take their REFLECT_101
-                // value (the next level's taps read them); the sources are inside
-                // the image and inside the region for every entry the owned tiles need
-                constexpr int NO = G::n(k);
-                // in-image part of the region: rows [r0, r1), columns [c0, c1)
-                const int c0 = max(0, -ox), c1 = min(NO, lw - ox);
-                const int r0 = max(0, -oy), r1 = min(MO, lh - oy);
-                if (c0 > 0 || c1 < NO || r0 > 0 || r1 < MO) {
-                    auto fix = [&](int r, int c) {
-                        const int sr = refl(oy + r, lh) - oy, sc = refl(ox + c, lw) - ox;
-                        if ((unsigned)sr < (unsigned)MO && (unsigned)sc < (unsigned)NO)
-                            out[r * RSO + c] = out[sr * RSO + sc];
-                    };
-                    // out-of-image columns over all rows, then out-of-image rows
-                    // over the in-image columns (sources are in-image entries only)
-                    const int ncl = c0, ncr = NO - c1, ncol = ncl + ncr;
-                    for (int i = tid; i < MO * ncol; i += 256) {
-                        const int r = i / ncol, j = i - r * ncol;
-                        fix(r, j < ncl ? j : c1 + (j - ncl));
-                    }
-                    const int nrt = r0, nrb = MO - r1, nrow = nrt + nrb, ncin = c1 - c0;
-                    for (int i = tid; i < nrow * ncin; i += 256) {
-                        const int j = i / ncin, c = c0 + (i - j * ncin);
-                        fix(j < nrt ? j : r1 + (j - nrt), c);
-                    }
-                }
-                lds_barrier();
-            }
-        };
-        // level 1 from the staged source (its byte plane overwrites the staged
-        // rows only after the horizontal pass has consumed them)
-        build(std::integral_constant<int, 1>{}, bufA, 160, bufA);
-        constexpr int RS1 = G::rs(1), RS2 = G::rs(2);
-        if constexpr (NL >= 2) build(std::integral_constant<int, 2>{}, bufA, RS1, bufB);
-        if constexpr (NL >= 3) build(std::integral_constant<int, 3>{}, bufB, RS2, bufA);
-        if constexpr (STOP < 99) {  // keep the truncated phases' LDS results live
-            sink ^= reinterpret_cast<const uint32_t*>(bufA)[tid] ^ hs[tid] ^ bufB[tid & 15];
-        }
-        lds_barrier();  // the last level's LDS reads precede the next staging store
-    }
-    if constexpr (STOP < 99) reinterpret_cast<uint32_t*>(pyr)[blockIdx.x * 256 + tid] = sink;
-}
 
 // ------------------------------------------------------- streaming pyrDown
 // Row-streaming build of NL levels (the production path).  One wavefront owns
@@ -782,29 +575,6 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
     }
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(base + (int64_t)(refl(prow - PAD, h) + PAD) * pitch);
     *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = ring_dword(rw, pcol, w);
-}
-
-template <int NL>
-void launch_fused(gvx_ctx* c, const uint8_t* src, int64_t src_img_stride, int src_pitch, int src_w, int src_h,
-                  int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
-    // l0: source level index; builds levels l0+1 .. l0+NL
-    DownLevels D{};
-    for (int k = 0; k < NL; ++k) {
-        D.off[k] = lay.off[l0 + 1 + k];
-        D.pitch[k] = lay.pitch[l0 + 1 + k];
-        D.w[k] = lay.w[l0 + 1 + k];
-        D.h[k] = lay.h[l0 + 1 + k];
-    }
-    const int vec16 = (src_pitch % 16 == 0) && (src_img_stride % 16 == 0) &&
-                      (reinterpret_cast<uintptr_t>(src) % 16 == 0);
-    const int tiles_x = (src_w + 127) / 128, tiles_y = (src_h + 63) / 64;
-    const int n_tiles = tiles_x * tiles_y * n_img;
-    // resident workgroups per CU (LDS-bound: 27.7 / 21.9 / 19.6 KB for NL = 3 / 2 / 1)
-    const int slots = c->n_cu * (NL == 3 ? 5 : NL == 2 ? 7 : 8);
-    const int per_wg = (n_tiles + slots - 1) / slots;
-    const int n_wg = (n_tiles + per_wg - 1) / per_wg;
-    hipLaunchKernelGGL(fused_kernel<NL>, dim3(N_XCD * xcd_per(n_wg)), dim3(256), 0, c->stream, src, src_img_stride, src_pitch,
-                       src_w, src_h, vec16, dst, lay.bytes, D, tiles_x, tiles_y, n_tiles, per_wg);
 }
 
 // Rings of levels lo..hi.  sides_only: the streaming pass already wrote the

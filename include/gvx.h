@@ -57,7 +57,14 @@ gvx_status gvx_profile_reset(gvx_ctx* ctx);
    gvx_graph_launch replays with one launch: one frame pair per graph launch
    (BASELINE configs[1]) instead of one host call per kernel.
    Only *_dev entry points may be captured, after one uncaptured call with the
-   same sizes (so no scratch buffer grows during capture), with profiling off. */
+   same sizes (so no scratch buffer grows during capture), with profiling off.
+   A captured graph holds raw pointers to the context's scratch buffers and to
+   the cached frame pyramids.  Any later call that reallocates them (a scratch
+   buffer growing for larger sizes, gvx_frame_put with a bigger layout,
+   gvx_frame_drop) invalidates every graph of the context: gvx_graph_launch then
+   refuses with GVX_ERR_INVALID instead of touching freed memory.  Calls that
+   would reallocate during an open capture fail (GVX_ERR_INVALID / GVX_ERR_OOM)
+   and gvx_capture_end then refuses the graph. */
 typedef struct gvx_graph gvx_graph;
 gvx_status gvx_capture_begin(gvx_ctx* ctx);
 gvx_status gvx_capture_end(gvx_ctx* ctx, gvx_graph** out);

@@ -92,6 +92,9 @@ typedef struct {
 } orc_pyramid;
 
 void orc_klt_params_default(orc_klt_params* p);
+/* Window-sum accumulation order of LK (klt.c; parity experiment). */
+enum { ORC_ACC_EXACT = 0, ORC_ACC_F32 = 1, ORC_ACC_F32X4 = 2 };
+void orc_set_lk_accum(int mode);
 
 /* Returns the highest level built (<= max_level). Levels are padded by `win`
    pixels with BORDER_REFLECT_101, exactly as buildOpticalFlowPyramid does. */

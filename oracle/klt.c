@@ -226,6 +226,28 @@ typedef struct {
     const orc_klt_params* p;
 } lk_job;
 
+/* Accumulation order of the window sums A11/A12/A22 and b1/b2 (a parity
+ * experiment switch; the default is the one the GPU matches):
+ *   ORC_ACC_EXACT   exact int64 sums, rounded once to fp32 (the restatement's
+ *                   documented choice: machine-independent, bit-exact on the GPU)
+ *   ORC_ACC_F32     OpenCV 4.x's scalar loop: float accumulators, each int32
+ *                   product converted to float and added in row-major order
+ *                   (`iA11 += (itemtype)(ixval*ixval)`, itemtype = float)
+ *   ORC_ACC_F32X4   OpenCV 4.x's CV_SIMD128 path: pixels 0..15 of each 21-pixel
+ *                   row in 4-lane float accumulators (A: lane = x mod 4, fx*fx
+ *                   then add, no FMA; b: int32 products of (dx,dy)x(diff,diff)
+ *                   pairs, lanes (b1,b2,b1,b2) split over two accumulators),
+ *                   pixels 16..20 in the scalar float accumulator, the lanes
+ *                   reduced ((l0+l1)+(l2+l3)) and added last.
+ * Not thread-safe to change while an LK call runs. */
+static int lk_accum = ORC_ACC_EXACT;
+void orc_set_lk_accum(int mode) { lk_accum = mode; }
+
+typedef struct {
+    float l[4];
+} f4;
+static float f4_sum(f4 v) { return (v.l[0] + v.l[1]) + (v.l[2] + v.l[3]); }
+
 /* LKTrackerInvoker::operator() for points [begin, end) at one level. */
 static void lk_level(const lk_job* jb) {
     const orc_u8plane* I = jb->I;
@@ -279,6 +301,9 @@ static void lk_level(const lk_job* jb) {
         int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
 
         int64_t iA11 = 0, iA12 = 0, iA22 = 0;
+        float fA11 = 0.f, fA12 = 0.f, fA22 = 0.f;
+        f4 qA11 = {{0}}, qA12 = {{0}}, qA22 = {{0}};
+        const int simd_w = lk_accum == ORC_ACC_F32X4 ? win / 8 * 8 : 0;
         for (int y = 0; y < win; y++) {
             const uint8_t* src = px(I, ipx, ipy + y);
             const int16_t* dsrc = dI->buf + 2 * ((size_t)(ipy + y + dI->pad) * dI->pitch + ipx + dI->pad);
@@ -299,11 +324,34 @@ static void lk_level(const lk_job* jb) {
                 iA11 += (int64_t)ixval * ixval;
                 iA12 += (int64_t)ixval * iyval;
                 iA22 += (int64_t)iyval * iyval;
+                if (x < simd_w) {
+                    const float fx = (float)ixval, fy = (float)iyval;
+                    volatile float t11 = fx * fx, t12 = fx * fy, t22 = fy * fy;  /* no contraction */
+                    qA22.l[x & 3] += t22;
+                    qA12.l[x & 3] += t12;
+                    qA11.l[x & 3] += t11;
+                } else {
+                    fA11 += (float)(ixval * ixval);
+                    fA12 += (float)(ixval * iyval);
+                    fA22 += (float)(iyval * iyval);
+                }
             }
         }
-        float A11 = (float)iA11 * FLT_SCALE;
-        float A12 = (float)iA12 * FLT_SCALE;
-        float A22 = (float)iA22 * FLT_SCALE;
+        float A11, A12, A22;
+        if (lk_accum == ORC_ACC_EXACT) {
+            A11 = (float)iA11 * FLT_SCALE;
+            A12 = (float)iA12 * FLT_SCALE;
+            A22 = (float)iA22 * FLT_SCALE;
+        } else {
+            if (lk_accum == ORC_ACC_F32X4) {
+                fA11 += f4_sum(qA11);
+                fA12 += f4_sum(qA12);
+                fA22 += f4_sum(qA22);
+            }
+            A11 = fA11 * FLT_SCALE;
+            A12 = fA12 * FLT_SCALE;
+            A22 = fA22 * FLT_SCALE;
+        }
         float D = A11 * A22 - A12 * A12;
         float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
                        (float)(2 * win * win);
@@ -338,6 +386,8 @@ static void lk_level(const lk_job* jb) {
             iw10 = cv_round((1.f - a) * b * (1 << W_BITS));
             iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
             int64_t ib1 = 0, ib2 = 0;
+            float fb1 = 0.f, fb2 = 0.f;
+            f4 qb0 = {{0}}, qb1 = {{0}};
             for (int y = 0; y < win; y++) {
                 const uint8_t* Jp = px(J, inx, iny + y);
                 int stepJ = J->pitch;
@@ -346,12 +396,36 @@ static void lk_level(const lk_job* jb) {
                                            Jp[x + stepJ + 1] * iw11,
                                        W_BITS1 - 5) -
                                Iwin[y * win + x];
-                    ib1 += (int64_t)diff * dIwin[(y * win + x) * 2];
-                    ib2 += (int64_t)diff * dIwin[(y * win + x) * 2 + 1];
+                    const int p1 = diff * dIwin[(y * win + x) * 2], p2 = diff * dIwin[(y * win + x) * 2 + 1];
+                    ib1 += p1;
+                    ib2 += p2;
+                    if (x < simd_w) {
+                        /* v_mul_expand of (dx,dy) pairs by (diff,diff): pixels x%4 in {0,1}
+                           feed qb0 lanes (2(x%2), 2(x%2)+1), pixels x%4 in {2,3} feed qb1 */
+                        f4* q = (x & 2) ? &qb1 : &qb0;
+                        q->l[2 * (x & 1)] += (float)p1;
+                        q->l[2 * (x & 1) + 1] += (float)p2;
+                    } else {
+                        fb1 += (float)p1;
+                        fb2 += (float)p2;
+                    }
                 }
             }
-            float b1 = (float)ib1 * FLT_SCALE;
-            float b2 = (float)ib2 * FLT_SCALE;
+            float b1, b2;
+            if (lk_accum == ORC_ACC_EXACT) {
+                b1 = (float)ib1 * FLT_SCALE;
+                b2 = (float)ib2 * FLT_SCALE;
+            } else {
+                if (lk_accum == ORC_ACC_F32X4) {
+                    /* v_recombine(v_interleave_pairs(qb0 + qb1), 0): (l0, l2) -> b1, (l1, l3) -> b2 */
+                    f4 s4;
+                    for (int k = 0; k < 4; k++) s4.l[k] = qb0.l[k] + qb1.l[k];
+                    fb1 += (s4.l[0] + s4.l[2]);
+                    fb2 += (s4.l[1] + s4.l[3]);
+                }
+                b1 = fb1 * FLT_SCALE;
+                b2 = fb2 * FLT_SCALE;
+            }
             float dx = (A12 * b2 - A22 * b1) * D;
             float dy = (A12 * b1 - A11 * b2) * D;
             nextx += dx;

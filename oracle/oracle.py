@@ -124,6 +124,7 @@ def lib():
                                  C.c_double, C.c_double, C.c_int, C.c_int, C.POINTER(KltParams),
                                  C.c_int, C.c_int]
         L.orc_klt_fb.restype = C.c_int
+        L.orc_set_lk_accum.argtypes = [C.c_int]
         L.orc_block_grid_make.argtypes = [C.c_int, C.c_int, C.POINTER(DetectParams), C.POINTER(BlockGrid)]
         L.orc_mask_circles.argtypes = [P, C.c_int, C.c_int, P, C.c_int, C.c_int]
         L.orc_corner_min_eigen_val.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -223,6 +224,26 @@ def calc_optical_flow_pyr_lk(prev, nxt, prev_pts, next_pts=None, params=None, nt
     lib().orc_calc_optical_flow_pyr_lk(_p(prev), _p(nxt), w, h, w, _p(pp), _p(npts), _p(st), _p(err), n,
                                        C.byref(p), nthreads)
     return npts, st, err
+
+
+ACC_EXACT, ACC_F32, ACC_F32X4 = 0, 1, 2
+
+
+class lk_accum:
+    """Context manager selecting LK's window-sum accumulation order (klt.c
+    ORC_ACC_*): the exact int64 default, or OpenCV 4.x's fp32 scalar / 4-lane
+    SIMD orders for the parity-sensitivity experiment."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        lib().orc_set_lk_accum(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_lk_accum(ACC_EXACT)
+        return False
 
 
 def klt_fb(prev, nxt, prev_pts, init_pts, cam_w=None, cam_h=None, fb=0.5, border=5.0, params=None,

@@ -51,7 +51,7 @@ def test_small_factor_rejects_bad_blocks(ctx, gvx_mod):
         ctx.small_factor_eval(7, None, np.zeros(9), [0])
 
 
-@pytest.mark.parametrize("n_kf", [1, 9, 40])
+@pytest.mark.parametrize("n_kf", [1, 2, 4, 9, 40])
 def test_marg_factor_matches_oracle(ctx, orc, n_kf):
     rng = np.random.default_rng(n_kf)
     size = [7, 9] * n_kf + [7, 1]

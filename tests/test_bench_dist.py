@@ -44,3 +44,24 @@ def test_bench_mock_sequence_gather_gloo():
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
     assert json.loads(lines[0])["gathered_ok"] is True
+
+
+def test_bench_spawns_ranks_itself():
+    """`bench.py --gpus 2` with no launcher starts its own 2 ranks (the driver's
+    N-GPU runs and a user's plain invocation give the same job)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mock", "--backend", "gloo", "--gpus", "2",
+           "--steps", "10", "--warmup", "1", "--pairs", "4"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    assert json.loads(lines[0])["n_gpus"] == 2
+
+
+def test_bench_rejects_world_mismatch():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mock", "--gpus", "2"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr

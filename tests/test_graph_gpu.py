@@ -53,3 +53,40 @@ def test_capture_refused_while_profiling(ctx, gvx_mod):
             ctx.capture_begin()
     finally:
         ctx.profile(False)
+
+
+def test_stale_graph_refused(ctx, gvx_mod):
+    """A graph holds raw pointers into the context's scratch: once a larger call
+    reallocates the batch pyramids, replaying it must be refused (not read freed
+    memory)."""
+    import torch
+    from gvx import synth
+    W, H, N = 320, 140, 16
+    dev = torch.device("cuda", 0)
+    params = gvx_mod.KltParams.default()
+
+    def bufs(n):
+        I, J, P, Q = synth.make_batch(n, W, H, N, seed=synth.SEED, distinct=1)
+        d = {k: torch.from_numpy(a).to(dev) for k, a in zip("IJPQ", (I, J, P, Q))}
+        d.update(N=d["Q"].clone(), B=torch.empty_like(d["Q"]), F=torch.zeros((n, N), dtype=torch.uint8, device=dev),
+                 K=torch.zeros((n, N), dtype=torch.int32, device=dev), NK=torch.zeros((n,), dtype=torch.int32, device=dev))
+        return d
+
+    def enqueue(d, n):
+        ctx.klt_fb_batch_dev(n, W, H, d["I"].data_ptr(), d["J"].data_ptr(), N, d["P"].data_ptr(), d["N"].data_ptr(),
+                             d["B"].data_ptr(), d["F"].data_ptr(), d["K"].data_ptr(), d["NK"].data_ptr(),
+                             params=params)
+
+    small, big = bufs(1), bufs(64)
+    enqueue(small, 1)
+    ctx.sync()
+    ctx.capture_begin()
+    enqueue(small, 1)
+    g = ctx.capture_end()
+    g.launch()
+    ctx.sync()
+    enqueue(big, 64)  # grows the batch pyramid scratch: the graph's pointers are freed
+    ctx.sync()
+    with pytest.raises(gvx_mod.GvxError):
+        g.launch()
+    g.destroy()
