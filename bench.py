@@ -145,6 +145,7 @@ def main():
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic pairs (tiled)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pre", action="store_true", help="skip the CLAHE preprocessing leg")
+    ap.add_argument("--no-factors", action="store_true", help="skip the configs[3] factor leg of the default line")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
     ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
@@ -259,6 +260,10 @@ def main():
         collect_once = [torch.empty_like(dNK) for _ in range(world)]
         dist.all_gather(collect_once, dNK)  # results check, outside the timed region
 
+    # the metric's second half (BASELINE.json: factor-Jacobian eval/s), timed in
+    # the same run: configs[3]'s factor batch (its own line under "factors")
+    factors = None if args.no_factors else factor_leg(args, ctx, dev, dist, world, rank,
+                                                      steps=max(10, args.steps // 2), window_extras=False)
     kept_frac = float(dNK.float().mean().item()) / N
     total_pairs = world * Pn * args.steps
     value = total_pairs / elapsed
@@ -311,6 +316,7 @@ def main():
             "preprocess": pre,
             "single_pair": single,
             "host_buffers": pcie,
+            "factors": factors,
         }
         print(json.dumps(line))
     if dist:
@@ -400,16 +406,9 @@ def preprocess_leg(ctx, dI, dJ, Pn, W, H, steps):
 
 
 def factors_main(args):
-    """configs[3]: sliding-window BA factor evaluation (10 keyframes x 200
-    landmarks -> 1800 ReprojectionFactor + 9 Earth PreintegrationFactor with
-    M = 100 IMU samples, SURVEY.md 8d), replicated to >= 2^20 reprojection
-    factors per launch (the window's parameter blocks are shared, read once per
-    batch).  A step = one LM iteration's residual + Jacobian evaluation of the
-    whole batch (reprojection + preintegration factors); preintegration steps/s
-    (9 x replicas segments) are timed separately."""
+    """`--config 4`: the factor leg on its own, as the line's headline."""
     import torch
     import gvx
-    from gvx import synth_ba
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -423,7 +422,25 @@ def factors_main(args):
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ctx = gvx.Context(local)
-    stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
+    line = factor_leg(args, ctx, dev, dist, world, rank, args.steps, window_extras=True)
+    if rank == 0:
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
+    """configs[3]: sliding-window BA factor evaluation (10 keyframes x 200
+    landmarks -> 1800 ReprojectionFactor + 9 Earth PreintegrationFactor with
+    M = 100 IMU samples, SURVEY.md 8d), replicated to >= 2^20 reprojection
+    factors per launch (the window's parameter blocks are shared, read once per
+    batch).  A step = one LM iteration's residual + Jacobian evaluation of the
+    whole batch (reprojection + preintegration factors); preintegration steps/s
+    (9 x replicas segments) are timed separately."""
+    import torch
+    import gvx
+    from gvx import synth_ba
 
     prob = synth_ba.make_ba_problem()
     n_kf = prob["poses"].shape[0]
@@ -505,8 +522,8 @@ def factors_main(args):
         ctx.profile(False)
         return el, fam
 
-    el, fam = timed(step, args.steps)
-    el_i, fam_i = timed(integ, max(1, args.steps // 4))
+    el, fam = timed(step, steps)
+    el_i, fam_i = timed(integ, max(1, steps // 4))
 
     # one window at problem size (1800 + 9 factors, latency-bound): device-pointer
     # launches, and the two-phase FactorSet prepare (block gather, H2D, both
@@ -519,7 +536,7 @@ def factors_main(args):
         ctx.preint_factor_eval_dev(n_kf - 1, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
                                    d_params.data_ptr(), d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr())
 
-    k_w = max(50, args.steps)
+    k_w = max(50, steps)
     el_w, _ = timed(window, k_w)
     # parameter blocks as views of the packed vector (the layout the offsets index)
     starts = sorted({int(v) for v in prob["offs"].ravel()} | {int(v) for v in poffs.ravel()})
@@ -535,18 +552,22 @@ def factors_main(args):
                          np.vectorize(bidx.get)(poffs).astype(np.int32))
     el_p, _ = timed(lambda: fset.prepare(True), k_w)
     fset.close()
-    k_i = max(1, args.steps // 4)
-    evals = world * (n_r + n_p) * args.steps
+    k_i = max(1, steps // 4)
+    evals = world * (n_r + n_p) * steps
     value = evals / el
-    rp_ms = fam["reproj"][0] / args.steps
+    rp_ms = fam["reproj"][0] / steps
+    pf_ms = fam["preint_factor"][0] / steps
+    B_pf = 8 * (16 + 225 + 225 + 4 * M + 7) + 8 * (15 + 15 * 32)  # SURVEY 8d, M = 100: 10,944 B
     B_rp = 15 * 8 + 5 * 4 + 48 * 8  # consts + offsets in, residual + 5 Jacobian blocks out
     achieved = B_rp * n_r / (rp_ms * 1e-3) / 1e9 if rp_ms > 0 else None
+    line = None
     if rank == 0:
-        wf = window_factor_leg(ctx, dev)
+        wf = window_factor_leg(ctx, dev) if window_extras else None
+        pf_achieved = B_pf * n_p / (pf_ms * 1e-3) / 1e9 if pf_ms > 0 else None
         line = {
             "metric": "BA factor-Jacobian evaluations/s (configs[3])",
-            "value": round(value, 1), "unit": "factor evals/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+            "value": round(value, 1), "unit": "factor evals/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(el / steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic sliding window (seed 20261015)",
             "config": {"workload": f"configs[3]: {n_kf} keyframes x 200 landmarks = {n_rp} ReprojectionFactor + "
                                    f"{n_kf - 1} Earth PreintegrationFactor (M={M}), x{reps} windows per launch",
@@ -555,7 +576,12 @@ def factors_main(args):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
                          "algorithmic_bytes_per_factor": B_rp,
-                         "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
+                         "device_ms_per_step": {k: round(v[0] / steps, 4) for k, v in fam.items()}},
+            "preint_factor_roofline": {"bound": "hbm", "kernel": "preint_factor_kernel",
+                                       "achieved": round(pf_achieved, 1) if pf_achieved else None,
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(pf_achieved / HBM_PEAK_GBS, 4) if pf_achieved else None,
+                                       "algorithmic_bytes_per_factor": B_pf},
             "preint_steps_per_s": round(world * S * (M - 1) * k_i / el_i, 1),
             "preint_device_ms_per_launch": round(fam_i["preint"][0] / k_i, 4),
             "problem_size": {"window_factors": n_w,
@@ -573,10 +599,7 @@ def factors_main(args):
                 ref["all_cores_value"] = allc["value"]
                 ref["all_cores_sample"] = allc["sample"]
             line["cpu_baseline"] = ref
-        print(json.dumps(line))
-    if dist:
-        dist.destroy_process_group()
-    ctx.close()
+    return line
 
 
 def window_factor_leg(ctx, dev, reps=20):
@@ -688,36 +711,23 @@ def sequence_main(args):
     frames, _ = synth.make_sequence(W, H, F, dev, seed=synth.SEED + 7919 * rank)
     torch.cuda.synchronize()
     ctx = gvx.Context(local)
+    from gvx.tracking import SequenceTracker
     kp = gvx.KltParams.default(max_level=L)
-    dp = gvx.DetectParams.default(max_features=N)
+    tracker = SequenceTracker(ctx, W, H, N, klt=kp, detect=gvx.DetectParams.default(max_features=N))
     tracks = np.zeros((F, N, 2), np.float32)
     counts = np.zeros(F, np.int32)
     stats = {"detect_frames": 0}
 
-    def frame(t, pts, vel):
-        # Tracking::preprocessing (CLAHE, tracking.cc:139) + the frame's pyramid
-        ctx.frame_preprocess_dev(t % 2, frames[t].data_ptr(), W, H, params=kp)
-        if t > 0 and pts.shape[0]:
-            r = ctx.track_fb((t - 1) % 2, t % 2, pts, pts + vel, W, H, params=kp)
-            k = r["kept_idx"]
-            nxt = r["next"][k]
-            vel = nxt - pts[k]
-            pts = nxt
-        if pts.shape[0] < N:
-            corners, _ = ctx.detect(t % 2, pts, pts, True, int(pts.shape[0]), dp)
-            if corners is not None and corners.shape[0]:
-                add = corners[:N - pts.shape[0]]
-                pts = np.concatenate([pts, add]).astype(np.float32)
-                vel = np.concatenate([vel, np.zeros_like(add)]).astype(np.float32)
+    def frame(t):
+        pts = tracker.step(frames[t].data_ptr())
+        if "corners" in tracker.last:
             stats["detect_frames"] += 1
         tracks[t, :pts.shape[0]] = pts
         counts[t] = pts.shape[0]
-        return pts, vel
 
-    pts, vel = np.zeros((0, 2), np.float32), np.zeros((0, 2), np.float32)
     t = 0
     for _ in range(args.warmup):
-        pts, vel = frame(t, pts, vel)
+        frame(t)
         t += 1
     ctx.sync()
     if dist:
@@ -728,7 +738,7 @@ def sequence_main(args):
     t0 = time.perf_counter()
     timed = 0
     while t < F:
-        pts, vel = frame(t, pts, vel)
+        frame(t)
         t += 1
         timed += 1
     ctx.sync()

@@ -1,0 +1,44 @@
+"""How far LK's window-sum accumulation order can move the tracks (DESIGN.md 2,
+VERDICT r01 item 2).  The restatement and the GPU sum the 21x21 window products
+exactly (int64, one rounding to fp32); OpenCV 4.x sums them in fp32 -- in its
+scalar-loop order (non-SIMD builds, `iA11 += (float)(ixval*ixval)`) or in its
+4-lane CV_SIMD128 order (x86 builds).  oracle/klt.c restates all three
+(orc_set_lk_accum).  On the configs[1] / configs[2] synthetic inputs the measured
+effect (tools/accum_flips.py, profiles/r02_accum_flips.json: 17,600 points per
+mode) is: no status or keep flip, max |dnext| 1.3e-3 px (scalar) / 5.5e-4 px
+(SIMD) and max |dback| 3.0e-3 / 2.6e-3 px.  This test pins that on a small
+sample: a restatement change that makes the exact order drift further from
+OpenCV's fails here."""
+import numpy as np
+
+from gvx import synth
+
+BOUND_PX = 5e-3
+
+
+def test_accumulation_order_effect_is_bounded(orc):
+    p = orc.KltParams.default(max_level=3)
+    flips, dmax, moved, total = 0, 0.0, 0, 0
+    for i in range(4):
+        I, J, P, Q, _ = synth.make_pair(1280, 560, 150, synth.SEED + i)
+        e = orc.klt_fb(I, J, P, Q, params=p, nthreads=4)
+        total += len(P)
+        for mode in (orc.ACC_F32, orc.ACC_F32X4):
+            with orc.lk_accum(mode):
+                f = orc.klt_fb(I, J, P, Q, params=p, nthreads=4)
+            flips += int(np.sum(e["st_f"] != f["st_f"]) + np.sum(e["st_b"] != f["st_b"]) +
+                         np.sum(e["keep"] != f["keep"]))
+            ok = (e["st_f"] > 0) & (e["st_b"] > 0)
+            d = max(np.abs(e["next"][ok] - f["next"][ok]).max(initial=0.0),
+                    np.abs(e["back"][ok] - f["back"][ok]).max(initial=0.0))
+            dmax = max(dmax, float(d))
+            moved += int(np.sum(np.any(e["next"][ok] != f["next"][ok], axis=1)))
+    # the switch really changes the arithmetic, but never a status / keep decision
+    assert flips == 0
+    assert moved > 0
+    assert dmax <= BOUND_PX, f"max |dnext| {dmax:.3e} px"
+    # the default restores the exact order
+    I, J, P, Q, _ = synth.make_pair(1280, 560, 150, synth.SEED)
+    a = orc.klt_fb(I, J, P, Q, params=p)
+    b = orc.klt_fb(I, J, P, Q, params=p)
+    assert np.array_equal(a["next"], b["next"])

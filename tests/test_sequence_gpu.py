@@ -1,0 +1,80 @@
+"""configs[4]: the sequence replay's per-frame loop on the GPU
+against the same loop on the oracle, frame by frame.
+
+Tracking::track's image path (tracking/tracking.cc:107-245): CLAHE (:139) ->
+pyramid -> forward + backward LK with the initial flow (:385, :390) -> FB /
+border / status filter + reduceVector (:396-408, :831-849) -> block-grid
+detection topping the tracks up to track_max_features_ (:220, :576-688).
+gvx.tracking.SequenceTracker runs it on libgvx; `_oracle_sequence` below runs the
+same order on the C restatement.  Per frame the forward/backward flow, status,
+keep flags and kept indices must be bit-exact, and so must the detected corners
+and the resulting track list (the frames are rendered once on the device and
+copied to the host for the oracle)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W, H, N, L = 1280, 560, 150, 3
+
+
+def _oracle_sequence(orc, frames, kp, dp):
+    pts, vel = np.zeros((0, 2), np.float32), np.zeros((0, 2), np.float32)
+    prev_eq = None
+    out = []
+    for t, f in enumerate(frames):
+        eq = orc.clahe(f)
+        rec = {}
+        if t > 0 and pts.shape[0]:
+            r = orc.klt_fb(prev_eq, eq, pts, pts + vel, params=kp)
+            k = r["kept_idx"]
+            nxt = r["next"][k]
+            vel = nxt - pts[k]
+            pts = nxt
+            rec["track"] = r
+        if pts.shape[0] < N:
+            corners, _ = orc.features_detection(eq, pts, pts, True, int(pts.shape[0]), dp)
+            rec["corners"] = corners
+            if corners is not None and corners.shape[0]:
+                add = corners[:N - pts.shape[0]]
+                pts = np.concatenate([pts, add]).astype(np.float32)
+                vel = np.concatenate([vel, np.zeros_like(add)]).astype(np.float32)
+        rec["pts"] = pts.copy()
+        out.append(rec)
+        prev_eq = eq
+    return out
+
+
+@pytest.mark.parametrize("n_frames", [30])
+def test_sequence_replay_bit_exact(ctx, orc, gvx_mod, n_frames):
+    import torch
+    from gvx import synth
+    from gvx.tracking import SequenceTracker
+    dev = torch.device("cuda", 0)
+    frames, _ = synth.make_sequence(W, H, n_frames, dev, seed=synth.SEED)
+    host = frames.cpu().numpy()
+    kp = gvx_mod.KltParams.default(max_level=L)
+    dp = gvx_mod.DetectParams.default(max_features=N)
+    okp = orc.KltParams.default(max_level=L)
+    odp = orc.DetectParams.default() if hasattr(orc.DetectParams, "default") else None
+    ref = _oracle_sequence(orc, host, okp, odp)
+    tr = SequenceTracker(ctx, W, H, N, klt=kp, detect=dp)
+    n_tracked = n_detect = 0
+    for t in range(n_frames):
+        pts = tr.step(frames[t].data_ptr())
+        g, o = tr.last, ref[t]
+        assert ("track" in g) == ("track" in o), f"frame {t}: tracking ran on one side only"
+        if "track" in g:
+            for k in ("next", "back", "st_f", "st_b", "keep", "kept_idx"):
+                assert np.array_equal(g["track"][k], o["track"][k]), f"frame {t}: {k}"
+            n_tracked += len(g["track"]["kept_idx"])
+        assert ("corners" in g) == ("corners" in o), f"frame {t}: detection ran on one side only"
+        if "corners" in g:
+            gc, oc = g["corners"], o["corners"]
+            assert (gc is None) == (oc is None), f"frame {t}: detection early exit differs"
+            if gc is not None:
+                assert np.array_equal(gc, oc), f"frame {t}: corners"
+                n_detect += 1
+        assert np.array_equal(pts, o["pts"]), f"frame {t}: track list"
+    # the sequence exercised both halves of the loop
+    assert n_tracked > 100 * (n_frames - 1) and n_detect >= 2
