@@ -74,7 +74,41 @@ gvx_status gvx_preint_integrate_dev(gvx_ctx* c, int32_t variant, const gvx_imu_p
     prof_begin(c, "preint", &ev);
     hipError_t e = launch_preint(c, variant, *prm, n_seg, d_imu, d_seg_off, d_state0, d_iewn, d_out, d_pn);
     prof_end(c, "preint", ev);
-    return hip_err(c, e, "preint kernel");
+    if (e != hipSuccess) return hip_err(c, e, "preint kernel");
+    prof_begin(c, "sqrt_info", &ev);
+    e = launch_sqrt_info(c, n_seg, d_out);
+    prof_end(c, "sqrt_info", ev);
+    return hip_err(c, e, "sqrt_info kernel");
+}
+
+gvx_status gvx_preint_sqrt_info_dev(gvx_ctx* c, int32_t n, gvx_preint_result* d_pre) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n < 0) return set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (n == 0) return GVX_OK;
+    if (!d_pre) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    hipEvent_t ev{};
+    prof_begin(c, "sqrt_info", &ev);
+    hipError_t e = launch_sqrt_info(c, n, d_pre);
+    prof_end(c, "sqrt_info", ev);
+    return hip_err(c, e, "sqrt_info kernel");
+}
+
+gvx_status gvx_preint_sqrt_info(gvx_ctx* c, int32_t n, gvx_preint_result* pre) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n < 0) return set_err(c, GVX_ERR_INVALID, "n < 0");
+    if (n == 0) return GVX_OK;
+    if (!pre) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    hipSetDevice(c->device);
+    gvx_preint_result* d = (gvx_preint_result*)scratch(c, "sqrt_info", sizeof(gvx_preint_result) * n);
+    if (!d) return set_err(c, GVX_ERR_OOM, "sqrt_info staging");
+    hipError_t e = hipMemcpyAsync(d, pre, sizeof(gvx_preint_result) * n, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "sqrt_info H2D");
+    gvx_status s = gvx_preint_sqrt_info_dev(c, n, d);
+    if (s) return s;
+    e = hipMemcpyAsync(pre, d, sizeof(gvx_preint_result) * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_err(c, e, "sqrt_info D2H");
 }
 
 gvx_status gvx_preint_integrate(gvx_ctx* c, int32_t variant, const gvx_imu_params* prm, int32_t n_seg,
@@ -204,6 +238,10 @@ gvx_status gvx_preint_factor_eval(gvx_ctx* c, int32_t n, const gvx_preint_result
             if (!pn || !pn_off || pn_off[i] < 0 || pn_off[i] + pre[i].m - 1 > n_pn)
                 return set_err(c, GVX_ERR_INVALID, "factor %d: pn list out of range", i);
         }
+        for (int k = 0; k < 15; ++k)
+            if (!(pre[i].sqrt_info[16 * k] > 0.0))
+                return set_err(c, GVX_ERR_INVALID,
+                               "factor %d: sqrt_info not formed (gvx_preint_integrate or gvx_preint_sqrt_info)", i);
         const int sz[4] = {7, 9, 7, 9};
         for (int k = 0; k < 4; ++k)
             if (offs[4 * i + k] < 0 || offs[4 * i + k] + sz[k] > n_params)

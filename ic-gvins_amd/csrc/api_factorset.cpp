@@ -163,6 +163,9 @@ gvx_status gvx_factor_set_create(gvx_ctx* c, int32_t n_blocks, const double* con
             e = hipMemsetAsync(s->d_pn_off, 0, sizeof(int32_t) * n_preint, c->stream);
         }
         if (e == hipSuccess) e = hipMemcpyAsync(s->d_poffs, poffs.data(), sz[5], hipMemcpyHostToDevice, c->stream);
+        // sqrt_information_ once per factor for the set's lifetime (the
+        // reference recomputes it in every Evaluate; same bits)
+        if (e == hipSuccess) e = launch_sqrt_info(c, n_preint, s->d_pre);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {

@@ -8,12 +8,13 @@
 // Reprojection: one lane per factor; parameter blocks are gathered through the
 // per-factor offset table (the Ceres parameter-block pointers), outputs are
 // staged through LDS so that the 46-double Jacobian rows leave as coalesced
-// stores.  Preintegration: one wavefront per factor; the reference recomputes
-// sqrt_information_ = LLT(P^-1)^T on every call (quirk),
-// done here with a partial-pivot LU, axpy-form substitutions and the
-// left-looking LLT spread over the lanes in LDS, each entry updated in the same
-// k order as the sequential CPU restatement.
+// stores.  Preintegration: 16 lanes per factor (preint_factor_kernel); the
+// reference's per-call sqrt_information_ = LLT(P^-1)^T (quirk, SURVEY.md App.
+// C.2) is formed once per segment by sqrt_info_kernel with the same arithmetic.
 #include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdlib>
 
 #include "dmath.h"
 #include "gvx_internal.h"
@@ -181,23 +182,22 @@ __device__ __forceinline__ void set3(double* J, int ld, int r, int c, const doub
         for (int j = 0; j < 3; ++j) J[(r + i) * ld + c + j] = B[3 * i + j];
 }
 
-__global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
-                                                           const double* __restrict__ pn,
-                                                           const int32_t* __restrict__ pn_off,
-                                                           const double* __restrict__ params,
-                                                           const int32_t* __restrict__ offs,
-                                                           double* __restrict__ res,
-                                                           double* __restrict__ jac) {
+// sqrt_information_ = LLT(covariance_.inverse()).matrixL().transpose()
+// (preintegration_earth.cc:39-40; the Normal variant likewise), one wavefront
+// per segment: partial-pivot LU, axpy-form substitutions for the inverse and
+// the left-looking unblocked LLT spread over the lanes in LDS, each entry
+// updated in the same k order as the sequential CPU restatement.  The reference
+// recomputes it inside every Evaluate; it depends on covariance_ alone, so it is
+// formed once here (after integration / at factor-set creation) with the same
+// arithmetic and stored upper triangular in gvx_preint_result::sqrt_info.
+__global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result* __restrict__ pre) {
     __shared__ double A[NS * NS];   // LU
     __shared__ double X[NS * NS];   // inverse, then Cholesky factor
-    __shared__ double Jr[NS * 32];  // raw (un-whitened) Jacobians [J0 7 | J1 9 | J2 7 | J3 9]
-    __shared__ double rr[NS];
     __shared__ int perm[NS];
     const int fi = blockIdx.x;
     if (fi >= n) return;
     const int lane = threadIdx.x;
-    const gvx_preint_result* s = pre + fi;
-    const bool earth = s->variant == GVX_PREINT_EARTH;
+    gvx_preint_result* s = pre + fi;
 
     // ---- sqrt_information_ = LLT(covariance_.inverse()).matrixL().transpose() ----
     for (int e = lane; e < NS * NS; e += 64) A[e] = s->covariance[e];
@@ -282,14 +282,60 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
         __syncthreads();
     }
     // sqrt_info[i][j] = L[j][i] for j >= i  (upper triangular)
+    __syncthreads();
+    for (int e = lane; e < NS * NS; e += 64) {
+        const int i = e / NS, j = e - i * NS;
+        s->sqrt_info[e] = j >= i ? X[j * NS + i] : 0.0;
+    }
+}
 
-    // ---- residual and raw Jacobian blocks (uniform, every lane) ----
+// One factor per 16-lane group, 4 factors per 64-lane workgroup (one wave).
+// The residual and the raw Jacobian blocks are uniform per factor: the group's
+// lanes compute them together (one instruction stream for the wave's four
+// factors) and lane 0 of the group stores them into the group's LDS tile
+// Jr[15][33] (32 Jacobian columns [J0 7 | J1 9 | J2 7 | J3 9] + the residual).
+// The Earth position-correction sum over pn_ runs on lanes 0..2, one
+// component each, in the reference's order.  Whitening: lane i < 15 holds row
+// i of sqrt_info (upper triangular, formed once per segment by
+// sqrt_info_kernel) in registers and forms row i of sqrt_info * [Jr | r]
+// column by column (the k >= i terms in ascending k, the oracle's order),
+// writing it back in place; the wave then stores its four factors' residuals
+// and Jacobians as contiguous coalesced runs.
+// Measured (configs[3], 5,247 factors, M = 100): 47 us per launch, ~85k cycles
+// per wave of which ~38k wait on memory; the uniform per-factor chain, not
+// bandwidth, bounds it (column-wise whitening with sqrt_info in LDS: 65 us at
+// one wave/SIMD; 10 lanes per factor, 875 waves: 46 us; LDS-staged inputs:
+// 61 us; pn_ through LDS chunks: 50 us; pn_ as per-lane partial sums + butterfly
+// (one wave/SIMD): 57 us).
+constexpr int PF_L = 16;                 // lanes per factor (>= 15: one sqrt_info row per lane)
+constexpr int PF_GROUPS = 64 / PF_L;     // factors per workgroup (one wave)
+constexpr int PF_SLOTS = (64 + PF_L - 1) / PF_L;  // groups incl. a partial one (idle lanes)
+constexpr int PF_LD = 33;                // tile row: 32 Jacobian columns + the residual
+
+__global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
+                                                           const double* __restrict__ pn,
+                                                           const int32_t* __restrict__ pn_off,
+                                                           const double* __restrict__ params,
+                                                           const int32_t* __restrict__ offs,
+                                                           double* __restrict__ res,
+                                                           double* __restrict__ jac) {
+    __shared__ double tile[PF_SLOTS * NS * PF_LD];
+    const int grp = threadIdx.x / PF_L, lane = threadIdx.x % PF_L;
+    const int f0 = blockIdx.x * PF_GROUPS;
+    // dead groups (past n, or the partial group) recompute a valid factor and store nothing
+    const int fi = min(f0 + min(grp, PF_GROUPS - 1), n - 1);
+    double* Jr = tile + grp * NS * PF_LD;
+    const gvx_preint_result* s = pre + fi;
+    const bool earth = s->variant == GVX_PREINT_EARTH;
+    for (int e = lane; e < NS * PF_LD; e += PF_L) Jr[e] = 0.0;
+    __syncthreads();
     const int32_t* o = offs + 4 * (int64_t)fi;
     const double *ps0 = params + o[0], *m0 = params + o[1], *ps1 = params + o[2], *m1 = params + o[3];
     const dq q0 = dq_make(ps0[6], ps0[3], ps0[4], ps0[5]);
     const dq q1 = dq_make(ps1[6], ps1[3], ps1[4], ps1[5]);
     const double *p0 = ps0, *p1 = ps1, *v0 = m0, *v1 = m1;
     const double *bg0 = m0 + 3, *ba0 = m0 + 6, *bg1 = m1 + 3, *ba1 = m1 + 6;
+    // ---- residual and raw Jacobian blocks (uniform over the group) ----
     const double dtt = s->delta_time;
     const double* Jc = s->jacobian;
     double dp_dbg[9], dp_dba[9], dv_dbg[9], dv_dba[9], dq_dbg[9];
@@ -320,16 +366,25 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     double cnb0[9], M[9], N[9];
     dq_rot(q0i, cnb0);
     double r[NS];
-    for (int e = lane; e < NS * 32; e += 64) Jr[e] = 0.0;
-    __syncthreads();
-    const bool w0 = lane == 0;  // lane 0 writes the uniform blocks
+    const bool w0 = lane == 0;  // lane 0 of the group writes the uniform blocks
     if (earth) {
         double S[9], S2[9];
         skew(s->iewn, S);
-        double pc[3] = {0, 0, 0};
-        const double* pl = pn + 4 * (int64_t)pn_off[fi];
-        for (int k = 0; k < s->m - 1; ++k)
-            for (int i = 0; i < 3; ++i) pc[i] = pc[i] + (pl[4 * k + 1 + i] - p0[i]) * pl[4 * k];
+        // p_cor += (pn.second - state0.p) * pn.first over pn_, in the reference's
+        // order: component c on lane c of the group, then broadcast
+        double pcc = 0.0;
+        {
+            const double* pl = pn + 4 * (int64_t)pn_off[fi];
+            const int c = lane < 3 ? lane : 0;
+            const double p0c = p0[c];
+            const int m1n = s->m - 1;
+            if (lane < 3) {
+#pragma unroll 8
+                for (int k = 0; k < m1n; ++k) pcc = pcc + (pl[4 * k + 1 + c] - p0c) * pl[4 * k];
+            }
+        }
+        const int gl = threadIdx.x - lane;
+        double pc[3] = {__shfl(pcc, gl, 64), __shfl(pcc, gl + 1, 64), __shfl(pcc, gl + 2, 64)};
         for (int i = 0; i < 9; ++i) S2[i] = 2.0 * S[i];
         mv3(S2, pc, pc);
         double dp[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]}, vc[3];
@@ -355,30 +410,30 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
             for (int i = 0; i < 9; ++i) C2[i] = 2.0 * cnb0[i];
             mm3(C2, S, M);
             for (int i = 0; i < 9; ++i) N[i] = -cnb0[i] - M[i] * dtt;
-            set3(Jr, 32, 0, 0, N);
+            set3(Jr, PF_LD, 0, 0, N);
             mv3(cnb0, dpn, t);
             skew(t, N);
-            set3(Jr, 32, 0, 3, N);
+            set3(Jr, PF_LD, 0, 3, N);
             for (int i = 0; i < 9; ++i) C2[i] = -2.0 * cnb0[i];
             mm3(C2, S, N);
-            set3(Jr, 32, 3, 0, N);
+            set3(Jr, PF_LD, 3, 0, N);
             mv3(cnb0, dvn, t);
             skew(t, N);
-            set3(Jr, 32, 3, 3, N);
+            set3(Jr, PF_LD, 3, 3, N);
             qlr_br(qb0b1, cq, N);
-            set3(Jr, 32, 6, 3, N);
+            set3(Jr, PF_LD, 6, 3, N);
             // pose1 (columns 16..22)
-            set3(Jr, 32, 0, 16, cnb0);
+            set3(Jr, PF_LD, 0, 16, cnb0);
             for (int i = 0; i < 9; ++i) C2[i] = 2.0 * cnb0[i];
             mm3(C2, S, N);
-            set3(Jr, 32, 3, 16, N);
+            set3(Jr, PF_LD, 3, 16, N);
             qright_br(dq_mul(qb0b1, cq), N);
             for (int i = 0; i < 9; ++i) N[i] = -N[i];
-            set3(Jr, 32, 6, 19, N);
+            set3(Jr, PF_LD, 6, 19, N);
             // mix0 (columns 7..15)
             qleft_br(dq_mul(qb0b1, dqd), M);
             mm3(M, dq_dbg, N);
-            set3(Jr, 32, 6, 10, N);
+            set3(Jr, PF_LD, 6, 10, N);
         }
     } else {
         double dp[3], dv[3], rp[3], rv[3];
@@ -398,21 +453,21 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
         r[8] = 2 * e.z;
         if (jac && w0) {
             for (int i = 0; i < 9; ++i) N[i] = -cnb0[i];
-            set3(Jr, 32, 0, 0, N);
+            set3(Jr, PF_LD, 0, 0, N);
             skew(rp, N);
-            set3(Jr, 32, 0, 3, N);
+            set3(Jr, PF_LD, 0, 3, N);
             skew(rv, N);
-            set3(Jr, 32, 3, 3, N);
+            set3(Jr, PF_LD, 3, 3, N);
             qlr_br(dq_mul(dq_inv(q1), q0), cq, N);
             for (int i = 0; i < 9; ++i) N[i] = -N[i];
-            set3(Jr, 32, 6, 3, N);
-            set3(Jr, 32, 0, 16, cnb0);
+            set3(Jr, PF_LD, 6, 3, N);
+            set3(Jr, PF_LD, 0, 16, cnb0);
             qleft_br(e, N);
-            set3(Jr, 32, 6, 19, N);
+            set3(Jr, PF_LD, 6, 19, N);
             qleft_br(dq_mul(dq_mul(dq_inv(q1), q0), dqd), M);
             for (int i = 0; i < 9; ++i) M[i] = -M[i];
             mm3(M, dq_dbg, N);
-            set3(Jr, 32, 6, 10, N);
+            set3(Jr, PF_LD, 6, 10, N);
         }
     }
     for (int i = 0; i < 3; ++i) {
@@ -422,48 +477,61 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     if (jac && w0) {
         // common mix0 / mix1 blocks
         for (int i = 0; i < 9; ++i) N[i] = -cnb0[i] * dtt;
-        set3(Jr, 32, 0, 7, N);
+        set3(Jr, PF_LD, 0, 7, N);
         for (int i = 0; i < 9; ++i) N[i] = -dp_dbg[i];
-        set3(Jr, 32, 0, 10, N);
+        set3(Jr, PF_LD, 0, 10, N);
         for (int i = 0; i < 9; ++i) N[i] = -dp_dba[i];
-        set3(Jr, 32, 0, 13, N);
+        set3(Jr, PF_LD, 0, 13, N);
         for (int i = 0; i < 9; ++i) N[i] = -cnb0[i];
-        set3(Jr, 32, 3, 7, N);
+        set3(Jr, PF_LD, 3, 7, N);
         for (int i = 0; i < 9; ++i) N[i] = -dv_dbg[i];
-        set3(Jr, 32, 3, 10, N);
+        set3(Jr, PF_LD, 3, 10, N);
         for (int i = 0; i < 9; ++i) N[i] = -dv_dba[i];
-        set3(Jr, 32, 3, 13, N);
+        set3(Jr, PF_LD, 3, 13, N);
         for (int i = 0; i < 3; ++i) {
-            Jr[(9 + i) * 32 + 10 + i] = -1.0;
-            Jr[(12 + i) * 32 + 13 + i] = -1.0;
-            Jr[(9 + i) * 32 + 26 + i] = 1.0;
-            Jr[(12 + i) * 32 + 29 + i] = 1.0;
+            Jr[(9 + i) * PF_LD + 10 + i] = -1.0;
+            Jr[(12 + i) * PF_LD + 13 + i] = -1.0;
+            Jr[(9 + i) * PF_LD + 26 + i] = 1.0;
+            Jr[(12 + i) * PF_LD + 29 + i] = 1.0;
         }
-        set3(Jr, 32, 3, 23, cnb0);
+        set3(Jr, PF_LD, 3, 23, cnb0);
     }
     if (w0)
-        for (int i = 0; i < NS; ++i) rr[i] = r[i];
+        for (int i = 0; i < NS; ++i) Jr[i * PF_LD + 32] = r[i];
     __syncthreads();
-    // ---- whitening: sqrt_info (upper, = L^T) times residual / Jacobians ----
-    if (lane < NS) {
-        const int i = lane;
-        double sacc = X[i * NS + i] * rr[i];
-        for (int k = i + 1; k < NS; ++k) sacc = sacc + X[k * NS + i] * rr[k];
-        res[(int64_t)fi * NS + i] = sacc;
+    // ---- whitening: row `lane` of sqrt_info * [Jr | r], in place ----
+    double srow[NS];  // row `lane` of sqrt_info (upper triangular)
+#pragma unroll
+    for (int k = 0; k < NS; ++k) srow[k] = (lane < NS && k >= lane) ? s->sqrt_info[lane * NS + k] : 0.0;
+    const int ncol = jac ? PF_LD : 1;
+#pragma unroll 1
+    for (int cc = 0; cc < ncol; ++cc) {
+        const int col = jac ? cc : 32;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const double t = srow[k] * Jr[k * PF_LD + col];
+            acc = k == lane ? t : (k > lane ? acc + t : acc);
+        }
+        if (lane < NS) Jr[lane * PF_LD + col] = acc;
+    }
+    __syncthreads();
+    // ---- coalesced stores of the workgroup's factors ----
+    const int nf = min(PF_GROUPS, n - f0);
+    for (int e = threadIdx.x; e < nf * NS; e += 64) {
+        const int f = e / NS, i = e - f * NS;
+        res[(int64_t)f0 * NS + e] = tile[f * NS * PF_LD + i * PF_LD + 32];
     }
     if (jac) {
-        double* jo = jac + (int64_t)fi * 480;
-        // output layout [J0 15x7 | J1 15x9 | J2 15x7 | J3 15x9], Jr columns [0..7 | 7..16 | 16..23 | 23..32]
-        for (int e = lane; e < NS * 32; e += 64) {
-            int blk, i, c, col;
-            if (e < 105) { blk = 0; i = e / 7; c = e % 7; col = c; }
-            else if (e < 240) { blk = 105; i = (e - 105) / 9; c = (e - 105) % 9; col = 7 + c; }
-            else if (e < 345) { blk = 240; i = (e - 240) / 7; c = (e - 240) % 7; col = 16 + c; }
-            else { blk = 345; i = (e - 345) / 9; c = (e - 345) % 9; col = 23 + c; }
-            (void)blk;
-            double sacc = X[i * NS + i] * Jr[i * 32 + col];
-            for (int k = i + 1; k < NS; ++k) sacc = sacc + X[k * NS + i] * Jr[k * 32 + col];
-            jo[e] = sacc;
+        // per factor [J0 15x7 | J1 15x9 | J2 15x7 | J3 15x9], Jr columns [0..7 | 7..16 | 16..23 | 23..32]
+        for (int e = threadIdx.x; e < nf * 480; e += 64) {
+            const int f = e / 480, q = e - f * 480;
+            int i, col;
+            if (q < 105) { i = q / 7; col = q - 7 * i; }
+            else if (q < 240) { i = (q - 105) / 9; col = 7 + (q - 105) - 9 * i; }
+            else if (q < 345) { i = (q - 240) / 7; col = 16 + (q - 240) - 7 * i; }
+            else { i = (q - 345) / 9; col = 23 + (q - 345) - 9 * i; }
+            jac[(int64_t)f0 * 480 + e] = tile[f * NS * PF_LD + i * PF_LD + col];
         }
     }
 }
@@ -482,8 +550,14 @@ hipError_t launch_preint_factor(gvx_ctx* c, int n, const gvx_preint_result* pre,
                                 const int32_t* pn_off, const double* params, const int32_t* offs,
                                 double* res, double* jac) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(preint_factor_kernel, dim3(n), dim3(64), 0, c->stream, n, pre, pn, pn_off, params,
-                       offs, res, jac);
+    hipLaunchKernelGGL(preint_factor_kernel, dim3((n + PF_GROUPS - 1) / PF_GROUPS), dim3(64), 0, c->stream, n, pre,
+                       pn, pn_off, params, offs, res, jac);
+    return hipGetLastError();
+}
+
+hipError_t launch_sqrt_info(gvx_ctx* c, int n, gvx_preint_result* pre) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sqrt_info_kernel, dim3(n), dim3(64), 0, c->stream, n, pre);
     return hipGetLastError();
 }
 

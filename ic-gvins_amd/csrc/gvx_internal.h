@@ -186,6 +186,7 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                          const double* iewn, gvx_preint_result* out, double* pn);
 hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
                          const int32_t* offs, double* res, double* jac);
+hipError_t launch_sqrt_info(gvx_ctx* c, int n, gvx_preint_result* pre);
 hipError_t launch_preint_factor(gvx_ctx* c, int n, const gvx_preint_result* pre, const double* pn,
                                 const int32_t* pn_off, const double* params, const int32_t* offs,
                                 double* res, double* jac);

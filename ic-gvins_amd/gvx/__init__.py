@@ -50,7 +50,8 @@ STATE_DTYPE = np.dtype([("time", "f8"), ("p", "f8", 3), ("q", "f8", 4), ("v", "f
 PREINT_DTYPE = np.dtype([("variant", "i4"), ("m", "i4"), ("delta_time", "f8"), ("start_time", "f8"),
                          ("end_time", "f8"), ("current", STATE_DTYPE), ("delta", STATE_DTYPE),
                          ("gravity", "f8", 3), ("iewn", "f8", 3), ("q0", "f8", 4),
-                         ("jacobian", "f8", 225), ("covariance", "f8", 225)], align=True)
+                         ("jacobian", "f8", 225), ("covariance", "f8", 225),
+                         ("sqrt_info", "f8", 225)], align=True)
 REPROJ_DTYPE = np.dtype([("pts0", "f8", 3), ("pts1", "f8", 3), ("vel0", "f8", 3), ("vel1", "f8", 3),
                          ("td0", "f8"), ("td1", "f8"), ("std", "f8")], align=True)
 

@@ -285,7 +285,14 @@ typedef struct {
 
 /* A PreintegrationBase after its segment: deltaState(), currentState(),
    deltaTime(), jacobian_, covariance_ (row-major 15x15), plus what the Earth
-   variant's evaluate() needs (iewn_, gravity_). */
+   variant's evaluate() needs (iewn_, gravity_).  sqrt_info is
+   sqrt_information_ = LLT(covariance_^-1).matrixL().transpose() (row-major,
+   upper triangular): the reference recomputes it inside every
+   PreintegrationFactor::Evaluate (preintegration_earth.cc:39-40,
+   preintegration_normal.cc), but it depends on covariance_ alone, so
+   gvx_preint_integrate[_dev] forms it once per segment with the same
+   arithmetic (identical bits) and the factor kernels read it.  A result built
+   by other means must pass through gvx_preint_sqrt_info[_dev] first. */
 typedef struct {
     int32_t variant, m; /* m = imu_buffer_.size() */
     double delta_time, start_time, end_time;
@@ -293,7 +300,14 @@ typedef struct {
     double gravity[3], iewn[3], q0[4];
     double jacobian[225];
     double covariance[225];
+    double sqrt_info[225];
 } gvx_preint_result;
+
+/* (Re)compute pre[i].sqrt_info from pre[i].covariance for n results in place
+   (partial-pivot LU inverse, then Eigen's unblocked LLT; one wavefront per
+   result).  Called by gvx_preint_integrate[_dev] and gvx_factor_set_create. */
+gvx_status gvx_preint_sqrt_info(gvx_ctx* ctx, int32_t n, gvx_preint_result* pre);
+gvx_status gvx_preint_sqrt_info_dev(gvx_ctx* ctx, int32_t n, gvx_preint_result* d_pre);
 
 /* Preintegration::createPreintegration + addNewImu(series[k]), k = 1..m-1
    (ic_gvins.cc:946-953, preintegration_base.cc:72-75), batched over segments:
@@ -389,7 +403,9 @@ gvx_status gvx_imu_series_from_to(const gvx_imu* imu, int32_t n, double start, d
    params + offs[4i+k] (params holds n_params doubles) (k:
    pose0[7], mix0[9], pose1[7], mix1[9]).  residuals n x 15; jacobians (may be
    NULL) n x 480 doubles = [J_pose0 15x7 | J_mix0 15x9 | J_pose1 15x7 |
-   J_mix1 15x9], each row-major like Ceres. */
+   J_mix1 15x9], each row-major like Ceres.  pre[i].sqrt_info must be filled
+   (gvx_preint_integrate does; otherwise gvx_preint_sqrt_info): the host entry
+   refuses a result whose sqrt_info diagonal is not positive. */
 gvx_status gvx_preint_factor_eval(gvx_ctx* ctx, int32_t n, const gvx_preint_result* pre,
                                   const double* pn, int32_t n_pn, const int32_t* pn_off,
                                   const double* params, int32_t n_params, const int32_t* offs,

@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Per-dispatch PMC values of one kernel (largest grid) from a rocprofv3 --pmc
+output directory, per wave, with the gfx950 quad-cycle correction for SQ_*CYCLES
+/ SQ_WAIT_* / SQ_ACTIVE_INST_* (MI355X_MICROARCH.md).
+    python3 tools/pmc_kernel.py <dir> <kernel-substring>"""
+import collections
+import csv
+import glob
+import sys
+
+root, name = sys.argv[1], sys.argv[2]
+acc = collections.defaultdict(dict)
+for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if name not in r["Kernel_Name"]:
+            continue
+        key = (int(r["Grid_Size"]), r["Dispatch_Id"])
+        acc[key][r["Counter_Name"]] = acc[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+if not acc:
+    sys.exit(f"no dispatch of {name}")
+grid = max(k[0] for k in acc)
+rows = [v for k, v in acc.items() if k[0] == grid]
+avg = {c: sum(r.get(c, 0.0) for r in rows) / len(rows) for c in rows[0]}
+waves = avg.get("SQ_WAVES", 0.0)
+print(f"{name}: grid {grid}, {len(rows)} dispatches")
+for c in sorted(avg):
+    v = avg[c]
+    scale = 4 if ("CYCLES" in c or c.startswith("SQ_WAIT") or c.startswith("SQ_ACTIVE_INST")) and c != "SQ_BUSY_CYCLES" else 1
+    per = f"  per wave {v * scale / waves:.4g}" if waves and c != "SQ_WAVES" else ""
+    print(f"  {c:28s} {v:.4g}{per}")
