@@ -166,6 +166,33 @@ hipError_t launch_small_factor(gvx_ctx* c, int kind, int n, const double* consts
 hipError_t launch_marg_factor(gvx_ctx* c, int r, int nb, const int32_t* blk, const double* x0, const double* x,
                               const double* J0, const double* e0, double* residuals, double* jacobians);
 
+// ---- marg.hip ----
+constexpr int GVX_EIG_MAX_N = 512;  // largest SelfAdjointEigenSolver the one-workgroup kernel takes
+// One lower block pair (row block P at row0, column block Q at col0) of H0, or
+// (col0 = -1, lq = 1) one block of b0; its contributions are contrib[c0 .. c1).
+struct MargPairRec {
+    int32_t row0, col0, lp, lq, c0, c1;
+};
+struct MargLaunch {
+    int n_pairs, n_bvec;              // H0 records first, then the b0 records
+    const MargPairRec* pairs;         // device
+    const int4* contrib;              // device
+    int n_fac;
+    const int32_t* nres;              // device (loss only)
+    const int64_t* res_off;           // device (loss only)
+    const double* loss;               // device, nullable
+    double* sr;                       // device scratch [n_fac]
+    const double* data;               // device: the evaluated residual blocks
+    int L, m;
+    double *H0, *b0, *V1, *w1, *Hinv, *T, *Hp, *bp, *V2, *w2, *hc;
+    int* info;                        // device [2]: Hmm and Hp eigen-solver status
+    double *J0, *e0;
+};
+hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p);
+// SelfAdjointEigenSolver of the lower triangle of src (ld lds): V n x n, w n, hc n scratch, info 1 int
+hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc,
+                            int* info);
+
 // ---- ins.hip ----
 hipError_t launch_ins(gvx_ctx* c, const gvx_ins_config& cfg, int n_chain, const gvx_imu* imu, const int32_t* off,
                       const gvx_state* state0, gvx_state* states);

@@ -192,6 +192,9 @@ def _declare(L):
         "gvx_small_factor_eval": (i32, [P, i32, i32, P, P, i32, P, P, P]),
         "gvx_small_factor_eval_dev": (i32, [P, i32, i32, P, P, P, P, P]),
         "gvx_marg_factor_eval": (i32, [P, i32, i32, P, P, P, i32, P, P, P, P, P, P]),
+        "gvx_marginalize": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
+        "gvx_marginalize_dev": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
+        "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
         "gvx_capture_begin": (i32, [P]),
         "gvx_capture_end": (i32, [P, C.POINTER(P)]),
         "gvx_graph_launch": (i32, [P, P]),
@@ -587,6 +590,53 @@ class Context:
                                                  _ptr(x), _ptr(J), _ptr(e), _ptr(res), _ptr(jac)),
                     "gvx_marg_factor_eval")
         return res, jac
+
+    # ---------------------------------------------------- marginalisation
+    @staticmethod
+    def _marg_struct(p):
+        return (np.ascontiguousarray(p["nres"], np.int32), np.ascontiguousarray(p["blk_off"], np.int32),
+                np.ascontiguousarray(p["blk"], np.int32), np.ascontiguousarray(p["res_off"], np.int64),
+                np.ascontiguousarray(p["jac_off"], np.int64), np.ascontiguousarray(p["size"], np.int32),
+                np.ascontiguousarray(p["index"], np.int32), int(p["m"]), int(p["L"]))
+
+    def marginalize(self, p):
+        """MarginalizationInfo::marginalization() after preMarginalization on a
+        problem dict (gvx.synth_ba.marg_problem) -> dict(J0 [r, r], e0, Hp [r, r],
+        bp, eval, info [2])."""
+        nres, boff, blk, roff, joff, size, index, m, L = self._marg_struct(p)
+        data = np.ascontiguousarray(p["data"], np.float64)
+        loss = p.get("loss")
+        loss = None if loss is None else np.ascontiguousarray(loss, np.float64)
+        r = L - m
+        J0, Hp = np.zeros(max(r * r, 1)), np.zeros(max(r * r, 1))
+        e0, bp, ev = np.zeros(max(r, 1)), np.zeros(max(r, 1)), np.zeros(max(r, 1))
+        info = np.zeros(2, np.int32)
+        self._check(self._L.gvx_marginalize(self._h, nres.size, _ptr(nres), _ptr(boff), _ptr(blk), _ptr(roff),
+                                            _ptr(joff), _ptr(data), data.size, _ptr(loss), size.size, _ptr(size),
+                                            _ptr(index), m, L, _ptr(J0), _ptr(e0), _ptr(Hp), _ptr(bp), _ptr(ev),
+                                            _ptr(info)), "gvx_marginalize")
+        cm = lambda a: a[:r * r].reshape(r, r).T.copy()  # column-major -> (r, r)
+        return dict(J0=cm(J0), e0=e0[:r], Hp=cm(Hp), bp=bp[:r], eval=ev[:r], info=info)
+
+    def marginalize_dev(self, p, d_data, d_J0, d_e0, d_Hp=None, d_bp=None, d_eval=None, d_info=None, d_loss=None):
+        """Device-pointer marginalisation, async on the context stream (structure from p)."""
+        nres, boff, blk, roff, joff, size, index, m, L = self._marg_struct(p)
+        n_data = int(p["n_data"]) if "n_data" in p else int(np.asarray(p["data"]).size)
+        self._check(self._L.gvx_marginalize_dev(self._h, nres.size, _ptr(nres), _ptr(boff), _ptr(blk), _ptr(roff),
+                                                _ptr(joff), d_data, n_data, d_loss, size.size, _ptr(size),
+                                                _ptr(index), m, L, d_J0, d_e0, d_Hp, d_bp, d_eval, d_info),
+                    "gvx_marginalize_dev")
+
+    def sym_eigen(self, A):
+        """Eigen::SelfAdjointEigenSolver on the device (lower triangle of A) ->
+        (eigenvalues ascending, eigenvectors as columns, info)."""
+        A = np.asarray(A, np.float64)
+        n = A.shape[0]
+        a = np.ascontiguousarray(A.T)
+        w, V = np.zeros(max(n, 1)), np.zeros(max(n * n, 1))
+        info = C.c_int32(0)
+        self._check(self._L.gvx_sym_eigen(self._h, n, _ptr(a), n, _ptr(w), _ptr(V), C.byref(info)), "gvx_sym_eigen")
+        return w[:n], V[:n * n].reshape(n, n).T.copy(), int(info.value)
 
     # ---------------------------------------------------- INS mechanization
     def ins_propagate(self, cfg: InsConfig, chains, states0):

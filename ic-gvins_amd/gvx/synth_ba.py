@@ -131,3 +131,148 @@ def make_ba_problem(seed=20261015, n_kf=10, n_lm=200, dt_kf=0.5):
     offs = np.array([[o_pose + 7 * a, o_pose + 7 * b, o_ext, o_id + j, o_td] for a, b, _, j, _ in offs],
                     np.int32)
     return dict(params=params, offs=offs, consts=consts, poses=poses, ext=ext, invdepth=invdepth)
+
+
+def _pose_block_values(rng, n):
+    q = np.array([quat_from_rotvec(rng.normal(0, 0.3, 3)) for _ in range(n)])
+    return np.concatenate([rng.normal(0, 10, (n, 3)), q / np.linalg.norm(q, axis=1, keepdims=True)], axis=1)
+
+
+def make_marg_problem(ev, seed=20261015, n_kf=10, n_lm=200, n_prior_kf=None, gnss=True, huber=None):
+    """MarginalizationInfo input when the oldest keyframe leaves the window, in
+    the order IC-GVINS adds the residual blocks (ic_gvins.cc:1514-1644):
+      1. the previous MarginalizationFactor over pose/mix of keyframes
+         0..n_prior_kf-1 + extrinsic + td (marginalized: pose0, mix0),
+      2. a GnssFactor on pose0,
+      3. the PreintegrationFactor 0 -> 1 (Earth variant, M = 100; marginalized: pose0, mix0),
+      4. the ReprojectionFactors of the landmarks referenced in keyframe 0, observed in
+         keyframes 1..n_kf-1 (the configs[3] window; marginalized: pose0, invdepth),
+    each evaluated by `ev` (an object with reproj / preint / gnss / marg methods:
+    the oracle in tests, the device in the benchmark).  huber: HuberLoss parameter
+    for the reprojection blocks (the reference passes nullptr, i.e. None).
+    Marginalized blocks get the first local indices (pose0, mix0, invdepths), the
+    remained ones follow in block order.  Returns the dict gvx.Context.marginalize
+    and oracle.marg_construct take."""
+    rng = np.random.default_rng(seed)
+    n_prior_kf = n_kf if n_prior_kf is None else n_prior_kf
+    ba = make_ba_problem(seed, n_kf, n_lm)
+    poses, ext, invd = ba["poses"], ba["ext"], ba["invdepth"]
+    mixes = np.concatenate([np.tile([5.0, 0.0, 0.0], (n_kf, 1)) + rng.normal(0, 0.1, (n_kf, 3)),
+                            rng.normal(0, CFG_GBSTD * D2R / 3600.0, (n_kf, 3)),
+                            rng.normal(0, CFG_ABSTD * 1e-5, (n_kf, 3))], axis=1)
+    # block table: pose k, mix k, ext, td, invdepth j
+    names, size, vals = [], [], []
+    for k in range(n_kf):
+        names += [f"pose{k}", f"mix{k}"]
+        size += [7, 9]
+        vals += [poses[k], mixes[k]]
+    names += ["ext", "td"]
+    size += [7, 1]
+    vals += [ext, np.zeros(1)]
+    for j in range(n_lm):
+        names.append(f"invdepth{j}")
+        size.append(1)
+        vals.append(invd[j:j + 1])
+    bid = {n: i for i, n in enumerate(names)}
+    facs = []  # (blocks, residuals, jacobian)
+    # 1. previous marginalisation factor
+    pb = [bid[f"{t}{k}"] for k in range(n_prior_kf) for t in ("pose", "mix")] + [bid["ext"], bid["td"]]
+    psz = [size[b] for b in pb]
+    ploc = [6 if s == 7 else s for s in psz]
+    r_prev = int(sum(ploc))
+    pidx = np.concatenate([[0], np.cumsum(ploc)[:-1]]).astype(np.int32)
+    pxo = np.concatenate([[0], np.cumsum(psz)[:-1]]).astype(np.int32)
+    x = np.concatenate([vals[b] for b in pb])
+    x0 = x.copy()
+    for b, o in zip(pb, pxo):
+        if size[b] == 7:
+            x0[o:o + 3] += rng.normal(0, 0.01, 3)
+            q = quat_mul(x0[o + 3:o + 7], quat_from_rotvec(rng.normal(0, 1e-3, 3)))
+            x0[o + 3:o + 7] = q / np.linalg.norm(q)
+        else:
+            x0[o:o + size[b]] += rng.normal(0, 1e-3, size[b])
+    # J0 of a previous Hp: information from 1e0 to 1e8 across the remained states
+    A = rng.normal(size=(r_prev, r_prev))
+    H = A @ A.T / r_prev + np.eye(r_prev)
+    D = np.diag(10 ** rng.uniform(0, 4, r_prev))
+    J0 = np.linalg.cholesky(D @ H @ D).T
+    e0 = rng.normal(0, 1, r_prev)
+    res, jac = ev.marg(psz, pidx, pxo, x0, x, J0, e0)
+    facs.append((pb, res, jac))
+    # 2. GNSS on pose0
+    if gnss:
+        gc = np.concatenate([poses[0, :3] + rng.normal(0, 0.05, 3), [0.02, 0.02, 0.05], [0.1, -0.2, 0.3]])
+        res, jac = ev.gnss(gc, poses[0])
+        facs.append(([bid["pose0"]], res, jac))
+    # 3. preintegration 0 -> 1
+    imu = make_imu_segment(rng, 100)
+    st = random_state(rng)
+    st["p"], st["q"] = poses[0, :3], poses[0, 3:]
+    st["v"], st["bg"], st["ba"] = mixes[0, :3], mixes[0, 3:6], mixes[0, 6:]
+    res, jac = ev.preint(imu, st, poses[0], mixes[0], poses[1], mixes[1])
+    facs.append(([bid["pose0"], bid["mix0"], bid["pose1"], bid["mix1"]], res, jac))
+    # 4. reprojection factors of the landmarks referenced in keyframe 0
+    res, jac = ev.reproj(ba["consts"], ba["params"], ba["offs"])
+    for f, o in enumerate(ba["offs"]):
+        k = int(o[1]) // 7
+        j = int(o[3]) - (7 * n_kf + 7)
+        facs.append(([bid["pose0"], bid[f"pose{k}"], bid["ext"], bid[f"invdepth{j}"], bid["td"]], res[f], jac[f]))
+    # local indices: marginalized first
+    used = sorted({b for f in facs for b in f[0]})
+    marg = [bid["pose0"], bid["mix0"]] + [bid[f"invdepth{j}"] for j in range(n_lm)]
+    rem = [b for b in used if b not in set(marg)]
+    index = np.full(len(names), -1, np.int32)
+    o = 0
+    for b in marg + rem:
+        index[b] = o
+        o += 6 if size[b] == 7 else size[b]
+    m = sum(6 if size[b] == 7 else size[b] for b in marg)
+    # compact block table to the used blocks
+    remap = {b: i for i, b in enumerate(used)}
+    nres, blk_off, blk, res_off, jac_off, data = [], [0], [], [], [], []
+    pos = 0
+    for bl, r_, j_ in facs:
+        r_, j_ = np.asarray(r_, np.float64).ravel(), np.asarray(j_, np.float64).ravel()
+        nres.append(r_.size)
+        blk += [remap[b] for b in bl]
+        blk_off.append(len(blk))
+        res_off.append(pos)
+        jac_off.append(pos + r_.size)
+        data += [r_, j_]
+        pos += r_.size + j_.size
+    loss = None
+    if huber is not None:
+        loss = np.array([huber if len(bl) == 5 else 0.0 for bl, _, _ in facs])
+    return dict(nres=np.array(nres, np.int32), blk_off=np.array(blk_off, np.int32), blk=np.array(blk, np.int32),
+                res_off=np.array(res_off, np.int64), jac_off=np.array(jac_off, np.int64),
+                data=np.concatenate(data), loss=loss, size=np.array([size[b] for b in used], np.int32),
+                index=index[used], m=int(m), L=int(o), names=[names[b] for b in used])
+
+
+class DeviceFactorEvaluator:
+    """make_marg_problem's evaluator on the device (gvx.Context factor entry points)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def reproj(self, consts, params, offs):
+        from gvx import REPROJ_DTYPE
+        return self.ctx.reproj_eval(np.asarray(consts).astype(REPROJ_DTYPE), params, offs)
+
+    def preint(self, imu, st, p0, m0, p1, m1):
+        from gvx import STATE_DTYPE as GS
+        gs = np.zeros(1, GS)
+        for k in ("time", "p", "q", "v", "bg", "ba"):
+            gs[k] = st[k]
+        iewn = np.zeros((1, 3))
+        out, pn, pn_off = self.ctx.preint_integrate(2, imu_params(), [imu], gs, iewn)
+        params = np.concatenate([p0, m0, p1, m1])
+        res, jac = self.ctx.preint_factor_eval(out, pn, pn_off, params, np.array([[0, 7, 16, 23]], np.int32))
+        return res[0], jac[0]
+
+    def gnss(self, consts, pose):
+        res, jac = self.ctx.small_factor_eval(0, consts.reshape(1, -1), pose, np.array([0], np.int32))
+        return res[0], jac[0]
+
+    def marg(self, size, index, xoff, x0, x, J0, e0):
+        return self.ctx.marg_factor_eval(size, index, xoff, x0, x, J0, e0)

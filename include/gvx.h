@@ -362,6 +362,48 @@ gvx_status gvx_marg_factor_eval(gvx_ctx* ctx, int32_t r, int32_t nb, const int32
                                 const int32_t* xoff, int32_t n_x, const double* x0, const double* params,
                                 const double* J0, const double* e0, double* residuals, double* jacobians);
 
+/* ------------------------------------------------------- marginalisation */
+/* MarginalizationInfo::marginalization() once its residual blocks are evaluated
+   (factors/marginalization_info.h:73-101): constructEquation (:195-230,
+   H0 = sum J^T J, b0 = -sum J^T e over the local columns), schurElimination
+   (:170-192, Hmm^-1 through Eigen's SelfAdjointEigenSolver with eigenvalues
+   <= 1e-8 dropped, Hp = Hrr - Hrm Hmm^-1 Hmr, bp = brr - Hrm Hmm^-1 bm) and
+   linearization (:153-167, J0 = S^1/2 V^T, e0 = -S^-1/2 V^T bp of Hp's
+   eigen-decomposition), all on the device.
+   Residual block f (ResidualBlockInfo, factors/residual_block_info.h): nres[f]
+   residuals at data[res_off[f]]; its parameter blocks are blk[blk_off[f] ..
+   blk_off[f+1]) (ids into the block table), and their row-major nres x size
+   Jacobians follow one another from data[jac_off[f]] (ResidualBlockInfo::
+   jacobians(), Ceres' global columns).  loss (nullable): per-block HuberLoss
+   parameter, <= 0 for none (the reference passes nullptr, ic_gvins.cc:1529-1642;
+   ResidualBlockInfo::Evaluate :59-87 corrects by sqrt(rho')).
+   Block table: size[b] = global size (7 = pose, local 6), index[b] = local
+   offset in H0 as updateParameterBlocksIndex (:232-253) assigns it (marginalized
+   blocks first); m = marginalizedSize() > 0, L = local size, r = L - m; m and r
+   at most 512.  Outputs: J0 (r x r column-major, linearizedJacobians()), e0 [r]
+   (linearizedResiduals()); optional Hp (r x r column-major), bp [r], eval [r]
+   (Hp's eigenvalues, ascending) and info [2] (the two eigen solves: 0 =
+   Success, 1 = NoConvergence, which the reference does not check either). */
+gvx_status gvx_marginalize(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
+                           const int32_t* blk, const int64_t* res_off, const int64_t* jac_off, const double* data,
+                           int64_t n_data, const double* loss, int32_t nb, const int32_t* size, const int32_t* index,
+                           int32_t m, int32_t L, double* J0, double* e0, double* Hp, double* bp, double* eval,
+                           int32_t* info);
+/* The same with data, loss and every output as device pointers (d_info: 2 ints,
+   nullable), enqueued on the context stream; the structure arrays stay host
+   arrays (the host turns them into the per-pair contribution lists).  Waits
+   for earlier work on the stream before it reuses its pinned list staging. */
+gvx_status gvx_marginalize_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
+                               const int32_t* blk, const int64_t* res_off, const int64_t* jac_off,
+                               const double* d_data, int64_t n_data, const double* d_loss, int32_t nb,
+                               const int32_t* size, const int32_t* index, int32_t m, int32_t L, double* d_J0,
+                               double* d_e0, double* d_Hp, double* d_bp, double* d_eval, int32_t* d_info);
+/* Eigen::SelfAdjointEigenSolver<MatrixXd>(A) with eigenvectors, the solver both
+   steps above use: A n x n column-major (ld lda), lower triangle read, n <= 512.
+   w [n] ascending, V n x n column-major, info 0 / 1 (NoConvergence). */
+gvx_status gvx_sym_eigen(gvx_ctx* ctx, int32_t n, const double* A, int32_t lda, double* w, double* V,
+                         int32_t* info);
+
 /* ------------------------------------------------------ INS mechanization */
 /* IntegrationConfiguration as MISC::insMechanization reads it
    (integration_state.h:91-99): iswithearth selects the Earth-rotation variant

@@ -316,6 +316,24 @@ void orc_marg_factor_eval(int r, int nb, const int* size, const int* index, cons
                           double* jacobians);
 
 /* ------------------------------------------------------------------------- */
+/* Marginalisation (marg.c): MarginalizationInfo::constructEquation /         */
+/* schurElimination / linearization and Eigen's SelfAdjointEigenSolver        */
+/* ------------------------------------------------------------------------- */
+/* A column-major (ld lda), lower triangle read -> eigenvalues w ascending,
+   eigenvectors V (n x n column-major).  Returns 0, or 1 on NoConvergence. */
+int orc_sym_eigen(int n, const double* A, int lda, double* w, double* V);
+/* factor f: residuals then per block the row-major nres x size Jacobian at
+   data + fac_off[f]; blocks blk[blk_off[f] .. blk_off[f+1]); loss[f] > 0: HuberLoss
+   parameter (nullable).  H0 L x L column-major, b0 [L]. */
+void orc_marg_construct(int n_fac, const int* nres, const int* blk_off, const int* blk, const long* fac_off,
+                        const double* data, const double* loss, const int* size, const int* index, int L,
+                        double* H0, double* b0);
+/* Hp r x r column-major, bp [r], r = L - m.  Returns the eigen-solver info. */
+int orc_marg_schur(int L, int m, const double* H0, const double* b0, double* Hp, double* bp);
+/* J0 r x r column-major, e0 [r], eval [r] (nullable): Hp's eigenvalues */
+int orc_marg_linearize(int r, const double* Hp, const double* bp, double* J0, double* e0, double* eval);
+
+/* ------------------------------------------------------------------------- */
 /* Camera operations (camera.c)                                               */
 /* ------------------------------------------------------------------------- */
 typedef struct {

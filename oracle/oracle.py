@@ -166,6 +166,13 @@ def lib():
         L.orc_small_factor_eval.argtypes = [C.c_int, C.c_int, P, P, P, P, P]
         L.orc_small_factor_eval.restype = C.c_int
         L.orc_marg_factor_eval.argtypes = [C.c_int, C.c_int, P, P, P, P, P, P, P, P, P]
+        L.orc_sym_eigen.argtypes = [C.c_int, P, C.c_int, P, P]
+        L.orc_sym_eigen.restype = C.c_int
+        L.orc_marg_construct.argtypes = [C.c_int, P, P, P, P, P, P, P, P, C.c_int, P, P]
+        L.orc_marg_schur.argtypes = [C.c_int, C.c_int, P, P, P, P]
+        L.orc_marg_schur.restype = C.c_int
+        L.orc_marg_linearize.argtypes = [C.c_int, P, P, P, P, P]
+        L.orc_marg_linearize.restype = C.c_int
         CP = C.POINTER(Camera)
         L.orc_undistort_points.argtypes = [CP, C.c_int, P, P]
         L.orc_distort_points.argtypes = [CP, C.c_int, P, P]
@@ -607,3 +614,85 @@ def marg_factor_eval(size, index, xoff, x0, params, J0, e0, jacobians=True):
     jac = np.zeros(r * int(sz.sum())) if jacobians else None
     lib().orc_marg_factor_eval(r, sz.size, _p(sz), _p(ix), _p(xo), _p(z), _p(x), _p(J), _p(e), _p(res), _p(jac))
     return res, jac
+
+
+# ------------------------------------------------------ marginalisation
+def sym_eigen(A):
+    """Eigen::SelfAdjointEigenSolver (marg.c): lower triangle of A read ->
+    (eigenvalues ascending, eigenvectors as columns, info)."""
+    A = np.asarray(A, np.float64)
+    n = A.shape[0]
+    a = np.ascontiguousarray(A.T)  # column-major data
+    w = np.zeros(max(n, 1))
+    V = np.zeros(max(n * n, 1))
+    info = lib().orc_sym_eigen(n, _p(a), n, _p(w), _p(V))
+    return w[:n], V[:n * n].reshape(n, n).T.copy(), int(info)
+
+
+def marg_construct(problem):
+    """constructEquation (marg.c) over a problem dict (gvx.synth_ba.marg_problem:
+    nres, blk_off, blk, res_off, jac_off, data, loss, size, index, m, L) -> (H0 [L, L], b0 [L])."""
+    p = problem
+    L = int(p["L"])
+    H0 = np.zeros(L * L)
+    b0 = np.zeros(L)
+    nres = np.ascontiguousarray(p["nres"], np.int32)
+    boff = np.ascontiguousarray(p["blk_off"], np.int32)
+    blk = np.ascontiguousarray(p["blk"], np.int32)
+    foff = np.ascontiguousarray(p["res_off"], np.int64)
+    assert np.array_equal(np.asarray(p["jac_off"]), foff + nres), "oracle layout: Jacobians follow the residuals"
+    data = np.ascontiguousarray(p["data"], np.float64)
+    loss = p.get("loss")
+    loss = None if loss is None else np.ascontiguousarray(loss, np.float64)
+    size = np.ascontiguousarray(p["size"], np.int32)
+    index = np.ascontiguousarray(p["index"], np.int32)
+    lib().orc_marg_construct(nres.size, _p(nres), _p(boff), _p(blk), _p(foff), _p(data), _p(loss), _p(size),
+                             _p(index), L, _p(H0), _p(b0))
+    return H0.reshape(L, L).T.copy(), b0
+
+
+def marg_schur(H0, b0, m):
+    """schurElimination (marg.c) -> (Hp [r, r], bp [r], info)."""
+    H0 = np.asarray(H0, np.float64)
+    L = H0.shape[0]
+    r = L - m
+    h = np.ascontiguousarray(H0.T)
+    b = np.ascontiguousarray(b0, np.float64)
+    Hp = np.zeros(max(r * r, 1))
+    bp = np.zeros(max(r, 1))
+    info = lib().orc_marg_schur(L, m, _p(h), _p(b), _p(Hp), _p(bp))
+    return Hp[:r * r].reshape(r, r).T.copy(), bp[:r], int(info)
+
+
+def marg_linearize(Hp, bp):
+    """linearization (marg.c) -> (J0 [r, r], e0 [r], eigenvalues [r], info)."""
+    Hp = np.asarray(Hp, np.float64)
+    r = Hp.shape[0]
+    h = np.ascontiguousarray(Hp.T)
+    b = np.ascontiguousarray(bp, np.float64)
+    J0 = np.zeros(max(r * r, 1))
+    e0 = np.zeros(max(r, 1))
+    ev = np.zeros(max(r, 1))
+    info = lib().orc_marg_linearize(r, _p(h), _p(b), _p(J0), _p(e0), _p(ev))
+    return J0[:r * r].reshape(r, r).T.copy(), e0[:r], ev[:r], int(info)
+
+
+class FactorEvaluator:
+    """synth_ba.make_marg_problem's evaluator on the CPU restatement (tests only)."""
+
+    def reproj(self, consts, params, offs):
+        return reproj_eval_batch(consts, params, offs)
+
+    def preint(self, imu, st, p0, m0, p1, m1):
+        from gvx import synth_ba  # the synthetic IMU's noise parameters
+        s = make_state(float(st["time"]), st["p"], st["q"], st["v"], st["bg"], st["ba"])
+        seg = PreintSeg(2, imu_params(*synth_ba.imu_params()), imu, s, np.zeros(3))
+        r, J = seg.evaluate(p0, m0, p1, m1)
+        return r, np.concatenate([j.ravel() for j in J])
+
+    def gnss(self, consts, pose):
+        res, jac = small_factor_eval(0, np.asarray(consts).reshape(1, -1), pose, np.array([0], np.int32))
+        return res[0], jac[0]
+
+    def marg(self, size, index, xoff, x0, x, J0, e0):
+        return marg_factor_eval(size, index, xoff, x0, x, J0, e0)
