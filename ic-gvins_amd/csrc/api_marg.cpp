@@ -8,6 +8,7 @@
 // the numbers themselves never leave the device in the _dev variant.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -300,12 +301,16 @@ gvx_status gvx_sym_eigen(gvx_ctx* c, int32_t n, const double* A, int32_t lda, do
     hipSetDevice(c->device);
     double *d_A, *h_A, *d_V, *h_V, *d_w, *h_w, *d_hc;
     int32_t *d_info, *h_info;
+    unsigned long long *d_ts, *h_ts;
     Staging st;
     st.add((size_t)n * n, &d_A, &h_A);
     st.add((size_t)n * n, &d_V, &h_V);
     st.add((size_t)n, &d_w, &h_w);
     st.add(1, &d_info, &h_info);
+    st.add(8, &d_ts, &h_ts);
     st.add((size_t)n, &d_hc);
+    // GVX_EIG_TIMING=1: the solver's phase times to stderr (diagnostics)
+    static const bool timing = getenv("GVX_EIG_TIMING") && *getenv("GVX_EIG_TIMING") == '1';
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_err(c, e, "eigen: stream");
     void* hb = pinned(c, "eigen", st.bytes());
@@ -317,14 +322,18 @@ gvx_status gvx_sym_eigen(gvx_ctx* c, int32_t n, const double* A, int32_t lda, do
     if (e != hipSuccess) return hip_err(c, e, "eigen upload");
     hipEvent_t ev{};
     prof_begin(c, "eigen", &ev);
-    e = launch_sym_eigen(c, n, d_A, n, d_V, d_w, d_hc, d_info);
+    e = launch_sym_eigen(c, n, d_A, n, d_V, d_w, d_hc, d_info, timing ? d_ts : nullptr);
     prof_end(c, "eigen", ev);
     if (e != hipSuccess) return hip_err(c, e, "eigen kernel");
-    e = hipMemcpyAsync(h_V, d_V, (size_t)((char*)(d_info + 1) - (char*)d_V), hipMemcpyDeviceToHost, c->stream);
+    e = hipMemcpyAsync(h_V, d_V, (size_t)((char*)(d_ts + 8) - (char*)d_V), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_err(c, e, "eigen download");
     std::memcpy(V, h_V, sizeof(double) * (size_t)n * n);
     std::memcpy(w, h_w, sizeof(double) * n);
     if (info) *info = *h_info;
+    if (timing && n > 1)
+        fprintf(stderr, "gvx eigen n=%d us: scale %.1f tridiag %.1f Q %.1f QR %.1f (%llu sweeps, %llu rotations) sort %.1f\n",
+                n, (h_ts[1] - h_ts[0]) * 0.01, (h_ts[2] - h_ts[1]) * 0.01, (h_ts[3] - h_ts[2]) * 0.01,
+                (h_ts[4] - h_ts[3]) * 0.01, h_ts[6], h_ts[7], (h_ts[5] - h_ts[4]) * 0.01);
     return GVX_OK;
 }

@@ -189,9 +189,10 @@ struct MargLaunch {
     double *J0, *e0;
 };
 hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p);
-// SelfAdjointEigenSolver of the lower triangle of src (ld lds): V n x n, w n, hc n scratch, info 1 int
+// SelfAdjointEigenSolver of the lower triangle of src (ld lds): V n x n, w n, hc n scratch, info 1 int;
+// ts (nullable, diagnostics): 7 u64, wall-clock stamps (100 MHz) of the solver's phases + QR iterations
 hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc,
-                            int* info);
+                            int* info, unsigned long long* ts = nullptr);
 
 // ---- ins.hip ----
 hipError_t launch_ins(gvx_ctx* c, const gvx_ins_config& cfg, int n_chain, const gvx_imu* imu, const int32_t* off,

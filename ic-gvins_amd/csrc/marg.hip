@@ -23,9 +23,10 @@
 //   coalesced column walks; every sum is one thread's sequential loop, in
 //   oracle/marg.c's order, so the two agree bit for bit), Q accumulated in
 //   place, then the implicit QR sweeps:
-//   wave 0 runs the scalar Givens chain of sweep s+1 while waves 1-15 apply the
-//   rotations of sweep s to the rows of Q (a row's rotations need no other row,
-//   so a sweep costs one barrier), and finally the selection sort.
+//   wave 0 runs the scalar Givens chain of sweep s+1 while 12 waves (not those on
+//   wave 0's SIMD) apply the rotations of sweep s to the rows of Q (a row's
+//   rotations need no other row, so a sweep costs one barrier), and finally the
+//   selection sort.
 // hinv / schur_t / schur_p / linearize: one thread per output entry, ordered
 //   inner sums (K <= a few hundred): coalesced over the row index, the other
 //   operand broadcast.
@@ -43,6 +44,21 @@ constexpr int H0_THREADS = 128;
 constexpr int EIG_THREADS = 1024;
 constexpr int EIG_WAVES = EIG_THREADS / 64;
 constexpr double MARG_EPS = 1e-8;  // MarginalizationInfo::EPS (marginalization_info.h:308)
+
+// the restatement's sum64 fold (oracle/marg.c): lane l holds the partial sum of
+// elements l, l + 64, ...; the xor butterfly leaves the total in every lane
+__device__ inline double bfly_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = v + __shfl_xor(v, o);
+    return v;
+}
+
+// column chunks of the tridiagonalisation mat-vec (oracle/marg.c eig_groups)
+__device__ inline int eig_groups(int rem) {
+    const int rpad = (rem + 63) & ~63;
+    const int g = 1024 / rpad;
+    return g > 16 ? 16 : g;
+}
 
 __device__ inline double wave_max(double v) {
 #pragma unroll
@@ -163,6 +179,7 @@ struct QrState {
     int start, end;
     long iter;
     int info;
+    long rot;  // rotations produced (diagnostics)
 };
 
 // One turn of computeFromTridiagonal_impl's loop up to and including one
@@ -268,6 +285,7 @@ __device__ void qr_produce(EigShared& S, QrState& st, int n, int b, int lane) {
             S.sw[b][0] = start;
             S.sw[b][1] = k - start;
         }
+        st.rot += k - start;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -280,9 +298,14 @@ __device__ void qr_produce(EigShared& S, QrState& st, int n, int b, int lane) {
 // w the eigenvalues (ascending), hc n doubles of scratch.
 __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const double* __restrict__ src, int lds,
                                                                 double* __restrict__ A, double* __restrict__ w,
-                                                                double* __restrict__ hc, int* __restrict__ info) {
+                                                                double* __restrict__ hc, int* __restrict__ info,
+                                                                unsigned long long* __restrict__ ts) {
     __shared__ EigShared S;
+    // ts (nullable, diagnostics): wall clock (100 MHz) at the phase boundaries
+#define EIG_STAMP(k) \
+    if (ts && tid == 0) ts[k] = wall_clock64()
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    EIG_STAMP(0);
     if (n == 1) {
         if (tid == 0) {
             w[0] = src[0];
@@ -310,69 +333,118 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
     }
     __syncthreads();
 
-    // ---- tridiagonalization_inplace.  Every sum runs in the oracle's sequential
-    // order (one thread per sum), so the device and oracle/marg.c agree bit for bit.
+    EIG_STAMP(1);
+    // ---- tridiagonalization_inplace.  Sums use the restatement's fixed orders
+    // (oracle/marg.c: sum64 = 64 lane-strided partial sums folded by an xor
+    // butterfly; the mat-vec = G column chunks folded in order), so the device
+    // and the restatement agree bit for bit.
     for (int i = 0; i < n - 1; ++i) {
         const int rem = n - i - 1, o = i + 1;
         double* col = A + (long)i * n;
-        for (int k = tid; k < rem; k += EIG_THREADS) S.v[k] = col[o + k];
-        __syncthreads();
-        if (tid == 0) {
+        if (wid == 0) {
+            // makeHouseholderInPlace on v = col[i+1 ..)
             double t = 0.0;
-            for (int k = 1; k < rem; ++k) t += S.v[k] * S.v[k];
-            const double c0 = S.v[0];
-            double tau, beta;
+            for (int k = 1 + lane; k < rem; k += 64) {
+                const double x = col[o + k];
+                S.v[k] = x;
+                t += x * x;
+            }
+            t = bfly_sum(t);
+            const double c0 = col[o];
+            double tau, beta, d = 0.0;
             if (t <= DBL_MIN) {
                 tau = 0.0;
                 beta = c0;
-                S.sc[1] = 0.0;  // essential.setZero()
             } else {
                 beta = sqrt(c0 * c0 + t);
                 if (c0 >= 0.0) beta = -beta;
                 tau = (beta - c0) / beta;
-                S.sc[1] = c0 - beta;
+                d = c0 - beta;
             }
-            S.sc[0] = beta;
-            S.red[0] = tau;
+            for (int k = 1 + lane; k < rem; k += 64) {
+                const double ek = d == 0.0 ? 0.0 : S.v[k] / d;  // tail / (c0 - beta), or setZero()
+                S.v[k] = ek;
+                col[o + k] = ek;
+            }
+            if (lane == 0) {
+                S.v[0] = 1.0;
+                S.sc[0] = beta;
+                S.sc[1] = tau;
+            }
         }
         __syncthreads();
-        const double h = S.red[0], dv = S.sc[1];
-        // essential = tail / (c0 - beta) (or zero), stored in place and in v
-        for (int k = 1 + tid; k < rem; k += EIG_THREADS) {
-            const double ek = dv == 0.0 ? 0.0 : S.v[k] / dv;
-            S.v[k] = ek;
-            col[o + k] = ek;
+        const double h = S.sc[1];
+        // p = A_sub.selfadjointView<Lower>() * (h v): rows over lanes (coalesced
+        // column walks), G chunks of columns over the thread groups
+        const int G = eig_groups(rem), chunk = (rem + G - 1) / G, rpad = (rem + 63) & ~63;
+        {
+            const int j = tid % rpad, g = tid / rpad;
+            if (g < G && j < rem) {
+                const int k0 = g * chunk, k1 = min(rem, k0 + chunk);
+                const double* a = A + (long)(o + k0) * n + o + j;
+                double acc = 0.0;
+                int k = k0;
+                for (; k + 8 <= k1; k += 8, a += 8 * (long)n) {
+                    double x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = a[(long)u * n];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc += x[u] * (h * S.v[k + u]);
+                }
+                for (; k < k1; ++k, a += n) acc += *a * (h * S.v[k]);
+                S.part[g * rpad + j] = acc;
+            }
         }
-        if (tid == 0) S.v[0] = 1.0;
         __syncthreads();
-        // p = A_sub.selfadjointView<Lower>() * (h v): one thread per row, coalesced column walk
-        if (tid < rem) {
-            const double* a = A + (long)o * n + o + tid;
-            double acc = 0.0;
-            for (int k = 0; k < rem; ++k, a += n) acc += *a * (h * S.v[k]);
-            S.p[tid] = acc;
+        if (wid == 0) {
+            double dt = 0.0;
+            for (int j = lane; j < rem; j += 64) {
+                double s = 0.0;
+                for (int g = 0; g < G; ++g) s += S.part[g * rpad + j];
+                S.p[j] = s;
+                dt += s * S.v[j];
+            }
+            dt = bfly_sum(dt);
+            if (lane == 0) {
+                S.sc[1] = (h * -0.5) * dt;
+                col[o] = S.sc[0];  // the subdiagonal: beta
+                hc[i] = h;
+            }
         }
         __syncthreads();
-        if (tid == 0) {
-            double d = 0.0;
-            for (int k = 0; k < rem; ++k) d += S.p[k] * S.v[k];
-            S.sc[1] = (h * -0.5) * d;
-        }
-        __syncthreads();
+        // A_sub -= v p'^T + p' v^T, p' = p + sc v (rankUpdate, lower formula mirrored):
+        // lanes over the rows, 2 columns per wave per batch with every load issued
+        // before the first store (the matrix lives in L2: latency, not bandwidth)
         {
             const double sc = S.sc[1];
-            for (int k = tid; k < rem; k += EIG_THREADS) S.part[k] = S.p[k] + sc * S.v[k];
-        }
-        __syncthreads();
-        // A_sub -= v p^T + p v^T (rankUpdate, lower formula mirrored)
-        for (int e = tid; e < rem * rem; e += EIG_THREADS) {
-            const int jj = e % rem, kk = e / rem;
-            const int hi = jj > kk ? jj : kk, lo = jj > kk ? kk : jj;
-            A[(long)(o + kk) * n + o + jj] += (-S.v[lo]) * S.part[hi] + (-S.part[lo]) * S.v[hi];
-        }
-        if (tid == 0) {
-            col[i + 1] = S.sc[0];
-            hc[i] = h;
+            const int nr = (rem + 63) >> 6;  // row slots per lane (<= 8)
+            for (int k0 = wid * 2; k0 < rem; k0 += 2 * EIG_WAVES) {
+                double x[2][8];
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc) {
+                    const double* ac = A + (long)(o + k0 + cc) * n + o;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int jj = lane + 64 * u;
+                        if (u < nr && k0 + cc < rem && jj < rem) x[cc][u] = ac[jj];
+                    }
+                }
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc) {
+                    const int kk = k0 + cc;
+                    double* ac = A + (long)(o + kk) * n + o;
+                    const double vk = S.v[kk], pk = S.p[kk] + sc * vk;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int jj = lane + 64 * u;
+                        if (u < nr && jj < rem && kk < rem) {
+                            const double vj = S.v[jj], pj = S.p[jj] + sc * vj;
+                            // lower formula of element (hi, lo): (-v_lo) p'_hi + (-p'_lo) v_hi
+                            ac[jj] = x[cc][u] + (jj >= kk ? (-vk) * pj + (-pk) * vj : (-vj) * pk + (-pj) * vk);
+                        }
+                    }
+                }
+            }
         }
         __syncthreads();
     }
@@ -382,6 +454,7 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
     }
     __syncthreads();
 
+    EIG_STAMP(2);
     // ---- Householder sequence evaluated in place (HouseholderSequence::evalTo)
     for (int e = tid; e < n * n; e += EIG_THREADS) {
         const int i = e % n, j = e / n;
@@ -393,26 +466,52 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
         const int cs = n - k - 1;
         const double tau = hc[k];
         double* C = A + (long)(k + 1) * n + (k + 1);
+        const double* ess = A + (long)k * n + k + 2;  // cs - 1 entries
         if (cs == 1) {
             if (tid == 0) C[0] *= 1.0 - tau;
         } else if (tau != 0.0) {
-            const double* ess = A + (long)k * n + k + 2;
-            for (int r = tid; r < cs - 1; r += EIG_THREADS) S.v[r] = ess[r];
-            __syncthreads();
-            // tmp = ess^T * bottom + row0: one thread per column, sequential over rows
-            if (tid < cs) {
-                const double* cc = C + (long)tid * n;
-                double acc = 0.0;
-                for (int r = 0; r < cs - 1; ++r) acc += S.v[r] * cc[1 + r];
-                S.p[tid] = acc + cc[0];
+            // tmp = ess^T * bottom + row0: one wave per column, sum64 over the rows
+            for (int c0 = wid * 2; c0 < cs; c0 += 2 * EIG_WAVES) {
+                double acc[2] = {0.0, 0.0};
+                const int c1 = min(c0 + 1, cs - 1);
+                for (int r = lane; r < cs - 1; r += 64) {
+                    const double er = ess[r];
+                    acc[0] += er * C[(long)c0 * n + 1 + r];
+                    acc[1] += er * C[(long)c1 * n + 1 + r];
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double t = bfly_sum(acc[q]);
+                    if (lane == 0 && c0 + q < cs) S.p[c0 + q] = t + C[(long)(c0 + q) * n];
+                }
             }
             __syncthreads();
-            for (int e = tid; e < cs * cs; e += EIG_THREADS) {
-                const int rr = e % cs, c = e / cs;
-                if (rr == 0)
-                    C[(long)c * n] -= tau * S.p[c];
-                else
-                    C[(long)c * n + rr] -= (tau * S.v[rr - 1]) * S.p[c];
+            const int nr = (cs + 63) >> 6;
+            double f[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int rr = lane + 64 * u;
+                f[u] = (u < nr && rr < cs) ? (rr == 0 ? tau : tau * ess[rr - 1]) : 0.0;
+            }
+            for (int c0 = wid * 2; c0 < cs; c0 += 2 * EIG_WAVES) {
+                double x[2][8];
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int rr = lane + 64 * u;
+                        if (u < nr && c0 + q < cs && rr < cs) x[q][u] = C[(long)(c0 + q) * n + rr];
+                    }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double tc = S.p[min(c0 + q, cs - 1)];
+                    double* cc = C + (long)(c0 + q) * n;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int rr = lane + 64 * u;
+                        if (u < nr && rr < cs && c0 + q < cs) cc[rr] = x[q][u] - f[u] * tc;
+                    }
+                }
             }
         }
         __syncthreads();
@@ -420,8 +519,9 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
     }
     __syncthreads();
 
+    EIG_STAMP(3);
     // ---- implicit symmetric QR: wave 0 produces sweeps, waves 1.. apply them to Q's rows
-    QrState st{0, n - 1, 0, 0};
+    QrState st{0, n - 1, 0, 0, 0};
     if (wid == 0) qr_produce(S, st, n, 0, lane);
     __syncthreads();
     for (int s = 0;; ++s) {
@@ -430,24 +530,42 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
         if (cnt < 0) break;
         if (wid == 0) {
             qr_produce(S, st, n, b ^ 1, lane);
-        } else {
-            const int i = tid - 64;
+        } else if (wid & 3) {
+            // waves 4, 8, 12 share wave 0's SIMD (round-robin placement): they stay
+            // idle so the dependent Givens chain has that SIMD to itself
+            const int i = (wid - 1 - (wid >> 2)) * 64 + lane;
             if (i < n && cnt > 0) {
+                // Q = Q G_k for k = k0 .. k0+cnt-1 on row i; the row's columns are
+                // loaded 8 ahead so the L2 latency is paid once per 8 rotations
                 const int k0 = S.sw[b][0];
-                double* q = A + i;
-                double x = q[(long)k0 * n];
-                for (int t = 0; t < cnt; ++t) {
-                    const int k = k0 + t;
+                double* q = A + i + (long)k0 * n;
+                double x = q[0];
+                int t = 0;
+                for (; t + 8 <= cnt; t += 8, q += 8 * (long)n) {
+                    double y[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) y[u] = q[(long)(u + 1) * n];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const double c = S.rc[b][t + u], sn = S.rs[b][t + u];
+                        q[(long)u * n] = c * x - sn * y[u];
+                        x = sn * x + c * y[u];
+                    }
+                }
+                for (; t < cnt; ++t, q += n) {
                     const double c = S.rc[b][t], sn = S.rs[b][t];
-                    const double y = q[(long)(k + 1) * n];
-                    q[(long)k * n] = c * x - sn * y;
+                    const double y = q[n];
+                    q[0] = c * x - sn * y;
                     x = sn * x + c * y;
                 }
-                q[(long)(k0 + cnt) * n] = x;
+                q[0] = x;
             }
         }
         __syncthreads();
     }
+    EIG_STAMP(4);
+    if (ts && tid == 0) ts[6] = st.iter;
+    if (ts && tid == 0) ts[7] = st.rot;
     // ---- selection sort (minCoeff: first index of the minimum), then the column swaps per row
     if (wid == 0) {
         if (st.info == 0) {
@@ -502,6 +620,8 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
     }
     for (int i = tid; i < n; i += EIG_THREADS) w[i] = S.diag[i] * scale;
     if (tid == 0) *info = inf;
+    EIG_STAMP(5);
+#undef EIG_STAMP
 }
 
 // ------------------------------------------------------------ Schur complement
@@ -565,17 +685,18 @@ __global__ void __launch_bounds__(256) linearize_kernel(int r, const double* __r
     }
 }
 
-hipError_t launch_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc, int* info) {
+hipError_t launch_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc, int* info,
+                        unsigned long long* ts = nullptr) {
     if (n <= 0) return hipSuccess;
-    sym_eigen_kernel<<<1, EIG_THREADS, 0, c->stream>>>(n, src, lds, V, w, hc, info);
+    sym_eigen_kernel<<<1, EIG_THREADS, 0, c->stream>>>(n, src, lds, V, w, hc, info, ts);
     return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc,
-                            int* info) {
-    return launch_eigen(c, n, src, lds, V, w, hc, info);
+                            int* info, unsigned long long* ts) {
+    return launch_eigen(c, n, src, lds, V, w, hc, info, ts);
 }
 
 hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p) {

@@ -19,9 +19,14 @@
  *
  * Order: each Eigen expression is evaluated in its own order of operations (products
  * formed before they are added, Givens rotations and Householder reflections in
- * Eigen's formulas), but dense reductions (squaredNorm, dot, GEMV / GEMM inner
- * sums) are plain sequential sums here, where Eigen's SIMD kernels reassociate
- * them.  Parity is therefore a tolerance (fp64), not bits.
+ * Eigen's formulas).  Dense reductions, which Eigen's SIMD kernels reassociate in
+ * their own way, use fixed orders here that the device kernels reproduce: the
+ * solver's vector sums (squaredNorm, dot, the Householder column dots) are sum64
+ * (64 lane-strided partial sums folded by an xor butterfly), its symmetric
+ * mat-vec is eig_groups() column chunks folded in order, and every other sum
+ * (GEMV / GEMM inner sums, J^T J) is sequential.  So the device results are
+ * bit-identical to this restatement, while the restatement sits within
+ * reassociation distance (a fp64 tolerance) of Eigen.
  * Parity unpinned against the reference binaries (Eigen and Ceres absent);
  * pinned by numpy (LAPACK) eigen-decompositions, dense normal equations and the
  * Schur-complement identities in tests/test_oracle_marg.py.
@@ -73,17 +78,38 @@ static void make_givens(double p, double q, double* c, double* s) {
     }
 }
 
+/* Sum of x[0..N): lane-strided partials P_l = sum of x[l], x[l+64], ... in order,
+   then P_l <- P_l + P_(l xor o) for o = 32, 16, ..., 1; the result is P_0 (the
+   device's per-wave reduction, marg.hip bfly_sum). */
+static double sum64(const double* x, int N) {
+    double P[64], Q[64];
+    for (int l = 0; l < 64; l++) P[l] = 0.0;
+    for (int i = 0; i < N; i++) P[i & 63] += x[i];
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int l = 0; l < 64; l++) Q[l] = P[l] + P[l ^ o];
+        memcpy(P, Q, sizeof P);
+    }
+    return P[0];
+}
+
+/* column chunks of the symmetric mat-vec (marg.hip eig_groups) */
+static int eig_groups(int rem) {
+    const int rpad = (rem + 63) & ~63;
+    const int g = 1024 / rpad;
+    return g > 16 ? 16 : g;
+}
+
 /* tridiagonalization_inplace(matA, hCoeffs) (Eigen/src/Eigenvalues/Tridiagonalization.h):
    a is n x n column-major, lower triangle meaningful.  On return the lower part
    holds the essential Householder vectors below the subdiagonal. */
-static void tridiagonalize(int n, double* a, double* hc, double* p) {
+static void tridiagonalize(int n, double* a, double* hc, double* p, double* x) {
     for (int i = 0; i < n - 1; i++) {
         const int rem = n - i - 1;
         double* col = a + (long)i * n;
         /* makeHouseholderInPlace on v = col[i+1 .. n) */
         const double c0 = col[i + 1];
-        double tail = 0.0;
-        for (int k = i + 2; k < n; k++) tail += col[k] * col[k];
+        for (int k = i + 2; k < n; k++) x[k - i - 2] = col[k] * col[k];
+        const double tail = sum64(x, rem - 1);
         double tau, beta;
         if (tail <= DBL_MIN) {
             tau = 0.0;
@@ -100,17 +126,23 @@ static void tridiagonalize(int n, double* a, double* hc, double* p) {
         col[i + 1] = 1.0;
         const double* v = col + i + 1;
         double* S = a + (long)(i + 1) * n + (i + 1); /* bottom-right rem x rem, ld n */
-        /* p = A_sub.selfadjointView<Lower>() * (h * v) */
+        /* p = A_sub.selfadjointView<Lower>() * (h * v), G column chunks folded in order */
+        const int G = eig_groups(rem), chunk = (rem + G - 1) / G;
         for (int j = 0; j < rem; j++) {
-            double acc = 0.0;
-            for (int k = 0; k < rem; k++) {
-                const double ajk = j >= k ? S[(long)k * n + j] : S[(long)j * n + k];
-                acc += ajk * (h * v[k]);
+            double s = 0.0;
+            for (int g = 0; g < G; g++) {
+                const int k1 = (g + 1) * chunk < rem ? (g + 1) * chunk : rem;
+                double acc = 0.0;
+                for (int k = g * chunk; k < k1; k++) {
+                    const double ajk = j >= k ? S[(long)k * n + j] : S[(long)j * n + k];
+                    acc += ajk * (h * v[k]);
+                }
+                s += acc;
             }
-            p[j] = acc;
+            p[j] = s;
         }
-        double dot = 0.0;
-        for (int k = 0; k < rem; k++) dot += p[k] * v[k];
+        for (int k = 0; k < rem; k++) x[k] = p[k] * v[k];
+        const double dot = sum64(x, rem);
         const double sc = (h * -0.5) * dot;
         for (int k = 0; k < rem; k++) p[k] += sc * v[k];
         /* rankUpdate(v, p, -1) on the lower triangle */
@@ -126,7 +158,7 @@ static void tridiagonalize(int n, double* a, double* hc, double* p) {
 /* HouseholderSequence(mat, hCoeffs).setLength(n-1).setShift(1) evaluated into mat
    itself (HouseholderSequence::evalTo, in-place branch), with
    applyHouseholderOnTheLeft (Eigen/src/Householder/Householder.h). */
-static void householder_q(int n, double* a, const double* hc, double* tmp) {
+static void householder_q(int n, double* a, const double* hc, double* tmp, double* x) {
     for (int j = 0; j < n; j++) {
         for (int i = 0; i < j; i++) a[(long)j * n + i] = 0.0;
         a[(long)j * n + j] = 1.0;
@@ -140,9 +172,8 @@ static void householder_q(int n, double* a, const double* hc, double* tmp) {
             C[0] *= 1.0 - tau;
         } else if (tau != 0.0) {
             for (int c = 0; c < cs; c++) {
-                double acc = 0.0;
-                for (int r = 0; r < cs - 1; r++) acc += ess[r] * C[(long)c * n + 1 + r];
-                tmp[c] = acc + C[(long)c * n];
+                for (int r = 0; r < cs - 1; r++) x[r] = ess[r] * C[(long)c * n + 1 + r];
+                tmp[c] = sum64(x, cs - 1) + C[(long)c * n];
             }
             for (int c = 0; c < cs; c++) C[(long)c * n] -= tau * tmp[c];
             for (int c = 0; c < cs; c++)
@@ -212,11 +243,11 @@ int orc_sym_eigen(int n, const double* A, int lda, double* w, double* V) {
     for (int j = 0; j < n; j++)
         for (int i = j; i < n; i++) V[(long)j * n + i] /= scale;
     double* work = (double*)malloc(sizeof(double) * 4 * (size_t)n);
-    double *hc = work, *tmp = work + n, *diag = w, *sub = work + 2 * n;
-    tridiagonalize(n, V, hc, tmp);
+    double *hc = work, *tmp = work + n, *diag = w, *sub = work + 2 * n, *x = work + 3 * n;
+    tridiagonalize(n, V, hc, tmp, x);
     for (int i = 0; i < n; i++) diag[i] = V[(long)i * n + i];
     for (int i = 0; i < n - 1; i++) sub[i] = V[(long)i * n + i + 1];
-    householder_q(n, V, hc, tmp);
+    householder_q(n, V, hc, tmp, x);
 
     /* computeFromTridiagonal_impl */
     int end = n - 1, start = 0, info = 0;
