@@ -562,7 +562,7 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     achieved = B_rp * n_r / (rp_ms * 1e-3) / 1e9 if rp_ms > 0 else None
     line = None
     if rank == 0:
-        wf = window_factor_leg(ctx, dev) if window_extras else None
+        wf = window_factor_leg(ctx, dev, cpu=world == 1 and not args.no_cpu) if window_extras else None
         pf_achieved = B_pf * n_p / (pf_ms * 1e-3) / 1e9 if pf_ms > 0 else None
         line = {
             "metric": "BA factor-Jacobian evaluations/s (configs[3])",
@@ -602,12 +602,13 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     return line
 
 
-def window_factor_leg(ctx, dev, reps=20):
-    """SURVEY 8f rank 3 (partial), beside configs[3]: GnssFactor as a device batch
-    (2^20 factors per launch for a throughput figure; the live system has one per
-    GNSS epoch) and one MarginalizationFactor of an IC-GVINS-shaped window (9
-    keyframes' pose + mix, extrinsic, td: r = 142) through the host entry, PCIe
-    included.  Not part of `value`."""
+def window_factor_leg(ctx, dev, reps=20, cpu=True):
+    """SURVEY 8f rank 3, beside configs[3]: GnssFactor as a device batch (2^20
+    factors per launch for a throughput figure; the live system has one per GNSS
+    epoch), one MarginalizationFactor of an IC-GVINS-shaped window (9 keyframes'
+    pose + mix, extrinsic, td: r = 142) through the host entry, PCIe included, and
+    the device marginalisation of the configs[3] window (marg_leg).  Not part of
+    `value`."""
     import torch
     import gvx
     rng = np.random.default_rng(7)
@@ -660,7 +661,62 @@ def window_factor_leg(ctx, dev, reps=20):
             "gnss_factor_evals_per_s": round(n / (per * 1e-3)),
             "gnss_roofline": {"bound": "hbm", "achieved": round(n * bytes_per / (per * 1e-3) / 1e9, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "algorithmic_bytes_per_factor": bytes_per},
-            "marg_factor_r": r, "marg_factor_host_call_us": round(marg_us, 1)}
+            "marg_factor_r": r, "marg_factor_host_call_us": round(marg_us, 1),
+            "marginalization": marg_leg(ctx, dev, cpu=cpu)}
+
+
+def marg_leg(ctx, dev, reps=10, cpu=True):
+    """MarginalizationInfo::marginalization() of the configs[3] window when its
+    oldest keyframe leaves (synth_ba.make_marg_problem: the previous prior, a GNSS
+    factor, preintegration 0->1 and the 1,800 reprojection factors; m = 215
+    marginalized, r = 142 remained), residual blocks evaluated on the device, then
+    gvx_marginalize_dev: H0/b0, Hmm's eigen-decomposition, Hp/bp, Hp's
+    eigen-decomposition, J0/e0.  Once per keyframe in the live system: a latency
+    item, bound by the dependent fp64 Givens chain of the two eigen-solvers."""
+    import torch
+    from gvx import synth_ba
+    p = synth_ba.make_marg_problem(synth_ba.DeviceFactorEvaluator(ctx))
+    r = p["L"] - p["m"]
+    d_data = torch.from_numpy(p["data"]).to(dev)
+    d_J0 = torch.empty(r * r, dtype=torch.float64, device=dev)
+    d_e0 = torch.empty(r, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def run():
+        ctx.marginalize_dev(p, d_data.data_ptr(), d_J0.data_ptr(), d_e0.data_ptr())
+
+    for _ in range(2):
+        run()
+    ctx.sync()
+    ctx.profile_reset()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+        ctx.sync()
+    wall = (time.perf_counter() - t0) / reps
+    ms, k = ctx.profile_read("marg")
+    ctx.profile(False)
+    out = {"what": "device marginalisation of the configs[3] window (constructEquation + schurElimination + "
+                   "linearization, marginalization_info.h:153-230)",
+           "marginalized": p["m"], "remained": r, "residual_blocks": len(p["nres"]),
+           "device_ms_per_call": round(ms / max(k, 1), 3), "call_ms": round(wall * 1e3, 3),
+           "bound": "latency (dependent fp64 Givens chain, one workgroup per eigen-solver)", "cpu_baseline": None}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc  # test-infrastructure import: cpu_baseline leg only
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 3.0 or n < 2:
+            H0, b0 = orc.marg_construct(p)
+            Hp, bp, _ = orc.marg_schur(H0, b0, p["m"])
+            orc.marg_linearize(Hp, bp)
+            n += 1
+        el = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": round(el * 1e3, 2), "unit": "ms per marginalisation", "cores": 1,
+                               "kind": "port", "sample": f"{n} marginalisations of the same problem (oracle/marg.c, "
+                                                        "scalar C, Eigen's algorithms), 1 thread"}
+    return out
 
 
 def gather_tracks(tracks, counts, dist, dev):
