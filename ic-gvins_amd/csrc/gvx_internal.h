@@ -194,6 +194,12 @@ hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p);
 hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc,
                             int* info, unsigned long long* ts = nullptr);
 
+// ---- fmat.hip ----
+// cv::findFundamentalMat(FM_RANSAC) per point set: set i = points off[i] .. off[i+1]
+hipError_t launch_fm_ransac(gvx_ctx* c, int n_prob, const int32_t* off, const float* p1, const float* p2,
+                            double thresh, double confidence, int max_iters, uint8_t* mask, double* F,
+                            int32_t* result, unsigned long long* ts = nullptr);
+
 // ---- ins.hip ----
 hipError_t launch_ins(gvx_ctx* c, const gvx_ins_config& cfg, int n_chain, const gvx_imu* imu, const int32_t* off,
                       const gvx_state* state0, gvx_state* states);

@@ -195,6 +195,8 @@ def _declare(L):
         "gvx_marginalize": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
         "gvx_marginalize_dev": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
         "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
+        "gvx_find_fundamental_ransac": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
+        "gvx_find_fundamental_ransac_dev": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
         "gvx_capture_begin": (i32, [P]),
         "gvx_capture_end": (i32, [P, C.POINTER(P)]),
         "gvx_graph_launch": (i32, [P, P]),
@@ -335,6 +337,29 @@ class Context:
                                                      d_clahe_out), "frame_preprocess_dev")
 
     # ----------------------------------------------------------- camera ops
+    def find_fundamental_ransac(self, sets, thresh=1.5, confidence=0.99, max_iters=1000):
+        """cv::findFundamentalMat(p1, p2, FM_RANSAC, thresh, confidence, mask) per
+        (p1, p2) pair of float [n, 2] arrays in `sets` (tracking.cc:547-548) ->
+        list of (result, mask u8 [n], F [3, 3])."""
+        n = [len(np.asarray(a).reshape(-1, 2)) for a, _ in sets]
+        off = np.zeros(len(sets) + 1, np.int32)
+        off[1:] = np.cumsum(n)
+        p1 = np.ascontiguousarray(np.concatenate([np.asarray(a, np.float32).reshape(-1, 2) for a, _ in sets]))
+        p2 = np.ascontiguousarray(np.concatenate([np.asarray(b, np.float32).reshape(-1, 2) for _, b in sets]))
+        mask = np.zeros(max(int(off[-1]), 1), np.uint8)
+        F = np.zeros((len(sets), 9))
+        res = np.zeros(len(sets), np.int32)
+        self._check(self._L.gvx_find_fundamental_ransac(self._h, len(sets), _ptr(off), _ptr(p1), _ptr(p2), thresh,
+                                                        confidence, max_iters, _ptr(mask), _ptr(F), _ptr(res)),
+                    "gvx_find_fundamental_ransac")
+        return [(int(res[i]), mask[off[i]:off[i + 1]].copy(), F[i].reshape(3, 3)) for i in range(len(sets))]
+
+    def find_fundamental_ransac_dev(self, n_sets, d_off, d_p1, d_p2, d_mask, d_F, d_result, thresh=1.5,
+                                    confidence=0.99, max_iters=1000):
+        self._check(self._L.gvx_find_fundamental_ransac_dev(self._h, n_sets, d_off, d_p1, d_p2, thresh, confidence,
+                                                            max_iters, d_mask, d_F, d_result),
+                    "gvx_find_fundamental_ransac_dev")
+
     def undistort_points(self, cam: Camera, pts):
         """Camera::undistortPoints (camera.cc:72-74)."""
         p = _f32xy(pts)

@@ -194,3 +194,27 @@ def make_sequence(w: int, h: int, n_frames: int, device, seed: int = SEED, tex=N
         v = v + torch.randint(-2, 3, v.shape, device=device, generator=gen, dtype=torch.int32).to(v.dtype)
         out[t] = v.round().clamp(0, 255).to(torch.uint8)
     return out, tex
+
+
+def two_view_scene(n, outlier_frac=0.2, noise_px=0.3, seed=20261015, w=1280, h=560, f=787.0):
+    """Undistorted pixel correspondences of a static scene seen from two camera
+    poses (the reference points Tracking::trackReferenceFrame passes to
+    findFundamentalMat, tracking.cc:547), with Gaussian pixel noise and a fraction
+    of gross outliers.  -> (p1 f32 [n, 2], p2 f32 [n, 2], true-inlier bool [n])."""
+    rng = np.random.default_rng(seed)
+    K = np.array([[f, 0, w / 2], [0, f, h / 2], [0, 0, 1.0]])
+    X = np.c_[rng.uniform(-10, 10, n), rng.uniform(-4, 4, n), rng.uniform(5, 50, n)]
+    r = rng.normal(0, 0.02, 3)
+    th = np.linalg.norm(r)
+    kx = np.array([[0, -r[2], r[1]], [r[2], 0, -r[0]], [-r[1], r[0], 0]]) / max(th, 1e-12)
+    R = np.eye(3) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+    t = np.array([0.5, 0.02, 0.1]) + rng.normal(0, 0.05, 3)
+    x1 = (K @ X.T).T
+    x2 = (K @ (R @ X.T + t[:, None])).T
+    x1 = x1[:, :2] / x1[:, 2:]
+    x2 = x2[:, :2] / x2[:, 2:]
+    x1 += rng.normal(0, noise_px, x1.shape)
+    x2 += rng.normal(0, noise_px, x2.shape)
+    out = rng.random(n) < outlier_frac
+    x2[out] += rng.uniform(-30, 30, (int(out.sum()), 2))
+    return (np.ascontiguousarray(x1, np.float32), np.ascontiguousarray(x2, np.float32), ~out)

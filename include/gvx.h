@@ -237,6 +237,22 @@ gvx_status gvx_keypoint_parallax(gvx_ctx* ctx, const gvx_camera* cam, const doub
                                  int32_t n, const float* ref, const float* cur, double* out);
 gvx_status gvx_keypoint_parallax_dev(gvx_ctx* ctx, const gvx_camera* cam, const double* R0, const double* R1,
                                      int32_t n, const float* d_ref, const float* d_cur, double* d_out);
+/* cv::findFundamentalMat(p1, p2, FM_RANSAC, thresh, confidence, mask) with
+   OpenCV's maxIters (1000 in the reference's overload), the outlier rejection
+   of Tracking::trackReferenceFrame (tracking.cc:547-555: undistorted points,
+   thresh = reprojection_error_std_, confidence 0.99, then reduceVector with the
+   mask).  Batched over n_sets independent point sets: set i is points
+   off[i] .. off[i+1] of p1 / p2 (float x, y pairs).  mask (u8 per point): 1 =
+   inlier; result[i]: 1 = a model was found, 0 = none (mask all zero; OpenCV
+   would leave the caller's buffer as it was), -1 = fewer than 15 points (the
+   reference never calls it then: mask all one).  F (nullable): the best model
+   per set, row-major 3x3. */
+gvx_status gvx_find_fundamental_ransac(gvx_ctx* ctx, int32_t n_sets, const int32_t* off, const float* p1,
+                                       const float* p2, double thresh, double confidence, int32_t max_iters,
+                                       uint8_t* mask, double* F, int32_t* result);
+gvx_status gvx_find_fundamental_ransac_dev(gvx_ctx* ctx, int32_t n_sets, const int32_t* d_off, const float* d_p1,
+                                           const float* d_p2, double thresh, double confidence, int32_t max_iters,
+                                           uint8_t* d_mask, double* d_F, int32_t* d_result);
 
 /* ------------------------------------------------------ feature detection */
 /* Tracking::featuresDetection (tracking/tracking.cc:576-688): block grid from

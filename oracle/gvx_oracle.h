@@ -334,6 +334,20 @@ int orc_marg_schur(int L, int m, const double* H0, const double* b0, double* Hp,
 int orc_marg_linearize(int r, const double* Hp, const double* bp, double* J0, double* e0, double* eval);
 
 /* ------------------------------------------------------------------------- */
+/* cv::findFundamentalMat(FM_RANSAC) (fmat.c, tracking.cc:547-548)            */
+/* ------------------------------------------------------------------------- */
+/* count >= 15 float2 point pairs -> mask (1 = inlier); returns 1 (model found),
+   0 (none: mask zeroed), -1 (count < 15: OpenCV would run LMeDS, not modelled).
+   F (nullable): the best model, row-major; iters_out (nullable): iterations run. */
+int orc_find_fundamental_ransac(int count, const float* m1, const float* m2, double thresh, double confidence,
+                                int max_iters, unsigned char* mask, double* F, int* iters_out);
+int orc_run7point(const float* m1, const float* m2, double* F);       /* up to 3 models */
+int orc_solve_cubic(const double* coeffs, double* roots);
+void orc_fm_error(int n, const float* m1, const float* m2, const double* F, float* err);
+int orc_ransac_update_num_iters(double p, double ep, int model_points, int max_iters);
+unsigned orc_cvrng_next(uint64_t* state);
+
+/* ------------------------------------------------------------------------- */
 /* Camera operations (camera.c)                                               */
 /* ------------------------------------------------------------------------- */
 typedef struct {

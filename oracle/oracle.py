@@ -173,6 +173,18 @@ def lib():
         L.orc_marg_schur.restype = C.c_int
         L.orc_marg_linearize.argtypes = [C.c_int, P, P, P, P, P]
         L.orc_marg_linearize.restype = C.c_int
+        L.orc_find_fundamental_ransac.argtypes = [C.c_int, P, P, C.c_double, C.c_double, C.c_int, P, P,
+                                                  C.POINTER(C.c_int)]
+        L.orc_find_fundamental_ransac.restype = C.c_int
+        L.orc_run7point.argtypes = [P, P, P]
+        L.orc_run7point.restype = C.c_int
+        L.orc_solve_cubic.argtypes = [P, P]
+        L.orc_solve_cubic.restype = C.c_int
+        L.orc_fm_error.argtypes = [C.c_int, P, P, P, P]
+        L.orc_ransac_update_num_iters.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int]
+        L.orc_ransac_update_num_iters.restype = C.c_int
+        L.orc_cvrng_next.argtypes = [C.POINTER(C.c_uint64)]
+        L.orc_cvrng_next.restype = C.c_uint
         CP = C.POINTER(Camera)
         L.orc_undistort_points.argtypes = [CP, C.c_int, P, P]
         L.orc_distort_points.argtypes = [CP, C.c_int, P, P]
@@ -696,3 +708,51 @@ class FactorEvaluator:
 
     def marg(self, size, index, xoff, x0, x, J0, e0):
         return marg_factor_eval(size, index, xoff, x0, x, J0, e0)
+
+
+# ------------------------------------------------ findFundamentalMat(FM_RANSAC)
+def find_fundamental_ransac(p1, p2, thresh=1.5, confidence=0.99, max_iters=1000):
+    """cv::findFundamentalMat(p1, p2, FM_RANSAC, thresh, confidence) (fmat.c) ->
+    (result, mask u8 [n], F [3, 3] or None, iterations)."""
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    n = a.shape[0]
+    mask = np.zeros(max(n, 1), np.uint8)
+    F = np.zeros(9)
+    it = C.c_int(0)
+    r = lib().orc_find_fundamental_ransac(n, _p(a), _p(b), thresh, confidence, max_iters, _p(mask), _p(F),
+                                          C.byref(it))
+    return int(r), mask[:n], (F.reshape(3, 3) if r > 0 else None), int(it.value)
+
+
+def run7point(p1, p2):
+    a = np.ascontiguousarray(p1, np.float32).reshape(7, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(7, 2)
+    F = np.zeros(27)
+    n = lib().orc_run7point(_p(a), _p(b), _p(F))
+    return [F[9 * k:9 * k + 9].reshape(3, 3) for k in range(max(n, 0))]
+
+
+def solve_cubic(coeffs):
+    c = np.ascontiguousarray(coeffs, np.float64)
+    r = np.zeros(3)
+    n = lib().orc_solve_cubic(_p(c), _p(r))
+    return n, r
+
+
+def fm_error(p1, p2, F):
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    f = np.ascontiguousarray(F, np.float64).reshape(9)
+    err = np.zeros(a.shape[0], np.float32)
+    lib().orc_fm_error(a.shape[0], _p(a), _p(b), _p(f), _p(err))
+    return err
+
+
+def ransac_update_num_iters(p, ep, model_points, max_iters):
+    return int(lib().orc_ransac_update_num_iters(p, ep, model_points, max_iters))
+
+
+def cvrng_sequence(state, n):
+    s = C.c_uint64(state)
+    return [int(lib().orc_cvrng_next(C.byref(s))) for _ in range(n)]
