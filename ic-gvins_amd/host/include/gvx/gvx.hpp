@@ -10,6 +10,10 @@
 //   PreintegrationBase / Earth / Normal (preintegration/*.h)          gvx::Preintegration
 //   PreintegrationFactor::Evaluate (preintegration_factor.h:45-69)    gvx::PreintegrationFactor
 //   ReprojectionFactor::Evaluate (factors/reprojection_factor.h:61)   gvx::ReprojectionFactor
+//   cv::findFundamentalMat(FM_RANSAC) (tracking/tracking.cc:548)      gvx::findFundamentalMat
+//   ResidualBlockInfo (factors/residual_block_info.h)                 gvx::ResidualBlockInfo
+//   MarginalizationInfo (factors/marginalization_info.h)              gvx::MarginalizationInfo
+//   MarginalizationFactor::Evaluate (marginalization_factor.h:54)     gvx::MarginalizationFactor
 //
 // Errors: the C ABI never throws; this layer converts a non-OK status into
 // gvx::Error (the role cv::Exception plays for bad arguments in the reference).
@@ -23,6 +27,9 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <memory>
+#include <unordered_map>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -206,6 +213,28 @@ void reduceVector(std::vector<T>& vec, const std::vector<uint8_t>& status) {
     for (size_t i = 0; i < vec.size(); ++i)
         if (status[i]) vec[j++] = vec[i];
     vec.resize(j);
+}
+
+enum { FM_RANSAC = 8 };  // cv::FM_RANSAC
+// cv::findFundamentalMat(points1, points2, FM_RANSAC, ransacReprojThreshold,
+// confidence, mask) as tracking/tracking.cc:548 calls it (>= 15 points); the mask
+// is resized to the point count.  Returns false when no model was found (the mask
+// is then all zero).  F (optional): the best model, row-major.
+inline bool findFundamentalMat(Context& ctx, const std::vector<Point2f>& points1, const std::vector<Point2f>& points2,
+                               int method, double ransacReprojThreshold, double confidence,
+                               std::vector<uint8_t>& mask, double* F = nullptr, int maxIters = 1000) {
+    if (method != FM_RANSAC) throw Error(GVX_ERR_UNSUPPORTED, "findFundamentalMat: only FM_RANSAC is on the path");
+    if (points1.size() != points2.size()) throw Error(GVX_ERR_INVALID, "findFundamentalMat: point count mismatch");
+    const int32_t off[2] = {0, (int32_t)points1.size()};
+    mask.resize(points1.size());
+    int32_t result = 0;
+    double f[9];
+    check(gvx_find_fundamental_ransac(ctx.get(), 1, off, reinterpret_cast<const float*>(points1.data()),
+                                      reinterpret_cast<const float*>(points2.data()), ransacReprojThreshold,
+                                      confidence, maxIters, mask.data(), f, &result),
+          ctx.get(), "findFundamentalMat");
+    if (F && result == 1) std::memcpy(F, f, sizeof f);
+    return result != 0;
 }
 
 // Tracking::featuresDetection (tracking/tracking.cc:576-688) on a device frame:
@@ -704,6 +733,233 @@ public:
 private:
     Context* ctx_;
     gvx_factor_set* set_ = nullptr;
+};
+
+// ------------------------------------------------------- marginalisation
+constexpr int POSE_LOCAL_SIZE = 6, POSE_GLOBAL_SIZE = 7;  // factors/residual_block_info.h:26-27
+
+// ResidualBlockInfo (factors/residual_block_info.h:32-120): a cost function with
+// Ceres' Evaluate signature, its parameter blocks and which of them are
+// marginalized.  huber > 0 stands for a ceres::HuberLoss(huber) (the reference
+// passes nullptr; the device applies ResidualBlockInfo::Evaluate's corrector).
+class ResidualBlockInfo {
+public:
+    using CostFunction = std::function<bool(double const* const*, double*, double**)>;
+    ResidualBlockInfo(CostFunction cost_function, int num_residuals, std::vector<int> block_sizes, double huber,
+                      std::vector<double*> parameter_blocks, std::vector<int> marg_para_index)
+        : cost_(std::move(cost_function)), nres_(num_residuals), sizes_(std::move(block_sizes)), huber_(huber),
+          blocks_(std::move(parameter_blocks)), marg_(std::move(marg_para_index)) {}
+    // residuals then the row-major Jacobian blocks, contiguous (the gvx_marginalize layout)
+    void Evaluate() {
+        size_t total = (size_t)nres_;
+        for (int s : sizes_) total += (size_t)nres_ * s;
+        data_.assign(total, 0.0);
+        std::vector<double*> jac(sizes_.size());
+        size_t o = (size_t)nres_;
+        for (size_t i = 0; i < sizes_.size(); ++i) {
+            jac[i] = data_.data() + o;
+            o += (size_t)nres_ * sizes_[i];
+        }
+        if (!cost_(blocks_.data(), data_.data(), jac.data()))
+            throw Error(GVX_ERR_INVALID, "ResidualBlockInfo::Evaluate: cost function failed");
+    }
+    const std::vector<int>& parameterBlockSizes() const { return sizes_; }
+    const std::vector<double*>& parameterBlocks() const { return blocks_; }
+    const std::vector<int>& marginalizationParametersIndex() const { return marg_; }
+    int numResiduals() const { return nres_; }
+    double huber() const { return huber_; }
+    const std::vector<double>& data() const { return data_; }
+
+private:
+    CostFunction cost_;
+    int nres_;
+    std::vector<int> sizes_;
+    double huber_;
+    std::vector<double*> blocks_;
+    std::vector<int> marg_;
+    std::vector<double> data_;
+};
+
+// MarginalizationInfo (factors/marginalization_info.h:31-316): the same calls
+// and the same std::unordered_map bookkeeping (so the block order that
+// updateParameterBlocksIndex derives from the map iteration is the reference's);
+// constructEquation / schurElimination / linearization run on the device
+// through gvx_marginalize.  linearizedJacobians() is column-major r x r.
+class MarginalizationInfo {
+public:
+    explicit MarginalizationInfo(Context& ctx) : ctx_(&ctx) {}
+    MarginalizationInfo(const MarginalizationInfo&) = delete;
+    MarginalizationInfo& operator=(const MarginalizationInfo&) = delete;
+
+    bool isValid() const { return isvalid_; }
+    static int localSize(int size) { return size == POSE_GLOBAL_SIZE ? POSE_LOCAL_SIZE : size; }
+    static int globalSize(int size) { return size == POSE_LOCAL_SIZE ? POSE_GLOBAL_SIZE : size; }
+
+    void addResidualBlockInfo(const std::shared_ptr<ResidualBlockInfo>& blockinfo) {
+        factors_.push_back(blockinfo);
+        const auto& parameter_blocks = blockinfo->parameterBlocks();
+        const auto& block_sizes = blockinfo->parameterBlockSizes();
+        for (size_t k = 0; k < parameter_blocks.size(); k++)
+            parameter_block_size_[parameters_ids_[reinterpret_cast<long>(parameter_blocks[k])]] = block_sizes[k];
+        for (int index : blockinfo->marginalizationParametersIndex())
+            parameter_block_index_[parameters_ids_[reinterpret_cast<long>(parameter_blocks[index])]] = 0;
+    }
+    void updateParamtersIds(const std::unordered_map<long, long>& parameters_ids) { parameters_ids_ = parameters_ids; }
+
+    bool marginalization() {
+        if (!updateParameterBlocksIndex()) {
+            isvalid_ = false;
+            factors_.clear();
+            return false;
+        }
+        preMarginalization();
+        // the residual blocks in the gvx_marginalize layout, blocks numbered by id
+        std::unordered_map<long, int32_t> slot;
+        std::vector<int32_t> size, index;
+        for (const auto& b : parameter_block_index_) {
+            slot[b.first] = (int32_t)size.size();
+            size.push_back(parameter_block_size_[b.first]);
+            index.push_back(b.second);
+        }
+        std::vector<int32_t> nres, blk_off{0}, blk;
+        std::vector<int64_t> res_off, jac_off;
+        std::vector<double> data, loss;
+        bool any_loss = false;
+        for (const auto& f : factors_) {
+            nres.push_back(f->numResiduals());
+            for (double* p : f->parameterBlocks()) blk.push_back(slot.at(parameters_ids_[reinterpret_cast<long>(p)]));
+            blk_off.push_back((int32_t)blk.size());
+            res_off.push_back((int64_t)data.size());
+            jac_off.push_back((int64_t)data.size() + f->numResiduals());
+            data.insert(data.end(), f->data().begin(), f->data().end());
+            loss.push_back(f->huber());
+            any_loss |= f->huber() > 0;
+        }
+        const int r = remained_size_;
+        linearized_jacobians_.assign((size_t)r * r, 0.0);
+        linearized_residuals_.assign((size_t)r, 0.0);
+        int32_t info[2] = {0, 0};
+        check(gvx_marginalize(ctx_->get(), (int32_t)factors_.size(), nres.data(), blk_off.data(), blk.data(),
+                              res_off.data(), jac_off.data(), data.data(), (int64_t)data.size(),
+                              any_loss ? loss.data() : nullptr, (int32_t)size.size(), size.data(), index.data(),
+                              marginalized_size_, local_size_, linearized_jacobians_.data(),
+                              linearized_residuals_.data(), nullptr, nullptr, nullptr, info),
+              ctx_->get(), "MarginalizationInfo::marginalization");
+        factors_.clear();
+        return true;
+    }
+
+    std::vector<double*> getParamterBlocks(std::unordered_map<long, double*>& address) {
+        std::vector<double*> remained_block_addr;
+        remained_block_data_.clear();
+        remained_block_index_.clear();
+        remained_block_size_.clear();
+        for (const auto& block : parameter_block_index_) {
+            if (block.second >= marginalized_size_) {
+                remained_block_data_.push_back(parameter_block_data_[block.first].data());
+                remained_block_size_.push_back(parameter_block_size_[block.first]);
+                remained_block_index_.push_back(parameter_block_index_[block.first]);
+                remained_block_addr.push_back(address[block.first]);
+            }
+        }
+        return remained_block_addr;
+    }
+    const std::vector<double>& linearizedJacobians() const { return linearized_jacobians_; }
+    const std::vector<double>& linearizedResiduals() const { return linearized_residuals_; }
+    int marginalizedSize() const { return marginalized_size_; }
+    int remainedSize() const { return remained_size_; }
+    const std::vector<int>& remainedBlockSize() const { return remained_block_size_; }
+    const std::vector<int>& remainedBlockIndex() const { return remained_block_index_; }
+    const std::vector<double*>& remainedBlockData() const { return remained_block_data_; }
+    // the local index updateParameterBlocksIndex gave the block with this id (-1: none)
+    int blockIndex(long id) const {
+        auto it = parameter_block_index_.find(id);
+        return it == parameter_block_index_.end() ? -1 : it->second;
+    }
+
+private:
+    bool updateParameterBlocksIndex() {
+        int index = 0;
+        for (auto& block : parameter_block_index_) {
+            block.second = index;
+            index += localSize(parameter_block_size_[block.first]);
+        }
+        marginalized_size_ = index;
+        for (const auto& block : parameter_block_size_) {
+            if (parameter_block_index_.find(block.first) == parameter_block_index_.end()) {
+                parameter_block_index_[block.first] = index;
+                index += localSize(block.second);
+            }
+        }
+        remained_size_ = index - marginalized_size_;
+        local_size_ = index;
+        return marginalized_size_ > 0;
+    }
+    void preMarginalization() {
+        for (const auto& factor : factors_) {
+            factor->Evaluate();
+            const auto& block_sizes = factor->parameterBlockSizes();
+            for (size_t k = 0; k < block_sizes.size(); k++) {
+                const long id = parameters_ids_[reinterpret_cast<long>(factor->parameterBlocks()[k])];
+                if (parameter_block_data_.find(id) == parameter_block_data_.end()) {
+                    const double* p = factor->parameterBlocks()[k];
+                    parameter_block_data_[id].assign(p, p + block_sizes[k]);
+                }
+            }
+        }
+    }
+
+    Context* ctx_;
+    std::unordered_map<long, long> parameters_ids_;
+    std::unordered_map<long, int> parameter_block_size_;
+    std::unordered_map<long, int> parameter_block_index_;
+    std::unordered_map<long, std::vector<double>> parameter_block_data_;
+    std::vector<int> remained_block_size_, remained_block_index_;
+    std::vector<double*> remained_block_data_;
+    int marginalized_size_ = 0, remained_size_ = 0, local_size_ = 0;
+    std::vector<std::shared_ptr<ResidualBlockInfo>> factors_;
+    std::vector<double> linearized_jacobians_, linearized_residuals_;
+    bool isvalid_ = true;
+};
+
+// MarginalizationFactor::Evaluate (factors/marginalization_factor.h:54-110) on
+// the device from the previous MarginalizationInfo's J0 / e0 / x0.
+class MarginalizationFactor {
+public:
+    MarginalizationFactor(Context& ctx, std::shared_ptr<MarginalizationInfo> info) : ctx_(&ctx), info_(std::move(info)) {
+        const auto& sz = info_->remainedBlockSize();
+        int32_t o = 0;
+        for (size_t b = 0; b < sz.size(); ++b) {
+            size_.push_back(sz[b]);
+            index_.push_back(info_->remainedBlockIndex()[b] - info_->marginalizedSize());
+            xoff_.push_back(o);
+            x0_.insert(x0_.end(), info_->remainedBlockData()[b], info_->remainedBlockData()[b] + sz[b]);
+            o += sz[b];
+        }
+    }
+    std::vector<int> parameter_block_sizes() const { return std::vector<int>(size_.begin(), size_.end()); }
+    int num_residuals() const { return info_->remainedSize(); }
+    bool Evaluate(double const* const* parameters, double* residuals, double** jacobians) const {
+        const int r = info_->remainedSize();
+        std::vector<double> x;
+        for (size_t b = 0; b < size_.size(); ++b) x.insert(x.end(), parameters[b], parameters[b] + size_[b]);
+        std::vector<double> jac(jacobians ? (size_t)r * x.size() : 0);
+        check(gvx_marg_factor_eval(ctx_->get(), r, (int32_t)size_.size(), size_.data(), index_.data(), xoff_.data(),
+                                   (int32_t)x.size(), x0_.data(), x.data(), info_->linearizedJacobians().data(),
+                                   info_->linearizedResiduals().data(), residuals, jacobians ? jac.data() : nullptr),
+              ctx_->get(), "MarginalizationFactor::Evaluate");
+        if (jacobians)
+            for (size_t b = 0; b < size_.size(); ++b)
+                if (jacobians[b])
+                    std::memcpy(jacobians[b], jac.data() + (size_t)r * xoff_[b], sizeof(double) * r * size_[b]);
+        return true;
+    }
+
+private:
+    Context* ctx_;
+    std::shared_ptr<MarginalizationInfo> info_;
+    std::vector<int32_t> size_, index_, xoff_;
+    std::vector<double> x0_;
 };
 
 }  // namespace gvx

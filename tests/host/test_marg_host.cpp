@@ -1,0 +1,105 @@
+// C++ host mirror of MarginalizationInfo / ResidualBlockInfo / MarginalizationFactor
+// (ic-gvins_amd/host/include/gvx/gvx.hpp) driven like ic_gvins.cc:1464-1661 drives
+// the reference's: parameter ids in the reference's order, residual blocks added
+// with their marginalized indices, marginalization(), getParamterBlocks(), then a
+// MarginalizationFactor evaluated at the linearisation point.  The residual blocks
+// replay precomputed residuals / Jacobians (files from tests/test_host_cpp.py).
+// Usage: test_marg_host <dir>; writes <dir>/index.bin, J0.bin, e0.bin, res.bin.
+#include <gvx/gvx.hpp>
+
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+
+template <class T>
+static std::vector<T> load(const std::string& path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    const size_t n = (size_t)f.tellg() / sizeof(T);
+    std::vector<T> v(n);
+    f.seekg(0);
+    f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)(n * sizeof(T)));
+    return v;
+}
+
+template <class T>
+static void save(const std::string& path, const std::vector<T>& v) {
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 2;
+    const std::string d = argv[1];
+    try {
+        // blocks: sizes and values; factors: nres, block lists, marg indices, data
+        const auto bsize = load<int32_t>(d + "/bsize.bin");
+        const auto bval = load<double>(d + "/bval.bin");
+        const auto fmeta = load<int32_t>(d + "/fmeta.bin");  // per factor: nres, nblk, nmarg
+        const auto fblk = load<int32_t>(d + "/fblk.bin");
+        const auto fmarg = load<int32_t>(d + "/fmarg.bin");
+        const auto fdata = load<double>(d + "/fdata.bin");
+        gvx::Context ctx(0);
+        std::vector<std::vector<double>> blocks;
+        size_t o = 0;
+        for (int s : bsize) {
+            blocks.emplace_back(bval.begin() + (long)o, bval.begin() + (long)(o + s));
+            o += (size_t)s;
+        }
+        // ids: the order ic_gvins.cc:1468-1507 assigns (here simply the block order)
+        std::unordered_map<long, long> ids;
+        for (size_t b = 0; b < blocks.size(); ++b) ids[reinterpret_cast<long>(blocks[b].data())] = (long)b;
+        auto info = std::make_shared<gvx::MarginalizationInfo>(ctx);
+        info->updateParamtersIds(ids);
+        size_t pb = 0, pm = 0, pd = 0;
+        for (size_t f = 0; 3 * f < fmeta.size(); ++f) {
+            const int nres = fmeta[3 * f], nblk = fmeta[3 * f + 1], nmarg = fmeta[3 * f + 2];
+            std::vector<int> sizes;
+            std::vector<double*> params;
+            for (int k = 0; k < nblk; ++k) {
+                const int b = fblk[pb + k];
+                sizes.push_back(bsize[b]);
+                params.push_back(blocks[b].data());
+            }
+            size_t len = (size_t)nres;
+            for (int s : sizes) len += (size_t)nres * s;
+            std::vector<double> rec(fdata.begin() + (long)pd, fdata.begin() + (long)(pd + len));
+            auto cost = [rec, nres, sizes](double const* const*, double* res, double** jac) {
+                std::memcpy(res, rec.data(), sizeof(double) * nres);
+                size_t q = (size_t)nres;
+                for (size_t k = 0; k < sizes.size(); ++k) {
+                    if (jac && jac[k]) std::memcpy(jac[k], rec.data() + q, sizeof(double) * nres * sizes[k]);
+                    q += (size_t)nres * sizes[k];
+                }
+                return true;
+            };
+            std::vector<int> marg(fmarg.begin() + (long)pm, fmarg.begin() + (long)(pm + nmarg));
+            info->addResidualBlockInfo(std::make_shared<gvx::ResidualBlockInfo>(cost, nres, sizes, 0.0, params, marg));
+            pb += (size_t)nblk;
+            pm += (size_t)nmarg;
+            pd += len;
+        }
+        if (!info->marginalization()) {
+            std::cout << "NOT VALID" << std::endl;
+            return 1;
+        }
+        std::vector<int32_t> index;
+        for (size_t b = 0; b < blocks.size(); ++b) index.push_back(info->blockIndex((long)b));
+        std::unordered_map<long, double*> address;
+        for (size_t b = 0; b < blocks.size(); ++b) address[(long)b] = blocks[b].data();
+        const auto remained = info->getParamterBlocks(address);
+        // the next window's prior at its linearisation point: residual = e0 (dx = 0)
+        gvx::MarginalizationFactor factor(ctx, info);
+        std::vector<double> res((size_t)info->remainedSize());
+        if (!factor.Evaluate(remained.data(), res.data(), nullptr)) return 1;
+        save(d + "/index.bin", index);
+        save(d + "/J0.bin", info->linearizedJacobians());
+        save(d + "/e0.bin", info->linearizedResiduals());
+        save(d + "/res.bin", res);
+        std::cout << "OK " << info->marginalizedSize() << " " << info->remainedSize() << std::endl;
+    } catch (const gvx::Error& e) {
+        std::cout << "ERROR " << e.status() << " " << e.what() << std::endl;
+        return argc > 2 && std::string(argv[2]) == "nodev" ? 0 : 1;
+    }
+    return 0;
+}

@@ -153,3 +153,75 @@ def test_host_mirror_matches_oracle(host_bin, orc, tmp_path, variant):
     rr, rj = orc.reproj_eval(rcc, *rblocks)
     assert np.array_equal(rf[:2], rr)
     assert np.array_equal(rf[2:], np.concatenate([x.ravel() for x in rj]))
+
+
+@pytest.fixture(scope="module")
+def marg_bin(tmp_path_factory, gvx_mod):
+    out = str(tmp_path_factory.mktemp("host") / "test_marg_host")
+    libdir = os.path.dirname(gvx_mod.LIB_PATH)
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(ROOT, "ic-gvins_amd", "host", "include"),
+           os.path.join(ROOT, "tests", "host", "test_marg_host.cpp"), "-o", out, "-L", libdir, "-lgvx",
+           f"-Wl,-rpath,{libdir}", "-Wl,-rpath-link,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return out
+
+
+def _marg_files(d, orc):
+    """The configs[3]-shaped problem (synth_ba.make_marg_problem, small) as
+    replayable residual blocks for the C++ mirror."""
+    from gvx import synth_ba
+    p = synth_ba.make_marg_problem(orc.FactorEvaluator(), n_kf=4, n_lm=12)
+    nb = len(p["size"])
+    rng = np.random.default_rng(2)
+    vals = [rng.normal(size=int(s)) for s in p["size"]]
+    np.asarray(p["size"], np.int32).tofile(f"{d}/bsize.bin")
+    np.concatenate(vals).tofile(f"{d}/bval.bin")
+    meta, blk, marg, data = [], [], [], []
+    for f in range(len(p["nres"])):
+        bl = p["blk"][p["blk_off"][f]:p["blk_off"][f + 1]]
+        mg = [k for k, b in enumerate(bl) if p["index"][b] < p["m"]]
+        meta += [int(p["nres"][f]), len(bl), len(mg)]
+        blk += list(bl)
+        marg += mg
+        n = int(p["nres"][f]) * (1 + int(p["size"][bl].sum()))
+        data.append(p["data"][p["res_off"][f]:p["res_off"][f] + n])
+    np.asarray(meta, np.int32).tofile(f"{d}/fmeta.bin")
+    np.asarray(blk, np.int32).tofile(f"{d}/fblk.bin")
+    np.asarray(marg, np.int32).tofile(f"{d}/fmarg.bin")
+    np.concatenate(data).tofile(f"{d}/fdata.bin")
+    return p, nb
+
+
+def test_marg_mirror_fails_loudly_without_device(marg_bin, orc, tmp_path):
+    import torch
+    _marg_files(str(tmp_path), orc)
+    r = subprocess.run([marg_bin, str(tmp_path), "nodev"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    if not torch.cuda.is_available():
+        assert r.stdout.startswith("ERROR -2"), r.stdout
+
+
+@pytest.mark.gpu
+def test_marg_mirror_matches_oracle(marg_bin, orc, tmp_path):
+    """The mirror's block order comes from the reference's unordered_map walk;
+    given that order, its device J0 / e0 equal the restatement's bit for bit, and
+    the next MarginalizationFactor at the linearisation point returns e0."""
+    d = str(tmp_path)
+    p, nb = _marg_files(d, orc)
+    r = subprocess.run([marg_bin, d], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+    index = np.fromfile(f"{d}/index.bin", np.int32)
+    marg = set(np.nonzero(p["index"] < p["m"])[0])
+    m = int(sum(6 if p["size"][b] == 7 else p["size"][b] for b in marg))
+    assert all(index[b] < m for b in marg) and all(index[b] >= m for b in range(nb) if b not in marg)
+    q = dict(p, index=index)
+    H0, b0 = orc.marg_construct(q)
+    Hp, bp, _ = orc.marg_schur(H0, b0, m)
+    J0, e0, _, _ = orc.marg_linearize(Hp, bp)
+    r_ = p["L"] - m
+    assert np.array_equal(np.fromfile(f"{d}/J0.bin").reshape(r_, r_).T, J0)
+    assert np.array_equal(np.fromfile(f"{d}/e0.bin"), e0)
+    res = np.fromfile(f"{d}/res.bin")
+    np.testing.assert_allclose(res, e0, rtol=0, atol=1e-14 * np.abs(J0).sum(1).max())
