@@ -86,5 +86,7 @@ gvx_status gvx_copy_dev(gvx_ctx* c, void* d_dst, const void* d_src, size_t bytes
     if (bytes == 0) return GVX_OK;
     if (!d_dst || !d_src) return set_err(c, GVX_ERR_INVALID, "null device pointer");
     hipSetDevice(c->device);
-    return hip_err(c, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, c->stream), "hipMemcpyAsync D2D");
+    // a kernel, not hipMemcpyAsync: in a captured graph a memcpy node made the
+    // one-pair replay slower than the eager calls (67 vs 60 us, r01)
+    return hip_err(c, launch_copy(c, d_dst, d_src, bytes), "copy kernel");
 }

@@ -1,0 +1,250 @@
+// api_track.cpp -- gvx_track_frame_dev: one frame of Tracking::track's image
+// path (tracking/tracking.cc:144-245 without the IMU parts) with the tracker
+// state in device memory: forward + backward LK of the tracked points on two
+// cached frames, the FB / border / status filter and reduceVector, then the
+// block-grid detection topping the tracks up to track_max_features_.  No
+// host round trip: every count lives on the device (kernels in klt.hip,
+// detect.hip and track.hip), so the call is capturable into a hipGraph once the
+// scratch buffers and the detection constants exist (one uncaptured call).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "gvx_internal.h"
+
+using namespace gvx;
+
+extern "C" gvx_status gvx_track_frame_dev(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, int32_t track,
+                                          float* d_pts, float* d_vel, float* d_init, int32_t* d_n, int32_t cap,
+                                          int32_t cam_w, int32_t cam_h, double fb_thresh, double border,
+                                          const gvx_klt_params* kp, const gvx_detect_params* dp, int32_t* d_kept,
+                                          float* d_corners, int32_t* d_n_corners) {
+    if (!c || !kp || !dp) return GVX_ERR_INVALID;
+    if (!d_pts || !d_vel || !d_init || !d_n) return set_err(c, GVX_ERR_INVALID, "null tracker state");
+    if (cap <= 0 || cap < dp->max_features) return set_err(c, GVX_ERR_INVALID, "capacity %d < max_features", cap);
+    if (kp->win != WIN) return set_err(c, GVX_ERR_UNSUPPORTED, "device LK supports win=21 only (got %d)", kp->win);
+    if (dp->subpix_win != 5) return set_err(c, GVX_ERR_UNSUPPORTED, "cornerSubPix win must be 5 (tracking.cc:623)");
+    auto in = c->frames.find(next_id);
+    if (in == c->frames.end()) return set_err(c, GVX_ERR_NOT_FOUND, "frame %llu", (unsigned long long)next_id);
+    const Frame& fn = in->second;
+    const int W = fn.w, H = fn.h;
+    const Frame* fp = nullptr;
+    if (track) {
+        auto ip = c->frames.find(prev_id);
+        if (ip == c->frames.end()) return set_err(c, GVX_ERR_NOT_FOUND, "frame %llu", (unsigned long long)prev_id);
+        fp = &ip->second;
+        if (fp->w != W || fp->h != H) return set_err(c, GVX_ERR_INVALID, "frame sizes differ");
+    }
+    // Tracking ctor block grid (tracking.cc:65-85), as gvx_detect
+    const int bcols = (int)std::lround(W / dp->block_size);
+    const int brows = (int)std::lround(H / dp->block_size);
+    const int bcnt = bcols * brows;
+    if (bcols <= 0 || brows <= 0 || bcnt > 1024) return set_err(c, GVX_ERR_INVALID, "block grid %dx%d", bcols, brows);
+    const int row = H / brows, col = W / bcols;
+    const int maxpb = (int)std::lround((double)dp->max_features / (double)bcnt);
+    const int mindist = maxpb > 0 ? (int)std::round(dp->block_size / std::sqrt(maxpb * 1.5)) : 0;
+    const int64_t stride = (int64_t)col * row;
+    const int mpb = maxpb > 0 ? maxpb : 1;
+    hipSetDevice(c->device);
+    // scratch: LK flags, detection buffers, the counts
+    uint8_t *flags, *mask;
+    int2 *cent, *corn;
+    int *want, *ids, *nact, *ncirc, *skip, *nc;
+    float* eig;
+    unsigned long long* cand;
+    float2* out;
+    Staging st;
+    st.add((size_t)cap, &flags);
+    st.add((size_t)cap, &cent);
+    st.add((size_t)bcnt, &want);
+    st.add((size_t)bcnt, &ids);
+    st.add(1, &nact);
+    st.add(1, &ncirc);
+    st.add(1, &skip);
+    st.add((size_t)W * H, &mask);
+    st.add((size_t)stride * bcnt, &eig);
+    st.add((size_t)stride * bcnt, &cand);
+    st.add((size_t)mpb * bcnt, &corn);
+    st.add((size_t)bcnt, &nc);
+    st.add((size_t)mpb * bcnt, &out);
+    void* db = scratch(c, "trk", st.bytes());
+    if (!db) return set_err(c, GVX_ERR_OOM, "track scratch");
+    st.bind(db);
+    // detection constants (ROIs, circle half-widths, cornerSubPix weights): built
+    // and uploaded when the geometry changes, never inside a capture
+    int4* rois;
+    int* hw;
+    float* gm;
+    Staging sc;
+    sc.add((size_t)bcnt, &rois);
+    sc.add((size_t)mindist + 1, &hw);
+    sc.add(121, &gm);
+    void* sb = scratch(c, "trk_static", sc.bytes());
+    if (!sb) return set_err(c, GVX_ERR_OOM, "track constants");
+    sc.bind(sb);
+    const uint64_t key = ((uint64_t)W << 40) ^ ((uint64_t)H << 24) ^ ((uint64_t)dp->max_features << 8) ^
+                         (uint64_t)std::lround(dp->block_size) ^ (c->mem_gen << 52);
+    if (c->track_static_key != key) {
+        if (c->capturing) return set_err(c, GVX_ERR_INVALID, "detection constants not uploaded before the capture");
+        std::vector<int4> r(bcnt);
+        for (int k = 0; k < bcnt; ++k) {
+            const int bc = k % bcols, br = k / bcols;
+            int cs = bc * col, ce = cs + col, rs = br * row, re = rs + row;
+            if (k != bcnt - 1) {
+                ce -= 5;
+                re -= 5;
+            }
+            r[k] = make_int4(cs, rs, ce - cs, re - rs);
+        }
+        std::vector<int> h(mindist + 1, -1);
+        {
+            int err = 0, dx = mindist, dy = 0, plus = 1, minus = (mindist << 1) - 1;
+            while (dx >= dy) {
+                if (dy <= mindist) h[dy] = std::max(h[dy], dx);
+                if (dx <= mindist) h[dx] = std::max(h[dx], dy);
+                dy++;
+                err += plus;
+                plus += 2;
+                const int m = (err <= 0) - 1;
+                err -= minus & m;
+                dx += m;
+                minus -= m & 2;
+            }
+        }
+        float g[121];
+        for (int i = 0; i < 11; ++i) {
+            const float y = (float)(i - 5) / 5;
+            const float vy = std::exp(-y * y);
+            for (int j = 0; j < 11; ++j) {
+                const float x = (float)(j - 5) / 5;
+                g[i * 11 + j] = (float)(vy * std::exp(-x * x));
+            }
+        }
+        hipError_t e = hipMemcpyAsync(rois, r.data(), sizeof(int4) * bcnt, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(hw, h.data(), sizeof(int) * h.size(), hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(gm, g, sizeof g, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // pageable sources
+        if (e != hipSuccess) return hip_err(c, e, "track constants upload");
+        c->track_static_key = key;
+    }
+    hipEvent_t ev{};
+    hipError_t e = hipSuccess;
+    if (track) {
+        PyrLayout lay = fp->lay;
+        lay.nlev = make_layout(W, H, kp->max_level, kp->win).nlev;
+        if (lay.nlev > fp->lay.nlev || lay.nlev > fn.lay.nlev)
+            return set_err(c, GVX_ERR_INVALID, "frames were put with a smaller max_level");
+        KltArgs a{};
+        int it = kp->max_iter;
+        a.max_iter = it < 0 ? 0 : (it > 100 ? 100 : it);
+        const double ce = kp->eps < 0 ? 0.0 : (kp->eps > 10.0 ? 10.0 : kp->eps);
+        a.crit_eps = ce * ce;
+        a.min_eig = kp->min_eig;
+        a.use_initial_flow = 1;  // pts + vel, as SequenceTracker / Tracking::track
+        a.n_pairs = 1;
+        a.n_pts = cap;
+        a.n_dev = d_n;
+        a.mode = 1;
+        a.fb_thresh = fb_thresh;
+        a.border = border;
+        a.cam_w = cam_w;
+        a.cam_h = cam_h;
+        const Level0 l0{fp->pyr + lay.off[0], fn.pyr + lay.off[0], 0, 0, PAD * lay.pitch[0] + PAD, lay.pitch[0], 0};
+        prof_begin(c, "klt", &ev);
+        // d_init is the initial flow in and the tracked positions out
+        e = launch_klt(c, a, lay, fp->pyr, fn.pyr, 0, 0, l0, d_pts, d_init, nullptr, flags, nullptr);
+        prof_end(c, "klt", ev);
+        if (e != hipSuccess) return hip_err(c, e, "klt kernel");
+        prof_begin(c, "compact", &ev);
+        e = launch_track_update(c, cap, d_n, flags, d_init, d_pts, d_vel, d_init, d_kept);
+        prof_end(c, "compact", ev);
+        if (e != hipSuccess) return hip_err(c, e, "track update");
+    }
+    DetectPrep pp{};
+    pp.bcols = bcols;
+    pp.brows = brows;
+    pp.col = col;
+    pp.row = row;
+    pp.maxpb = maxpb;
+    pp.max_features = dp->max_features;
+    pp.pts = d_pts;
+    pp.n = d_n;
+    pp.want = want;
+    pp.blk_ids = ids;
+    pp.n_active = nact;
+    pp.centers = cent;
+    pp.n_circles = ncirc;
+    pp.skip = skip;
+    pp.ncorner = nc;
+    prof_begin(c, "detect", &ev);
+    e = launch_detect_prep(c, pp);
+    if (e == hipSuccess) {
+        DetectLaunch d{};
+        d.w = W;
+        d.h = H;
+        d.pitch = fn.lay.pitch[0];
+        d.img0 = fn.pyr + fn.lay.off[0] + (int64_t)PAD * d.pitch + PAD;
+        d.centers = cent;
+        d.n_circles = 0;
+        d.radius = mindist;
+        d.fill_mask = 1;
+        d.hw = hw;
+        d.mask = mask;
+        d.rois = rois;
+        d.blk_ids = ids;
+        d.n_active = 0;
+        d.n_blocks = bcnt;
+        d.max_rw = col;
+        d.max_rh = row;
+        d.want = want;
+        d.eig_stride = stride;
+        d.eig = eig;
+        d.cand = cand;
+        d.corners = corn;
+        d.ncorner = nc;
+        d.max_per_block = mpb;
+        d.quality = dp->quality;
+        d.min_dist = (float)mindist;
+        double s = (double)(1 << (3 - 1)) * 3;
+        s *= 255.0;
+        s = 1.0 / s;
+        d.sc = (float)s;
+        d.sc2 = (float)(2.0 * s);
+        d.gmask = gm;
+        d.max_iters = dp->subpix_iters < 1 ? 1 : (dp->subpix_iters > 100 ? 100 : dp->subpix_iters);
+        const double eps = dp->subpix_eps > 0 ? dp->subpix_eps : 0.0;
+        d.eps2 = eps * eps;
+        d.out = out;
+        d.n_circles_dev = ncirc;
+        d.n_active_dev = nact;
+        d.skip_dev = skip;
+        e = launch_detect(c, d);
+    }
+    if (e == hipSuccess)
+        e = launch_detect_merge(c, bcnt, bcols, col, row, mpb, dp->max_features, skip, nc, out, d_pts, d_vel, d_init,
+                                d_n, d_corners, d_n_corners);
+    prof_end(c, "detect", ev);
+    return hip_err(c, e, "detection kernels");
+}
+
+extern "C" gvx_status gvx_copy_indexed_dev(gvx_ctx* c, void* d_dst, const void* d_src_base, size_t bytes,
+                                           const int32_t* d_index) {
+    if (!c) return GVX_ERR_INVALID;
+    if (bytes == 0) return GVX_OK;
+    if (!d_dst || !d_src_base || !d_index) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    return hip_err(c, launch_copy_indexed(c, d_dst, d_src_base, bytes, d_index), "indexed copy kernel");
+}
+
+extern "C" gvx_status gvx_track_record_dev(gvx_ctx* c, const float* d_pts, const int32_t* d_n, int32_t capacity,
+                                           float* d_tracks, int32_t* d_counts, int32_t* d_frame_index,
+                                           int32_t max_frames) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!d_pts || !d_n || !d_tracks || !d_counts || !d_frame_index || capacity <= 0 || max_frames < 0)
+        return set_err(c, GVX_ERR_INVALID, "bad record arguments");
+    hipSetDevice(c->device);
+    return hip_err(c, launch_track_record(c, d_pts, d_n, capacity, d_tracks, d_counts, d_frame_index, max_frames),
+                   "track record kernel");
+}

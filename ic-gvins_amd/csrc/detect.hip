@@ -39,8 +39,11 @@ __device__ __forceinline__ int refl(int p, int len) {
 // ------------------------------------------------------------------ mask
 __global__ void __launch_bounds__(256) mask_kernel(int w, int h, const int2* __restrict__ centers, int n,
                                                    const int* __restrict__ hw, int r,
-                                                   uint8_t* __restrict__ mask) {
+                                                   uint8_t* __restrict__ mask, const int* __restrict__ n_dev,
+                                                   const int* __restrict__ skip) {
     __shared__ int2 sc[256];
+    if (skip && *skip) return;   // device-resident call: no detection this frame
+    if (n_dev) n = *n_dev;
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     bool hit = false;
@@ -65,9 +68,10 @@ constexpr int ET_W = 64, ET_H = 16;
 __global__ void __launch_bounds__(256) eig_kernel(const uint8_t* __restrict__ img0, int pitch,
                                                   const int4* __restrict__ rois, const int* __restrict__ blk_ids,
                                                   int64_t eig_stride, float* __restrict__ eig, float sc,
-                                                  float sc2) {
+                                                  float sc2, const int* __restrict__ n_active_dev) {
     __shared__ uint8_t px[ET_H + 4][ET_W + 4];
     __shared__ float cov[3][ET_H + 2][ET_W + 2];
+    if (n_active_dev && (int)blockIdx.z >= *n_active_dev) return;
     const int k = blk_ids[blockIdx.z];
     const int4 roi = rois[k];  // x0, y0, rw, rh
     const int rw = roi.z, rh = roi.w;
@@ -157,7 +161,8 @@ __global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__
                                                        const int* __restrict__ want, double quality,
                                                        float min_dist, unsigned long long* __restrict__ cand,
                                                        int2* __restrict__ corners, int max_per_block,
-                                                       int* __restrict__ ncorner) {
+                                                       int* __restrict__ ncorner, const int* __restrict__ n_active_dev) {
+    if (n_active_dev && (int)blockIdx.x >= *n_active_dev) return;
     __shared__ float s_max[SEL_T / 64];
     __shared__ int s_found[SEL_T / 64];
     __shared__ unsigned long long s_key[SEL_T / 64];
@@ -411,20 +416,24 @@ __global__ void __launch_bounds__(64) subpix_kernel(const uint8_t* __restrict__ 
 }  // namespace
 
 hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d) {
-    if (d.n_circles > 0 || d.fill_mask) {
+    // device-resident counts (n_active_dev): every launch is sized for all blocks
+    // / the capacity and the kernels read the counts, so the topology is fixed
+    const bool dev_counts = d.n_active_dev != nullptr;
+    if (d.n_circles > 0 || d.fill_mask || dev_counts) {
         dim3 g((d.w + 63) / 64, (d.h + 3) / 4);
         hipLaunchKernelGGL(mask_kernel, g, dim3(256), 0, c->stream, d.w, d.h, d.centers, d.n_circles, d.hw,
-                           d.radius, d.mask);
+                           d.radius, d.mask, d.n_circles_dev, d.skip_dev);
     }
-    if (d.n_active <= 0) return hipGetLastError();
+    const int n_act = dev_counts ? d.n_blocks : d.n_active;
+    if (n_act <= 0) return hipGetLastError();
     {
-        dim3 g((d.max_rw + ET_W - 1) / ET_W, (d.max_rh + ET_H - 1) / ET_H, d.n_active);
+        dim3 g((d.max_rw + ET_W - 1) / ET_W, (d.max_rh + ET_H - 1) / ET_H, n_act);
         hipLaunchKernelGGL(eig_kernel, g, dim3(256), 0, c->stream, d.img0, d.pitch, d.rois, d.blk_ids,
-                           d.eig_stride, d.eig, d.sc, d.sc2);
+                           d.eig_stride, d.eig, d.sc, d.sc2, d.n_active_dev);
     }
-    hipLaunchKernelGGL(select_kernel, dim3(d.n_active), dim3(SEL_T), 0, c->stream, d.eig, d.eig_stride, d.mask,
+    hipLaunchKernelGGL(select_kernel, dim3(n_act), dim3(SEL_T), 0, c->stream, d.eig, d.eig_stride, d.mask,
                        d.w, d.rois, d.blk_ids, d.want, d.quality, d.min_dist, d.cand, d.corners,
-                       d.max_per_block, d.ncorner);
+                       d.max_per_block, d.ncorner, d.n_active_dev);
     {
         dim3 g(d.max_per_block, d.n_blocks);
         hipLaunchKernelGGL(subpix_kernel, g, dim3(64), 0, c->stream, d.img0, d.pitch, d.rois, d.corners,

@@ -69,6 +69,8 @@ struct gvx_ctx {
     uint64_t mem_gen = 0;
     bool capturing = false;
     uint64_t capture_gen = 0;
+    // gvx_track_frame_dev: key of the detection constants uploaded to "trk_static"
+    uint64_t track_static_key = 0;
     // profiling
     bool prof = false;
     std::map<std::string, gvx::ProfEntry> prof_acc;
@@ -120,6 +122,9 @@ struct KltArgs {
     int32_t mode;            // 0: single LK, 1: fwd + bwd + FB
     double fb_thresh, border;
     int32_t cam_w, cam_h;
+    // device-resident point count (n_pairs == 1 only): the launch is sized for
+    // n_pts points (the capacity), the kernel tracks min(*n_dev, n_pts)
+    const int32_t* n_dev = nullptr;
 };
 
 // Level 0 of pair i: prev plane at prev + i*prev_stride, pixel (x, y) at byte
@@ -253,8 +258,42 @@ struct DetectLaunch {
     int max_iters;
     double eps2;
     float2* out;
+    // device-resident counts (gvx_track_frame_dev): circles, active blocks and a
+    // skip flag read by the kernels; nullptr for host-counted calls
+    const int* n_circles_dev = nullptr;
+    const int* n_active_dev = nullptr;
+    const int* skip_dev = nullptr;
 };
 hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d);
+
+// ---- track.hip (gvx_track_frame_dev, gvx_copy_dev) ----
+hipError_t launch_copy(gvx_ctx* c, void* dst, const void* src, size_t bytes);
+hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index);
+hipError_t launch_track_record(gvx_ctx* c, const float* pts, const int32_t* n, int cap, float* tracks,
+                               int32_t* counts, int32_t* frame, int max_frames);
+// the device tracker state after the forward/backward LK: keep-flag compaction,
+// pts <- next[kept], vel <- next[kept] - pts[kept], init <- pts + vel, n <- kept
+hipError_t launch_track_update(gvx_ctx* c, int cap, int32_t* n, const uint8_t* flags, const float* next_xy,
+                               float* pts, float* vel, float* init, int32_t* kept_out);
+struct DetectPrep {
+    int bcols, brows, col, row, maxpb, max_features;
+    const float* pts;
+    const int32_t* n;
+    int* want;
+    int* blk_ids;
+    int* n_active;
+    int2* centers;
+    int* n_circles;
+    int* skip;
+    int* ncorner;
+};
+hipError_t launch_detect_prep(gvx_ctx* c, const DetectPrep& p);
+// append the detected corners (block order, block origin added) up to
+// max_features: pts / init = corner, vel = 0, n grows; corners_out (nullable)
+// receives every corner and *n_corners_out their count (-1 when skipped)
+hipError_t launch_detect_merge(gvx_ctx* c, int bcnt, int bcols, int col, int row, int maxpb, int max_features,
+                               const int* skip, const int* ncorner, const float2* out, float* pts, float* vel,
+                               float* init, int32_t* n, float* corners_out, int32_t* n_corners_out);
 
 // Staging layout for host-pointer API calls: ONE list of slices both sizes the
 // buffer and carves it (256-byte aligned, in declaration order), so the two can

@@ -624,15 +624,18 @@ __global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel
     const int grp = lane / G, gl = lane & (G - 1);
     uint32_t* win = wins[wv * PPW + grp];
     v4u* ust = &units[wv][lane];
-    const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair
+    const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair (launch capacity)
     const int n_waves = a.n_pairs * wpp;
     const int nb = (n_waves + KLT_WPB - 1) / KLT_WPB;
     const int wg = xcd_swizzle(blockIdx.x, nb) * KLT_WPB + wv;
     if (wg >= n_waves) return;
     const int pair = wg / wpp;
     const int pt_raw = (wg - pair * wpp) * PPW + grp;
-    const bool own = pt_raw < a.n_pts;
-    const int64_t gp = (int64_t)pair * a.n_pts + (own ? pt_raw : a.n_pts - 1);
+    // device-resident count (the per-frame loop without host round trips)
+    const int npt = a.n_dev ? min(a.n_pts, *a.n_dev) : a.n_pts;
+    if ((wg - pair * wpp) * PPW >= npt) return;  // the whole wave is past the count
+    const bool own = pt_raw < npt;
+    const int64_t gp = (int64_t)pair * a.n_pts + (own ? pt_raw : npt - 1);
     const bool writer = own && gl == 0;
     const uint8_t* I = pyr_prev + pair * prev_stride;
     const uint8_t* J = pyr_next + pair * next_stride;

@@ -196,6 +196,10 @@ def _declare(L):
         "gvx_marginalize_dev": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
         "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
         "gvx_find_fundamental_ransac": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
+        "gvx_copy_indexed_dev": (i32, [P, P, P, C.c_size_t, P]),
+        "gvx_track_record_dev": (i32, [P, P, P, i32, P, P, P, i32]),
+        "gvx_track_frame_dev": (i32, [P, u64, u64, i32, P, P, P, P, i32, i32, i32, f64, f64, C.POINTER(KltParams),
+                                      C.POINTER(DetectParams), P, P, P]),
         "gvx_find_fundamental_ransac_dev": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
         "gvx_capture_begin": (i32, [P]),
         "gvx_capture_end": (i32, [P, C.POINTER(P)]),
@@ -337,6 +341,27 @@ class Context:
                                                      d_clahe_out), "frame_preprocess_dev")
 
     # ----------------------------------------------------------- camera ops
+    def track_frame_dev(self, prev_id: int, next_id: int, track: bool, d_pts, d_vel, d_init, d_n, capacity: int,
+                        cam_w: int, cam_h: int, klt: Optional[KltParams] = None,
+                        detect: Optional[DetectParams] = None, fb_thresh=0.5, border=5.0, d_kept=None,
+                        d_corners=None, d_n_corners=None):
+        """One frame of Tracking::track's image path with the tracker state in
+        device memory (pointers as ints), no host round trip (gvx_track_frame_dev)."""
+        kp = klt or KltParams.default()
+        dp = detect or DetectParams.default()
+        self._check(self._L.gvx_track_frame_dev(self._h, prev_id, next_id, 1 if track else 0, d_pts, d_vel, d_init,
+                                                d_n, capacity, cam_w, cam_h, fb_thresh, border, C.byref(kp),
+                                                C.byref(dp), d_kept, d_corners, d_n_corners),
+                    "gvx_track_frame_dev")
+
+    def copy_indexed_dev(self, d_dst: int, d_src_base: int, nbytes: int, d_index: int):
+        self._check(self._L.gvx_copy_indexed_dev(self._h, d_dst, d_src_base, nbytes, d_index), "gvx_copy_indexed_dev")
+
+    def track_record_dev(self, d_pts: int, d_n: int, capacity: int, d_tracks: int, d_counts: int,
+                         d_frame_index: int, max_frames: int):
+        self._check(self._L.gvx_track_record_dev(self._h, d_pts, d_n, capacity, d_tracks, d_counts, d_frame_index,
+                                                 max_frames), "gvx_track_record_dev")
+
     def find_fundamental_ransac(self, sets, thresh=1.5, confidence=0.99, max_iters=1000):
         """cv::findFundamentalMat(p1, p2, FM_RANSAC, thresh, confidence, mask) per
         (p1, p2) pair of float [n, 2] arrays in `sets` (tracking.cc:547-548) ->

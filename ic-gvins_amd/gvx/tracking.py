@@ -66,3 +66,85 @@ class SequenceTracker:
         self.last = rec
         self.t += 1
         return pts
+
+
+class DeviceSequenceTracker:
+    """SequenceTracker's loop with the tracker state on the device
+    (gvx_track_frame_dev): no host round trip per frame.
+
+    frames (optional): the whole sequence resident in HBM ([F, h, w] u8 tensor).
+    The frame to process is then picked on the device (gvx_copy_indexed_dev at a
+    device-held frame index) and every frame's track list is appended to
+    self.rec_tracks / self.rec_counts (gvx_track_record_dev, which advances the
+    index), so with graph=True a frame is exactly one graph launch: the work
+    (frame copy + CLAHE + pyramid + LK + FB + compaction + detection top-up +
+    record) is captured once per frame parity (the two cached frame ids
+    alternate) and replayed.  Without frames, step(d_frame) takes the frame's
+    device pointer (copied into a fixed staging buffer first in graph mode)."""
+
+    def __init__(self, ctx: Context, w: int, h: int, n_features: int = 150,
+                 klt: Optional[KltParams] = None, detect: Optional[DetectParams] = None,
+                 ids=(0, 1), graph: bool = False, device=None, frames=None):
+        import torch
+        self.ctx, self.w, self.h, self.n = ctx, w, h, n_features
+        self.kp = klt or KltParams.default()
+        self.dp = detect or DetectParams.default(max_features=n_features)
+        self.ids = ids
+        self.t = 0
+        dev = device or torch.device("cuda")
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.pts = torch.zeros((n_features, 2), **f32)
+        self.vel = torch.zeros((n_features, 2), **f32)
+        self.init = torch.zeros((n_features, 2), **f32)
+        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph = graph
+        self.graphs = {}
+        self.frames = frames
+        self.stage = torch.empty((h, w), dtype=torch.uint8, device=dev) if (graph or frames is not None) else None
+        if frames is not None:
+            F = frames.shape[0]
+            self.index = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.rec_tracks = torch.zeros((F, n_features, 2), **f32)
+            self.rec_counts = torch.zeros(F, dtype=torch.int32, device=dev)
+
+    def _enqueue(self, d_frame: Optional[int], t: int):
+        ctx = self.ctx
+        cur, prev = self.ids[t % 2], self.ids[(t - 1) % 2]
+        if self.frames is not None:
+            ctx.copy_indexed_dev(self.stage.data_ptr(), self.frames.data_ptr(), self.w * self.h,
+                                 self.index.data_ptr())
+            d_frame = self.stage.data_ptr()
+        ctx.frame_preprocess_dev(cur, d_frame, self.w, self.h, None, params=self.kp)
+        ctx.track_frame_dev(prev, cur, t > 0, self.pts.data_ptr(), self.vel.data_ptr(), self.init.data_ptr(),
+                            self.count.data_ptr(), self.n, self.w, self.h, klt=self.kp, detect=self.dp)
+        if self.frames is not None:
+            ctx.track_record_dev(self.pts.data_ptr(), self.count.data_ptr(), self.n, self.rec_tracks.data_ptr(),
+                                 self.rec_counts.data_ptr(), self.index.data_ptr(), self.frames.shape[0])
+
+    def step(self, d_frame: Optional[int] = None) -> None:
+        """Enqueue one frame (nothing waits); the tracks are
+        self.pts[:self.count] once the stream has run it."""
+        t = self.t
+        if not self.graph or t < 3:
+            self._enqueue(d_frame, t)  # the first frames also size every buffer
+        else:
+            if self.frames is None:
+                self.ctx.copy_dev(self.stage.data_ptr(), d_frame, self.w * self.h)
+            g = self.graphs.get(t % 2)
+            if g is None:
+                self.ctx.capture_begin()
+                self._enqueue(None if self.frames is not None else self.stage.data_ptr(), t)
+                g = self.graphs[t % 2] = self.ctx.capture_end()
+            self.ctx.graph_launch(g)
+        self.t += 1
+
+    def tracks(self) -> np.ndarray:
+        """The current track list (synchronises)."""
+        self.ctx.sync()
+        n = int(self.count.cpu()[0])
+        return self.pts[:n].cpu().numpy()
+
+    def close(self):
+        for g in self.graphs.values():
+            g.destroy()
+        self.graphs = {}

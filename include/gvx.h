@@ -71,7 +71,8 @@ gvx_status gvx_capture_end(gvx_ctx* ctx, gvx_graph** out);
 gvx_status gvx_graph_launch(gvx_ctx* ctx, const gvx_graph* g);
 void gvx_graph_destroy(gvx_graph* g);
 /* Device-to-device copy on the context stream (capturable: e.g. the initial
-   flow copied into next_xy before each replay). */
+   flow copied into next_xy before each replay).  A copy kernel on the compute
+   queue (no DMA engine hand-off inside a graph). */
 gvx_status gvx_copy_dev(gvx_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 
 /* ------------------------------------------------------------------ KLT  */
@@ -279,6 +280,37 @@ gvx_status gvx_detect(gvx_ctx* ctx, uint64_t frame_id, const float* count_xy, in
                       const float* mask_xy, int32_t n_mask, int32_t ismask, int32_t n_existing,
                       const gvx_detect_params* p, float* out_xy, int32_t* out_block_counts,
                       int32_t* n_out);
+
+/* ------------------------------------------- one frame, device-resident */
+/* Tracking::track's image path for one frame (tracking/tracking.cc:144-245, the
+   parts SequenceTracker follows) with the tracker state in device memory and no
+   host round trip: when `track`, forward + backward LK of the *d_n points d_pts
+   from prev_frame into next_frame with the initial flow d_init, the FB / border /
+   status filter and reduceVector (:380-408, :831-849), giving d_pts <- tracked,
+   d_vel <- tracked - previous, d_init <- d_pts + d_vel, *d_n <- kept; then, while
+   *d_n < max_features (and not above max_features - 5), featuresDetection on
+   next_frame (:576-688) with the tracked points as counts and mask, its corners
+   appended in block order up to max_features (vel 0).  capacity >= max_features
+   entries per state array.  d_kept (nullable): the kept indices; d_corners
+   (nullable, blocks x maxCorners float2) / d_n_corners: every detected corner and
+   their count (-1: detection skipped).  Every count stays on the device, so after
+   one uncaptured call (it uploads the detection constants) the call can be
+   captured into a hipGraph and replayed per frame. */
+gvx_status gvx_track_frame_dev(gvx_ctx* ctx, uint64_t prev_frame, uint64_t next_frame, int32_t track, float* d_pts,
+                               float* d_vel, float* d_init, int32_t* d_n, int32_t capacity, int32_t cam_w,
+                               int32_t cam_h, double fb_thresh, double border, const gvx_klt_params* klt,
+                               const gvx_detect_params* detect, int32_t* d_kept, float* d_corners,
+                               int32_t* d_n_corners);
+/* Helpers that keep a replay loop inside one captured graph per frame: copy
+   bytes from d_src_base + (*d_index) * bytes (e.g. frame *d_index of a sequence
+   resident in HBM), and append the current track list (*d_n points of d_pts) to
+   d_tracks[*d_frame_index * capacity ..] / d_counts[*d_frame_index], then
+   advance *d_frame_index (frames >= max_frames are not stored). */
+gvx_status gvx_copy_indexed_dev(gvx_ctx* ctx, void* d_dst, const void* d_src_base, size_t bytes,
+                                const int32_t* d_index);
+gvx_status gvx_track_record_dev(gvx_ctx* ctx, const float* d_pts, const int32_t* d_n, int32_t capacity,
+                                float* d_tracks, int32_t* d_counts, int32_t* d_frame_index, int32_t max_frames);
+
 
 /* --------------------------------------------------- IMU preintegration */
 enum { GVX_PREINT_NORMAL = 0, GVX_PREINT_EARTH = 2 }; /* preintegration.h:38-43 */

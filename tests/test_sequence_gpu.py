@@ -78,3 +78,43 @@ def test_sequence_replay_bit_exact(ctx, orc, gvx_mod, n_frames):
         assert np.array_equal(pts, o["pts"]), f"frame {t}: track list"
     # the sequence exercised both halves of the loop
     assert n_tracked > 100 * (n_frames - 1) and n_detect >= 2
+
+
+@pytest.mark.parametrize("graph,resident", [(False, False), (True, False), (True, True)])
+def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident):
+    """gvx_track_frame_dev (the tracker state on the device, no host round trip;
+    with graph=True one captured graph per frame parity replayed per frame)
+    gives the same per-frame track list as SequenceTracker, whose every step the
+    test above holds bit-exact against the oracle."""
+    import torch
+    from gvx import synth
+    from gvx.tracking import DeviceSequenceTracker, SequenceTracker
+    dev = torch.device("cuda", 0)
+    n_frames = 30
+    frames, _ = synth.make_sequence(W, H, n_frames, dev, seed=synth.SEED + 1)
+    kp = gvx_mod.KltParams.default(max_level=L)
+    dp = gvx_mod.DetectParams.default(max_features=N)
+    ref = SequenceTracker(ctx, W, H, N, klt=kp, detect=dp, ids=(10, 11))
+    trk = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, ids=(20, 21), graph=graph, device=dev,
+                                frames=frames if resident else None)
+    try:
+        wants = []
+        for t in range(n_frames):
+            wants.append(ref.step(frames[t].data_ptr()))
+            if resident:
+                trk.step()  # the frame is picked on the device, nothing is read back per frame
+                continue
+            trk.step(frames[t].data_ptr())
+            got = trk.tracks()
+            assert np.array_equal(got, wants[t]), f"frame {t}: {got.shape} vs {wants[t].shape}"
+        if resident:
+            ctx.sync()
+            counts = trk.rec_counts.cpu().numpy()
+            tracks = trk.rec_tracks.cpu().numpy()
+            assert int(trk.index.cpu()[0]) == n_frames
+            for t in range(n_frames):
+                assert np.array_equal(tracks[t, :counts[t]], wants[t]), f"frame {t}"
+        if graph:
+            assert len(trk.graphs) == 2
+    finally:
+        trk.close()
