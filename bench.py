@@ -155,6 +155,9 @@ def main():
                          "3 = 1920x1200/500 L4 batch, 4 = sliding-window BA factor batch, "
                          "5 = sequence replay (one sequence per GPU, RCCL gather of the tracks)")
     ap.add_argument("--frames", type=int, default=2000, help="configs[4]: frames per sequence")
+    ap.add_argument("--host-loop", action="store_true",
+                    help="configs[4]: the per-frame loop with host round trips (SequenceTracker) instead of the "
+                         "device-resident one-graph-per-frame loop")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
     world_env = os.environ.get("WORLD_SIZE")
@@ -767,19 +770,30 @@ def sequence_main(args):
     frames, _ = synth.make_sequence(W, H, F, dev, seed=synth.SEED + 7919 * rank)
     torch.cuda.synchronize()
     ctx = gvx.Context(local)
-    from gvx.tracking import SequenceTracker
+    from gvx.tracking import DeviceSequenceTracker, SequenceTracker
     kp = gvx.KltParams.default(max_level=L)
-    tracker = SequenceTracker(ctx, W, H, N, klt=kp, detect=gvx.DetectParams.default(max_features=N))
+    dp = gvx.DetectParams.default(max_features=N)
     tracks = np.zeros((F, N, 2), np.float32)
     counts = np.zeros(F, np.int32)
     stats = {"detect_frames": 0}
+    device_loop = not args.host_loop
+    if device_loop:
+        # the whole frame (pick frame t on the device, CLAHE + pyramid, LK fwd/bwd +
+        # FB + compaction, detection top-up, record the track list) is one graph
+        # launch: no host round trip, the host only enqueues
+        tracker = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=True, device=dev, frames=frames)
 
-    def frame(t):
-        pts = tracker.step(frames[t].data_ptr())
-        if "corners" in tracker.last:
-            stats["detect_frames"] += 1
-        tracks[t, :pts.shape[0]] = pts
-        counts[t] = pts.shape[0]
+        def frame(t):
+            tracker.step()
+    else:
+        tracker = SequenceTracker(ctx, W, H, N, klt=kp, detect=dp)
+
+        def frame(t):
+            pts = tracker.step(frames[t].data_ptr())
+            if "corners" in tracker.last:
+                stats["detect_frames"] += 1
+            tracks[t, :pts.shape[0]] = pts
+            counts[t] = pts.shape[0]
 
     t = 0
     for _ in range(args.warmup):
@@ -790,22 +804,46 @@ def sequence_main(args):
         dist.barrier()
     stats["detect_frames"] = 0
     ctx.profile_reset()
-    ctx.profile(True)
+    # per-family device times need event brackets around each call: profile the
+    # host loop's calls, and the device loop on a separate pass below
+    ctx.profile(not device_loop)
     t0 = time.perf_counter()
     timed = 0
     while t < F:
         frame(t)
         t += 1
         timed += 1
+    if device_loop:
+        ctx.sync()
+        tracks[:] = tracker.rec_tracks.cpu().numpy()
+        counts[:] = tracker.rec_counts.cpu().numpy()
     ctx.sync()
     gathered = gather_tracks(torch.from_numpy(tracks), torch.from_numpy(counts), dist, dev)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    fam = {f: ctx.profile_read(f) for f in ("clahe", "pyramid", "klt", "compact", "detect")}
-    fam = {k: v for k, v in fam.items() if v[1] > 0}
-    ctx.profile(False)
+    if device_loop:
+        # device time per kernel family of the same per-frame work, eager with event
+        # brackets (outside the timed region: a captured graph cannot hold them)
+        prof = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=False, device=dev, frames=frames,
+                                     ids=(2, 3))
+        for _ in range(min(F, args.warmup + 2)):
+            prof.step()
+        ctx.sync()
+        ctx.profile_reset()
+        ctx.profile(True)
+        k_prof = min(F - prof.t, 200)
+        for _ in range(k_prof):
+            prof.step()
+        ctx.sync()
+        fam = {f: ctx.profile_read(f) for f in ("clahe", "pyramid", "klt", "compact", "detect")}
+        fam = {k: (v[0] * timed / k_prof, v[1]) for k, v in fam.items() if v[1] > 0}
+        ctx.profile(False)
+    else:
+        fam = {f: ctx.profile_read(f) for f in ("clahe", "pyramid", "klt", "compact", "detect")}
+        fam = {k: v for k, v in fam.items() if v[1] > 0}
+        ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
     if rank == 0:
         value = world * timed / elapsed
@@ -832,6 +870,8 @@ def sequence_main(args):
             "config": {"workload": f"configs[4]: one {F}-frame sequence per GPU, {W}x{H} mono, {N} feat, maxLevel "
                                    f"{L}: per frame CLAHE + pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
                                    f"RCCL gather of all per-frame tracks to rank 0",
+                       "loop": ("device-resident: one captured hipGraph launch per frame (gvx_track_frame_dev)"
+                                if device_loop else "host loop: SequenceTracker, host round trips per frame"),
                        "parallelism": f"sequences sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
@@ -839,7 +879,9 @@ def sequence_main(args):
                          "traffic": None, "algorithmic_bytes_per_frame": B,
                          "device_ms_per_frame": {k: round(v[0] / timed, 4) for k, v in fam.items()}},
             "cpu_baseline": cpu,
-            "tracks_per_frame_mean": round(float(tr.mean()), 1), "detect_frames": stats["detect_frames"],
+            "tracks_per_frame_mean": round(float(tr.mean()), 1),
+            "detect_frames": stats["detect_frames"] if not device_loop else None,
+            "host_overhead_frac": round(max(0.0, 1.0 - dev_ms / (elapsed / timed * 1e3)), 3) if dev_ms else None,
             "gathered_ranks": len(gathered) if gathered else 0,
         }))
     if dist:
