@@ -367,10 +367,27 @@ def single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps):
         ctx.graph_launch(g)
     ctx.sync()
     graph = (time.perf_counter() - t0) / reps
+    # two instantiations of the same work launched alternately: back-to-back
+    # launches of ONE graph exec serialise on the host in ROCm's runtime
+    ctx.capture_begin()
+    enqueue(outs[1])
+    g2 = ctx.capture_end()
+    for _ in range(20):
+        ctx.graph_launch(g)
+        ctx.graph_launch(g2)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps // 2):
+        ctx.graph_launch(g)
+        ctx.graph_launch(g2)
+    ctx.sync()
+    graph2 = (time.perf_counter() - t0) / (2 * (reps // 2))
     same = all(torch.equal(outs[0][k], outs[1][k]) for k in outs[0])
     g.destroy()
+    g2.destroy()
     return {"what": "one frame pair per launch, back to back: initial-flow copy + pyramids + LK + compaction",
             "us_per_pair_eager": round(eager * 1e6, 2), "us_per_pair_graph": round(graph * 1e6, 2),
+            "us_per_pair_two_graphs": round(graph2 * 1e6, 2),
             "pairs_per_s_graph": round(1.0 / graph, 1), "graph_matches_eager": same, "reps": reps}
 
 
