@@ -8,6 +8,7 @@ Usage: python3 tools/traffic.py gpurun_out/<tag> [--workload KEY]"""
 import argparse
 import json
 import os
+import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(__file__))
@@ -36,7 +37,12 @@ for name, n in PER_STEP.items():
     kern[name] = {"bytes_per_launch": b, "fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
                   "launches_per_step": n}
     step += n * b
-out = {"workload": a.workload, "pairs_per_step": a.pairs, "bytes_per_step": step,
+try:
+    commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                            cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip()
+except OSError:
+    commit = ""
+out = {"workload": a.workload, "pairs_per_step": a.pairs, "bytes_per_step": step, "commit": commit,
        "bytes_per_pair": step / a.pairs, "kernels": kern, "source": os.path.relpath(a.pmc_dir),
        "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md HBM"}
 json.dump(out, open(a.out, "w"), indent=1)
