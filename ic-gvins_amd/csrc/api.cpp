@@ -357,6 +357,38 @@ gvx_status gvx_frame_level_padded(gvx_ctx* c, uint64_t id, int32_t level, int32_
     return hip_err(c, hipStreamSynchronize(c->stream), "copy level sync");
 }
 
+gvx_status gvx_pyramid_layout(int32_t w, int32_t h, int32_t max_level, int32_t* nlev, int64_t* off,
+                              int32_t* pitch, int32_t* lw, int32_t* lh, int64_t* bytes) {
+    if (w <= WIN || h <= WIN || max_level < 0) return GVX_ERR_INVALID;
+    const PyrLayout L = make_layout(w, h, max_level, WIN);
+    if (nlev) *nlev = L.nlev;
+    for (int l = 0; l < L.nlev; ++l) {
+        if (off) off[l] = L.off[l];
+        if (pitch) pitch[l] = L.pitch[l];
+        if (lw) lw[l] = L.w[l];
+        if (lh) lh[l] = L.h[l];
+    }
+    if (bytes) *bytes = L.bytes;
+    return GVX_OK;
+}
+
+gvx_status gvx_build_pyramids_dev(gvx_ctx* c, int32_t n_img, int32_t w, int32_t h, const uint8_t* d_imgs,
+                                  int64_t img_stride, int32_t stride, int32_t max_level, uint8_t* d_out) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n_img < 0 || w <= WIN || h <= WIN || stride < w || img_stride < (int64_t)stride * (h - 1) + w ||
+        max_level < 0 || max_level >= MAX_LEVELS)
+        return set_err(c, GVX_ERR_INVALID, "bad pyramid batch");
+    if (n_img == 0) return GVX_OK;
+    if (!d_imgs || !d_out) return set_err(c, GVX_ERR_INVALID, "bad pyramid batch pointers");
+    hipSetDevice(c->device);
+    const PyrLayout lay = make_layout(w, h, max_level, WIN);
+    hipEvent_t ev{};
+    prof_begin(c, "pyramid", &ev);
+    hipError_t e = launch_build_pyramids(c, d_imgs, img_stride, stride, n_img, lay, d_out, false);
+    prof_end(c, "pyramid", ev);
+    return hip_err(c, e, "pyramid kernels");
+}
+
 // Shared single-pair path of gvx_klt / gvx_klt_fb.
 static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, const float* prev_xy,
                              float* next_xy, float* back_xy, uint8_t* flags_out, float* err,

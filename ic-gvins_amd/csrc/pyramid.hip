@@ -12,9 +12,9 @@
 // reads across ROI edges).
 //
 //   level0_kernel   padded copy of level 0 (frame cache only)
-//   edge_kernel     REFLECT_101 edge bands of level 0 (batched path)
-//   stream_kernel<NL> NL pyrDown levels in one streaming pass per band
-//   ring_kernel     the PAD rings of all built levels >= 1, one launch
+//   stream_kernel<NL> NL pyrDown levels and their PAD rings in one streaming
+//                   pass (level 0 read in place, REFLECT_101 gathered at its edges)
+//   ring_kernel     the rings of levels too small for the pass (< RING_MIN)
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -73,11 +73,6 @@ __global__ void __launch_bounds__(256) level0_kernel(const uint8_t* __restrict__
 }
 
 // ------------------------------------------------------------ pyrDown helpers
-struct DownLevels {
-    int64_t off[3];  // padded-level offsets (bytes) inside one pyramid
-    int32_t pitch[3], w[3], h[3];
-};
-
 // Horizontal [1 4 6 4 1] taps of one source row into four u16 outputs: outputs
 // 4g..4g+3 read source bytes 8g .. 8g+10 of the row (`sh` = byte shift of the row
 // start inside its first dword, 0 or 2).
@@ -132,30 +127,44 @@ __device__ __forceinline__ uint32_t hibytes(uint32_t lo, uint32_t hi) {
 //   neighbours from lanes L-1 / L+1 with DPP wave shifts, so valid results
 //   shrink by one lane per level and lanes 2..61 own the strip (480 source
 //   columns per strip, 7 % overlap).
-// Band b owns level-1 rows [BAND*b, BAND*(b+1)) (level k: the same >> (k-1)).
-// Borders: source rows / columns are REFLECT_101-extended at load.  Because the
-// filter is symmetric, the extension of a level computed from an extended
-// source IS the REFLECT_101 extension of that level at the left / top edges;
-// at the right / bottom edges it is not when the level size is even, so the
-// columns >= w are re-gathered from their mirror lanes (ds_bpermute) and the
-// rows >= h are taken from their mirror rows in the rolling registers.
+// Band b owns level-1 rows [band*b, band*(b+1)) (level k: the same >> (k-1)).
+// Borders, all inside this one pass:
+//  * source columns are REFLECT_101-extended at load: the strips that touch an
+//    edge of an unpadded level 0 gather each output dword with one v_perm of an
+//    aligned dword pair at a per-lane offset (fixed for the strip); a padded
+//    source is read through its ring;
+//  * because the filter is symmetric, a level computed from an extended source
+//    IS the REFLECT_101 extension of that level at the left / top edges; at the
+//    right / bottom edges it is not when the level size is even, so the columns
+//    >= w are re-gathered from their mirror lanes (DPP + v_perm) and the rows
+//    >= h are taken from their mirror rows in the rolling registers;
+//  * the PAD ring of each level is written by the lanes that hold its source
+//    pixels: the top / bottom ring rows are extra stores of the mirrored rows,
+//    the side bands extra stores of the mirrored columns (level 1: one dword per
+//    lane, built with a DPP neighbour and a v_perm; levels 2 and 3: bytes).
+//    Levels narrower or shorter than RING_MIN take their ring from ring_kernel.
 constexpr int ST_COLS = 480;  // source columns owned per strip
 #ifndef STREAM_BAND
 #define STREAM_BAND 32
 #endif
 constexpr int BAND = STREAM_BAND;  // level-1 rows owned per band (level k: BAND >> (k-1))
 
-// Levels of at least RING_MIRROR_H rows get their top / bottom ring rows from
-// the streaming pass (each ring row is a single-bounce REFLECT_101 copy of one
-// interior row); shorter levels get the whole ring from ring_kernel.
-constexpr int RING_MIRROR_H = 2 * PAD + 2;
+// Levels at least RING_MIN pixels wide and tall get their whole PAD ring from
+// the streaming pass (every ring pixel is then a single-bounce REFLECT_101 copy
+// of an interior pixel); smaller levels get it from ring_kernel.
+constexpr int RING_MIN = 2 * PAD + 2;
 // The top / bottom ring row that is the REFLECT_101 copy of row r (rows 1..PAD
 // -> -r, rows h-1-PAD..h-2 -> 2h-2-r), or r itself when none is.
 __device__ __forceinline__ int mirror_row(int r, int h) {
-    if (h < RING_MIRROR_H) return r;
+    if (h < RING_MIN) return r;
     if (r >= 1 && r <= PAD) return -r;
     if (r >= h - 1 - PAD && r <= h - 2) return 2 * h - 2 - r;
     return r;
+}
+// The side-band column that is the REFLECT_101 copy of column c (1..PAD -> -c,
+// w-1-PAD..w-2 -> 2w-2-c), or 0 when none is (column 0 is never a ring column).
+__device__ __forceinline__ int ring_col(int c, int w) {
+    return (c >= 1 && c <= PAD) ? -c : (c >= w - 1 - PAD && c <= w - 2) ? 2 * w - 2 - c : 0;
 }
 
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane L <- lane L-1
@@ -165,92 +174,72 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane L <- lane L
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
 }
 
-// Edge bands: for every source row, the REFLECT_101-extended columns
-// [-32, 16) and [w-16, w+32) are stored in a padded plane (the pyramid's unused
-// level-0 slot on the batched path, the padded level 0 itself in the frame
-// cache).  Lanes whose 16-byte window leaves [48, w-48) read the band instead
-// of the source, so the streaming loop never gathers bytes: every row is one
-// 16-byte load per lane and the prefetched rows stay in flight.
-struct EdgePlane {
-    const uint8_t* base;  // pixel (0,0) of image 0
+// Source of a pass: images [0, n_a) at a + i*img_stride, the rest at
+// b + (i - n_a)*img_stride (the prev and next frames of a batch in one launch);
+// pointers at pixel (0,0).  raw: the caller's unpadded level 0 (w % 4 == 0,
+// 4-byte aligned rows), read in place; otherwise a padded level, whose ring
+// the edge lanes read directly.
+struct StreamSrc {
+    const uint8_t* a;
+    const uint8_t* b;
+    int n_a;
     int64_t img_stride;
-    int pitch;
+    int pitch, w, h;
+    int raw;
 };
-constexpr int EDGE_L = 16, EDGE_R = 16;  // band extents inside the image
 
-__device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pitch, const uint8_t* __restrict__ E,
-                                           int epitch, int w, int h, int x, int y) {
-    const int ry = refl(y, h);
-    const bool edge = x < EDGE_L - 16 || x + 16 > w - (EDGE_R - 16);
-    const int xc = min(x, w + 16);  // lanes past the band are never used: keep them in range
-    const uint8_t* p = edge ? E + (int64_t)ry * epitch + xc : S + (int64_t)ry * pitch + x;
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);  // 4-byte aligned
-    return make_uint4(q[0], q[1], q[2], q[3]);
+// Edge strips of an unpadded source.  Every lane loads its 16 bytes at a
+// column clamped into the image, xc = clamp(x0, 0, w-16), and shifts them back
+// by r = (x0 - xc)/4 dwords.  The dwords past the ends that a level-1 output
+// inside the image still reads are REFLECT_101 copies of the first / last
+// loaded dword (one v_perm): lane 2 of strip 0 (x0 = -4, r = -1) needs columns
+// -2, -1 (= 2, 1) and the lane holding level-1 column w1-1 (r = 1 or 2) needs
+// column w (= w-2).  Lanes 0 and 1 of strip 0 (r < -1) and the lanes past the
+// right edge (r > 2) compute unused values, and their level-1 columns are
+// replaced afterwards (left: the mirrored level-1 pixels of lanes 2..4, right:
+// the fix-up below).  r is fixed for the strip, so the three per-lane choices
+// are lane masks in SGPRs.
+struct Gather {
+    int dx;                    // xc - x0
+    uint64_t m_left, m_1, m_2;  // lanes with r = -1 / 1 / 2 (the others: r = 0)
+};
+__device__ __forceinline__ Gather make_gather(int x0, int w) {
+    Gather g;
+    const int xc = min(max(x0, 0), w - 16);
+    const int r = (x0 - xc) >> 2;
+    g.dx = xc - x0;
+    g.m_left = __ballot(r == -1);
+    g.m_1 = __ballot(r == 1);
+    g.m_2 = __ballot(r >= 2);
+    return g;
 }
-
-// Fill the edge bands of n_img source images into the padded plane E: per row
-// three 16-byte chunks on each side.  Inside and outside chunks are separate
-// item ranges, so waves never mix paths: the chunk inside the image ([0, 16),
-// [w-16, w)) is a vector copy; the two outside chunks per side are the
-// byte-reversed mirror ranges, built from aligned dword loads and v_perm.
-// Requires w % 4 == 0 and 4-byte aligned rows (other inputs take the padded
-// level-0 copy instead); vec16: 16-byte aligned rows and w % 16 == 0.
-__global__ void __launch_bounds__(256) edge_kernel(const uint8_t* __restrict__ src, const uint8_t* __restrict__ src_b,
-                                                   int n_a, int64_t img_stride, int pitch, int w, int h,
-                                                   uint8_t* __restrict__ E, int64_t e_img_stride, int epitch,
-                                                   int vec16) {
-    const int img = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= h * 6) return;
-    // items [0, 2h): the chunk inside the image on each side; [2h, 6h): the 4
-    // mirrored chunks of a row
-    int q, y;
-    if (i < 2 * h) {
-        y = i >> 1;
-        q = 2 + (i & 1);
+__device__ __forceinline__ bool lane_in(uint64_t m) { return (m >> __lane_id()) & 1u; }
+// 16 source bytes of row y (REFLECT_101) for this lane
+template <bool GATHER>
+__device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pitch, int h, int x, const Gather& g,
+                                           int y) {
+    const uint8_t* row = S + (int64_t)refl(y, h) * pitch;
+    if constexpr (GATHER) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x + g.dx);  // 4-byte aligned
+        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+        const uint32_t el = __builtin_amdgcn_perm(d0, d0, 0x01020303u);  // columns -4..-1 <- (3,) 3, 2, 1
+        const uint32_t er = __builtin_amdgcn_perm(d3, d3, 0x00000102u);  // columns +16.. <- +14, +13, +12
+        const bool L = lane_in(g.m_left), R1 = lane_in(g.m_1), R2 = lane_in(g.m_2);
+        return make_uint4(L ? el : R1 ? d1 : R2 ? d2 : d0, L ? d0 : R1 ? d2 : R2 ? d3 : d1,
+                          L ? d1 : R1 ? d3 : R2 ? er : d2, L ? d2 : R1 ? er : R2 ? er : d3);
     } else {
-        const int j = i - 2 * h;
-        y = j >> 2;
-        q = (j & 3) < 2 ? (j & 3) : (j & 3) + 2;
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x);  // 4-byte aligned
+        return make_uint4(q[0], q[1], q[2], q[3]);
     }
-    const int x = q < 3 ? -32 + 16 * q : w - EDGE_R + 16 * (q - 3);
-    const uint8_t* row = (img < n_a ? src + img * img_stride : src_b + (img - n_a) * img_stride) + (int64_t)y * pitch;
-    const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);  // 4-byte aligned rows
-    uint32_t* o = reinterpret_cast<uint32_t*>(E + img * e_img_stride + (int64_t)y * epitch + x);
-    uint32_t d[4];
-    if (x >= 0 && x + 16 <= w) {
-        if (vec16) {
-            *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(row + x);
-            return;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = rw[(x >> 2) + k];
-    } else if (x < 0 && w >= 40) {
-        // columns x..x+15 mirror to -x .. -x-15 (descending): output dword k
-        // holds source bytes m-4k .. m-4k-3 with m = -x, a multiple of 16
-        const int m4 = (-x) >> 2;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = __builtin_amdgcn_perm(rw[m4 - k], rw[m4 - k - 1], 0x01020304u);
-    } else if (x >= w && (w & 3) == 0 && w >= 40) {
-        // columns x..x+15 mirror to 2w-2-x .. 2w-17-x (descending)
-        const int m4 = (2 * w - 2 - x) >> 2;  // dword holding the first source byte (its byte 2)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = __builtin_amdgcn_perm(rw[m4 - k], rw[m4 - k - 1], 0x03040506u);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint32_t t = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) t |= (uint32_t)row[refl(x + 4 * k + b, w)] << (8 * b);
-            d[k] = t;
-        }
-    }
-    if (vec16) {
-        *reinterpret_cast<uint4*>(o) = make_uint4(d[0], d[1], d[2], d[3]);
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = d[k];
+}
+// Strip 0 of an unpadded source: level-1 columns -8..-1 (lanes 0, 1) are the
+// REFLECT_101 copies of columns 8..1 (lanes 2..4), taken with DPP row shifts.
+__device__ __forceinline__ uint32_t left_mirror_l1(uint32_t l1, int lane) {
+    const uint32_t s1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l1, 0x101, 0xf, 0xf, false);  // row_shl:1
+    const uint32_t s2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l1, 0x102, 0xf, 0xf, false);  // row_shl:2
+    const uint32_t v = __builtin_amdgcn_perm(s2, s1, 0x01020304u);  // lane L: columns of lanes L+1, L+2 reversed
+    const uint32_t v2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x102, 0xf, 0xf, false);
+    return lane == 1 ? v : lane == 0 ? v2 : l1;
 }
 
 // four level-1 horizontal sums (u16 pairs) from the lane's 16 bytes (outputs
@@ -292,30 +281,35 @@ __device__ __forceinline__ uint32_t fix_sel2(int lane, int c0, int w) {
     return sel;
 }
 
+// the levels a pass writes (offsets of the padded (-PAD,-PAD) corners)
+struct DownLevels {
+    int64_t off[3];
+    int32_t pitch[3], w[3], h[3];
+    int32_t sides[3];  // 1: the pass writes the level's side bands (w, h >= RING_MIN)
+};
+
 // SKIP (tools/pyr_micro.hip only): bit k-1 set = level-k outputs are folded
 // into a register instead of stored (to time the store traffic).
 #ifndef STREAM_OCC
 #define STREAM_OCC 4
 #endif
-template <int NL, int SKIP = 0>
-__global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* __restrict__ src,
-                                                     const uint8_t* __restrict__ src_b, int n_a, int64_t src_img_stride,
-                                                     int src_pitch, int w0, int h0, EdgePlane ep,
-                                                     uint8_t* __restrict__ pyr, int64_t pyr_bytes, DownLevels L,
-                                                     int n_strips, int n_bands, int n_units, int band,
-                                                     uint8_t* __restrict__ trash) {
-    const int lane = threadIdx.x & 63;
-    const int nblk = (n_units + 3) / 4;
-    const int unit = xcd_swizzle(blockIdx.x, nblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (unit >= n_units) return;
-    const int st = unit % n_strips, rest = unit / n_strips;
-    const int bd = rest % n_bands, img = rest / n_bands;
-    // images [0, n_a) from src, the rest from src_b (prev and next frames of a
-    // batch in one launch); the edge plane and the pyramids are contiguous
-    const uint8_t* S = img < n_a ? src + img * src_img_stride : src_b + (img - n_a) * src_img_stride;
-    const uint8_t* E = ep.base + img * ep.img_stride;
+// One wave's walk over its (strip, band).  GATHER: this strip touches an edge
+// of an unpadded source (per-lane REFLECT_101 gathers); SIDES: it holds source
+// columns of some level's side bands.  Both are wave-uniform, so the kernel
+// branches once into one of three instances and the loop has no per-row path
+// choice (loads stay in flight across iterations).
+template <int NL, bool GATHER, bool SIDES, int SKIP>
+__device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __restrict__ pyr, int64_t pyr_bytes,
+                                            const DownLevels& L, int st, int bd, int img, int band, int lane,
+                                            uint8_t* __restrict__ tl, bool side1, bool side2, bool side3) {
+    const uint8_t* S = img < src.n_a ? src.a + img * src.img_stride : src.b + (img - src.n_a) * src.img_stride;
     uint8_t* P = pyr + img * pyr_bytes;
+    const int w0 = src.w, h0 = src.h, sp = src.pitch;
     const int x0 = ST_COLS * st + 8 * lane - 20;  // this lane's 16 source bytes
+    // padded sources: lanes past the ring read inside it (their outputs are unused)
+    const int xs = src.raw ? x0 : min(x0, w0 + 16);
+    Gather g{};
+    if constexpr (GATHER) g = make_gather(x0, w0);
     const bool own_lane = lane >= 2 && lane < 62;
     const int w1 = L.w[0], h1 = L.h[0], p1 = L.pitch[0];
     const int c1 = (ST_COLS / 2) * st;            // level-1 column of lane 2, byte 0
@@ -336,6 +330,13 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
     const int o1lo = band * bd, o1hi = min(band * bd + band, h1);
     const int o2lo = (band >> 1) * bd, o2hi = NL > 1 ? min((band >> 1) * (bd + 1), h2) : 0;
     const int o3lo = (band >> 2) * bd, o3hi = NL > 2 ? min((band >> 2) * (bd + 1), h3) : 0;
+    // the last source row the walk needs: the prefetch and the trip count's
+    // round-up re-read it (a cache hit) instead of fetching rows past the band
+    const int ylast = 2 * (r1s + n1 - 1) + 2;
+    // level-1 side bands as dwords: the left band always (ring dword [-a-4, -a-1]
+    // from lanes a, a+4), the right one when w1 % 4 == 0 ([2w1-4-a, 2w1-1-a] from
+    // lanes a-4, a); otherwise the right band byte by byte
+    const bool r1dw = (w1 & 3) == 0;
 
     // rolling state: horizontal sums of source rows 2r1-2 .. 2r1+2 (hr[0..4]),
     // level-2 horizontal sums of level-1 rows (g2[0..4], newest last), level-3
@@ -343,7 +344,7 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
     uint2 hr[5];
     uint32_t g2[5] = {0, 0, 0, 0, 0}, g3[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * r1s - 2 + k));
+    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16<GATHER>(S, sp, h0, xs, g, 2 * r1s - 2 + k));
     // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % RS;
     // they are fetched PF iterations ahead (2*PF rows x 1 KB in flight per wave).
     // PF = 4 at 4 waves per SIMD (99 VGPRs) measured 0.230 ms per 512 images
@@ -358,41 +359,66 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
     uint4 pa[RS], pb[RS];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-        pa[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 1);
-        pb[k] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1s + k) + 2);
+        pa[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 1, ylast));
+        pb[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 2, ylast));
     }
     // Loads are issued unconditionally and stores branch only on wave-uniform
     // row conditions (rows of the band, mirrored ring rows): on gfx9 stores and
     // loads share vmcnt, and a store under a lane-divergent branch would make the
     // compiler wait for all earlier stores before using a prefetched row; a
     // uniform branch costs at most one extra counted op at the join.  Lanes that
-    // own no output (lanes 0/1/62/63, columns past the level) store to this
-    // lane's dword of a trash line.
-    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
+    // own no output (lanes 0/1/62/63, columns past the level, no ring column)
+    // store to this lane's dword of the wave's trash line.
     uint32_t nsink = 0;
     auto body = [&](int k, auto slot_c) {
         constexpr int slot = decltype(slot_c)::value;
         const int r1 = r1s + k;
         hr[3] = hsum_row(pa[slot]);
         hr[4] = hsum_row(pb[slot]);
-        pa[(slot + PF) % RS] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 1);
-        pb[(slot + PF) % RS] = src_row16(S, src_pitch, E, ep.pitch, w0, h0, x0, 2 * (r1 + PF) + 2);
+        pa[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 1, ylast));
+        pb[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 2, ylast));
         // level-1 row r1
         uint32_t l1 = hibytes(vsum2(hr[0].x, hr[1].x, hr[2].x, hr[3].x, hr[4].x),
                               vsum2(hr[0].y, hr[1].y, hr[2].y, hr[3].y, hr[4].y));
         hr[0] = hr[2];
         hr[1] = hr[3];
         hr[2] = hr[4];
+        if constexpr (GATHER) {
+            if (st == 0) l1 = left_mirror_l1(l1, lane);  // wave-uniform
+        }
         if (fix1) l1 = __builtin_amdgcn_perm(l1, wave_shr1(l1), sel1);
         if (r1 >= o1lo && r1 < o1hi) {  // wave-uniform: rows of the band
-            const bool ok = own_lane && c1 + 4 * (lane - 2) < w1;
-            uint8_t* q = P + L.off[0] + c1 + 4 * (lane - 2) + PAD;
+            const int a = c1 + 4 * (lane - 2);
+            const bool ok = own_lane && a < w1;
+            uint8_t* const rb = P + L.off[0] + PAD;  // column 0 of padded row 0
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
             if constexpr ((SKIP & 1) != 0) {
                 nsink ^= l1;
             } else {
-                *reinterpret_cast<uint32_t*>(ok ? q + (int64_t)(r1 + PAD) * p1 : tl) = l1;
-                if (mr != r1) *reinterpret_cast<uint32_t*>(ok ? q + (int64_t)(mr + PAD) * p1 : tl) = l1;
+                *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(r1 + PAD) * p1 : tl) = l1;
+                if (mr != r1) *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p1 : tl) = l1;
+                if constexpr (SIDES) {
+                    if (side1) {  // wave-uniform
+                        const uint32_t nx = wave_shl1(l1), pv = wave_shr1(l1);
+                        const bool lw = own_lane && a <= PAD - 4;
+                        const bool rw = r1dw && own_lane && a >= w1 - PAD && a <= w1 - 4;
+                        const uint32_t v = lw ? __builtin_amdgcn_perm(nx, l1, 0x01020304u)
+                                              : __builtin_amdgcn_perm(l1, pv, 0x03040506u);
+                        const int col = lw ? -a - 4 : 2 * w1 - 4 - a;
+                        *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(r1 + PAD) * p1 : tl) = v;
+                        if (mr != r1)
+                            *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(mr + PAD) * p1 : tl) = v;
+                        if (!r1dw) {  // odd widths: the right band byte by byte
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) {
+                                const int c = a + b, rc = ring_col(c, w1);
+                                const bool wb = own_lane && rc > 0;
+                                *(wb ? rb + rc + (int64_t)(r1 + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
+                                if (mr != r1) *(wb ? rb + rc + (int64_t)(mr + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
+                            }
+                        }
+                    }
+                }
             }
         }
         if constexpr (NL > 1) {
@@ -424,15 +450,28 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
                     l2 = __builtin_amdgcn_perm(l2, (a2 & 0xffffu) | (a1 << 16), sel2);
                 }
                 if (k >= 4 && r2 >= o2lo && r2 < o2hi) {
-                    const bool ok = own_lane && c2 + 2 * (lane - 2) < w2;
-                    uint8_t* q = P + L.off[1] + c2 + 2 * (lane - 2) + PAD;
+                    const int a = c2 + 2 * (lane - 2);
+                    const bool ok = own_lane && a < w2;
+                    uint8_t* const rb = P + L.off[1] + PAD;
                     const int mr = mirror_row(r2, h2);
                     if constexpr ((SKIP & 2) != 0) {
                         nsink ^= l2 << 7;
                     } else {
-                        *reinterpret_cast<uint16_t*>(ok ? q + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
+                        *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
                         if (mr != r2)
-                            *reinterpret_cast<uint16_t*>(ok ? q + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
+                            *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
+                        if constexpr (SIDES) {
+                            if (side2) {  // wave-uniform
+#pragma unroll
+                                for (int b = 0; b < 2; ++b) {
+                                    const int rc = ring_col(a + b, w2);
+                                    const bool wb = own_lane && rc != 0;
+                                    const uint8_t v8 = (uint8_t)(l2 >> (8 * b));
+                                    *(wb ? rb + rc + (int64_t)(r2 + PAD) * p2 : tl) = v8;
+                                    if (mr != r2) *(wb ? rb + rc + (int64_t)(mr + PAD) * p2 : tl) = v8;
+                                }
+                            }
+                        }
                     }
                 }
                 if constexpr (NL > 2) {
@@ -454,14 +493,24 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
                     if constexpr ((slot & 3) == 0) {
                         const int r3 = (r2 - 2) >> 1;
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
-                        const bool ok = own_lane && c3 + (lane - 2) < w3;
-                        uint8_t* q = P + L.off[2] + c3 + (lane - 2) + PAD;
+                        const int a = c3 + (lane - 2);
+                        const bool ok = own_lane && a < w3;
+                        uint8_t* const rb = P + L.off[2] + PAD;
                         const int mr = mirror_row(r3, h3);
+                        const uint8_t v8 = (uint8_t)(s3 >> 8);
                         if constexpr ((SKIP & 4) != 0) {
                             nsink ^= s3 << 13;
                         } else if (k >= 12 && r3 >= o3lo && r3 < o3hi) {
-                            *(ok ? q + (int64_t)(r3 + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
-                            if (mr != r3) *(ok ? q + (int64_t)(mr + PAD) * p3 : tl) = (uint8_t)(s3 >> 8);
+                            *(ok ? rb + a + (int64_t)(r3 + PAD) * p3 : tl) = v8;
+                            if (mr != r3) *(ok ? rb + a + (int64_t)(mr + PAD) * p3 : tl) = v8;
+                            if constexpr (SIDES) {
+                                if (side3) {  // wave-uniform
+                                    const int rc = ring_col(a, w3);
+                                    const bool wb = own_lane && rc != 0;
+                                    *(wb ? rb + rc + (int64_t)(r3 + PAD) * p3 : tl) = v8;
+                                    if (mr != r3) *(wb ? rb + rc + (int64_t)(mr + PAD) * p3 : tl) = v8;
+                                }
+                            }
                         }
                     }
                 }
@@ -487,39 +536,77 @@ __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(const uint8_t* 
     if constexpr (SKIP != 0) *reinterpret_cast<uint32_t*>(tl) = nsink;
 }
 
+template <int NL, int SKIP = 0>
+__global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(StreamSrc src, uint8_t* __restrict__ pyr,
+                                                                  int64_t pyr_bytes, DownLevels L, int n_strips,
+                                                                  int n_bands, int n_units, int band,
+                                                                  uint8_t* __restrict__ trash) {
+    const int lane = threadIdx.x & 63;
+    const int nblk = (n_units + 3) / 4;
+    const int unit = xcd_swizzle(blockIdx.x, nblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (unit >= n_units) return;
+    const int st = unit % n_strips, rest = unit / n_strips;
+    const int bd = rest % n_bands, img = rest / n_bands;
+    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
+    // wave-uniform strip classes: source columns past an edge of an unpadded
+    // level 0 (lanes 0 / 63 read x0 = 480*st - 20 / 480*st + 484, 16 bytes), and
+    // owned columns (240 / 120 / 60 per strip) that some side band copies
+    const bool gather = src.raw && (st == 0 || ST_COLS * st + 8 * 63 - 20 + 16 > src.w);
+    const int c1 = (ST_COLS / 2) * st;
+    const bool side1 = L.sides[0] && (st == 0 || c1 + ST_COLS / 2 > L.w[0] - 1 - PAD);
+    const bool side2 = NL > 1 && L.sides[1] && (st == 0 || c1 / 2 + ST_COLS / 4 > L.w[1] - 1 - PAD);
+    const bool side3 = NL > 2 && L.sides[2] && (st == 0 || c1 / 4 + ST_COLS / 8 > L.w[2] - 1 - PAD);
+    if (gather)
+        stream_walk<NL, true, true, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, side1, side2, side3);
+    else if (side1 || side2 || side3)
+        stream_walk<NL, false, true, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, side1, side2, side3);
+    else
+        stream_walk<NL, false, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+}
+
+// Side bands of a pass's level written by the pass itself (wide and tall enough)
+__host__ __device__ inline bool pass_writes_sides(int w, int h) { return w >= RING_MIN && h >= RING_MIN; }
+
+// band height: BAND level-1 rows per wave when the batch fills the chip; a
+// small batch (the live tracker's single frame or pair) takes narrower bands
+// down to 4 rows: more waves, each walking band + 9 rows instead of BAND + 9 --
+// less latency for more halo work on an otherwise idle GPU
+inline int stream_band(int n_strips, int h1, int n_img, int n_cu) {
+    int band = BAND;
+    while (band > 4 && n_strips * ((h1 + band - 1) / band) * n_img < 4 * n_cu) band >>= 1;
+    // the same number of bands, balanced (a multiple of 4 rows each)
+    const int n_bands = (h1 + band - 1) / band;
+    return std::min(band, ((h1 + n_bands - 1) / n_bands + 3) / 4 * 4);
+}
+
 template <int NL>
-void launch_stream(gvx_ctx* c, const uint8_t* src, const uint8_t* src_b, int n_a, int64_t src_img_stride,
-                   int src_pitch, int src_w, int src_h, const EdgePlane& ep, int n_img, const PyrLayout& lay, int l0,
-                   uint8_t* dst) {
+void launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
     DownLevels D{};
     for (int k = 0; k < NL; ++k) {
         D.off[k] = lay.off[l0 + 1 + k];
         D.pitch[k] = lay.pitch[l0 + 1 + k];
         D.w[k] = lay.w[l0 + 1 + k];
         D.h[k] = lay.h[l0 + 1 + k];
+        D.sides[k] = pass_writes_sides(D.w[k], D.h[k]);
     }
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
-    // BAND level-1 rows per wave when the batch fills the chip; a small batch
-    // (the live tracker's single frame or pair) takes narrower bands down to 4
-    // rows: more waves, each walking band + 9 rows instead of BAND + 9 -- less
-    // latency for more halo work on an otherwise idle GPU
-    int band = BAND;
-    while (band > 4 && n_strips * ((D.h[0] + band - 1) / band) * n_img < 4 * c->n_cu) band >>= 1;
+    const int band = stream_band(n_strips, D.h[0], n_img, c->n_cu);
     const int n_bands = (D.h[0] + band - 1) / band;
     const int n_units = n_strips * n_bands * n_img;
     const int nblk = (n_units + 3) / 4;
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
-    hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, src_b, n_a,
-                       src_img_stride, src_pitch, src_w, src_h, ep, dst, lay.bytes, D, n_strips, n_bands, n_units,
-                       band, trash);
+    hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, dst, lay.bytes,
+                       D, n_strips, n_bands, n_units, band, trash);
 }
 
 
 // ------------------------------------------------------------------ rings
-// REFLECT_101 rings of levels lo..hi of every image in one launch.  Item = one
-// dword of ring: the top / bottom PAD rows over the padded width, then per
-// interior row the left PAD columns and the right columns [w, w+PAD) (dword
-// aligned; bytes of the last interior dword rewrite their own value).
+// Full REFLECT_101 rings of the levels too small for the streaming pass to
+// write them (narrower or shorter than RING_MIN: the ring reflects more than
+// once), all images in one launch.  Item = one ring dword: the top / bottom PAD
+// rows over the padded width, then per interior row the left PAD columns and
+// the right columns [w, w+PAD) (dword aligned; bytes of the last interior dword
+// rewrite their own value).
 struct RingLevels {
     int32_t n;                  // levels
     int64_t off[MAX_LEVELS];
@@ -527,7 +614,6 @@ struct RingLevels {
     int32_t dw[MAX_LEVELS];     // dwords per padded row (top/bottom bands)
     int32_t rd0[MAX_LEVELS];    // first dword (padded col / 4) of the right band
     int32_t rdn[MAX_LEVELS];    // dwords of the right band
-    int32_t sides[MAX_LEVELS];  // 1: top/bottom rows already written (side bands only)
     int32_t items[MAX_LEVELS];  // ring dwords of the level
 };
 
@@ -549,11 +635,6 @@ __device__ __forceinline__ uint32_t ring_dword(const uint32_t* rw, int pcol, int
     return __builtin_amdgcn_perm(rw[(lo >> 2) + 1], rw[lo >> 2], sel);
 }
 
-// Item = one ring dword.  Full ring: the top / bottom PAD rows over the
-// padded width, then the side bands of the interior rows.  Side-bands-only
-// levels: the left PAD columns and the right columns [w, w+PAD) of every padded
-// row (ring rows included: their sources are interior pixels).  Bytes of the
-// last interior dword of a row rewrite their own value.
 __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes, RingLevels R) {
     const int l = blockIdx.z;  // level slot (wave-uniform)
     int j = blockIdx.x * 256 + threadIdx.x;
@@ -561,7 +642,7 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
     const int w = R.w[l], h = R.h[l], pitch = R.pitch[l];
     uint8_t* base = pyr + (int64_t)blockIdx.y * pyr_bytes + R.off[l];
     int prow, pcol;  // padded row, padded byte column of the dword
-    const int nb = R.sides[l] ? 0 : 2 * PAD * R.dw[l];
+    const int nb = 2 * PAD * R.dw[l];
     if (j < nb) {
         const int r = j / R.dw[l];
         prow = r < PAD ? r : h + r;
@@ -570,21 +651,22 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
         j -= nb;
         const int per = PAD / 4 + R.rdn[l];
         const int r = j / per, c = j - r * per;
-        prow = R.sides[l] ? r : PAD + r;
+        prow = PAD + r;
         pcol = c < PAD / 4 ? 4 * c : 4 * (R.rd0[l] + c - PAD / 4);
     }
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(base + (int64_t)(refl(prow - PAD, h) + PAD) * pitch);
     *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = ring_dword(rw, pcol, w);
 }
 
-// Rings of levels lo..hi.  sides_only: the streaming pass already wrote the
-// top / bottom ring rows of every level tall enough (RING_MIRROR_H).
-void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst, bool sides_only) {
+// Rings of the levels lo..hi whose side bands the streaming pass did not write
+// (no launch when it wrote them all).
+void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst) {
     RingLevels R{};
-    R.n = hi - lo + 1;
     int most = 0;
-    for (int k = 0; k < R.n; ++k) {
-        const int lv = lo + k, w = lay.w[lv];
+    for (int lv = lo; lv <= hi; ++lv) {
+        const int w = lay.w[lv];
+        if (pass_writes_sides(w, lay.h[lv])) continue;
+        const int k = R.n++;
         R.off[k] = lay.off[lv];
         R.pitch[k] = lay.pitch[lv];
         R.w[k] = w;
@@ -592,11 +674,10 @@ void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, u
         R.dw[k] = (w + 2 * PAD + 3) / 4;
         R.rd0[k] = (w + PAD) / 4;
         R.rdn[k] = (w + 2 * PAD + 3) / 4 - R.rd0[k];
-        R.sides[k] = sides_only && lay.h[lv] >= RING_MIRROR_H;
-        R.items[k] = R.sides[k] ? (lay.h[lv] + 2 * PAD) * (PAD / 4 + R.rdn[k])
-                                : 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
+        R.items[k] = 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
         most = R.items[k] > most ? R.items[k] : most;
     }
+    if (R.n == 0) return;
     dim3 grid((most + 255) / 256, n_img, R.n);
     hipLaunchKernelGGL(ring_kernel, grid, dim3(256), 0, c->stream, dst, lay.bytes, R);
 }
@@ -643,8 +724,9 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         return launch_build_pyramids(c, src_b, img_stride, stride, n_img - n_a, lay, dst + (int64_t)n_a * lay.bytes,
                                      write_l0, nullptr, 0);
     }
-    if (write_l0 || !aligned) {
-        // full padded level-0 copy: the source of the build and its own edge plane
+    const bool raw = !(write_l0 || !aligned);
+    if (!raw) {
+        // full padded level-0 copy (ring included): the source of the build
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
         const int items = groups * (lay.h[0] + 2 * PAD);
         dim3 grid((items + 255) / 256, n_img);
@@ -653,33 +735,28 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         s0 = slot0;
         s0_img = lay.bytes;
         s0_pitch = lay.pitch[0];
-    } else {
-        // read level 0 in place; only its edge bands go to the (otherwise unused) slot
-        const int vec16 = stride % 16 == 0 && img_stride % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
-                          (n_a == n_img || reinterpret_cast<uintptr_t>(src_b) % 16 == 0) &&
-                          lay.w[0] % 16 == 0 && reinterpret_cast<uintptr_t>(slot0) % 16 == 0 && lay.pitch[0] % 16 == 0;
-        dim3 grid((lay.h[0] * 6 + 255) / 256, n_img);
-        hipLaunchKernelGGL(edge_kernel, grid, dim3(256), 0, c->stream, src, src_b, n_a, img_stride, stride, lay.w[0],
-                           lay.h[0], slot0, lay.bytes, lay.pitch[0], vec16);
     }
     // levels 1.. in streaming passes of up to 3 levels; a later pass reads the
-    // previous pass's deepest level (padded, its ring built first)
+    // previous pass's deepest level (padded, its ring complete)
     int l = 0;
     while (l + 1 < lay.nlev) {
         const int nl = lay.nlev - 1 - l >= 3 ? 3 : lay.nlev - 1 - l;
-        const uint8_t* s = l == 0 ? s0 : dst + lay.off[l] + (int64_t)PAD * lay.pitch[l] + PAD;
-        const uint8_t* sb = l == 0 ? src_b : nullptr;  // the level-0 copy path never has two sources here
-        const int na = l == 0 ? n_a : n_img;
-        const int64_t si = l == 0 ? s0_img : lay.bytes;
-        const int sp = l == 0 ? s0_pitch : lay.pitch[l];
-        const EdgePlane ep = l == 0 ? EdgePlane{slot0, lay.bytes, lay.pitch[0]} : EdgePlane{s, lay.bytes, sp};
+        StreamSrc s{};
+        s.a = l == 0 ? s0 : dst + lay.off[l] + (int64_t)PAD * lay.pitch[l] + PAD;
+        s.b = l == 0 ? src_b : nullptr;  // the level-0 copy path never has two sources here
+        s.n_a = l == 0 ? n_a : n_img;
+        s.img_stride = l == 0 ? s0_img : lay.bytes;
+        s.pitch = l == 0 ? s0_pitch : lay.pitch[l];
+        s.w = lay.w[l];
+        s.h = lay.h[l];
+        s.raw = l == 0 && raw;
         if (nl == 3)
-            launch_stream<3>(c, s, sb, na, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
+            launch_stream<3>(c, s, n_img, lay, l, dst);
         else if (nl == 2)
-            launch_stream<2>(c, s, sb, na, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
+            launch_stream<2>(c, s, n_img, lay, l, dst);
         else
-            launch_stream<1>(c, s, sb, na, si, sp, lay.w[l], lay.h[l], ep, n_img, lay, l, dst);
-        launch_rings(c, n_img, lay, l + 1, l + nl, dst, true);
+            launch_stream<1>(c, s, n_img, lay, l, dst);
+        launch_rings(c, n_img, lay, l + 1, l + nl, dst);
         l += nl;
     }
     return hipGetLastError();

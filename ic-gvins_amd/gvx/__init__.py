@@ -145,6 +145,8 @@ def _declare(L):
         "gvx_frame_level": (i32, [P, u64, i32, P, C.POINTER(i32), C.POINTER(i32)]),
         "gvx_frame_put_dev": (i32, [P, u64, P, i32, i32, i32, P]),
         "gvx_frame_level_padded": (i32, [P, u64, i32, i32, P]),
+        "gvx_pyramid_layout": (i32, [i32, i32, i32, P, P, P, P, P, P]),
+        "gvx_build_pyramids_dev": (i32, [P, i32, i32, i32, P, i64, i32, i32, P]),
         "gvx_klt": (i32, [P, u64, u64, P, P, P, P, i32, C.POINTER(KltParams)]),
         "gvx_klt_fb": (i32, [P, u64, u64, P, P, P, P, P, P, P, P, i32, f64, f64, i32, i32,
                              C.POINTER(KltParams)]),
@@ -211,6 +213,21 @@ def _declare(L):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+
+
+def pyramid_layout(w: int, h: int, max_level: int = 3):
+    """gvx_pyramid_layout (host only) -> dict(nlev, off, pitch, w, h, bytes) of one
+    image pyramid as gvx_build_pyramids_dev writes it."""
+    n = C.c_int32()
+    off = np.zeros(8, np.int64)
+    pitch, lw, lh = (np.zeros(8, np.int32) for _ in range(3))
+    b = C.c_int64()
+    st = lib().gvx_pyramid_layout(w, h, max_level, C.byref(n), off.ctypes.data, pitch.ctypes.data,
+                                  lw.ctypes.data, lh.ctypes.data, C.byref(b))
+    if st:
+        raise GvxError(f"gvx_pyramid_layout({w}, {h}, {max_level}): status {st}")
+    k = n.value
+    return dict(nlev=k, off=off[:k], pitch=pitch[:k], w=lw[:k], h=lh[:k], bytes=b.value)
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -576,6 +593,14 @@ class Context:
         self._check(self._L.gvx_reproj_eval(self._h, n, _ptr(cs), _ptr(prm), prm.size, _ptr(o), _ptr(res),
                                             _ptr(jac)), "gvx_reproj_eval")
         return res, jac
+
+    def pyramid_layout(self, w: int, h: int, max_level: int = 3):
+        return pyramid_layout(w, h, max_level)
+
+    def build_pyramids_dev(self, n_img, w, h, d_imgs, img_stride, stride, max_level, d_out):
+        """Device-pointer batched pyramid build (pointers as ints), async on the context stream."""
+        self._check(self._L.gvx_build_pyramids_dev(self._h, n_img, w, h, d_imgs, img_stride, stride, max_level,
+                                                   d_out), "gvx_build_pyramids_dev")
 
     def klt_fb_batch_dev(self, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_back_xy,
                          d_flags, d_kept, d_nkept, cam_w=None, cam_h=None, fb_thresh=0.5, border=5.0,

@@ -154,6 +154,21 @@ gvx_status gvx_frame_level(gvx_ctx* ctx, uint64_t id, int32_t level, uint8_t* ou
 #define GVX_PYR_PAD 32
 gvx_status gvx_frame_level_padded(gvx_ctx* ctx, uint64_t id, int32_t level, int32_t pad, uint8_t* out);
 
+/* Batched buildOpticalFlowPyramid (winSize 21, BORDER_REFLECT_101 pyramid border):
+   the pyramids that each cv::calcOpticalFlowPyrLK call at tracking/tracking.cc:385,
+   390, 487, 493 builds internally, for n_img device images (h x w u8, image i at
+   d_imgs + i*img_stride, rows `stride` bytes apart) in one launch, into
+   d_out + i*bytes.  gvx_pyramid_layout gives the layout: level l at byte off[l] is
+   (lh[l] + 2*GVX_PYR_PAD) rows of pitch[l] bytes, the level plus its ring starting at
+   its padded corner.  Levels >= 1 are always written, ring included.  Level 0 is
+   read in place when w % 4 == 0 and the rows are 4-byte aligned, and its slot is then
+   left unwritten; otherwise the slot holds the padded copy.  Async on the context
+   stream; d_out must hold n_img * bytes. */
+gvx_status gvx_pyramid_layout(int32_t w, int32_t h, int32_t max_level, int32_t* nlev, int64_t* off,
+                              int32_t* pitch, int32_t* lw, int32_t* lh, int64_t* bytes);
+gvx_status gvx_build_pyramids_dev(gvx_ctx* ctx, int32_t n_img, int32_t w, int32_t h, const uint8_t* d_imgs,
+                                  int64_t img_stride, int32_t stride, int32_t max_level, uint8_t* d_out);
+
 /* --------------------------------------------------------- preprocessing */
 /* Tracking::preprocessing (tracking/tracking.cc:107-141): CLAHE with
    clahe_ = cv::createCLAHE(3.0, cv::Size(21, 21)) (:63) applied in place (:139),

@@ -45,6 +45,26 @@ def test_params_defaults_match_reference(gvx_mod):
     assert p.eps == 0.01 and p.min_eig == np.float32(1e-4)
 
 
+def test_pyramid_layout(gvx_mod):
+    """gvx_pyramid_layout (host only): buildOpticalFlowPyramid's level count rule
+    (stop when the next level would be <= winSize), ceil-halved level sizes, 64-byte
+    pitches holding the 32-pixel ring, 256-byte aligned levels."""
+    lay = gvx_mod.pyramid_layout(1280, 560, 3)
+    assert lay["nlev"] == 4 and list(lay["w"]) == [1280, 640, 320, 160] and list(lay["h"]) == [560, 280, 140, 70]
+    assert gvx_mod.pyramid_layout(1920, 1200, 4)["nlev"] == 5
+    assert gvx_mod.pyramid_layout(100, 60, 3)["nlev"] == 2  # 50x30 -> 25x15 would be <= 21
+    for w, h, L in [(1280, 560, 3), (333, 149, 3), (1920, 1200, 4), (22, 22, 5)]:
+        lay = gvx_mod.pyramid_layout(w, h, L)
+        for l in range(lay["nlev"]):
+            assert lay["pitch"][l] % 64 == 0 and lay["pitch"][l] >= lay["w"][l] + 64
+            assert lay["off"][l] % 256 == 0
+            end = lay["off"][l] + lay["pitch"][l] * (lay["h"][l] + 64)
+            nxt = lay["off"][l + 1] if l + 1 < lay["nlev"] else lay["bytes"]
+            assert end <= nxt
+    with pytest.raises(gvx_mod.GvxError):
+        gvx_mod.pyramid_layout(21, 100, 3)
+
+
 def test_no_cpu_fallback_without_device(gvx_mod):
     import os
     if os.path.exists("/dev/kfd"):

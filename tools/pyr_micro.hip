@@ -1,6 +1,6 @@
 // Phase timing of the pyramid passes (diagnostics, not part of libgvx):
-// 256 random 1280x560 images; the streaming pass with and without its stores,
-// the edge-band and ring kernels, and a plain streaming read of the same bytes.
+// 256 random 1280x560 images; the streaming pass (levels 1-3 and their rings)
+// with and without its stores, and a plain streaming read of the same bytes.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off
 //        -Wno-unused-result -I include -I ic-gvins_amd/csrc tools/pyr_micro.hip -o tools/pyr_micro
 #include "../ic-gvins_amd/csrc/pyramid.hip"
@@ -58,8 +58,8 @@ int main() {
         D.w[k] = lay.w[1 + k];
         D.h[k] = lay.h[1 + k];
     }
-    uint8_t* slot0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
-    const EdgePlane ep{slot0, lay.bytes, lay.pitch[0]};
+    for (int k = 0; k < 3; ++k) D.sides[k] = pass_writes_sides(D.w[k], D.h[k]);
+    const StreamSrc ss{src, src, n, (int64_t)w * h, w, w, h, 1};
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2), n_bands = (D.h[0] + BAND - 1) / BAND;
     const int n_units = n_strips * n_bands * n;
     const int nblk = (n_units + 3) / 4;
@@ -69,15 +69,11 @@ int main() {
         const float us = timeit([&] { read_all<<<blocks, 256>>>((const uint4*)src, img.size() / 16, (uint32_t*)trash); }, reps);
         printf("read_all %5d blocks  %8.1f us  %6.2f TB/s\n", blocks, us, img.size() / us / 1e6);
     }
-    printf("edge_kernel            %8.1f us\n", timeit([&] {
-        hipLaunchKernelGGL(edge_kernel, dim3((h * 6 + 255) / 256, n), dim3(256), 0, 0, src, src, n, (int64_t)w * h, w, w, h,
-                           slot0, lay.bytes, lay.pitch[0], 1);
-    }, reps));
     auto run3 = [&](auto skip_c, const char* what) {
         constexpr int SK = decltype(skip_c)::value;
         printf("stream_kernel<3> %-28s %7.1f us\n", what, timeit([&] {
-            hipLaunchKernelGGL((stream_kernel<3, SK>), grid, dim3(256), 0, 0, src, src, n, (int64_t)w * h, w, w, h, ep, dst,
-                               lay.bytes, D, n_strips, n_bands, n_units, BAND, trash);
+            hipLaunchKernelGGL((stream_kernel<3, SK>), grid, dim3(256), 0, 0, ss, dst, lay.bytes, D, n_strips, n_bands,
+                               n_units, BAND, trash);
         }, reps));
     };
     run3(std::integral_constant<int, 0>{}, "all stores");

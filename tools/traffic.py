@@ -14,12 +14,12 @@ import sys
 sys.path.insert(0, os.path.dirname(__file__))
 from pmc_summary import load  # noqa: E402
 
-# launches per bench step of the KLT pipeline: one edge-band pass, one 3-level
-# streaming pass and one ring pass over the prev and next images together; one
-# LK launch for fwd+bwd; one compaction.  (Profiles before r01 v21 built prev
-# and next in separate launches: 2 of each pyramid kernel per step.)
-PER_STEP = {"edge_kernel": 1, "stream_kernel": 1, "ring_kernel": 1, "klt_kernel": 1, "compact_kernel": 1}
-
+# launches per bench step of the KLT pipeline: one 3-level streaming pass over
+# the prev and next images together (levels and rings; before r02 an edge-band
+# pass and a ring pass ran beside it, which are counted when present); one LK
+# launch for fwd+bwd; one compaction.
+PER_STEP = {"stream_kernel": 1, "klt_kernel": 1, "compact_kernel": 1}
+OPTIONAL = {"edge_kernel": 1, "ring_kernel": 1}
 ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
 ap.add_argument("--workload", default="klt_fb_batch 256x1280x560 N150 L3")
@@ -29,7 +29,7 @@ a = ap.parse_args()
 res = load(a.pmc_dir)
 kern = {}
 step = 0.0
-for name, n in PER_STEP.items():
+for name, n in list(PER_STEP.items()) + [(k, v) for k, v in OPTIONAL.items() if k in res]:
     d = res.get(name)
     if d is None or "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
         sys.exit(f"{name}: FETCH_SIZE / WRITE_SIZE missing in {a.pmc_dir}")
