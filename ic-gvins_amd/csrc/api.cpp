@@ -515,12 +515,12 @@ gvx_status gvx_klt_fb(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, const floa
     return GVX_OK;
 }
 
-gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h,
-                                const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
-                                const float* d_prev_xy, float* d_next_xy, float* d_back_xy,
-                                uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
-                                double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
-                                const gvx_klt_params* p) {
+gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h,
+                                     const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
+                                     const float* d_prev_xy, const float* d_init_xy, float* d_next_xy,
+                                     float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                     double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                     const gvx_klt_params* p) {
     if (!c) return GVX_ERR_INVALID;
     gvx_status s = check_klt_params(c, p);
     if (s) return s;
@@ -538,7 +538,7 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
     hipEvent_t ev{};
     prof_begin(c, "pyramid", &ev);
     // level 0 stays in the caller's images; levels >= 1 go to the pyramid slots
-    // one launch per kernel for both frames of every pair (pyr_next follows pyr_prev)
+    // one launch for both frames of every pair (pyr_next follows pyr_prev)
     hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, 2 * n_pairs, lay, pyr_prev, false, d_next,
                                          n_pairs);
     prof_end(c, "pyramid", ev);
@@ -555,11 +555,9 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
     a.border = border;
     a.cam_w = cam_w;
     a.cam_h = cam_h;
-    if (!p->use_initial_flow) {
-        e = hipMemcpyAsync(d_next_xy, d_prev_xy, sizeof(float) * 2 * (size_t)n_pairs * n_pts,
-                           hipMemcpyDeviceToDevice, c->stream);
-        if (e != hipSuccess) return hip_err(c, e, "init flow");
-    }
+    // without OPTFLOW_USE_INITIAL_FLOW the kernel starts from prevPts and never
+    // reads the initial flow
+    a.init_xy = d_init_xy;
     prof_begin(c, "klt", &ev);
     const Level0 l0{d_prev, d_next, (int64_t)w * h, (int64_t)w * h, 0, w, 1};
     e = launch_klt(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, l0, d_prev_xy, d_next_xy, d_back_xy,
@@ -570,6 +568,16 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t 
     e = launch_compact(c, n_pairs, n_pts, d_flags, d_kept_idx, d_n_kept);
     prof_end(c, "compact", ev);
     return hip_err(c, e, "compact kernel");
+}
+
+gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h,
+                                const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
+                                const float* d_prev_xy, float* d_next_xy, float* d_back_xy,
+                                uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                const gvx_klt_params* p) {
+    return gvx_klt_fb_batch_init_dev(c, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_next_xy,
+                                     d_back_xy, d_flags, d_kept_idx, d_n_kept, fb_thresh, border, cam_w, cam_h, p);
 }
 
 gvx_status gvx_klt_fb_batch(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* prev,

@@ -106,29 +106,32 @@ __global__ void __launch_bounds__(RP_THREADS) reproj_kernel(int n, const gvx_rep
             double red[6];
             for (int a = 0; a < 2; ++a)
                 for (int b = 0; b < 3; ++b) red[3 * a + b] = SI[2 * a] * red0[b] + SI[2 * a + 1] * red0[3 + b];
-            double A[9], B[9], C[9], S[9], ncbc[9];
-            for (int k = 0; k < 9; ++k) ncbc[k] = -cbc[k];
-            // J0: pose_i
+            double A[9], B[9], C[9], S[9];
+            // A = cbc*cnb1 and AC = A*cb0n are shared: J0 = [A | (-AC) S(pb0)],
+            // J1 = [-A | ...], J2's tmp_r = AC cbc^T (the restatement forms them
+            // separately; negation is exact, so the bits are the same)
+            double AC[9], nA[9];
             mm3(cbc, cnb1, A);
-            mm3(ncbc, cnb1, B);
-            mm3(B, cb0n, B);
+            mm3(A, cb0n, AC);
+            for (int k = 0; k < 9; ++k) {
+                nA[k] = -A[k];
+                B[k] = -AC[k];
+            }
+            // J0: pose_i
             skew(pb0, S);
             mm3(B, S, B);
             put_2x7(red, A, B, out + 2);
             // J1: pose_j
-            mm3(ncbc, cnb1, A);
             skew(pb1, S);
             mm3(cbc, S, B);
-            put_2x7(red, A, B, out + 16);
+            put_2x7(red, nA, B, out + 16);
             // J2: extrinsic
             mm3(cnb1, cb0n, C);
             for (int k = 0; k < 9; ++k) C[k] = C[k] - ((k % 4) == 0 ? 1.0 : 0.0);
             mm3(cbc, C, A);
             double tmp_r[9], cbcT[9], ntr[9], S1[9], S2[9], S3[9], u[3], w[3];
-            mm3(cbc, cnb1, tmp_r);
-            mm3(tmp_r, cb0n, tmp_r);
             mt3(cbc, cbcT);
-            mm3(tmp_r, cbcT, tmp_r);
+            mm3(AC, cbcT, tmp_r);
             for (int k = 0; k < 9; ++k) ntr[k] = -tmp_r[k];
             skew(pc0, S);
             mm3(ntr, S, S1);

@@ -125,6 +125,8 @@ struct KltArgs {
     // device-resident point count (n_pairs == 1 only): the launch is sized for
     // n_pts points (the capacity), the kernel tracks min(*n_dev, n_pts)
     const int32_t* n_dev = nullptr;
+    // initial flow read from here instead of next_xy (which is then output only)
+    const float* init_xy = nullptr;
 };
 
 // Level 0 of pair i: prev plane at prev + i*prev_stride, pixel (x, y) at byte

@@ -644,7 +644,8 @@ __global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel
     const L0Planes pb{pf.j, pf.i, pf.o0, pf.pitch, pf.raw};
     LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow, err_out != nullptr};
     const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
-    float nx = next_xy[2 * gp], ny = next_xy[2 * gp + 1];
+    const float* init_xy = a.init_xy ? a.init_xy : next_xy;
+    float nx = init_xy[2 * gp], ny = init_xy[2 * gp + 1];
     int st = 1;
     float e = 0.f;
     lk_group<PPW>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, gl, win, ust);

@@ -152,6 +152,8 @@ def _declare(L):
                              C.POINTER(KltParams)]),
         "gvx_klt_fb_batch_dev": (i32, [P, i32, i32, i32, P, P, i32, P, P, P, P, P, P, f64, f64, i32,
                                        i32, C.POINTER(KltParams)]),
+        "gvx_klt_fb_batch_init_dev": (i32, [P, i32, i32, i32, P, P, i32, P, P, P, P, P, P, P, f64, f64, i32,
+                                            i32, C.POINTER(KltParams)]),
         "gvx_klt_fb_batch": (i32, [P, i32, i32, i32, P, P, i32, P, P, P, P, P, P, f64, f64, i32, i32,
                                    C.POINTER(KltParams)]),
         "gvx_preint_integrate": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
@@ -210,7 +212,12 @@ def _declare(L):
         "gvx_copy_dev": (i32, [P, P, P, C.c_size_t]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        # an older build (a GVX_LIB variant timed against the tree) may lack newer
+        # entry points: those stay undeclared and fail at their call
+        # (tests/test_abi.py holds the in-tree library to every declared symbol)
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
 
@@ -601,6 +608,16 @@ class Context:
         """Device-pointer batched pyramid build (pointers as ints), async on the context stream."""
         self._check(self._L.gvx_build_pyramids_dev(self._h, n_img, w, h, d_imgs, img_stride, stride, max_level,
                                                    d_out), "gvx_build_pyramids_dev")
+
+    def klt_fb_batch_init_dev(self, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_init_xy, d_next_xy,
+                              d_back_xy, d_flags, d_kept, d_nkept, cam_w=None, cam_h=None, fb_thresh=0.5,
+                              border=5.0, params: Optional[KltParams] = None):
+        """Device-pointer batch with the initial flow read from d_init_xy (next output only)."""
+        p = params or KltParams.default()
+        self._check(self._L.gvx_klt_fb_batch_init_dev(self._h, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy,
+                                                      d_init_xy, d_next_xy, d_back_xy, d_flags, d_kept, d_nkept,
+                                                      fb_thresh, border, cam_w or w, cam_h or h, C.byref(p)),
+                    "gvx_klt_fb_batch_init_dev")
 
     def klt_fb_batch_dev(self, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_back_xy,
                          d_flags, d_kept, d_nkept, cam_w=None, cam_h=None, fb_thresh=0.5, border=5.0,

@@ -135,6 +135,16 @@ gvx_status gvx_klt_fb_batch_dev(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_
                                 uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
                                 double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
                                 const gvx_klt_params* p);
+/* The same with the initial flow read from d_init_xy (n_pairs x n_pts x 2 f32,
+   may equal d_next_xy) and d_next_xy output only: the nextPts in / out of
+   calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW (tracking.cc:385-390) without
+   a copy of the predictions into the output first. */
+gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h,
+                                     const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
+                                     const float* d_prev_xy, const float* d_init_xy, float* d_next_xy,
+                                     float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                     double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                     const gvx_klt_params* p);
 /* Host-pointer convenience wrapper of the above (copies in and out, synchronous). */
 gvx_status gvx_klt_fb_batch(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h,
                             const uint8_t* prev, const uint8_t* next, int32_t n_pts,
