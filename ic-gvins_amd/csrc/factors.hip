@@ -8,7 +8,8 @@
 // Reprojection: one lane per factor; parameter blocks are gathered through the
 // per-factor offset table (the Ceres parameter-block pointers), outputs are
 // staged through LDS so that the 46-double Jacobian rows leave as coalesced
-// stores.  Preintegration: 16 lanes per factor (preint_factor_kernel); the
+// stores.  Preintegration: 16 lanes per factor (preint_factor_kernel), the
+// whitening on the fp64 matrix cores; the
 // reference's per-call sqrt_information_ = LLT(P^-1)^T (quirk, SURVEY.md App.
 // C.2) is formed once per segment by sqrt_info_kernel with the same arithmetic.
 #include <hip/hip_runtime.h>
@@ -297,23 +298,26 @@ __global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result*
 // lanes compute them together (one instruction stream for the wave's four
 // factors) and lane 0 of the group stores them into the group's LDS tile
 // Jr[15][33] (32 Jacobian columns [J0 7 | J1 9 | J2 7 | J3 9] + the residual).
-// The Earth position-correction sum over pn_ runs on lanes 0..2, one
-// component each, in the reference's order.  Whitening: lane i < 15 holds row
-// i of sqrt_info (upper triangular, formed once per segment by
-// sqrt_info_kernel) in registers and forms row i of sqrt_info * [Jr | r]
-// column by column (the k >= i terms in ascending k, the oracle's order),
-// writing it back in place; the wave then stores its four factors' residuals
-// and Jacobians as contiguous coalesced runs.
-// Measured (configs[3], 5,247 factors, M = 100): 47 us per launch, ~85k cycles
-// per wave of which ~38k wait on memory; the uniform per-factor chain, not
-// bandwidth, bounds it (column-wise whitening with sqrt_info in LDS: 65 us at
-// one wave/SIMD; 10 lanes per factor, 875 waves: 46 us; LDS-staged inputs:
-// 61 us; pn_ through LDS chunks: 50 us; pn_ as per-lane partial sums + butterfly
-// (one wave/SIMD): 57 us).
-constexpr int PF_L = 16;                 // lanes per factor (>= 15: one sqrt_info row per lane)
+// Earth: the position-correction sum over pn_ runs on lanes 0..2, one
+// component each, in the reference's order, from pn_ staged into LDS by
+// global_load_lds in chunks of PN_CH samples.  Whitening sqrt_info * [Jr | r]
+// runs on the matrix cores (v_mfma_f64_16x16x4, 12 per factor); the wave then
+// stores its four factors' residuals and Jacobians as contiguous runs.
+// Measured (configs[3], 5,247 factors, M = 100): 47 -> 34 us per launch (r02:
+// select-free VALU whitening 41 us, MFMA whitening 37 us, pn_ through LDS 34 us;
+// 8 lanes per factor: 40 us; one 104-sample pn_ chunk: 49 us -- 32 KB of LDS
+// per wave leaves 1,280 wave slots for 1,312 waves).  Per wave (PMC): 61 k
+// cycles, half of them waiting on memory; the per-factor fp64 chain bounds it.
+#ifndef PF_LANES
+#define PF_LANES 16
+#endif
+constexpr int PF_L = PF_LANES;           // lanes per factor (>= 3: the p_cor components)
 constexpr int PF_GROUPS = 64 / PF_L;     // factors per workgroup (one wave)
 constexpr int PF_SLOTS = (64 + PF_L - 1) / PF_L;  // groups incl. a partial one (idle lanes)
 constexpr int PF_LD = 33;                // tile row: 32 Jacobian columns + the residual
+constexpr int PN_CH = 64;                // pn_ samples per factor per LDS chunk
+constexpr int PN_PER = PF_L / 2;         // samples per factor per global_load_lds (16 B per lane)
+constexpr int PN_INS = PN_CH / PN_PER;   // instructions per chunk (1 KB each)
 
 __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
                                                            const double* __restrict__ pn,
@@ -323,6 +327,7 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
                                                            double* __restrict__ res,
                                                            double* __restrict__ jac) {
     __shared__ double tile[PF_SLOTS * NS * PF_LD];
+    __shared__ double pnb[PN_INS * 128];  // pn_ chunk: PN_PER samples x PF_GROUPS groups per KB
     const int grp = threadIdx.x / PF_L, lane = threadIdx.x % PF_L;
     const int f0 = blockIdx.x * PF_GROUPS;
     // dead groups (past n, or the partial group) recompute a valid factor and store nothing
@@ -332,6 +337,23 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     const bool earth = s->variant == GVX_PREINT_EARTH;
     for (int e = lane; e < NS * PF_LD; e += PF_L) Jr[e] = 0.0;
     __syncthreads();
+    // pn_ chunk c0 of this group's factor into LDS (instruction j: lane pair
+    // (2q, 2q+1) of a group loads sample c0 + PN_PER*j + q, 16 bytes each, to
+    // pnb + j*1 KB + group*16*PF_L B + q*32 B); chunk 0 is issued here, ahead of
+    // the parameter loads, so its latency overlaps theirs
+    const double* pl = pn + 4 * (int64_t)pn_off[fi];
+    const int m1n = earth ? s->m - 1 : 0;
+    auto pn_chunk = [&](int c0) {
+#pragma unroll
+        for (int j = 0; j < PN_INS; ++j) {
+            const int smp = c0 + PN_PER * j + (lane >> 1);
+            if (smp < m1n)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(pl + 4 * smp + 2 * (lane & 1)),
+                    (__attribute__((address_space(3))) void*)(pnb + 128 * j), 16, 0, 0);
+        }
+    };
+    pn_chunk(0);
     const int32_t* o = offs + 4 * (int64_t)fi;
     const double *ps0 = params + o[0], *m0 = params + o[1], *ps1 = params + o[2], *m1 = params + o[3];
     const dq q0 = dq_make(ps0[6], ps0[3], ps0[4], ps0[5]);
@@ -370,22 +392,34 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     dq_rot(q0i, cnb0);
     double r[NS];
     const bool w0 = lane == 0;  // lane 0 of the group writes the uniform blocks
+    // Earth: p_cor += (pn.second - state0.p) * pn.first over pn_, in the
+    // reference's order, component c on lane c of the group (broadcast below).
+    // pn_ is staged into LDS in chunks of PN_CH samples per factor with
+    // global_load_lds (no registers; one memory latency per chunk instead of one
+    // per unrolled group of loads), then summed from LDS.
+    double pcc = 0.0;
+    {
+        const int c = lane < 3 ? lane : 0;
+        const double p0c = p0[c];
+        const int grpw = threadIdx.x / PF_L;  // this lane's group
+        for (int c0 = 0; __ballot(c0 < m1n); c0 += PN_CH) {
+            if (c0 > 0) pn_chunk(c0);
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane < 3) {
+                const int kn = min(PN_CH, m1n - c0);
+                const double* P = pnb + 2 * PF_L * grpw;
+#pragma unroll 8
+                for (int k = 0; k < kn; ++k) {
+                    const double* e = P + 128 * (k / PN_PER) + 4 * (k % PN_PER);
+                    pcc = pcc + (e[1 + c] - p0c) * e[0];
+                }
+            }
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next chunk lands
+        }
+    }
     if (earth) {
         double S[9], S2[9];
         skew(s->iewn, S);
-        // p_cor += (pn.second - state0.p) * pn.first over pn_, in the reference's
-        // order: component c on lane c of the group, then broadcast
-        double pcc = 0.0;
-        {
-            const double* pl = pn + 4 * (int64_t)pn_off[fi];
-            const int c = lane < 3 ? lane : 0;
-            const double p0c = p0[c];
-            const int m1n = s->m - 1;
-            if (lane < 3) {
-#pragma unroll 8
-                for (int k = 0; k < m1n; ++k) pcc = pcc + (pl[4 * k + 1 + c] - p0c) * pl[4 * k];
-            }
-        }
         const int gl = threadIdx.x - lane;
         double pc[3] = {__shfl(pcc, gl, 64), __shfl(pcc, gl + 1, 64), __shfl(pcc, gl + 2, 64)};
         for (int i = 0; i < 9; ++i) S2[i] = 2.0 * S[i];
@@ -409,16 +443,16 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
         r[7] = 2 * e.y;
         r[8] = 2 * e.z;
         if (jac && w0) {
-            double C2[9];
-            for (int i = 0; i < 9; ++i) C2[i] = 2.0 * cnb0[i];
-            mm3(C2, S, M);
+            // (2 cnb0) S, (-2 cnb0) S and (2 cnb0) S again in the reference: one
+            // product scaled by +-2 (exact), the same bits
+            mm3(cnb0, S, M);
+            for (int i = 0; i < 9; ++i) M[i] = 2.0 * M[i];
             for (int i = 0; i < 9; ++i) N[i] = -cnb0[i] - M[i] * dtt;
             set3(Jr, PF_LD, 0, 0, N);
             mv3(cnb0, dpn, t);
             skew(t, N);
             set3(Jr, PF_LD, 0, 3, N);
-            for (int i = 0; i < 9; ++i) C2[i] = -2.0 * cnb0[i];
-            mm3(C2, S, N);
+            for (int i = 0; i < 9; ++i) N[i] = -M[i];
             set3(Jr, PF_LD, 3, 0, N);
             mv3(cnb0, dvn, t);
             skew(t, N);
@@ -427,9 +461,7 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
             set3(Jr, PF_LD, 6, 3, N);
             // pose1 (columns 16..22)
             set3(Jr, PF_LD, 0, 16, cnb0);
-            for (int i = 0; i < 9; ++i) C2[i] = 2.0 * cnb0[i];
-            mm3(C2, S, N);
-            set3(Jr, PF_LD, 3, 16, N);
+            set3(Jr, PF_LD, 3, 16, M);
             qright_br(dq_mul(qb0b1, cq), N);
             for (int i = 0; i < 9; ++i) N[i] = -N[i];
             set3(Jr, PF_LD, 6, 19, N);
@@ -501,22 +533,53 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     }
     if (w0)
         for (int i = 0; i < NS; ++i) Jr[i * PF_LD + 32] = r[i];
-    __syncthreads();
-    // ---- whitening: row `lane` of sqrt_info * [Jr | r], in place ----
-    double srow[NS];  // row `lane` of sqrt_info (upper triangular)
+    // the whitening's A operands (sqrt_info rows / K) of the wave's four factors,
+    // loaded before the barrier so their latency overlaps it
+    const int wl = threadIdx.x, wr = wl & 15, wk = wl >> 4;
+    double SA[PF_GROUPS][4];
 #pragma unroll
-    for (int k = 0; k < NS; ++k) srow[k] = (lane < NS && k >= lane) ? s->sqrt_info[lane * NS + k] : 0.0;
-    const int ncol = jac ? PF_LD : 1;
-#pragma unroll 1
-    for (int cc = 0; cc < ncol; ++cc) {
-        const int col = jac ? cc : 32;
-        double acc = 0.0;
+    for (int f = 0; f < PF_GROUPS; ++f) {
+        const double* sq = pre[min(f0 + f, n - 1)].sqrt_info;
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const double t = srow[k] * Jr[k * PF_LD + col];
-            acc = k == lane ? t : (k > lane ? acc + t : acc);
+        for (int kk = 0; kk < 4; ++kk) {
+            const int k = 4 * kk + wk;
+            SA[f][kk] = (wr < NS && k < NS) ? sq[wr * NS + k] : 0.0;
         }
-        if (lane < NS) Jr[lane * PF_LD + col] = acc;
+    }
+    __syncthreads();
+    // ---- whitening: sqrt_info * [Jr | r] on the matrix cores, in place ----
+    // Per factor slot f of the wave: three 16-column blocks of the 15 x 33 tile
+    // (zero-padded to 16 x 48), each 4 v_mfma_f64_16x16x4 steps over K = 16.
+    // Operand layout (16x16x4 f64): A lane l = (row l%16, k l/16), B lane l =
+    // (k l/16, col l%16), D lane l = rows l/16 + 4i (i = 0..3) of col l%16
+    // (measured: tools/mfma_f64_probe.hip).  The MFMA sums
+    // the 15 products in its own order, not the restatement's sequential one
+    // (the parity bound is 1e-9 of the block's magnitude).
+    {
+        const int lr = wr, lk = wk;
+        const int cb0 = jac ? 0 : 2;  // residual only: the block holding column 32
+#pragma unroll
+        for (int f = 0; f < PF_GROUPS; ++f) {
+            const double* A = SA[f];
+            double* T = tile + f * NS * PF_LD;
+#pragma unroll 1
+            for (int cb = cb0; cb < 3; ++cb) {
+                const int col = 16 * cb + lr;
+                typedef double v4d __attribute__((ext_vector_type(4)));
+                v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int k = 4 * kk + lk;
+                    const double bv = (k < NS && col < PF_LD) ? T[k * PF_LD + col] : 0.0;
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[kk], bv, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = lk + 4 * i;
+                    if (row < NS && col < PF_LD) T[row * PF_LD + col] = acc[i];
+                }
+            }
+        }
     }
     __syncthreads();
     // ---- coalesced stores of the workgroup's factors ----
