@@ -279,33 +279,11 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
 gvx_status gvx_frame_put_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_gray, int32_t w, int32_t h,
                              int32_t stride, const gvx_klt_params* p) {
     if (!c || !d_gray || w <= 0 || h <= 0 || stride < w) return set_err(c, GVX_ERR_INVALID, "bad frame");
-    gvx_status s = check_klt_params(c, p);
+    Frame* fp = nullptr;
+    gvx_status s = frame_slot(c, id, w, h, p, &fp);
     if (s) return s;
-    if (w <= WIN || h <= WIN) return set_err(c, GVX_ERR_INVALID, "frame smaller than the window");
-    hipSetDevice(c->device);
-    PyrLayout lay = make_layout(w, h, p->max_level, p->win);
-    Frame& f = c->frames[id];
-    if (!f.pyr || f.lay.bytes < lay.bytes) {
-        if (c->capturing) {
-            if (!f.pyr) c->frames.erase(id);
-            return set_err(c, GVX_ERR_INVALID, "frame %llu needs a (re)allocation during a graph capture",
-                           (unsigned long long)id);
-        }
-        ++c->mem_gen;
-        if (f.pyr) {
-            hipStreamSynchronize(c->stream);
-            hipFree(f.pyr);
-            f.pyr = nullptr;
-        }
-        hipError_t e = hipMalloc(&f.pyr, lay.bytes);
-        if (e != hipSuccess) {
-            c->frames.erase(id);
-            return hip_err(c, e, "hipMalloc(pyramid)");
-        }
-    }
-    f.lay = lay;
-    f.w = w;
-    f.h = h;
+    Frame& f = *fp;
+    const PyrLayout& lay = f.lay;
     hipEvent_t ev{};
     prof_begin(c, "pyramid", &ev);
     // the padded level-0 copy reads the caller's device image in place (any stride)
@@ -627,3 +605,39 @@ gvx_status gvx_klt_fb_batch(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h, c
 }
 
 }  // extern "C"
+
+namespace gvx {
+
+gvx_status frame_slot(gvx_ctx* c, uint64_t id, int32_t w, int32_t h, const gvx_klt_params* p, Frame** out) {
+    gvx_status s = check_klt_params(c, p);
+    if (s) return s;
+    if (w <= WIN || h <= WIN) return set_err(c, GVX_ERR_INVALID, "frame smaller than the window");
+    hipSetDevice(c->device);
+    PyrLayout lay = make_layout(w, h, p->max_level, p->win);
+    Frame& f = c->frames[id];
+    if (!f.pyr || f.lay.bytes < lay.bytes) {
+        if (c->capturing) {
+            if (!f.pyr) c->frames.erase(id);
+            return set_err(c, GVX_ERR_INVALID, "frame %llu needs a (re)allocation during a graph capture",
+                           (unsigned long long)id);
+        }
+        ++c->mem_gen;
+        if (f.pyr) {
+            hipStreamSynchronize(c->stream);
+            hipFree(f.pyr);
+            f.pyr = nullptr;
+        }
+        hipError_t e = hipMalloc(&f.pyr, lay.bytes);
+        if (e != hipSuccess) {
+            c->frames.erase(id);
+            return hip_err(c, e, "hipMalloc(pyramid)");
+        }
+    }
+    f.lay = lay;
+    f.w = w;
+    f.h = h;
+    *out = &f;
+    return GVX_OK;
+}
+
+}  // namespace gvx

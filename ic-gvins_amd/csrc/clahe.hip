@@ -103,7 +103,8 @@ __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, 
 __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
                                                           int stride, ClaheGeom g, int vec8, int tpw,
                                                           uint8_t* __restrict__ lut,
-                                                          uint32_t* __restrict__ hist_img) {
+                                                          uint32_t* __restrict__ hist_img,
+                                                          const int32_t* __restrict__ src_index) {
     extern __shared__ uint32_t hs[];  // tpw histograms of 256 bins, HROW dwords apart
     const int ngrp = (g.tiles_x + tpw - 1) / tpw;
     const int img = blockIdx.x / (g.tiles_y * ngrp);
@@ -114,7 +115,8 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
     const int nbins = (txa1 - txa0) * HROW;
     for (int i = t; i < nbins; i += LUT_THREADS) hs[i] = 0;
     __syncthreads();
-    const uint8_t* s = src + img * img_stride;
+    // src_index (one image): the source image is picked on the device
+    const uint8_t* s = src + (src_index ? (int64_t)*src_index : (int64_t)img) * img_stride;
     const int y0 = ty * g.th;
     const int rows_in = max(0, min(y0 + g.th, g.h) - y0);
     const float inv_tw = 1.0f / g.tw;
@@ -208,10 +210,15 @@ __device__ __forceinline__ int first_row(int k, const ClaheGeom& g, float inv_th
 // is one dword {L[ty1][tx1c][v], L[ty1][tx2c][v], L[ty2][tx1c][v],
 // L[ty2][tx2c][v]} (tile indices clamped as the reference does), so each pixel
 // takes one ds_read_b32 for its four LUT values.
+// ring: dst is pixel (0,0) of a level with a PAD-pixel ring (a frame's padded
+// level-0 slot); every output pixel is also stored where the REFLECT_101 ring
+// copies it -- the mirrored ring row (top / bottom) and the mirrored side-band
+// column (left / right), both for the corners -- so the pyramid pass and the
+// detection read the equalised frame with its ring and no copy pass runs.
 __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t img_stride, int stride,
                                                      uint8_t* dst, int64_t dst_img_stride, int dst_stride,
                                                      ClaheGeom g, const uint8_t* __restrict__ lut, int nsplit,
-                                                     int vec8) {
+                                                     int vec8, const int32_t* __restrict__ src_index, int ring) {
     extern __shared__ uint32_t tab[];  // (tiles_x + 1) * TROW dwords
     const int nb = g.tiles_y + 1;
     const int img = blockIdx.x / (nb * nsplit);
@@ -259,7 +266,7 @@ __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t
         }
     }
     __syncthreads();
-    const uint8_t* s = src + img * img_stride;
+    const uint8_t* s = src + (src_index ? (int64_t)*src_index : (int64_t)img) * img_stride;
     uint8_t* dd = dst + img * dst_img_stride;
     for (int x0 = PPT * threadIdx.x; x0 < g.w; x0 += PPT * blockDim.x) {
         // column terms of CLAHE_Interpolation_Body's constructor, once per thread
@@ -317,6 +324,28 @@ __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t
                 } else {
                     for (int j = 0; j < nv; ++j) drow[j] = (uint8_t)(out[j >> 2] >> (8 * (j & 3)));
                 }
+                if (ring) {
+                    // REFLECT_101 ring: row y is copied to ring row -y (1 <= y <= PAD) or
+                    // 2h-2-y (h-1-PAD <= y <= h-2); column x to -x or 2w-2-x likewise
+                    const int my = (y >= 1 && y <= PAD) ? -y : ((y >= g.h - 1 - PAD && y <= g.h - 2) ? 2 * g.h - 2 - y : y);
+                    uint8_t* mrow = dd + (int64_t)my * dst_stride + x0;
+                    if (my != y) {
+                        if (fast)
+                            *reinterpret_cast<uint2*>(mrow) = uint2{out[0], out[1]};
+                        else
+                            for (int j = 0; j < nv; ++j) mrow[j] = (uint8_t)(out[j >> 2] >> (8 * (j & 3)));
+                    }
+                    if (x0 <= PAD || x0 + PPT >= g.w - 1 - PAD) {
+                        for (int j = 0; j < nv; ++j) {
+                            const int x = x0 + j;
+                            const int mx = (x >= 1 && x <= PAD) ? -x : ((x >= g.w - 1 - PAD && x <= g.w - 2) ? 2 * g.w - 2 - x : x);
+                            if (mx == x) continue;
+                            const uint8_t v8 = (uint8_t)(out[j >> 2] >> (8 * (j & 3)));
+                            drow[mx - x0] = v8;
+                            if (my != y) mrow[mx - x0] = v8;
+                        }
+                    }
+                }
             }
         }
     }
@@ -356,7 +385,7 @@ ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles
 
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
-                        uint32_t* hist_img, double* hist_mean) {
+                        uint32_t* hist_img, double* hist_mean, const int32_t* src_index, int ring) {
     if (n <= 0) return hipSuccess;
     if (hist_img) {
         hipError_t e = hipMemsetAsync(hist_img, 0, (size_t)n * 256 * sizeof(uint32_t), c->stream);
@@ -371,7 +400,7 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const int tpw = (g.tiles_x + ngrp - 1) / ngrp;
     ngrp = (g.tiles_x + tpw - 1) / tpw;
     hipLaunchKernelGGL(lut_kernel, dim3(n * g.tiles_y * ngrp), dim3(LUT_THREADS), (size_t)tpw * HROW * 4, c->stream,
-                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img);
+                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index);
     // bands of rows sharing one pair of LUT rows, split to fill the chip
     const int nb = g.tiles_y + 1;
     int nsplit = 1;
@@ -380,7 +409,8 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const int threads = std::min(1024, (cols + 63) / 64 * 64);
     const size_t lds = (size_t)(g.tiles_x + 1) * TROW * 4;
     hipLaunchKernelGGL(apply_kernel, dim3(n * nb * nsplit), dim3(threads), lds, c->stream, src, img_stride, stride,
-                       dst, dst_img_stride, dst_stride, g, (const uint8_t*)lut, nsplit, (int)(src8 && dst8));
+                       dst, dst_img_stride, dst_stride, g, (const uint8_t*)lut, nsplit, (int)(src8 && dst8), src_index,
+                       ring);
     if (hist_img && hist_mean)
         hipLaunchKernelGGL(mean_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, (const uint32_t*)hist_img, n,
                            g.w, g.h, hist_mean);

@@ -88,6 +88,9 @@ gvx_status set_err(gvx_ctx* c, gvx_status s, const char* fmt, ...);
 gvx_status hip_err(gvx_ctx* c, hipError_t e, const char* what);
 void* scratch(gvx_ctx* c, const std::string& name, size_t bytes);   // device
 void* pinned(gvx_ctx* c, const std::string& name, size_t bytes);    // pinned host
+// the cached frame `id` sized for (w, h, p) (allocated or grown; refuses to
+// reallocate during a graph capture)
+gvx_status frame_slot(gvx_ctx* c, uint64_t id, int32_t w, int32_t h, const gvx_klt_params* p, Frame** out);
 
 // Profiling brackets around a kernel family launch (no-ops when disabled).
 void prof_begin(gvx_ctx* c, const char* fam, hipEvent_t* a);
@@ -100,9 +103,11 @@ void prof_drain(gvx_ctx* c);
 // level-0 copy only when write_l0 (otherwise level 0 stays the caller's image).
 // src_b (optional): images n_a .. n_img-1 come from src_b + (i - n_a)*img_stride
 // instead (the prev and next frames of a batch built in one launch per kernel).
+// l0_in_slot: level 0 with its ring is already in dst's padded level-0 slot
+// (written there by the CLAHE pass); only levels >= 1 are built, from it.
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride,
                                  int n_img, const PyrLayout& lay, uint8_t* dst, bool write_l0,
-                                 const uint8_t* src_b = nullptr, int n_a = 0);
+                                 const uint8_t* src_b = nullptr, int n_a = 0, bool l0_in_slot = false);
 
 // Workgroups are dispatched to the 8 XCDs round-robin by id (each XCD has its
 // own L2).  xcd_swizzle maps the dispatch id to a logical id so that XCD k runs
@@ -160,9 +165,12 @@ struct ClaheGeom {
 ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles_y);
 // n images; lut: n*tiles*256 bytes scratch; hist_img (nullable): n*256 u32
 // scratch for the histogram check, whose means go to hist_mean (device).
+// src_index (n == 1): the source is src + (*src_index) * img_stride, picked on the
+// device; ring: dst is pixel (0,0) of a padded level (PAD ring written too)
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
-                        uint32_t* hist_img, double* hist_mean);
+                        uint32_t* hist_img, double* hist_mean, const int32_t* src_index = nullptr,
+                        int ring = 0);
 
 // ---- aux_factors.hip ----
 // residuals of a small factor kind (0: unknown kind); *P block size, *NC constants per factor

@@ -707,11 +707,21 @@ PyrLayout make_layout(int w, int h, int max_level, int win) {
 }
 
 hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_stride, int stride, int n_img,
-                                 const PyrLayout& lay, uint8_t* dst, bool write_l0, const uint8_t* src_b, int n_a) {
+                                 const PyrLayout& lay, uint8_t* dst, bool write_l0, const uint8_t* src_b, int n_a,
+                                 bool l0_in_slot) {
     if (n_img <= 0) return hipSuccess;
     if (!src_b) n_a = n_img;
     // level-0 slot of the pyramid: pixel (0,0) of image 0
     uint8_t* slot0 = dst + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
+    if (l0_in_slot) {
+        // the padded slot is the source of the first pass (ring included)
+        src = slot0;
+        img_stride = lay.bytes;
+        stride = lay.pitch[0];
+        src_b = nullptr;
+        n_a = n_img;
+        write_l0 = false;
+    }
     const bool aligned = stride % 4 == 0 && img_stride % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 4 == 0 &&
                          lay.w[0] % 4 == 0;
     const uint8_t* s0 = src;
@@ -724,8 +734,8 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         return launch_build_pyramids(c, src_b, img_stride, stride, n_img - n_a, lay, dst + (int64_t)n_a * lay.bytes,
                                      write_l0, nullptr, 0);
     }
-    const bool raw = !(write_l0 || !aligned);
-    if (!raw) {
+    const bool raw = !(write_l0 || !aligned) && !l0_in_slot;
+    if (!raw && !l0_in_slot) {
         // full padded level-0 copy (ring included): the source of the build
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
         const int items = groups * (lay.h[0] + 2 * PAD);

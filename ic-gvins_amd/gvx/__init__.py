@@ -189,6 +189,8 @@ def _declare(L):
                                        P, P]),
         "gvx_frame_preprocess_dev": (i32, [P, u64, P, i32, i32, i32, C.POINTER(ClaheParams),
                                            C.POINTER(KltParams), P, P]),
+        "gvx_frame_preprocess_indexed_dev": (i32, [P, u64, P, i64, P, i32, i32, i32, C.POINTER(ClaheParams),
+                                                   C.POINTER(KltParams), P]),
         "gvx_ins_propagate": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
         "gvx_ins_propagate_dev": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
         "gvx_redo_ins_mechanization": (i32, [P, C.POINTER(InsConfig), P, i32, P, P, C.POINTER(i32)]),
@@ -363,6 +365,15 @@ class Context:
                                                      C.byref(clahe or ClaheParams.default()),
                                                      C.byref(params or KltParams.default()), d_hist_mean,
                                                      d_clahe_out), "frame_preprocess_dev")
+
+    def frame_preprocess_indexed_dev(self, fid: int, d_frames: int, frame_stride: int, d_index: int, w: int,
+                                     h: int, stride: Optional[int] = None, clahe: Optional[ClaheParams] = None,
+                                     params: Optional[KltParams] = None, d_hist_mean=None):
+        """Preprocess frame *d_index of an HBM-resident sequence (index read on the device)."""
+        self._check(self._L.gvx_frame_preprocess_indexed_dev(self._h, fid, d_frames, frame_stride, d_index, w, h,
+                                                             stride or w, C.byref(clahe or ClaheParams.default()),
+                                                             C.byref(params or KltParams.default()), d_hist_mean),
+                    "frame_preprocess_indexed_dev")
 
     # ----------------------------------------------------------- camera ops
     def track_frame_dev(self, prev_id: int, next_id: int, track: bool, d_pts, d_vel, d_init, d_n, capacity: int,

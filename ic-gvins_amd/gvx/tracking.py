@@ -73,12 +73,12 @@ class DeviceSequenceTracker:
     (gvx_track_frame_dev): no host round trip per frame.
 
     frames (optional): the whole sequence resident in HBM ([F, h, w] u8 tensor).
-    The frame to process is then picked on the device (gvx_copy_indexed_dev at a
-    device-held frame index) and every frame's track list is appended to
+    The frame to process is then picked on the device (gvx_frame_preprocess_indexed_dev
+    at a device-held frame index) and every frame's track list is appended to
     self.rec_tracks / self.rec_counts (gvx_track_record_dev, which advances the
     index), so with graph=True a frame is exactly one graph launch: the work
-    (frame copy + CLAHE + pyramid + LK + FB + compaction + detection top-up +
-    record) is captured once per frame parity (the two cached frame ids
+    (CLAHE + pyramid + LK + FB + compaction + detection top-up + record) is
+    captured once per frame parity (the two cached frame ids
     alternate) and replayed.  Without frames, step(d_frame) takes the frame's
     device pointer (copied into a fixed staging buffer first in graph mode)."""
 
@@ -100,7 +100,7 @@ class DeviceSequenceTracker:
         self.graph = graph
         self.graphs = {}
         self.frames = frames
-        self.stage = torch.empty((h, w), dtype=torch.uint8, device=dev) if (graph or frames is not None) else None
+        self.stage = torch.empty((h, w), dtype=torch.uint8, device=dev) if (graph and frames is None) else None
         if frames is not None:
             F = frames.shape[0]
             self.index = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -111,10 +111,12 @@ class DeviceSequenceTracker:
         ctx = self.ctx
         cur, prev = self.ids[t % 2], self.ids[(t - 1) % 2]
         if self.frames is not None:
-            ctx.copy_indexed_dev(self.stage.data_ptr(), self.frames.data_ptr(), self.w * self.h,
-                                 self.index.data_ptr())
-            d_frame = self.stage.data_ptr()
-        ctx.frame_preprocess_dev(cur, d_frame, self.w, self.h, None, params=self.kp)
+            # frame *index of the HBM-resident sequence, equalised straight into the
+            # frame cache (no staging copy)
+            ctx.frame_preprocess_indexed_dev(cur, self.frames.data_ptr(), self.w * self.h, self.index.data_ptr(),
+                                             self.w, self.h, params=self.kp)
+        else:
+            ctx.frame_preprocess_dev(cur, d_frame, self.w, self.h, None, params=self.kp)
         ctx.track_frame_dev(prev, cur, t > 0, self.pts.data_ptr(), self.vel.data_ptr(), self.init.data_ptr(),
                             self.count.data_ptr(), self.n, self.w, self.h, klt=self.kp, detect=self.dp)
         if self.frames is not None:

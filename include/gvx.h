@@ -215,6 +215,14 @@ gvx_status gvx_frame_preprocess(gvx_ctx* ctx, uint64_t id, const uint8_t* gray, 
 gvx_status gvx_frame_preprocess_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_gray, int32_t w, int32_t h,
                                     int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
                                     double* d_hist_mean, uint8_t* d_clahe_out);
+/* The same for frame *d_index of a sequence resident in HBM (frame f at
+   d_frames + f * frame_stride, rows `stride` bytes apart), the index read on the
+   device: a captured per-frame graph picks its frame without a host round trip
+   (bench.py --config 5).  Frames of at least 66 x 66 px. */
+gvx_status gvx_frame_preprocess_indexed_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_frames,
+                                            int64_t frame_stride, const int32_t* d_index, int32_t w, int32_t h,
+                                            int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
+                                            double* d_hist_mean);
 
 /* ------------------------------------------------------------ camera ops */
 /* Camera (tracking/camera.cc:25-46): K = [fx skew cx; 0 fy cy; 0 0 1] and the

@@ -88,6 +88,29 @@ def test_frame_preprocess_feeds_pyramid(ctx, orc, gvx_mod):
     ctx.frame_drop(11)
 
 
+@pytest.mark.parametrize("w,h", [(1280, 560), (333, 149), (200, 70)])
+def test_frame_preprocess_into_slot_with_rings(ctx, orc, gvx_mod, w, h):
+    """gvx_frame_preprocess_dev without a CLAHE output buffer equalises straight
+    into the frame's padded level-0 slot, ring included, and builds the levels
+    from it: every level with its 32-pixel REFLECT_101 ring is the oracle's.  The
+    indexed entry (frame *d_index of an HBM-resident sequence) gives the same."""
+    import torch
+    rng = np.random.default_rng(w + 3 * h)
+    seq = np.stack([synth.make_image(w, h, rng) for _ in range(3)])
+    d_seq = torch.from_numpy(seq).cuda()
+    ref = orc.clahe(seq[2])
+    levels = [np.pad(r, 32, mode="reflect") for r in orc.build_pyramid(ref, 3)]
+    p = gvx_mod.KltParams.default(max_level=3)
+    ctx.frame_preprocess_dev(12, d_seq[2].data_ptr(), w, h, params=p)
+    idx = torch.tensor([2], dtype=torch.int32, device="cuda")
+    ctx.frame_preprocess_indexed_dev(13, d_seq.data_ptr(), w * h, idx.data_ptr(), w, h, params=p)
+    ctx.sync()
+    for fid in (12, 13):
+        for l, r in enumerate(levels):
+            _same(ctx.frame_level_padded(fid, l, 32), r, f"frame {fid} padded level {l}")
+        ctx.frame_drop(fid)
+
+
 def test_clahe_rejects_bad_grids(ctx, gvx_mod):
     img = _img(64, 40, 1)
     for p in (gvx_mod.ClaheParams.default(tiles_x=0), gvx_mod.ClaheParams.default(tiles_y=65),
