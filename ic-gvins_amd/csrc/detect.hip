@@ -37,27 +37,41 @@ __device__ __forceinline__ int refl(int p, int len) {
 }
 
 // ------------------------------------------------------------------ mask
+// One workgroup per 64 x 4 tile.  The circle centres are taken 256 at a time,
+// and only those whose (2r+1)^2 box meets the tile are kept (LDS append), so a
+// pixel tests the few circles near it instead of all of them (the raster is a
+// logical OR: the order of the tests does not matter).
 __global__ void __launch_bounds__(256) mask_kernel(int w, int h, const int2* __restrict__ centers, int n,
                                                    const int* __restrict__ hw, int r,
                                                    uint8_t* __restrict__ mask, const int* __restrict__ n_dev,
                                                    const int* __restrict__ skip) {
     __shared__ int2 sc[256];
+    __shared__ int s_n;
     if (skip && *skip) return;   // device-resident call: no detection this frame
     if (n_dev) n = *n_dev;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int tx0 = blockIdx.x * 64, ty0 = blockIdx.y * 4;
+    const int x = tx0 + (threadIdx.x & 63);
+    const int y = ty0 + (threadIdx.x >> 6);
     bool hit = false;
     for (int base = 0; base < n; base += 256) {
+        if (threadIdx.x == 0) s_n = 0;
         __syncthreads();
-        if (base + (int)threadIdx.x < n) sc[threadIdx.x] = centers[base + threadIdx.x];
+        const int i = base + (int)threadIdx.x;
+        if (i < n) {
+            const int2 cc = centers[i];
+            const int ddx = cc.x < tx0 ? tx0 - cc.x : (cc.x > tx0 + 63 ? cc.x - tx0 - 63 : 0);
+            const int ddy = cc.y < ty0 ? ty0 - cc.y : (cc.y > ty0 + 3 ? cc.y - ty0 - 3 : 0);
+            if (ddx <= r && ddy <= r) sc[atomicAdd(&s_n, 1)] = cc;
+        }
         __syncthreads();
-        const int cnt = min(256, n - base);
-        for (int i = 0; i < cnt && !hit; ++i) {
-            const int dy = abs(y - sc[i].y);
+        const int cnt = s_n;
+        for (int k = 0; k < cnt && !hit; ++k) {
+            const int dy = abs(y - sc[k].y);
             if (dy > r) continue;
             const int hwv = hw[dy];
-            hit = hwv >= 0 && abs(x - sc[i].x) <= hwv;
+            hit = hwv >= 0 && abs(x - sc[k].x) <= hwv;
         }
+        __syncthreads();
     }
     if (x < w && y < h) mask[(int64_t)y * w + x] = hit ? 0 : 255;
 }
