@@ -16,11 +16,10 @@
 
 using namespace gvx;
 
-extern "C" gvx_status gvx_track_frame_dev(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, int32_t track,
-                                          float* d_pts, float* d_vel, float* d_init, int32_t* d_n, int32_t cap,
-                                          int32_t cam_w, int32_t cam_h, double fb_thresh, double border,
-                                          const gvx_klt_params* kp, const gvx_detect_params* dp, int32_t* d_kept,
-                                          float* d_corners, int32_t* d_n_corners) {
+static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, int32_t track, float* d_pts,
+                              float* d_vel, float* d_init, int32_t* d_n, int32_t cap, int32_t cam_w, int32_t cam_h,
+                              double fb_thresh, double border, const gvx_klt_params* kp, const gvx_detect_params* dp,
+                              int32_t* d_kept, float* d_corners, int32_t* d_n_corners, const TrackRecord* rec) {
     if (!c || !kp || !dp) return GVX_ERR_INVALID;
     if (!d_pts || !d_vel || !d_init || !d_n) return set_err(c, GVX_ERR_INVALID, "null tracker state");
     if (cap <= 0 || cap < dp->max_features) return set_err(c, GVX_ERR_INVALID, "capacity %d < max_features", cap);
@@ -157,12 +156,20 @@ extern "C" gvx_status gvx_track_frame_dev(gvx_ctx* c, uint64_t prev_id, uint64_t
         e = launch_klt(c, a, lay, fp->pyr, fn.pyr, 0, 0, l0, d_pts, d_init, nullptr, flags, nullptr);
         prof_end(c, "klt", ev);
         if (e != hipSuccess) return hip_err(c, e, "klt kernel");
-        prof_begin(c, "compact", &ev);
-        e = launch_track_update(c, cap, d_n, flags, d_init, d_pts, d_vel, d_init, d_kept);
-        prof_end(c, "compact", ev);
-        if (e != hipSuccess) return hip_err(c, e, "track update");
     }
+    // reduceVector of the FB result (track frames) and the detection's counts /
+    // circle centres: one single-workgroup launch
     DetectPrep pp{};
+    if (track) {
+        pp.update_cap = cap;
+        pp.flags = flags;
+        pp.next_xy = d_init;
+        pp.upd_pts = d_pts;
+        pp.vel = d_vel;
+        pp.init = d_init;
+        pp.kept_out = d_kept;
+        pp.n_upd = d_n;
+    }
     pp.bcols = bcols;
     pp.brows = brows;
     pp.col = col;
@@ -224,9 +231,32 @@ extern "C" gvx_status gvx_track_frame_dev(gvx_ctx* c, uint64_t prev_id, uint64_t
     }
     if (e == hipSuccess)
         e = launch_detect_merge(c, bcnt, bcols, col, row, mpb, dp->max_features, skip, nc, out, d_pts, d_vel, d_init,
-                                d_n, d_corners, d_n_corners);
+                                d_n, d_corners, d_n_corners, rec);
     prof_end(c, "detect", ev);
     return hip_err(c, e, "detection kernels");
+}
+
+extern "C" gvx_status gvx_track_frame_dev(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, int32_t track,
+                                          float* d_pts, float* d_vel, float* d_init, int32_t* d_n, int32_t cap,
+                                          int32_t cam_w, int32_t cam_h, double fb_thresh, double border,
+                                          const gvx_klt_params* kp, const gvx_detect_params* dp, int32_t* d_kept,
+                                          float* d_corners, int32_t* d_n_corners) {
+    return track_frame(c, prev_id, next_id, track, d_pts, d_vel, d_init, d_n, cap, cam_w, cam_h, fb_thresh, border,
+                       kp, dp, d_kept, d_corners, d_n_corners, nullptr);
+}
+
+extern "C" gvx_status gvx_track_frame_record_dev(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, int32_t track,
+                                                 float* d_pts, float* d_vel, float* d_init, int32_t* d_n, int32_t cap,
+                                                 int32_t cam_w, int32_t cam_h, double fb_thresh, double border,
+                                                 const gvx_klt_params* kp, const gvx_detect_params* dp,
+                                                 float* d_tracks, int32_t* d_counts, int32_t* d_frame_index,
+                                                 int32_t max_frames) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!d_tracks || !d_counts || !d_frame_index || max_frames < 0)
+        return set_err(c, GVX_ERR_INVALID, "bad record arguments");
+    const TrackRecord rec{d_tracks, d_counts, d_frame_index, max_frames, cap};
+    return track_frame(c, prev_id, next_id, track, d_pts, d_vel, d_init, d_n, cap, cam_w, cam_h, fb_thresh, border,
+                       kp, dp, nullptr, nullptr, nullptr, &rec);
 }
 
 extern "C" gvx_status gvx_copy_indexed_dev(gvx_ctx* c, void* d_dst, const void* d_src_base, size_t bytes,

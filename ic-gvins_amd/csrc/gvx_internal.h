@@ -289,6 +289,16 @@ struct DetectPrep {
     int bcols, brows, col, row, maxpb, max_features;
     const float* pts;
     const int32_t* n;
+    // the reduceVector update of the FB result first, in the same launch (track
+    // frames): flags / next_xy -> pts (compacted), vel, init, kept_out, *n
+    int update_cap;  // 0: no update
+    const uint8_t* flags;
+    const float* next_xy;
+    float* upd_pts;
+    float* vel;
+    float* init;
+    int32_t* kept_out;
+    int32_t* n_upd;
     int* want;
     int* blk_ids;
     int* n_active;
@@ -301,9 +311,18 @@ hipError_t launch_detect_prep(gvx_ctx* c, const DetectPrep& p);
 // append the detected corners (block order, block origin added) up to
 // max_features: pts / init = corner, vel = 0, n grows; corners_out (nullable)
 // receives every corner and *n_corners_out their count (-1 when skipped)
+// rec (nullable): then append the track list to the per-frame record (as
+// launch_track_record) in the same launch
+struct TrackRecord {
+    float* tracks;
+    int32_t* counts;
+    int32_t* frame;
+    int max_frames, cap;
+};
 hipError_t launch_detect_merge(gvx_ctx* c, int bcnt, int bcols, int col, int row, int maxpb, int max_features,
                                const int* skip, const int* ncorner, const float2* out, float* pts, float* vel,
-                               float* init, int32_t* n, float* corners_out, int32_t* n_corners_out);
+                               float* init, int32_t* n, float* corners_out, int32_t* n_corners_out,
+                               const TrackRecord* rec = nullptr);
 
 // Staging layout for host-pointer API calls: ONE list of slices both sizes the
 // buffer and carves it (256-byte aligned, in declaration order), so the two can

@@ -22,14 +22,10 @@ namespace {
 
 constexpr int TU_THREADS = 256;
 
-__global__ void __launch_bounds__(TU_THREADS) track_update_kernel(int cap, int32_t* __restrict__ n_ptr,
-                                                                  const uint8_t* __restrict__ flags,
-                                                                  const float2* __restrict__ next_xy,
-                                                                  float2* __restrict__ pts, float2* __restrict__ vel,
-                                                                  float2* __restrict__ init,
-                                                                  int32_t* __restrict__ kept_out) {
-    __shared__ int wsum[TU_THREADS / 64];
-    __shared__ int base_s;
+__device__ __forceinline__ void track_update(int cap, int32_t* __restrict__ n_ptr, const uint8_t* __restrict__ flags,
+                                             const float2* __restrict__ next_xy, float2* __restrict__ pts,
+                                             float2* __restrict__ vel, float2* __restrict__ init,
+                                             int32_t* __restrict__ kept_out, int* wsum, int& base_s) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = min(*n_ptr, cap);
     int base = 0;
@@ -68,9 +64,30 @@ __global__ void __launch_bounds__(TU_THREADS) track_update_kernel(int cap, int32
     if (tid == 0) *n_ptr = base_s;
 }
 
+__global__ void __launch_bounds__(TU_THREADS) track_update_kernel(int cap, int32_t* __restrict__ n_ptr,
+                                                                  const uint8_t* __restrict__ flags,
+                                                                  const float2* __restrict__ next_xy,
+                                                                  float2* __restrict__ pts, float2* __restrict__ vel,
+                                                                  float2* __restrict__ init,
+                                                                  int32_t* __restrict__ kept_out) {
+    __shared__ int wsum[TU_THREADS / 64];
+    __shared__ int base_s;
+    track_update(cap, n_ptr, flags, next_xy, pts, vel, init, kept_out, wsum, base_s);
+}
+
 __global__ void __launch_bounds__(256) detect_prep_kernel(DetectPrep p) {
     __shared__ int cnt[1024];
     const int tid = threadIdx.x;
+    if (p.update_cap > 0) {
+        // the frame's reduceVector first (one launch instead of two; the writes
+        // are visible to this workgroup after the barrier)
+        __shared__ int wsum[TU_THREADS / 64];
+        __shared__ int base_s;
+        track_update(p.update_cap, p.n_upd, p.flags, reinterpret_cast<const float2*>(p.next_xy),
+                     reinterpret_cast<float2*>(p.upd_pts), reinterpret_cast<float2*>(p.vel),
+                     reinterpret_cast<float2*>(p.init), p.kept_out, wsum, base_s);
+        __syncthreads();
+    }
     const int bcnt = p.bcols * p.brows;
     const int n = *p.n;
     // featuresDetection is called while the tracks are below track_max_features_
@@ -105,19 +122,15 @@ __global__ void __launch_bounds__(256) detect_prep_kernel(DetectPrep p) {
     }
 }
 
-__global__ void __launch_bounds__(256) detect_merge_kernel(int bcnt, int bcols, int col, int row, int maxpb,
-                                                           int max_features, const int* __restrict__ skip,
-                                                           const int* __restrict__ ncorner,
-                                                           const float2* __restrict__ out, float2* __restrict__ pts,
-                                                           float2* __restrict__ vel, float2* __restrict__ init,
-                                                           int32_t* __restrict__ n_ptr, float2* __restrict__ corners_out,
-                                                           int32_t* __restrict__ n_corners_out) {
-    __shared__ int off[1025];
+// the detected corners in block order with the block origin, appended to the
+// track list up to max_features (tracking.cc:669-685)
+__device__ __forceinline__ void merge_corners(int bcnt, int bcols, int col, int row, int maxpb, int max_features,
+                                              const int* __restrict__ ncorner, const float2* __restrict__ out,
+                                              float2* __restrict__ pts, float2* __restrict__ vel,
+                                              float2* __restrict__ init, int32_t* __restrict__ n_ptr,
+                                              float2* __restrict__ corners_out, int32_t* __restrict__ n_corners_out,
+                                              int* off) {
     const int tid = threadIdx.x;
-    if (*skip) {
-        if (tid == 0 && n_corners_out) *n_corners_out = -1;
-        return;
-    }
     if (tid == 0) {
         int t = 0;
         for (int k = 0; k < bcnt; ++k) {
@@ -149,6 +162,36 @@ __global__ void __launch_bounds__(256) detect_merge_kernel(int bcnt, int bcols, 
     if (tid == 0) {
         if (add > 0) *n_ptr = n + add;
         if (n_corners_out) *n_corners_out = total;
+    }
+}
+
+__global__ void __launch_bounds__(256) detect_merge_kernel(int bcnt, int bcols, int col, int row, int maxpb,
+                                                           int max_features, const int* __restrict__ skip,
+                                                           const int* __restrict__ ncorner,
+                                                           const float2* __restrict__ out, float2* __restrict__ pts,
+                                                           float2* __restrict__ vel, float2* __restrict__ init,
+                                                           int32_t* __restrict__ n_ptr, float2* __restrict__ corners_out,
+                                                           int32_t* __restrict__ n_corners_out, TrackRecord rec) {
+    __shared__ int off[1025];
+    const int tid = threadIdx.x;
+    if (*skip) {  // wave-uniform (one value for the launch)
+        if (tid == 0 && n_corners_out) *n_corners_out = -1;
+    } else {
+        merge_corners(bcnt, bcols, col, row, maxpb, max_features, ncorner, out, pts, vel, init, n_ptr, corners_out,
+                      n_corners_out, off);
+    }
+    if (rec.tracks) {
+        // the track list appended to the per-frame record at *rec.frame, which
+        // advances (launch_track_record, fused: one launch less per frame)
+        __syncthreads();  // the merged list (pts, *n_ptr) is visible to the workgroup
+        const int f = *rec.frame;
+        const int n = min(*n_ptr, rec.cap);
+        if (f < rec.max_frames) {
+            for (int i = tid; i < n; i += 256) reinterpret_cast<float2*>(rec.tracks)[(int64_t)f * rec.cap + i] = pts[i];
+            if (tid == 0) rec.counts[f] = n;
+        }
+        __syncthreads();
+        if (tid == 0) *rec.frame = f + 1;
     }
 }
 
@@ -243,12 +286,14 @@ hipError_t launch_detect_prep(gvx_ctx* c, const DetectPrep& p) {
 
 hipError_t launch_detect_merge(gvx_ctx* c, int bcnt, int bcols, int col, int row, int maxpb, int max_features,
                                const int* skip, const int* ncorner, const float2* out, float* pts, float* vel,
-                               float* init, int32_t* n, float* corners_out, int32_t* n_corners_out) {
+                               float* init, int32_t* n, float* corners_out, int32_t* n_corners_out,
+                               const TrackRecord* rec) {
     if (bcnt > 1024) return hipErrorInvalidValue;
+    const TrackRecord r = rec ? *rec : TrackRecord{};
     detect_merge_kernel<<<1, 256, 0, c->stream>>>(bcnt, bcols, col, row, maxpb, max_features, skip, ncorner, out,
                                                   reinterpret_cast<float2*>(pts), reinterpret_cast<float2*>(vel),
                                                   reinterpret_cast<float2*>(init), n,
-                                                  reinterpret_cast<float2*>(corners_out), n_corners_out);
+                                                  reinterpret_cast<float2*>(corners_out), n_corners_out, r);
     return hipGetLastError();
 }
 

@@ -206,6 +206,8 @@ def _declare(L):
         "gvx_track_record_dev": (i32, [P, P, P, i32, P, P, P, i32]),
         "gvx_track_frame_dev": (i32, [P, u64, u64, i32, P, P, P, P, i32, i32, i32, f64, f64, C.POINTER(KltParams),
                                       C.POINTER(DetectParams), P, P, P]),
+        "gvx_track_frame_record_dev": (i32, [P, u64, u64, i32, P, P, P, P, i32, i32, i32, f64, f64,
+                                             C.POINTER(KltParams), C.POINTER(DetectParams), P, P, P, i32]),
         "gvx_find_fundamental_ransac_dev": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
         "gvx_capture_begin": (i32, [P]),
         "gvx_capture_end": (i32, [P, C.POINTER(P)]),
@@ -388,6 +390,18 @@ class Context:
                                                 d_n, capacity, cam_w, cam_h, fb_thresh, border, C.byref(kp),
                                                 C.byref(dp), d_kept, d_corners, d_n_corners),
                     "gvx_track_frame_dev")
+
+    def track_frame_record_dev(self, prev_id: int, next_id: int, track: bool, d_pts, d_vel, d_init, d_n,
+                               capacity: int, cam_w: int, cam_h: int, d_tracks, d_counts, d_frame_index,
+                               max_frames: int, klt: Optional[KltParams] = None,
+                               detect: Optional[DetectParams] = None, fb_thresh=0.5, border=5.0):
+        """track_frame_dev then track_record_dev, the record fused into the last kernel."""
+        kp = klt or KltParams.default()
+        dp = detect or DetectParams.default()
+        self._check(self._L.gvx_track_frame_record_dev(self._h, prev_id, next_id, 1 if track else 0, d_pts, d_vel,
+                                                       d_init, d_n, capacity, cam_w, cam_h, fb_thresh, border,
+                                                       C.byref(kp), C.byref(dp), d_tracks, d_counts, d_frame_index,
+                                                       max_frames), "gvx_track_frame_record_dev")
 
     def copy_indexed_dev(self, d_dst: int, d_src_base: int, nbytes: int, d_index: int):
         self._check(self._L.gvx_copy_indexed_dev(self._h, d_dst, d_src_base, nbytes, d_index), "gvx_copy_indexed_dev")

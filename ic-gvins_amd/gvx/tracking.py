@@ -117,11 +117,16 @@ class DeviceSequenceTracker:
                                              self.w, self.h, params=self.kp)
         else:
             ctx.frame_preprocess_dev(cur, d_frame, self.w, self.h, None, params=self.kp)
-        ctx.track_frame_dev(prev, cur, t > 0, self.pts.data_ptr(), self.vel.data_ptr(), self.init.data_ptr(),
-                            self.count.data_ptr(), self.n, self.w, self.h, klt=self.kp, detect=self.dp)
         if self.frames is not None:
-            ctx.track_record_dev(self.pts.data_ptr(), self.count.data_ptr(), self.n, self.rec_tracks.data_ptr(),
-                                 self.rec_counts.data_ptr(), self.index.data_ptr(), self.frames.shape[0])
+            # the frame and its track-list record (appended by the detection's
+            # last kernel, which advances the frame index)
+            ctx.track_frame_record_dev(prev, cur, t > 0, self.pts.data_ptr(), self.vel.data_ptr(),
+                                       self.init.data_ptr(), self.count.data_ptr(), self.n, self.w, self.h,
+                                       self.rec_tracks.data_ptr(), self.rec_counts.data_ptr(), self.index.data_ptr(),
+                                       self.frames.shape[0], klt=self.kp, detect=self.dp)
+        else:
+            ctx.track_frame_dev(prev, cur, t > 0, self.pts.data_ptr(), self.vel.data_ptr(), self.init.data_ptr(),
+                                self.count.data_ptr(), self.n, self.w, self.h, klt=self.kp, detect=self.dp)
 
     def step(self, d_frame: Optional[int] = None) -> None:
         """Enqueue one frame (nothing waits); the tracks are

@@ -334,6 +334,13 @@ gvx_status gvx_track_frame_dev(gvx_ctx* ctx, uint64_t prev_frame, uint64_t next_
                                int32_t cam_h, double fb_thresh, double border, const gvx_klt_params* klt,
                                const gvx_detect_params* detect, int32_t* d_kept, float* d_corners,
                                int32_t* d_n_corners);
+/* gvx_track_frame_dev followed by gvx_track_record_dev (below) on the same state,
+   the record appended by the detection's last kernel (one launch less per frame). */
+gvx_status gvx_track_frame_record_dev(gvx_ctx* ctx, uint64_t prev_frame, uint64_t next_frame, int32_t track,
+                                      float* d_pts, float* d_vel, float* d_init, int32_t* d_n, int32_t capacity,
+                                      int32_t cam_w, int32_t cam_h, double fb_thresh, double border,
+                                      const gvx_klt_params* klt, const gvx_detect_params* detect, float* d_tracks,
+                                      int32_t* d_counts, int32_t* d_frame_index, int32_t max_frames);
 /* Helpers that keep a replay loop inside one captured graph per frame: copy
    bytes from d_src_base + (*d_index) * bytes (e.g. frame *d_index of a sequence
    resident in HBM), and append the current track list (*d_n points of d_pts) to
