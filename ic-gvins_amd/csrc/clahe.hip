@@ -27,6 +27,8 @@
 //  mean_kernel   Tracking::calculateHistigram from the image histogram.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gvx_internal.h"
 
 namespace gvx {
@@ -403,8 +405,16 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
                        src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index);
     // bands of rows sharing one pair of LUT rows, split to fill the chip
     const int nb = g.tiles_y + 1;
+    // workgroups wanted for the apply pass: each one first builds its band's
+    // interleaved LUT table (an L2 round trip), so splitting a single frame's
+    // bands down to a row or two each costs more than it hides
+    static const int apply_wg = [] {
+        const char* e = getenv("GVX_CLAHE_APPLY_WG");
+        return e ? atoi(e) : 0;
+    }();
+    const int64_t want_wg = apply_wg > 0 ? apply_wg : (n > 1 ? 4LL * c->n_cu : (int64_t)c->n_cu / 2);
     int nsplit = 1;
-    while ((int64_t)n * nb * nsplit < 4LL * c->n_cu && nsplit < g.th) nsplit *= 2;
+    while ((int64_t)n * nb * nsplit < want_wg && nsplit < g.th) nsplit *= 2;
     const int cols = (g.w + PPT - 1) / PPT;
     const int threads = std::min(1024, (cols + 63) / 64 * 64);
     const size_t lds = (size_t)(g.tiles_x + 1) * TROW * 4;

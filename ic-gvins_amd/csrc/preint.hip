@@ -16,6 +16,8 @@
 // rotation-vector exponentials.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dmath.h"
 #include "gvx_internal.h"
 
@@ -368,12 +370,402 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
     }
 }
 
+// ------------------------------------------------ three-phase preintegration
+// preint_kernel's sequential part runs on every lane of a wave that serves 4
+// segments: the wave's issue time per step is the same whether it advances 4
+// segments or 64, and 5,247 segments give 1.3 k such waves for 1,024 SIMDs.
+// The three-phase form splits the step by what it depends on:
+//   preint_pre_kernel    one lane per STEP (a workgroup per segment): the
+//                        StepPre terms -- every transcendental (rotvec2quaternion)
+//                        of the step -- fully parallel;
+//   preint_state_kernel  one lane per SEGMENT: the state recursion alone (64
+//                        segments per wave), StepPre prefetched three steps
+//                        ahead; writes pn_ and the step's cbb0;
+//   preint_cov_kernel    16 lanes per segment: J <- Phi J, P <- Phi P Phi^T + Qk
+//                        with Phi and W rebuilt from cbb0 and the IMU sample.
+// Every value is formed by the same operations in the same order as in
+// preint_kernel, so the results are the same bits (tests/test_ba_gpu.py).
+struct PreG {                // StepPre terms of one step (scratch, per IMU step)
+    double dtime;            // delta_time after the step
+    double dvfb[3];
+    double qd[4];
+    double qnn[4], qa[4], qb[4];  // Earth only
+};
+constexpr int PREG_DW = sizeof(PreG) / 8;  // 20
+constexpr int PREG_NORMAL_DW = 8;          // dtime, dvfb, qd
+constexpr int CB_DW = 9;                   // cbb0 per step (state -> cov)
+
+__global__ void __launch_bounds__(64) preint_pre_kernel(int variant, int n_seg, const gvx_imu* __restrict__ imu,
+                                                        const int32_t* __restrict__ seg_off,
+                                                        const gvx_state* __restrict__ state0,
+                                                        const double* __restrict__ iewn_in, PreG* __restrict__ pre) {
+    const int seg = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int b0 = seg_off[seg];
+    const int m = seg_off[seg + 1] - b0;
+    const gvx_imu* im = imu + b0;
+    PreG* pg = pre + (b0 - seg);
+    const bool earth = variant == GVX_PREINT_EARTH;
+    const gvx_state& s0 = state0[seg];
+    double bg[3], ba[3], iewn[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        bg[i] = s0.bg[i];
+        ba[i] = s0.ba[i];
+    }
+    const dq q0 = dq_load(s0.q);
+    const dq q0i = dq_inv(q0);
+    if (earth)
+        for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    double base = 0.0;  // delta_time before the chunk
+    for (int kc = 1; kc < m; kc += 64) {
+        const int k = kc + lane;
+        const int kend = min(kc + 64, m);
+        // delta_time_ += dt in sample order: lane k sums samples kc..k onto base
+        double dtime = base;
+        for (int i = kc; i < kend; ++i)
+            if (i <= k) dtime += im[i].dt;
+        base = __shfl(dtime, kend - 1 - kc);
+        if (k >= m) continue;
+        const Imu pr = load_imu(im + k - 1, bg, ba);
+        const Imu ic = load_imu(im + k, bg, ba);
+        PreG g;
+        g.dtime = dtime;
+        double c1[3], c2[3], c3[3], dth[3];
+        cross3(ic.dth, ic.dv, c1);
+        cross3(pr.dth, ic.dv, c2);
+        cross3(pr.dv, ic.dth, c3);
+        for (int i = 0; i < 3; ++i) g.dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
+        cross3(pr.dth, ic.dth, c1);
+        for (int i = 0; i < 3; ++i) dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
+        dq_store(dq_from_rotvec(dth), g.qd);
+        double* dst = reinterpret_cast<double*>(pg + (k - 1));
+        const double* w = reinterpret_cast<const double*>(&g);
+        if (earth) {
+            const double dt = ic.dt;
+            const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
+            dq_store(dq_from_rotvec(dnn), g.qnn);
+            const double sc = -(dtime - 0.5 * dt);
+            const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
+            dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), g.qa);
+            const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
+            dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), g.qb);
+#pragma unroll
+            for (int i = 0; i < PREG_DW; i += 2)
+                *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+        } else {
+#pragma unroll
+            for (int i = 0; i < PREG_NORMAL_DW; i += 2)
+                *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) preint_state_kernel(int variant, gvx_imu_params prm, int n_seg,
+                                                          const gvx_imu* __restrict__ imu,
+                                                          const int32_t* __restrict__ seg_off,
+                                                          const gvx_state* __restrict__ state0,
+                                                          const double* __restrict__ iewn_in,
+                                                          const PreG* __restrict__ pre,
+                                                          gvx_preint_result* __restrict__ out,
+                                                          double* __restrict__ pn, double* __restrict__ cb) {
+    const int seg = blockIdx.x * 64 + threadIdx.x;
+    if (seg >= n_seg) return;  // no barriers below
+    const int b0 = seg_off[seg];
+    const int m = seg_off[seg + 1] - b0;
+    const gvx_imu* im = imu + b0;
+    double* pns = pn ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    const double* pg = reinterpret_cast<const double*>(pre + (b0 - seg));
+    double* cbs = cb + (size_t)(b0 - seg) * CB_DW;
+    const bool earth = variant == GVX_PREINT_EARTH;
+    const int ndw = earth ? PREG_DW : PREG_NORMAL_DW;
+    gvx_state cur = state0[seg];
+    double dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+    dq dqt = dq_make(1, 0, 0, 0);
+    const dq q0 = dq_load(cur.q);
+    double iewn[3] = {0, 0, 0};
+    if (earth)
+        for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    const double g3[3] = {0, 0, prm.gravity};
+    double delta_time = 0.0;
+    // StepPre of step k, and the step's dt, into registers
+    auto ld = [&](int k, double (&r)[PREG_DW + 1]) {
+        if (k >= m) return;
+        const double* src = pg + (size_t)(k - 1) * PREG_DW;
+#pragma unroll
+        for (int i = 0; i < PREG_DW; i += 2) {
+            if (i < ndw) {
+                const double2 v = *reinterpret_cast<const double2*>(src + i);
+                r[i] = v.x;
+                r[i + 1] = v.y;
+            }
+        }
+        r[PREG_DW] = im[k].dt;
+    };
+    auto step = [&](int k, const double (&r)[PREG_DW + 1]) {
+        const PreG& sp = *reinterpret_cast<const PreG*>(r);
+        const double dt = r[PREG_DW];
+        delta_time = sp.dtime;
+        const dq qd = dq_load(sp.qd);
+        double R[9], dvel[3], cbb0[9];
+        if (!earth) {
+            dq_rot(dq_load(cur.q), R);
+            mv3(R, sp.dvfb, dvel);
+            for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + g3[i] * dt;
+            for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
+            for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
+            dq_store(dq_normalized(dq_mul(dq_load(cur.q), qd)), cur.q);
+            dq_rot(dqt, R);
+            mv3(R, sp.dvfb, dvel);
+            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
+            for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
+            dqt = dq_normalized(dq_mul(dqt, qd));
+            dq_rot(dqt, R);
+            for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
+        } else {
+            double cc[3], dvcg[3], T[9], M1[9];
+            cross3(iewn, cur.v, cc);
+            for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc[i]) * dt;
+            dq_rot(dq_load(sp.qnn), T);
+            for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
+            dq_rot(dq_load(cur.q), R);
+            mm3(M1, R, T);
+            mv3(T, sp.dvfb, dvel);
+            for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + dvcg[i];
+            for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
+            for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
+            if (pns)
+                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, cur.p[0], cur.p[1], cur.p[2]};
+            dq_store(dq_normalized(dq_mul(dq_mul(dq_load(sp.qnn), dq_load(cur.q)), qd)), cur.q);
+            dq_rot(dq_mul(dq_load(sp.qa), dqt), R);
+            mv3(R, sp.dvfb, dvel);
+            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
+            for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
+            dqt = dq_normalized(dq_mul(dqt, qd));
+            dq_rot(dq_mul(dq_load(sp.qb), dqt), R);
+            for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
+        }
+        double* dst = cbs + (size_t)(k - 1) * CB_DW;
+#pragma unroll
+        for (int i = 0; i < CB_DW; ++i) dst[i] = cbb0[i];
+    };
+    // three register buffers: step k's loads are issued two steps before it runs
+    double A[PREG_DW + 1], B[PREG_DW + 1], C[PREG_DW + 1];
+    ld(1, A);
+    ld(2, B);
+    ld(3, C);
+    for (int k = 1; k < m; k += 3) {
+        step(k, A);
+        ld(k + 3, A);
+        if (k + 1 >= m) break;
+        step(k + 1, B);
+        ld(k + 4, B);
+        if (k + 2 >= m) break;
+        step(k + 2, C);
+        ld(k + 5, C);
+    }
+    if (m > 1) cur.time = im[m - 1].time;
+    gvx_preint_result* o = out + seg;
+    o->variant = variant;
+    o->m = m;
+    o->delta_time = delta_time;
+    o->start_time = im[0].time;
+    o->end_time = m > 1 ? im[m - 1].time : im[0].time;
+    o->current = cur;
+    gvx_state d;
+    d.time = 0;
+    for (int i = 0; i < 3; ++i) {
+        d.p[i] = dp[i];
+        d.v[i] = dv[i];
+        d.bg[i] = cur.bg[i];
+        d.ba[i] = cur.ba[i];
+        o->gravity[i] = g3[i];
+        o->iewn[i] = iewn[i];
+    }
+    dq_store(dqt, d.q);
+    o->delta = d;
+    dq_store(q0, o->q0);
+}
+
+__global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_params prm, int n_seg,
+                                                        const gvx_imu* __restrict__ imu,
+                                                        const int32_t* __restrict__ seg_off,
+                                                        const gvx_state* __restrict__ state0,
+                                                        const double* __restrict__ cb,
+                                                        gvx_preint_result* __restrict__ out) {
+    __shared__ double sIn[SPW][2][GL];
+    __shared__ double sG[SPW][MS];
+    const int lane = threadIdx.x;
+    const int grp = lane / GL, c = lane % GL;
+    const int seg = blockIdx.x * SPW + grp;
+    const bool live = seg < n_seg;
+    const int b0 = live ? seg_off[seg] : 0;
+    const int m = live ? seg_off[seg + 1] - b0 : 0;
+    int mmax = m;
+#pragma unroll
+    for (int o = GL; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+    const bool earth = variant == GVX_PREINT_EARTH;
+    double bg[3] = {0, 0, 0}, ba[3] = {0, 0, 0};
+    if (live)
+        for (int i = 0; i < 3; ++i) {
+            bg[i] = state0[seg].bg[i];
+            ba[i] = state0[seg].ba[i];
+        }
+    const double nacc = prm.acc_vrw * prm.acc_vrw;
+    const double ngyr = prm.gyr_arw * prm.gyr_arw;
+    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
+    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
+    const double g60 = earth ? -1.0 : 1.0;
+    const double wg = (g60 * ngyr) * g60;
+    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    double Jc[NS], Pc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        Jc[i] = i == c ? 1.0 : 0.0;
+        Pc[i] = 0.0;
+    }
+    // lane c of the group loads one double of step k: cbb0[c] (c < 9) or the
+    // sample's dt, dtheta, dvel (c = 9..15)
+    const double* src_cb = cb + (size_t)(live ? b0 - seg : 0) * CB_DW + c;
+    const double* src_im = reinterpret_cast<const double*>(imu + b0) + (c - 8);
+    auto fetch = [&](int k) -> double {
+        if (k >= m) return 0.0;
+        return c < CB_DW ? src_cb[(size_t)(k - 1) * CB_DW] : src_im[(size_t)k * (sizeof(gvx_imu) / 8)];
+    };
+    double pf0 = fetch(1), pf1 = fetch(2);
+    for (int k = 1; k < mmax; ++k) {
+        const bool act = k < m;
+        double* sp = sIn[grp][k & 1];
+        sp[c] = pf0;
+        pf0 = pf1;
+        pf1 = fetch(k + 2);
+        __syncthreads();
+        Phi f;
+        double Wv[9];
+        if (act) {
+            double cbb0[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cbb0[i] = sp[i];
+            const double dt = sp[9];
+            double sdth[3], sdv[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                sdth[i] = sp[10 + i] - dt * bg[i];
+                sdv[i] = sp[13 + i] - dt * ba[i];
+            }
+            const double sg = earth ? 1.0 : -1.0;
+            double gR[9];
+            for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double g = (gR[3 * a] * nacc) * gR[3 * b];
+                    g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+                    g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+                    Wv[3 * a + b] = g;
+                }
+            double S[9];
+            skew(sdv, S);
+            mm3(cbb0, S, f.C);
+            for (int i = 0; i < 9; ++i) f.D[i] = cbb0[i] * dt;
+            skew(sdth, S);
+            for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+            f.dt = dt;
+            f.f = 1 - dt / prm.corr_time;
+            double y[NS];
+            phi_mv(f, Pc, y);
+            if (c < NS) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
+            }
+            phi_mv(f, Jc, y);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+        }
+        __syncthreads();
+        if (act) {
+            const double a = 0.5 * f.dt;
+            const int cl = c < NS ? c : 0;
+            double K[NS];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
+            if (c >= 3 && c < 6) {
+                K[3] = K[3] + a * Wv[c - 3];
+                K[4] = K[4] + a * Wv[3 + c - 3];
+                K[5] = K[5] + a * Wv[6 + c - 3];
+            }
+#pragma unroll
+            for (int i = 6; i < NS; ++i)
+                if (i == c) K[i] = K[i] + a * wd(i);
+            const int r3 = c - 3, r6 = c - 6;
+            double phr[NS];
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                phr[3 + b] = (c == b) ? f.dt : (c == 3 + b ? 1.0 : 0.0);
+                const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
+                const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
+                const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
+                phr[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
+                phr[9 + b] = (c == 6 + b) ? -f.dt : (c == 9 + b ? f.f : 0.0);
+                phr[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (c == 12 + b ? f.f : 0.0);
+            }
+            double y[NS];
+            phi_mv(f, K, y);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Pc[i] = y[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                double u = Wv[3 * i] * phr[3];
+                u = u + Wv[3 * i + 1] * phr[4];
+                u = u + Wv[3 * i + 2] * phr[5];
+                Pc[3 + i] = y[3 + i] + a * u;
+            }
+#pragma unroll
+            for (int i = 6; i < NS; ++i) Pc[i] = y[i] + a * (wd(i) * phr[i]);
+        }
+    }
+    if (!live) return;
+    gvx_preint_result* o = out + seg;
+    if (c < NS) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            o->jacobian[i * NS + c] = Jc[i];
+            o->covariance[c * NS + i] = Pc[i];
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
                          const double* iewn, gvx_preint_result* out, double* pn) {
     if (n_seg <= 0) return hipSuccess;
+    // Three-phase form when the per-step scratch can be sized without a round trip:
+    // the IMU allocation bounds the number of samples (hipMemGetAddressRange).
+    // A pointer into a large pooled block bounds nothing useful: above 1 GiB of
+    // scratch the single kernel runs.  GVX_PREINT_ONEPHASE=1 forces it (A/B and
+    // the bit-identity test; read per call).
+    const char* e1 = getenv("GVX_PREINT_ONEPHASE");
+    const bool one_phase = e1 && atoi(e1) != 0;
+    hipDeviceptr_t base = nullptr;
+    size_t range = 0;
+    if (!one_phase && hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)imu) == hipSuccess && range > 0) {
+        const size_t samples = (reinterpret_cast<const char*>(base) + range - reinterpret_cast<const char*>(imu)) /
+                               sizeof(gvx_imu);
+        const size_t bytes = samples * (sizeof(PreG) + CB_DW * sizeof(double));
+        char* d = bytes <= (size_t(1) << 30) ? (char*)scratch(c, "preint_steps", bytes) : nullptr;
+        if (d) {
+            PreG* pre = reinterpret_cast<PreG*>(d);
+            double* cb = reinterpret_cast<double*>(d + samples * sizeof(PreG));
+            hipLaunchKernelGGL(preint_pre_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, imu, seg_off,
+                               state0, iewn, pre);
+            hipLaunchKernelGGL(preint_state_kernel, dim3((n_seg + 63) / 64), dim3(64), 0, c->stream, variant, prm,
+                               n_seg, imu, seg_off, state0, iewn, (const PreG*)pre, out, pn, cb);
+            hipLaunchKernelGGL(preint_cov_kernel, dim3((n_seg + SPW - 1) / SPW), dim3(64), 0, c->stream, variant,
+                               prm, n_seg, imu, seg_off, state0, (const double*)cb, out);
+            return hipGetLastError();
+        }
+    }
+    (void)hipGetLastError();  // a failed range query is not an error of this call
     hipLaunchKernelGGL(preint_kernel, dim3((n_seg + SPW - 1) / SPW), dim3(64), 0, c->stream, variant, prm, n_seg, imu,
                        seg_off, state0, iewn, out, pn);
     return hipGetLastError();

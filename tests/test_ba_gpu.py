@@ -128,3 +128,24 @@ def test_reproj_bad_offsets_rejected(ctx, gvx_mod):
     offs[0, 0] = 10 ** 6
     with pytest.raises(gvx_mod.GvxError):
         ctx.reproj_eval(prob["consts"].astype(gvx_mod.REPROJ_DTYPE), prob["params"], offs)
+
+
+@pytest.mark.parametrize("variant", [NORMAL, EARTH])
+def test_preint_two_phase_bits_equal_one_phase(ctx, gvx_mod, variant, monkeypatch):
+    """launch_preint's two-phase form (state recursion once per segment, then the
+    16-lane covariance pass) does the same operations in the same order as the
+    single kernel: every output byte equal, ragged segments included."""
+    rng = np.random.default_rng(5 + variant)
+    ms = [1, 2, 3, 17, 64, 100, 101, 5, 100, 33]
+    segs, states = _segments(rng, ms)
+    iewn = np.array([[0.0, 4.1e-5, -5.7e-5]] * len(ms)) + rng.normal(0, 1e-6, (len(ms), 3))
+    gstates = np.zeros(len(ms), gvx_mod.STATE_DTYPE)
+    for k in ("time", "p", "q", "v", "bg", "ba"):
+        gstates[k] = states[k]
+    monkeypatch.setenv("GVX_PREINT_ONEPHASE", "1")
+    o1, pn1, _ = ctx.preint_integrate(variant, synth_ba.imu_params(), segs, gstates, iewn)
+    monkeypatch.setenv("GVX_PREINT_ONEPHASE", "0")
+    o2, pn2, _ = ctx.preint_integrate(variant, synth_ba.imu_params(), segs, gstates, iewn)
+    assert o1.tobytes() == o2.tobytes()
+    if variant == EARTH:
+        assert np.array_equal(pn1, pn2)

@@ -40,4 +40,19 @@ for name, imgs in contents.items():
     ctx.profile(False)
     print(f"{name:10s} {ms / n:.4f} ms per {N} images ({2.0 * W * H * N / (ms / n * 1e-3) / 1e9:.0f} GB/s algorithmic)",
           flush=True)
+# single frames (the live tracker / sequence replay), 1280x560, synthetic content
+src1 = torch.from_numpy(np.ascontiguousarray(I[0])).cuda()
+dst1 = torch.empty_like(src1)
+for _ in range(20):
+    ctx.clahe_batch_dev(1, W, H, src1.data_ptr(), dst1.data_ptr())
+ctx.sync()
+ctx.profile_reset()
+ctx.profile(True)
+for _ in range(200):
+    ctx.clahe_batch_dev(1, W, H, src1.data_ptr(), dst1.data_ptr())
+ctx.sync()
+ms, n = ctx.profile_read("clahe")
+ctx.profile(False)
+print(f"single     {1e3 * ms / n:.2f} us per frame (apply workgroups: GVX_CLAHE_APPLY_WG={os.environ.get('GVX_CLAHE_APPLY_WG', 'default')})",
+      flush=True)
 ctx.close()
