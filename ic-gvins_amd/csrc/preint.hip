@@ -370,19 +370,23 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
     }
 }
 
-// ------------------------------------------------ three-phase preintegration
+// ------------------------------------------------ four-launch preintegration
 // preint_kernel's sequential part runs on every lane of a wave that serves 4
 // segments: the wave's issue time per step is the same whether it advances 4
 // segments or 64, and 5,247 segments give 1.3 k such waves for 1,024 SIMDs.
-// The three-phase form splits the step by what it depends on:
+// Of that part only the two quaternion chains (cur.q and the delta rotation
+// dqt) and the velocity / position sums are truly sequential; the rotation
+// matrices and rotated increments of a step follow from the chain values.  So:
 //   preint_pre_kernel    one lane per STEP (a workgroup per segment): the
-//                        StepPre terms -- every transcendental (rotvec2quaternion)
-//                        of the step -- fully parallel;
-//   preint_state_kernel  one lane per SEGMENT: the state recursion alone (64
-//                        segments per wave), StepPre prefetched three steps
-//                        ahead; writes pn_ and the step's cbb0;
-//   preint_cov_kernel    16 lanes per segment: J <- Phi J, P <- Phi P Phi^T + Qk
-//                        with Phi and W rebuilt from cbb0 and the IMU sample.
+//                        StepPre terms -- every transcendental of the step;
+//   preint_chain_kernel  one lane per SEGMENT (64 per wave): the two quaternion
+//                        chains alone, StepPre prefetched three steps ahead;
+//   preint_rot_kernel    one lane per STEP: the rotated increments of the
+//                        velocity updates and cbb0 from the chain values;
+//   preint_cov_kernel    16 lanes per segment: the velocity / position sums
+//                        (a few adds per step, on every lane of the group), J <-
+//                        Phi J and P <- Phi P Phi^T + Qk with Phi and W rebuilt
+//                        from cbb0 and the IMU sample.
 // Every value is formed by the same operations in the same order as in
 // preint_kernel, so the results are the same bits (tests/test_ba_gpu.py).
 struct PreG {                // StepPre terms of one step (scratch, per IMU step)
@@ -393,7 +397,17 @@ struct PreG {                // StepPre terms of one step (scratch, per IMU step
 };
 constexpr int PREG_DW = sizeof(PreG) / 8;  // 20
 constexpr int PREG_NORMAL_DW = 8;          // dtime, dvfb, qd
-constexpr int CB_DW = 9;                   // cbb0 per step (state -> cov)
+struct QRec {                // the chains after step k
+    double q[4], dqt[4];
+};
+struct RRec {                // rotated terms of step k
+    double cbb0[9];          // -R(dqt) (Normal) or -R(qb dqt) (Earth)
+    double a[3];             // velocity increment before gravity / Coriolis
+    double b[3];             // delta-velocity increment
+    double pad;
+};
+constexpr int RREC_DW = sizeof(RRec) / 8;  // 16
+constexpr size_t STEP_SCRATCH = sizeof(PreG) + sizeof(QRec) + sizeof(RRec);
 
 __global__ void __launch_bounds__(64) preint_pre_kernel(int variant, int n_seg, const gvx_imu* __restrict__ imu,
                                                         const int32_t* __restrict__ seg_off,
@@ -419,12 +433,16 @@ __global__ void __launch_bounds__(64) preint_pre_kernel(int variant, int n_seg, 
     double base = 0.0;  // delta_time before the chunk
     for (int kc = 1; kc < m; kc += 64) {
         const int k = kc + lane;
-        const int kend = min(kc + 64, m);
-        // delta_time_ += dt in sample order: lane k sums samples kc..k onto base
-        double dtime = base;
-        for (int i = kc; i < kend; ++i)
-            if (i <= k) dtime += im[i].dt;
-        base = __shfl(dtime, kend - 1 - kc);
+        const int cnt = min(64, m - kc);
+        // delta_time_ += dt in sample order: a running sum over the chunk's
+        // samples (read lane by lane), lane k keeps its prefix
+        const double mydt = k < m ? im[k].dt : 0.0;
+        double acc = base, dtime = 0.0;
+        for (int i = 0; i < cnt; ++i) {
+            acc += __shfl(mydt, i);
+            if (lane == i) dtime = acc;
+        }
+        base = acc;
         if (k >= m) continue;
         const Imu pr = load_imu(im + k - 1, bg, ba);
         const Imu ic = load_imu(im + k, bg, ba);
@@ -460,139 +478,154 @@ __global__ void __launch_bounds__(64) preint_pre_kernel(int variant, int n_seg, 
     }
 }
 
-__global__ void __launch_bounds__(64) preint_state_kernel(int variant, gvx_imu_params prm, int n_seg,
-                                                          const gvx_imu* __restrict__ imu,
-                                                          const int32_t* __restrict__ seg_off,
-                                                          const gvx_state* __restrict__ state0,
-                                                          const double* __restrict__ iewn_in,
-                                                          const PreG* __restrict__ pre,
-                                                          gvx_preint_result* __restrict__ out,
-                                                          double* __restrict__ pn, double* __restrict__ cb) {
-    const int seg = blockIdx.x * 64 + threadIdx.x;
+// The quaternion chains, and every output field that does not depend on the
+// velocity / position sums or on J / P.
+template <bool EARTH>
+__global__ void __launch_bounds__(128) preint_chain_kernel(gvx_imu_params prm, int n_seg,
+                                                           const gvx_imu* __restrict__ imu,
+                                                           const int32_t* __restrict__ seg_off,
+                                                           const gvx_state* __restrict__ state0,
+                                                           const double* __restrict__ iewn_in,
+                                                           const PreG* __restrict__ pre, QRec* __restrict__ qrec,
+                                                           gvx_preint_result* __restrict__ out) {
+    // wave 0 runs the cur.q chain, wave 1 the dqt chain of the same 64 segments:
+    // the two chains are independent, and each wave issues half the work
+    const bool dwave = threadIdx.x >= 64;
+    const int seg = blockIdx.x * 64 + (threadIdx.x & 63);
     if (seg >= n_seg) return;  // no barriers below
     const int b0 = seg_off[seg];
     const int m = seg_off[seg + 1] - b0;
     const gvx_imu* im = imu + b0;
-    double* pns = pn ? pn + (size_t)(b0 - seg) * 4 : nullptr;
     const double* pg = reinterpret_cast<const double*>(pre + (b0 - seg));
-    double* cbs = cb + (size_t)(b0 - seg) * CB_DW;
-    const bool earth = variant == GVX_PREINT_EARTH;
-    const int ndw = earth ? PREG_DW : PREG_NORMAL_DW;
-    gvx_state cur = state0[seg];
-    double dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
-    dq dqt = dq_make(1, 0, 0, 0);
-    const dq q0 = dq_load(cur.q);
-    double iewn[3] = {0, 0, 0};
-    if (earth)
-        for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
-    const double g3[3] = {0, 0, prm.gravity};
-    double delta_time = 0.0;
-    // StepPre of step k, and the step's dt, into registers
-    auto ld = [&](int k, double (&r)[PREG_DW + 1]) {
-        if (k >= m) return;
-        const double* src = pg + (size_t)(k - 1) * PREG_DW;
+    double* qs = reinterpret_cast<double*>(qrec + (b0 - seg)) + (dwave ? 4 : 0);
+    constexpr bool earth = EARTH;
+    constexpr int variant = EARTH ? GVX_PREINT_EARTH : GVX_PREINT_NORMAL;
+    const gvx_state s0 = state0[seg];
+    // the q chain reads qd and qnn (PreG doubles 4..11), the dqt chain qd
+    const bool two = earth && !dwave;
+    dq q = dwave ? dq_make(1, 0, 0, 0) : dq_load(s0.q);
+    // StepPre inputs in chunks of CK steps: chunk i+1 is loaded while chunk i
+    // runs and copied over at the chunk's end, so each load has CK steps of the
+    // chain to land (loads never predicated: a clamped index)
+    constexpr int CK = 4;
+    const int last = m >= 2 ? m - 2 : 0;
+    auto ldc = [&](int kc, double (&X)[CK][8]) {
 #pragma unroll
-        for (int i = 0; i < PREG_DW; i += 2) {
-            if (i < ndw) {
-                const double2 v = *reinterpret_cast<const double2*>(src + i);
-                r[i] = v.x;
-                r[i + 1] = v.y;
+        for (int j = 0; j < CK; ++j) {
+            const double* src = pg + (size_t)min(kc + j - 1, last) * PREG_DW + 4;
+            const double2 v0 = *reinterpret_cast<const double2*>(src);
+            const double2 v1 = *reinterpret_cast<const double2*>(src + 2);
+            X[j][0] = v0.x;
+            X[j][1] = v0.y;
+            X[j][2] = v1.x;
+            X[j][3] = v1.y;
+            if (two) {
+                const double2 v2 = *reinterpret_cast<const double2*>(src + 4);
+                const double2 v3 = *reinterpret_cast<const double2*>(src + 6);
+                X[j][4] = v2.x;
+                X[j][5] = v2.y;
+                X[j][6] = v3.x;
+                X[j][7] = v3.y;
             }
         }
-        r[PREG_DW] = im[k].dt;
     };
-    auto step = [&](int k, const double (&r)[PREG_DW + 1]) {
-        const PreG& sp = *reinterpret_cast<const PreG*>(r);
-        const double dt = r[PREG_DW];
-        delta_time = sp.dtime;
-        const dq qd = dq_load(sp.qd);
-        double R[9], dvel[3], cbb0[9];
-        if (!earth) {
-            dq_rot(dq_load(cur.q), R);
-            mv3(R, sp.dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + g3[i] * dt;
-            for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
-            dq_store(dq_normalized(dq_mul(dq_load(cur.q), qd)), cur.q);
-            dq_rot(dqt, R);
-            mv3(R, sp.dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
-            dqt = dq_normalized(dq_mul(dqt, qd));
-            dq_rot(dqt, R);
-            for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
-        } else {
-            double cc[3], dvcg[3], T[9], M1[9];
-            cross3(iewn, cur.v, cc);
-            for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc[i]) * dt;
-            dq_rot(dq_load(sp.qnn), T);
-            for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
-            dq_rot(dq_load(cur.q), R);
-            mm3(M1, R, T);
-            mv3(T, sp.dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + dvcg[i];
-            for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
-            if (pns)
-                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, cur.p[0], cur.p[1], cur.p[2]};
-            dq_store(dq_normalized(dq_mul(dq_mul(dq_load(sp.qnn), dq_load(cur.q)), qd)), cur.q);
-            dq_rot(dq_mul(dq_load(sp.qa), dqt), R);
-            mv3(R, sp.dvfb, dvel);
-            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
-            dqt = dq_normalized(dq_mul(dqt, qd));
-            dq_rot(dq_mul(dq_load(sp.qb), dqt), R);
-            for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
-        }
-        double* dst = cbs + (size_t)(k - 1) * CB_DW;
+    auto step = [&](int k, const double (&r)[8]) {
+        const dq qd = dq_load(r);
+        if (two)
+            q = dq_normalized(dq_mul(dq_mul(dq_load(r + 4), q), qd));
+        else  // Normal cur.q, and dqt in both variants
+            q = dq_normalized(dq_mul(q, qd));
+        *reinterpret_cast<double4*>(qs + (size_t)(k - 1) * 8) = double4{q.x, q.y, q.z, q.w};
+    };
+    double X[CK][8], Y[CK][8];
+    if (m > 1) ldc(1, X);
+    for (int kc = 1; kc < m; kc += CK) {
+        ldc(kc + CK, Y);
 #pragma unroll
-        for (int i = 0; i < CB_DW; ++i) dst[i] = cbb0[i];
-    };
-    // three register buffers: step k's loads are issued two steps before it runs
-    double A[PREG_DW + 1], B[PREG_DW + 1], C[PREG_DW + 1];
-    ld(1, A);
-    ld(2, B);
-    ld(3, C);
-    for (int k = 1; k < m; k += 3) {
-        step(k, A);
-        ld(k + 3, A);
-        if (k + 1 >= m) break;
-        step(k + 1, B);
-        ld(k + 4, B);
-        if (k + 2 >= m) break;
-        step(k + 2, C);
-        ld(k + 5, C);
+        for (int j = 0; j < CK; ++j)
+            if (kc + j < m) step(kc + j, X[j]);
+#pragma unroll
+        for (int j = 0; j < CK; ++j)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) X[j][i] = Y[j][i];
     }
-    if (m > 1) cur.time = im[m - 1].time;
     gvx_preint_result* o = out + seg;
+    if (dwave) {
+        o->delta.time = 0;
+        dq_store(q, o->delta.q);
+        return;
+    }
+    dq_store(q, o->current.q);
     o->variant = variant;
     o->m = m;
-    o->delta_time = delta_time;
+    o->delta_time = m > 1 ? pg[(size_t)(m - 2) * PREG_DW] : 0.0;
     o->start_time = im[0].time;
     o->end_time = m > 1 ? im[m - 1].time : im[0].time;
-    o->current = cur;
-    gvx_state d;
-    d.time = 0;
+    o->current.time = m > 1 ? im[m - 1].time : s0.time;
     for (int i = 0; i < 3; ++i) {
-        d.p[i] = dp[i];
-        d.v[i] = dv[i];
-        d.bg[i] = cur.bg[i];
-        d.ba[i] = cur.ba[i];
-        o->gravity[i] = g3[i];
-        o->iewn[i] = iewn[i];
+        o->current.bg[i] = s0.bg[i];
+        o->current.ba[i] = s0.ba[i];
+        o->delta.bg[i] = s0.bg[i];
+        o->delta.ba[i] = s0.ba[i];
+        o->gravity[i] = i == 2 ? prm.gravity : 0.0;
+        o->iewn[i] = earth ? iewn_in[3 * seg + i] : 0.0;
     }
-    dq_store(dqt, d.q);
-    o->delta = d;
-    dq_store(q0, o->q0);
+    dq_store(dq_load(s0.q), o->q0);
+}
+
+__global__ void __launch_bounds__(64) preint_rot_kernel(int variant, int n_seg, const int32_t* __restrict__ seg_off,
+                                                        const gvx_state* __restrict__ state0,
+                                                        const PreG* __restrict__ pre,
+                                                        const QRec* __restrict__ qrec, RRec* __restrict__ rrec) {
+    const int seg = blockIdx.x;
+    const int b0 = seg_off[seg];
+    const int m = seg_off[seg + 1] - b0;
+    const bool earth = variant == GVX_PREINT_EARTH;
+    const size_t o0 = (size_t)(b0 - seg);
+    for (int k = 1 + threadIdx.x; k < m; k += 64) {
+        const PreG& g = pre[o0 + k - 1];
+        const dq qprev = k > 1 ? dq_load(qrec[o0 + k - 2].q) : dq_load(state0[seg].q);
+        const dq dprev = k > 1 ? dq_load(qrec[o0 + k - 2].dqt) : dq_make(1, 0, 0, 0);
+        const dq dcur = dq_load(qrec[o0 + k - 1].dqt);
+        double dvfb[3] = {g.dvfb[0], g.dvfb[1], g.dvfb[2]};
+        RRec r;
+        double R[9];
+        if (!earth) {
+            dq_rot(qprev, R);
+            mv3(R, dvfb, r.a);
+            dq_rot(dprev, R);
+            mv3(R, dvfb, r.b);
+            dq_rot(dcur, R);
+        } else {
+            double T[9], M1[9];
+            dq_rot(dq_load(g.qnn), T);
+            for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
+            dq_rot(qprev, R);
+            mm3(M1, R, T);
+            mv3(T, dvfb, r.a);
+            dq_rot(dq_mul(dq_load(g.qa), dprev), R);
+            mv3(R, dvfb, r.b);
+            dq_rot(dq_mul(dq_load(g.qb), dcur), R);
+        }
+        for (int i = 0; i < 9; ++i) r.cbb0[i] = -R[i];
+        r.pad = 0.0;
+        double* dst = reinterpret_cast<double*>(rrec + o0 + k - 1);
+        const double* w = reinterpret_cast<const double*>(&r);
+#pragma unroll
+        for (int i = 0; i < RREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+    }
 }
 
 __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_params prm, int n_seg,
                                                         const gvx_imu* __restrict__ imu,
                                                         const int32_t* __restrict__ seg_off,
                                                         const gvx_state* __restrict__ state0,
-                                                        const double* __restrict__ cb,
-                                                        gvx_preint_result* __restrict__ out) {
-    __shared__ double sIn[SPW][2][GL];
+                                                        const double* __restrict__ iewn_in,
+                                                        const RRec* __restrict__ rrec,
+                                                        gvx_preint_result* __restrict__ out,
+                                                        double* __restrict__ pn) {
+    constexpr int NIN = RREC_DW + 7;  // + the sample's dt, dtheta, dvel
+    __shared__ double sIn[SPW][2][NIN + 1];
     __shared__ double sG[SPW][MS];
     const int lane = threadIdx.x;
     const int grp = lane / GL, c = lane % GL;
@@ -604,12 +637,20 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
 #pragma unroll
     for (int o = GL; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
     const bool earth = variant == GVX_PREINT_EARTH;
-    double bg[3] = {0, 0, 0}, ba[3] = {0, 0, 0};
-    if (live)
-        for (int i = 0; i < 3; ++i) {
-            bg[i] = state0[seg].bg[i];
-            ba[i] = state0[seg].ba[i];
-        }
+    double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    gvx_state s0{};
+    double iewn[3] = {0, 0, 0};
+    if (live) {
+        s0 = state0[seg];
+        if (earth)
+            for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    }
+    double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        p[i] = s0.p[i];
+        v[i] = s0.v[i];
+    }
+    const double g3[3] = {0, 0, prm.gravity};
     const double nacc = prm.acc_vrw * prm.acc_vrw;
     const double ngyr = prm.gyr_arw * prm.gyr_arw;
     const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
@@ -623,34 +664,60 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
         Jc[i] = i == c ? 1.0 : 0.0;
         Pc[i] = 0.0;
     }
-    // lane c of the group loads one double of step k: cbb0[c] (c < 9) or the
-    // sample's dt, dtheta, dvel (c = 9..15)
-    const double* src_cb = cb + (size_t)(live ? b0 - seg : 0) * CB_DW + c;
-    const double* src_im = reinterpret_cast<const double*>(imu + b0) + (c - 8);
-    auto fetch = [&](int k) -> double {
-        if (k >= m) return 0.0;
-        return c < CB_DW ? src_cb[(size_t)(k - 1) * CB_DW] : src_im[(size_t)k * (sizeof(gvx_imu) / 8)];
+    // lane c of the group loads RRec double c and, for c < 7, the sample's
+    // double c + 1 (dt, dtheta, dvel)
+    const double* src_r = reinterpret_cast<const double*>(rrec + (live ? b0 - seg : 0)) + c;
+    const double* src_im = reinterpret_cast<const double*>(imu + b0) + 1 + (c < 7 ? c : 0);
+    // never predicated (a clamped step; lanes c >= 7 re-read dt), so the
+    // compiler's counters keep both prefetches in flight across the step
+    const int klast = m >= 2 ? m - 1 : 1;
+    auto fetch = [&](int k, double& x, double& y) {
+        const int kk = min(k, klast);
+        x = src_r[(size_t)(kk - 1) * RREC_DW];
+        y = src_im[(size_t)kk * (sizeof(gvx_imu) / 8)];
     };
-    double pf0 = fetch(1), pf1 = fetch(2);
+    double x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    fetch(1, x0, y0);
+    fetch(2, x1, y1);
     for (int k = 1; k < mmax; ++k) {
         const bool act = k < m;
         double* sp = sIn[grp][k & 1];
-        sp[c] = pf0;
-        pf0 = pf1;
-        pf1 = fetch(k + 2);
+        sp[c] = x0;
+        if (c < 7) sp[RREC_DW + c] = y0;
+        x0 = x1;
+        y0 = y1;
+        fetch(k + 2, x1, y1);
         __syncthreads();
         Phi f;
         double Wv[9];
         if (act) {
+            const RRec& rr = *reinterpret_cast<const RRec*>(sp);
+            const double dt = sp[RREC_DW];
+            // the velocity / position sums (integrationProcess, the order of preint_kernel)
+            double dvel[3];
+            if (!earth) {
+                for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + g3[i] * dt;
+            } else {
+                double cc[3], dvcg[3];
+                cross3(iewn, v, cc);
+                for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc[i]) * dt;
+                for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + dvcg[i];
+            }
+            for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
+            for (int i = 0; i < 3; ++i) v[i] += dvel[i];
+            if (pns && c == 0)
+                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
+            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * rr.b[i];
+            for (int i = 0; i < 3; ++i) dv[i] += rr.b[i];
+
             double cbb0[9];
 #pragma unroll
-            for (int i = 0; i < 9; ++i) cbb0[i] = sp[i];
-            const double dt = sp[9];
+            for (int i = 0; i < 9; ++i) cbb0[i] = rr.cbb0[i];
             double sdth[3], sdv[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                sdth[i] = sp[10 + i] - dt * bg[i];
-                sdv[i] = sp[13 + i] - dt * ba[i];
+                sdth[i] = sp[RREC_DW + 1 + i] - dt * s0.bg[i];
+                sdv[i] = sp[RREC_DW + 4 + i] - dt * s0.ba[i];
             }
             const double sg = earth ? 1.0 : -1.0;
             double gR[9];
@@ -731,6 +798,13 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
             o->covariance[c * NS + i] = Pc[i];
         }
     }
+    if (c == 0)
+        for (int i = 0; i < 3; ++i) {
+            o->current.p[i] = p[i];
+            o->current.v[i] = v[i];
+            o->delta.p[i] = dp[i];
+            o->delta.v[i] = dv[i];
+        }
 }
 
 }  // namespace
@@ -739,7 +813,7 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
                          const double* iewn, gvx_preint_result* out, double* pn) {
     if (n_seg <= 0) return hipSuccess;
-    // Three-phase form when the per-step scratch can be sized without a round trip:
+    // Four-launch form when the per-step scratch can be sized without a round trip:
     // the IMU allocation bounds the number of samples (hipMemGetAddressRange).
     // A pointer into a large pooled block bounds nothing useful: above 1 GiB of
     // scratch the single kernel runs.  GVX_PREINT_ONEPHASE=1 forces it (A/B and
@@ -751,17 +825,21 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
     if (!one_phase && hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)imu) == hipSuccess && range > 0) {
         const size_t samples = (reinterpret_cast<const char*>(base) + range - reinterpret_cast<const char*>(imu)) /
                                sizeof(gvx_imu);
-        const size_t bytes = samples * (sizeof(PreG) + CB_DW * sizeof(double));
+        const size_t bytes = samples * STEP_SCRATCH;
         char* d = bytes <= (size_t(1) << 30) ? (char*)scratch(c, "preint_steps", bytes) : nullptr;
         if (d) {
             PreG* pre = reinterpret_cast<PreG*>(d);
-            double* cb = reinterpret_cast<double*>(d + samples * sizeof(PreG));
+            QRec* qr = reinterpret_cast<QRec*>(d + samples * sizeof(PreG));
+            RRec* rr = reinterpret_cast<RRec*>(d + samples * (sizeof(PreG) + sizeof(QRec)));
             hipLaunchKernelGGL(preint_pre_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, imu, seg_off,
                                state0, iewn, pre);
-            hipLaunchKernelGGL(preint_state_kernel, dim3((n_seg + 63) / 64), dim3(64), 0, c->stream, variant, prm,
-                               n_seg, imu, seg_off, state0, iewn, (const PreG*)pre, out, pn, cb);
+            hipLaunchKernelGGL(variant == GVX_PREINT_EARTH ? preint_chain_kernel<true> : preint_chain_kernel<false>,
+                               dim3((n_seg + 63) / 64), dim3(128), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
+                               (const PreG*)pre, qr, out);
+            hipLaunchKernelGGL(preint_rot_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, seg_off,
+                               state0, (const PreG*)pre, (const QRec*)qr, rr);
             hipLaunchKernelGGL(preint_cov_kernel, dim3((n_seg + SPW - 1) / SPW), dim3(64), 0, c->stream, variant,
-                               prm, n_seg, imu, seg_off, state0, (const double*)cb, out);
+                               prm, n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
             return hipGetLastError();
         }
     }
