@@ -55,12 +55,14 @@ def test_capture_refused_while_profiling(ctx, gvx_mod):
         ctx.profile(False)
 
 
-def test_stale_graph_refused(ctx, gvx_mod):
+def test_stale_graph_refused(gvx_mod):
     """A graph holds raw pointers into the context's scratch: once a larger call
     reallocates the batch pyramids, replaying it must be refused (not read freed
-    memory)."""
+    memory).  A private context: the session one's scratch may already be larger
+    than `big` needs."""
     import torch
     from gvx import synth
+    ctx = gvx_mod.Context(0)
     W, H, N = 320, 140, 16
     dev = torch.device("cuda", 0)
     params = gvx_mod.KltParams.default()
@@ -90,3 +92,4 @@ def test_stale_graph_refused(ctx, gvx_mod):
     with pytest.raises(gvx_mod.GvxError):
         g.launch()
     g.destroy()
+    ctx.close()
