@@ -6,7 +6,7 @@ mkdir -p gpurun_out/$T
 for r in $(seq 1 $ROUNDS); do
   for n in "$@"; do
     if [ "$n" = base ]; then L=""; else L=$PWD/ic-gvins_amd/gvx/variants/libgvx_$n.so; fi
-    GVX_LIB=$L timeout -k 10 200 python bench.py --no-cpu --no-pre --steps 40 --warmup 30 > gpurun_out/$T/b_${n}_$r.json 2> gpurun_out/$T/b_${n}_$r.err
+    GVX_LIB=$L timeout -k 10 200 python bench.py --no-cpu --no-pre --no-factors --steps 40 --warmup 30 > gpurun_out/$T/b_${n}_$r.json 2> gpurun_out/$T/b_${n}_$r.err
   done
 done
 python3 - "$T" "$ROUNDS" "$@" <<'PY'
