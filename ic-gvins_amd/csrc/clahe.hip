@@ -405,14 +405,14 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
                        src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index);
     // bands of rows sharing one pair of LUT rows, split to fill the chip
     const int nb = g.tiles_y + 1;
-    // workgroups wanted for the apply pass: each one first builds its band's
-    // interleaved LUT table (an L2 round trip), so splitting a single frame's
-    // bands down to a row or two each costs more than it hides
+    // workgroups wanted for the apply pass (GVX_CLAHE_APPLY_WG overrides; the
+    // sequence replay's single frames measured 17.5 us at 1,024 against 19.9 at
+    // 128, r02 v16)
     static const int apply_wg = [] {
         const char* e = getenv("GVX_CLAHE_APPLY_WG");
         return e ? atoi(e) : 0;
     }();
-    const int64_t want_wg = apply_wg > 0 ? apply_wg : (n > 1 ? 4LL * c->n_cu : (int64_t)c->n_cu / 2);
+    const int64_t want_wg = apply_wg > 0 ? apply_wg : 4LL * c->n_cu;
     int nsplit = 1;
     while ((int64_t)n * nb * nsplit < want_wg && nsplit < g.th) nsplit *= 2;
     const int cols = (g.w + PPT - 1) / PPT;
