@@ -41,15 +41,14 @@ __device__ __forceinline__ int refl(int p, int len) {
 // and only those whose (2r+1)^2 box meets the tile are kept (LDS append), so a
 // pixel tests the few circles near it instead of all of them (the raster is a
 // logical OR: the order of the tests does not matter).
-__global__ void __launch_bounds__(256) mask_kernel(int w, int h, const int2* __restrict__ centers, int n,
-                                                   const int* __restrict__ hw, int r,
-                                                   uint8_t* __restrict__ mask, const int* __restrict__ n_dev,
-                                                   const int* __restrict__ skip) {
+__device__ void mask_tile(int bx, int by, int w, int h, const int2* __restrict__ centers, int n,
+                          const int* __restrict__ hw, int r, uint8_t* __restrict__ mask,
+                          const int* __restrict__ n_dev, const int* __restrict__ skip) {
     __shared__ int2 sc[256];
     __shared__ int s_n;
     if (skip && *skip) return;   // device-resident call: no detection this frame
     if (n_dev) n = *n_dev;
-    const int tx0 = blockIdx.x * 64, ty0 = blockIdx.y * 4;
+    const int tx0 = bx * 64, ty0 = by * 4;
     const int x = tx0 + (threadIdx.x & 63);
     const int y = ty0 + (threadIdx.x >> 6);
     bool hit = false;
@@ -79,17 +78,16 @@ __global__ void __launch_bounds__(256) mask_kernel(int w, int h, const int2* __r
 // ------------------------------------------------------------------ eig
 constexpr int ET_W = 64, ET_H = 16;
 
-__global__ void __launch_bounds__(256) eig_kernel(const uint8_t* __restrict__ img0, int pitch,
-                                                  const int4* __restrict__ rois, const int* __restrict__ blk_ids,
-                                                  int64_t eig_stride, float* __restrict__ eig, float sc,
-                                                  float sc2, const int* __restrict__ n_active_dev) {
+__device__ void eig_tile(int bx, int by, int bz, const uint8_t* __restrict__ img0, int pitch,
+                         const int4* __restrict__ rois, const int* __restrict__ blk_ids, int64_t eig_stride,
+                         float* __restrict__ eig, float sc, float sc2, const int* __restrict__ n_active_dev) {
     __shared__ uint8_t px[ET_H + 4][ET_W + 4];
     __shared__ float cov[3][ET_H + 2][ET_W + 2];
-    if (n_active_dev && (int)blockIdx.z >= *n_active_dev) return;
-    const int k = blk_ids[blockIdx.z];
+    if (n_active_dev && bz >= *n_active_dev) return;
+    const int k = blk_ids[bz];
     const int4 roi = rois[k];  // x0, y0, rw, rh
     const int rw = roi.z, rh = roi.w;
-    const int tx0 = blockIdx.x * ET_W, ty0 = blockIdx.y * ET_H;
+    const int tx0 = bx * ET_W, ty0 = by * ET_H;
     if (tx0 >= rw || ty0 >= rh) return;
     // parent pixels for ROI coords [tx0-2, tx0+ET_W+1] x [ty0-2, ty0+ET_H+1]
     // (ROI coords beyond rw+1 / rh+1 are never used; clamp them so the reads stay
@@ -152,6 +150,210 @@ __global__ void __launch_bounds__(256) eig_kernel(const uint8_t* __restrict__ im
     }
 }
 
+// The circle mask and the eigenvalue tiles do not depend on each other: one
+// launch, the first n_mask workgroups rasterise mask tiles (mx per row), the
+// rest compute eig tiles (ex x ey per block).  One kernel node less per frame
+// (a node costs ~4.5 us in the sequence replay's graph, however little it does).
+__global__ void __launch_bounds__(256) mask_eig_kernel(int n_mask, int mx, int w, int h,
+                                                       const int2* __restrict__ centers, int n_circles,
+                                                       const int* __restrict__ hw, int radius,
+                                                       uint8_t* __restrict__ mask, const int* __restrict__ n_dev,
+                                                       const int* __restrict__ skip, int ex, int ey,
+                                                       const uint8_t* __restrict__ img0, int pitch,
+                                                       const int4* __restrict__ rois,
+                                                       const int* __restrict__ blk_ids, int64_t eig_stride,
+                                                       float* __restrict__ eig, float sc, float sc2,
+                                                       const int* __restrict__ n_active_dev) {
+    const int b = blockIdx.x;
+    if (b < n_mask) {
+        mask_tile(b % mx, b / mx, w, h, centers, n_circles, hw, radius, mask, n_dev, skip);
+        return;
+    }
+    const int e = b - n_mask;
+    const int per = ex * ey;
+    const int bz = e / per, r = e - bz * per;
+    eig_tile(r % ex, r / ex, bz, img0, pitch, rois, blk_ids, eig_stride, eig, sc, sc2, n_active_dev);
+}
+
+// ------------------------------------------------------------------ subpix
+constexpr int SP_WIN = 5;
+constexpr int SP_W = 2 * SP_WIN + 1;  // 11
+constexpr int SP_B = SP_W + 2;        // 13
+
+// The ROI pixels around a corner's start, staged in LDS once per corner: every
+// iteration's 13x13 patch reads them from there while the centre stays inside
+// (ROI pixel (x, y) at win[(y - oy) * SW_W + x - ox]); other reads go to memory.
+constexpr int SW_W = 32;
+struct SubpixWin {
+    const uint8_t* win;
+    int ox, oy, nx, ny;  // origin and extent (clipped to the ROI)
+};
+__device__ __forceinline__ float roi_px(const uint8_t* __restrict__ src, int pitch, const SubpixWin& sw, int x,
+                                        int y) {
+    const unsigned dx = (unsigned)(x - sw.ox), dy = (unsigned)(y - sw.oy);
+    if (dx < (unsigned)sw.nx && dy < (unsigned)sw.ny) return (float)sw.win[dy * SW_W + dx];
+    return (float)src[(int64_t)y * pitch + x];
+}
+
+// getRectSubPix(ROI, 13x13, centre, CV_32F): value of patch pixel (i, j).
+__device__ float rect_subpix_px(const uint8_t* __restrict__ src, int pitch, int sw, int sh, float cx0,
+                                float cy0, int i, int j, const SubpixWin& win) {
+    const float cx = cx0 - (SP_B - 1) * 0.5f;
+    const float cy = cy0 - (SP_B - 1) * 0.5f;
+    const int ipx = (int)floorf(cx), ipy = (int)floorf(cy);
+    if (0 <= ipx && ipx + SP_B < sw && 0 <= ipy && ipy + SP_B < sh) {
+        float a = cx - ipx;
+        const float b = cy - ipy;
+        a = a > 0.0001f ? a : 0.0001f;
+        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
+        const double s = (1. - a) / a;
+        const int y0 = ipy + i, x0 = ipx;
+        const float t = a12 * roi_px(src, pitch, win, x0 + j + 1, y0) + a22 * roi_px(src, pitch, win, x0 + j + 1, y0 + 1);
+        float prev;
+        if (j == 0) {
+            prev = (1 - a) * (b1 * roi_px(src, pitch, win, x0, y0) + b2 * roi_px(src, pitch, win, x0, y0 + 1));
+        } else {
+            const float tp = a12 * roi_px(src, pitch, win, x0 + j, y0) + a22 * roi_px(src, pitch, win, x0 + j, y0 + 1);
+            prev = (float)(tp * s);
+        }
+        return prev + t;
+    }
+    const float a = cx - ipx, b = cy - ipy;
+    const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+    const float b1 = 1.f - b, b2 = b;
+    // adjustRect
+    int64_t off = 0;
+    int rx, rwid, ry, rhei;
+    if (ipx >= 0) {
+        off += ipx;
+        rx = 0;
+    } else {
+        rx = -ipx;
+        if (rx > SP_B) rx = SP_B;
+    }
+    if (ipx < sw - SP_B)
+        rwid = SP_B;
+    else {
+        rwid = sw - ipx - 1;
+        if (rwid < 0) {
+            off += rwid;
+            rwid = 0;
+        }
+    }
+    if (ipy >= 0) {
+        off += (int64_t)ipy * pitch;
+        ry = 0;
+    } else
+        ry = -ipy;
+    if (ipy < sh - SP_B)
+        rhei = SP_B;
+    else {
+        rhei = sh - ipy - 1;
+        if (rhei < 0) {
+            off += (int64_t)rhei * pitch;
+            rhei = 0;
+        }
+    }
+    const uint8_t* s = src + off - rx;
+    for (int q = 0; q < i; ++q) {
+        const uint8_t* s2 = s + pitch;
+        if (q < ry || q >= rhei) s2 -= pitch;
+        if (q < rhei) s = s2;
+    }
+    const uint8_t* s2 = s + pitch;
+    if (i < ry || i >= rhei) s2 -= pitch;
+    if (j < rx) return (float)s[rx] * b1 + (float)s2[rx] * b2;
+    if (j >= rwid) return (float)s[rwid] * b1 + (float)s2[rwid] * b2;
+    return (float)s[j] * a11 + (float)s[j + 1] * a12 + (float)s2[j] * a21 + (float)s2[j + 1] * a22;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// cornerSubPix of one corner by one wavefront (per-wave LDS: the 13x13 patch,
+// the five term arrays, their sums and the staged pixel window): getRectSubPix +
+// gradient normal equations; the five fp64 sums run sequentially in one lane
+// each, in OpenCV's row-major order, so corners are bit-exact.
+struct SubpixLds {
+    float patch[SP_B * SP_B];
+    double terms[5][SP_W * SP_W];
+    double sums[5];
+    uint8_t win[SW_W * SW_W];
+};
+__device__ float2 subpix_corner(const uint8_t* __restrict__ src, int pitch, int4 roi, int2 c0,
+                                const float* __restrict__ gmask, int max_iters, double eps2, int lane,
+                                SubpixLds& L) {
+    float* patch = L.patch;
+    const float cTx = (float)c0.x, cTy = (float)c0.y;
+    // stage the ROI pixels around the start (the patch of a centre within
+    // about +-9 px of it): lane l copies 16 bytes of row l/2
+    SubpixWin win;
+    win.win = L.win;
+    win.ox = max(0, min(c0.x - SW_W / 2 + 1, roi.z - SW_W));
+    win.oy = max(0, min(c0.y - SW_W / 2 + 1, roi.w - SW_W));
+    win.nx = min(SW_W, roi.z - win.ox);
+    win.ny = min(SW_W, roi.w - win.oy);
+    {
+        const int r = lane >> 1, c = (lane & 1) * 16;
+        if (r < win.ny) {
+            const uint8_t* g = src + (int64_t)(win.oy + r) * pitch + win.ox + c;
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (c + q < win.nx) L.win[r * SW_W + c + q] = g[q];
+        }
+    }
+    wave_lds_sync();
+    float cIx = cTx, cIy = cTy;
+    int iter = 0;
+    double err = 0;
+    do {
+        for (int e = lane; e < SP_B * SP_B; e += 64)
+            patch[e] = rect_subpix_px(src, pitch, roi.z, roi.w, cIx, cIy, e / SP_B, e % SP_B, win);
+        wave_lds_sync();
+        for (int e = lane; e < SP_W * SP_W; e += 64) {
+            const int i = e / SP_W, j = e - i * SP_W;
+            const float* sp = patch + (i + 1) * SP_B + 1;
+            const double m = gmask[e];
+            const double tgx = sp[j + 1] - sp[j - 1];
+            const double tgy = sp[j + SP_B] - sp[j - SP_B];
+            const double gxx = tgx * tgx * m;
+            const double gxy = tgx * tgy * m;
+            const double gyy = tgy * tgy * m;
+            const double pxx = j - SP_WIN, py = i - SP_WIN;
+            L.terms[0][e] = gxx;
+            L.terms[1][e] = gxy;
+            L.terms[2][e] = gyy;
+            L.terms[3][e] = gxx * pxx + gxy * py;
+            L.terms[4][e] = gxy * pxx + gyy * py;
+        }
+        wave_lds_sync();
+        if (lane < 5) {
+            double acc = 0;
+            for (int e = 0; e < SP_W * SP_W; ++e) acc += L.terms[lane][e];
+            L.sums[lane] = acc;
+        }
+        wave_lds_sync();
+        const double a = L.sums[0], b = L.sums[1], c = L.sums[2], bb1 = L.sums[3], bb2 = L.sums[4];
+        const double det = a * c - b * b;
+        if (fabs(det) <= __DBL_EPSILON__ * __DBL_EPSILON__) break;
+        const double scale = 1.0 / det;
+        const float nx = (float)(cIx + c * scale * bb1 - b * scale * bb2);
+        const float ny = (float)(cIy - b * scale * bb1 + a * scale * bb2);
+        err = (nx - cIx) * (nx - cIx) + (ny - cIy) * (ny - cIy);
+        cIx = nx;
+        cIy = ny;
+        if (cIx < 0 || cIx >= roi.z || cIy < 0 || cIy >= roi.w) break;
+    } while (++iter < max_iters && err > eps2);
+    if (fabsf(cIx - cTx) > SP_WIN || fabsf(cIy - cTy) > SP_WIN) {
+        cIx = cTx;
+        cIy = cTy;
+    }
+    return make_float2(cIx, cIy);
+}
+
 // ------------------------------------------------------------------ select
 __device__ __forceinline__ uint32_t fkey(float v) {
     const uint32_t b = __float_as_uint(v);
@@ -175,7 +377,11 @@ __global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__
                                                        const int* __restrict__ want, double quality,
                                                        float min_dist, unsigned long long* __restrict__ cand,
                                                        int2* __restrict__ corners, int max_per_block,
-                                                       int* __restrict__ ncorner, const int* __restrict__ n_active_dev) {
+                                                       int* __restrict__ ncorner, const int* __restrict__ n_active_dev,
+                                                       const uint8_t* __restrict__ img0, int pitch,
+                                                       const float* __restrict__ gmask, int max_iters, double eps2,
+                                                       float2* __restrict__ out) {
+    __shared__ SubpixLds s_sub[SEL_T / 64];
     if (n_active_dev && (int)blockIdx.x >= *n_active_dev) return;
     __shared__ float s_max[SEL_T / 64];
     __shared__ int s_found[SEL_T / 64];
@@ -283,148 +489,16 @@ __global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__
         if (s_nacc == round) break;  // nothing accepted this round
     }
     if (t == 0) ncorner[k] = s_nacc;
-}
-
-// ------------------------------------------------------------------ subpix
-constexpr int SP_WIN = 5;
-constexpr int SP_W = 2 * SP_WIN + 1;  // 11
-constexpr int SP_B = SP_W + 2;        // 13
-
-// getRectSubPix(ROI, 13x13, centre, CV_32F): value of patch pixel (i, j).
-__device__ float rect_subpix_px(const uint8_t* __restrict__ src, int pitch, int sw, int sh, float cx0,
-                                float cy0, int i, int j) {
-    const float cx = cx0 - (SP_B - 1) * 0.5f;
-    const float cy = cy0 - (SP_B - 1) * 0.5f;
-    const int ipx = (int)floorf(cx), ipy = (int)floorf(cy);
-    if (0 <= ipx && ipx + SP_B < sw && 0 <= ipy && ipy + SP_B < sh) {
-        float a = cx - ipx;
-        const float b = cy - ipy;
-        a = a > 0.0001f ? a : 0.0001f;
-        const float a12 = a * (1.f - b), a22 = a * b, b1 = 1.f - b, b2 = b;
-        const double s = (1. - a) / a;
-        const uint8_t* p = src + (int64_t)(ipy + i) * pitch + ipx;
-        const float t = a12 * (float)p[j + 1] + a22 * (float)p[j + 1 + pitch];
-        float prev;
-        if (j == 0) {
-            prev = (1 - a) * (b1 * (float)p[0] + b2 * (float)p[pitch]);
-        } else {
-            const float tp = a12 * (float)p[j] + a22 * (float)p[j + pitch];
-            prev = (float)(tp * s);
-        }
-        return prev + t;
-    }
-    const float a = cx - ipx, b = cy - ipy;
-    const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
-    const float b1 = 1.f - b, b2 = b;
-    // adjustRect
-    int64_t off = 0;
-    int rx, rwid, ry, rhei;
-    if (ipx >= 0) {
-        off += ipx;
-        rx = 0;
-    } else {
-        rx = -ipx;
-        if (rx > SP_B) rx = SP_B;
-    }
-    if (ipx < sw - SP_B)
-        rwid = SP_B;
-    else {
-        rwid = sw - ipx - 1;
-        if (rwid < 0) {
-            off += rwid;
-            rwid = 0;
-        }
-    }
-    if (ipy >= 0) {
-        off += (int64_t)ipy * pitch;
-        ry = 0;
-    } else
-        ry = -ipy;
-    if (ipy < sh - SP_B)
-        rhei = SP_B;
-    else {
-        rhei = sh - ipy - 1;
-        if (rhei < 0) {
-            off += (int64_t)rhei * pitch;
-            rhei = 0;
-        }
-    }
-    const uint8_t* s = src + off - rx;
-    for (int q = 0; q < i; ++q) {
-        const uint8_t* s2 = s + pitch;
-        if (q < ry || q >= rhei) s2 -= pitch;
-        if (q < rhei) s = s2;
-    }
-    const uint8_t* s2 = s + pitch;
-    if (i < ry || i >= rhei) s2 -= pitch;
-    if (j < rx) return (float)s[rx] * b1 + (float)s2[rx] * b2;
-    if (j >= rwid) return (float)s[rwid] * b1 + (float)s2[rwid] * b2;
-    return (float)s[j] * a11 + (float)s[j + 1] * a12 + (float)s2[j] * a21 + (float)s2[j + 1] * a22;
-}
-
-__global__ void __launch_bounds__(64) subpix_kernel(const uint8_t* __restrict__ img0, int pitch,
-                                                    const int4* __restrict__ rois,
-                                                    const int2* __restrict__ corners,
-                                                    const int* __restrict__ ncorner, int max_per_block,
-                                                    const float* __restrict__ gmask, int max_iters,
-                                                    double eps2, float2* __restrict__ out) {
-    __shared__ float patch[SP_B * SP_B];
-    __shared__ double terms[5][SP_W * SP_W];
-    __shared__ double sums[5];
-    const int k = blockIdx.y;
-    const int ci = blockIdx.x;
-    if (ci >= ncorner[k]) return;
-    const int lane = threadIdx.x;
-    const int4 roi = rois[k];
+    // cornerSubPix of the block's corners (the old separate launch), one wave
+    // per corner: the block's ROI and corner list are already here
+    __syncthreads();
+    const int nacc = s_nacc;
     const uint8_t* src = img0 + (int64_t)roi.y * pitch + roi.x;
-    const int2 c0 = corners[k * max_per_block + ci];
-    const float cTx = (float)c0.x, cTy = (float)c0.y;
-    float cIx = cTx, cIy = cTy;
-    int iter = 0;
-    double err = 0;
-    do {
-        for (int e = lane; e < SP_B * SP_B; e += 64)
-            patch[e] = rect_subpix_px(src, pitch, roi.z, roi.w, cIx, cIy, e / SP_B, e % SP_B);
-        __syncthreads();
-        for (int e = lane; e < SP_W * SP_W; e += 64) {
-            const int i = e / SP_W, j = e - i * SP_W;
-            const float* sp = patch + (i + 1) * SP_B + 1;
-            const double m = gmask[e];
-            const double tgx = sp[j + 1] - sp[j - 1];
-            const double tgy = sp[j + SP_B] - sp[j - SP_B];
-            const double gxx = tgx * tgx * m;
-            const double gxy = tgx * tgy * m;
-            const double gyy = tgy * tgy * m;
-            const double pxx = j - SP_WIN, py = i - SP_WIN;
-            terms[0][e] = gxx;
-            terms[1][e] = gxy;
-            terms[2][e] = gyy;
-            terms[3][e] = gxx * pxx + gxy * py;
-            terms[4][e] = gxy * pxx + gyy * py;
-        }
-        __syncthreads();
-        if (lane < 5) {
-            double acc = 0;
-            for (int e = 0; e < SP_W * SP_W; ++e) acc += terms[lane][e];
-            sums[lane] = acc;
-        }
-        __syncthreads();
-        const double a = sums[0], b = sums[1], c = sums[2], bb1 = sums[3], bb2 = sums[4];
-        const double det = a * c - b * b;
-        if (fabs(det) <= __DBL_EPSILON__ * __DBL_EPSILON__) break;
-        const double scale = 1.0 / det;
-        const float nx = (float)(cIx + c * scale * bb1 - b * scale * bb2);
-        const float ny = (float)(cIy - b * scale * bb1 + a * scale * bb2);
-        err = (nx - cIx) * (nx - cIx) + (ny - cIy) * (ny - cIy);
-        cIx = nx;
-        cIy = ny;
-        if (cIx < 0 || cIx >= roi.z || cIy < 0 || cIy >= roi.w) break;
-    } while (++iter < max_iters && err > eps2);
-    if (fabsf(cIx - cTx) > SP_WIN || fabsf(cIy - cTy) > SP_WIN) {
-        cIx = cTx;
-        cIy = cTy;
+    for (int ci = wv; ci < nacc; ci += SEL_T / 64) {
+        const int2 c0 = make_int2((int)s_acc[ci][0], (int)s_acc[ci][1]);
+        const float2 r = subpix_corner(src, pitch, roi, c0, gmask, max_iters, eps2, lane, s_sub[wv]);
+        if (lane == 0) out[k * max_per_block + ci] = r;
     }
-    if (lane == 0) out[k * max_per_block + ci] = make_float2(cIx, cIy);
 }
 
 }  // namespace
@@ -433,26 +507,21 @@ hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d) {
     // device-resident counts (n_active_dev): every launch is sized for all blocks
     // / the capacity and the kernels read the counts, so the topology is fixed
     const bool dev_counts = d.n_active_dev != nullptr;
-    if (d.n_circles > 0 || d.fill_mask || dev_counts) {
-        dim3 g((d.w + 63) / 64, (d.h + 3) / 4);
-        hipLaunchKernelGGL(mask_kernel, g, dim3(256), 0, c->stream, d.w, d.h, d.centers, d.n_circles, d.hw,
-                           d.radius, d.mask, d.n_circles_dev, d.skip_dev);
-    }
+    const bool with_mask = d.n_circles > 0 || d.fill_mask || dev_counts;
     const int n_act = dev_counts ? d.n_blocks : d.n_active;
+    const int mx = (d.w + 63) / 64, my = (d.h + 3) / 4;
+    const int n_mask = with_mask ? mx * my : 0;
+    const int ex = (d.max_rw + ET_W - 1) / ET_W, ey = (d.max_rh + ET_H - 1) / ET_H;
+    const int n_eig = n_act > 0 ? ex * ey * n_act : 0;
+    if (n_mask + n_eig > 0)
+        hipLaunchKernelGGL(mask_eig_kernel, dim3(n_mask + n_eig), dim3(256), 0, c->stream, n_mask, mx, d.w, d.h,
+                           d.centers, d.n_circles, d.hw, d.radius, d.mask, d.n_circles_dev, d.skip_dev, ex, ey,
+                           d.img0, d.pitch, d.rois, d.blk_ids, d.eig_stride, d.eig, d.sc, d.sc2, d.n_active_dev);
     if (n_act <= 0) return hipGetLastError();
-    {
-        dim3 g((d.max_rw + ET_W - 1) / ET_W, (d.max_rh + ET_H - 1) / ET_H, n_act);
-        hipLaunchKernelGGL(eig_kernel, g, dim3(256), 0, c->stream, d.img0, d.pitch, d.rois, d.blk_ids,
-                           d.eig_stride, d.eig, d.sc, d.sc2, d.n_active_dev);
-    }
     hipLaunchKernelGGL(select_kernel, dim3(n_act), dim3(SEL_T), 0, c->stream, d.eig, d.eig_stride, d.mask,
                        d.w, d.rois, d.blk_ids, d.want, d.quality, d.min_dist, d.cand, d.corners,
-                       d.max_per_block, d.ncorner, d.n_active_dev);
-    {
-        dim3 g(d.max_per_block, d.n_blocks);
-        hipLaunchKernelGGL(subpix_kernel, g, dim3(64), 0, c->stream, d.img0, d.pitch, d.rois, d.corners,
-                           d.ncorner, d.max_per_block, d.gmask, d.max_iters, d.eps2, d.out);
-    }
+                       d.max_per_block, d.ncorner, d.n_active_dev, d.img0, d.pitch, d.gmask, d.max_iters, d.eps2,
+                       d.out);
     return hipGetLastError();
 }
 
