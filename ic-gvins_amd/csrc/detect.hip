@@ -3,11 +3,12 @@
 // circle mask (:609-620), per-block cv::goodFeaturesToTrack (:647-648) and
 // cv::cornerSubPix (:651), whose TBB fan-out over blocks (:656) becomes the grid.
 //
-// Kernels:
-//  mask_kernel    FILLED integer-midpoint circles (cv::circle, LINE_8) as a
-//                 per-row half-width table -> u8 mask (255 / 0).
-//  eig_kernel     cornerMinEigenVal(blockSize 3, ksize 3) per block ROI: the
-//                 Sobel reads the parent image across the ROI edge (padded
+// Kernels (two launches):
+//  mask_eig_kernel  the first workgroups rasterise the circle mask (FILLED
+//                 integer-midpoint circles, cv::circle LINE_8, as a per-row
+//                 half-width table -> u8 255 / 0), the rest compute
+//                 cornerMinEigenVal(blockSize 3, ksize 3) tiles per block ROI:
+//                 the Sobel reads the parent image across the ROI edge (padded
 //                 level 0 supplies REFLECT_101 at the image border), the 3x3 box
 //                 of the covariance reflects inside the ROI; fp32 products and
 //                 fp64 box sums in the CPU restatement's order.
@@ -15,10 +16,10 @@
 //                 3x3 dilate, local-max candidates (keys = value, raster index),
 //                 then the greedy minDistance suppression as <= maxCorners
 //                 rounds of a block-wide argmax -- identical to sorting by
-//                 (value desc, address desc) and scanning (goodFeaturesToTrack).
-//  subpix_kernel  one wavefront per corner: getRectSubPix + gradient normal
-//                 equations; the five fp64 sums run sequentially in one lane
-//                 each, in OpenCV's row-major order, so corners are bit-exact.
+//                 (value desc, address desc) and scanning (goodFeaturesToTrack);
+//                 then cornerSubPix, one wavefront per corner: getRectSubPix +
+//                 gradient normal equations, the five fp64 sums sequentially in
+//                 one lane each, in OpenCV's row-major order (bit-exact corners).
 #include <hip/hip_runtime.h>
 
 #include "gvx_internal.h"
