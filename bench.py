@@ -48,10 +48,13 @@ def algorithmic_bytes(w, h, levels, n):
     return 2 * a0 + 4 * ap + 16 * (a0 + ap) + 58 * n
 
 
-def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False, clahe=False):
+def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False, clahe=False, pair_workers=0):
     """Oracle (C restatement) on the reference's 4-call pattern (each
     calcOpticalFlowPyrLK rebuilds both pyramids; LK points split over `threads`
-    like OpenCV's parallel_for_), bounded sample of about budget_s seconds."""
+    like OpenCV's parallel_for_), bounded sample of about budget_s seconds.
+    pair_workers > 0: independent frame pairs on that many host threads at once
+    (one thread each; the oracle's ctypes calls release the GIL) -- the batch
+    throughput a CPU system would get from separate sequences."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc  # test-infrastructure import: cpu_baseline leg only
     from gvx import synth
@@ -72,15 +75,34 @@ def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False, clahe=Fa
         orc.klt_fb(I, J, P[half:], Q[half:], params=p, reuse_pyramids=False, nthreads=threads)
 
     frame(*pairs[0][:4])  # warm
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        I, J, P, Q, _ = pairs[done % len(pairs)]
-        frame(I, J, P, Q)
-        done += 1
-    dt = time.perf_counter() - t0
+    if pair_workers > 0:
+        from concurrent.futures import ThreadPoolExecutor
+        t0 = time.perf_counter()
+
+        def worker(wi):
+            k = 0
+            while time.perf_counter() - t0 < budget_s:
+                I, J, P, Q, _ = pairs[(wi + k) % len(pairs)]
+                frame(I, J, P, Q)
+                k += 1
+            return k
+
+        with ThreadPoolExecutor(pair_workers) as ex:
+            done = sum(ex.map(worker, range(pair_workers)))
+        dt = time.perf_counter() - t0
+        threads = pair_workers
+    else:
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            I, J, P, Q, _ = pairs[done % len(pairs)]
+            frame(I, J, P, Q)
+            done += 1
+        dt = time.perf_counter() - t0
     what = ("fwd + bwd LK of all points, each pyramid built once (baseline b)" if reuse else
             f"({half} map + {n - half} reference points), 4 LK calls each rebuilding both pyramids "
             f"(tracking.cc:385,390,487,493)")
+    if pair_workers > 0:
+        what += f"; {pair_workers} pairs at a time, one host thread each"
     if clahe:
         what += " + CLAHE of the new frame (1 thread)"
     return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
@@ -281,12 +303,19 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             nt = host_threads()
-            cpu = cpu_baseline(W, H, N, L, args.cpu_budget, threads=nt)
-            reuse = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=nt, reuse=True)
+            # value: independent pairs on every host thread at once (the batch
+            # throughput of the CPU share); beside it the reference's per-frame
+            # pattern with its LK points split over the threads, the pyramid-reuse
+            # variant (b) and one thread
+            cpu = cpu_baseline(W, H, N, L, args.cpu_budget / 2, pair_workers=nt)
+            pf = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=nt)
+            cpu["per_frame_parallel_value"] = pf["value"]
+            cpu["per_frame_parallel_sample"] = pf["sample"]
+            reuse = cpu_baseline(W, H, N, L, args.cpu_budget / 4, threads=nt, reuse=True)
             cpu["reuse_value"] = reuse["value"]
             cpu["reuse_sample"] = reuse["sample"]
             if nt > 1:
-                one = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=1)
+                one = cpu_baseline(W, H, N, L, args.cpu_budget / 4, threads=1)
                 cpu["single_thread_value"] = one["value"]
                 cpu["single_thread_sample"] = one["sample"]
         line = {
