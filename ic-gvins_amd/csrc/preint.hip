@@ -616,6 +616,7 @@ __global__ void __launch_bounds__(64) preint_rot_kernel(int variant, int n_seg, 
     }
 }
 
+template <int LANES>
 __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_params prm, int n_seg,
                                                         const gvx_imu* __restrict__ imu,
                                                         const int32_t* __restrict__ seg_off,
@@ -624,18 +625,24 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
                                                         const RRec* __restrict__ rrec,
                                                         gvx_preint_result* __restrict__ out,
                                                         double* __restrict__ pn) {
-    constexpr int NIN = RREC_DW + 7;  // + the sample's dt, dtheta, dvel
-    __shared__ double sIn[SPW][2][NIN + 1];
-    __shared__ double sG[SPW][MS];
+    // LANES lanes per segment; lane c owns columns c, c + LANES, .. (< 15) of J
+    // and rows of P.  The per-step scalar work (the velocity / position sums, Phi
+    // and W) is issued once per wave for 64 / LANES segments.
+    constexpr int SPWL = 64 / LANES;
+    constexpr int CPL = (NS + LANES - 1) / LANES;  // columns per lane
+    constexpr int NIN = RREC_DW + 7;               // + the sample's dt, dtheta, dvel
+    constexpr int LPL = (NIN + LANES - 1) / LANES; // inputs loaded per lane per step
+    __shared__ double sIn[SPWL][2][LPL * LANES];
+    __shared__ double sG[SPWL][MS];
     const int lane = threadIdx.x;
-    const int grp = lane / GL, c = lane % GL;
-    const int seg = blockIdx.x * SPW + grp;
+    const int grp = lane / LANES, c = lane % LANES;
+    const int seg = blockIdx.x * SPWL + grp;
     const bool live = seg < n_seg;
     const int b0 = live ? seg_off[seg] : 0;
     const int m = live ? seg_off[seg + 1] - b0 : 0;
     int mmax = m;
 #pragma unroll
-    for (int o = GL; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+    for (int o = LANES; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
     const bool earth = variant == GVX_PREINT_EARTH;
     double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
     gvx_state s0{};
@@ -658,35 +665,41 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
     const double g60 = earth ? -1.0 : 1.0;
     const double wg = (g60 * ngyr) * g60;
     auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
-    double Jc[NS], Pc[NS];
+    double Jc[CPL][NS], Pc[CPL][NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        Jc[i] = i == c ? 1.0 : 0.0;
-        Pc[i] = 0.0;
-    }
-    // lane c of the group loads RRec double c and, for c < 7, the sample's
-    // double c + 1 (dt, dtheta, dvel)
-    const double* src_r = reinterpret_cast<const double*>(rrec + (live ? b0 - seg : 0)) + c;
-    const double* src_im = reinterpret_cast<const double*>(imu + b0) + 1 + (c < 7 ? c : 0);
-    // never predicated (a clamped step; lanes c >= 7 re-read dt), so the
-    // compiler's counters keep both prefetches in flight across the step
+    for (int j = 0; j < CPL; ++j)
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            Jc[j][i] = i == c + j * LANES ? 1.0 : 0.0;
+            Pc[j][i] = 0.0;
+        }
+    // input e of a step (e < 16: RRec double e; 16..22: the sample's double
+    // e - 15, i.e. dt, dtheta, dvel); lane c loads inputs c, c + LANES, ..
+    // never predicated (a clamped step; spare slots re-read an input), so the
+    // compiler's counters keep the prefetches in flight across the step
+    const double* src_r = reinterpret_cast<const double*>(rrec + (live ? b0 - seg : 0));
+    const double* src_im = reinterpret_cast<const double*>(imu + b0);
     const int klast = m >= 2 ? m - 1 : 1;
-    auto fetch = [&](int k, double& x, double& y) {
+    auto fetch = [&](int k, double (&x)[LPL]) {
         const int kk = min(k, klast);
-        x = src_r[(size_t)(kk - 1) * RREC_DW];
-        y = src_im[(size_t)kk * (sizeof(gvx_imu) / 8)];
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) {
+            const int e = c + q * LANES;
+            x[q] = e < RREC_DW ? src_r[(size_t)(kk - 1) * RREC_DW + e]
+                               : src_im[(size_t)kk * (sizeof(gvx_imu) / 8) + 1 + min(e - RREC_DW, 6)];
+        }
     };
-    double x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    fetch(1, x0, y0);
-    fetch(2, x1, y1);
+    double x0[LPL], x1[LPL];
+    fetch(1, x0);
+    fetch(2, x1);
     for (int k = 1; k < mmax; ++k) {
         const bool act = k < m;
         double* sp = sIn[grp][k & 1];
-        sp[c] = x0;
-        if (c < 7) sp[RREC_DW + c] = y0;
-        x0 = x1;
-        y0 = y1;
-        fetch(k + 2, x1, y1);
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) sp[c + q * LANES] = x0[q];
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) x0[q] = x1[q];
+        fetch(k + 2, x1);
         __syncthreads();
         Phi f;
         double Wv[9];
@@ -698,9 +711,9 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
             if (!earth) {
                 for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + g3[i] * dt;
             } else {
-                double cc[3], dvcg[3];
-                cross3(iewn, v, cc);
-                for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc[i]) * dt;
+                double cc3[3], dvcg[3];
+                cross3(iewn, v, cc3);
+                for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
                 for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + dvcg[i];
             }
             for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
@@ -737,65 +750,77 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
             for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
             f.dt = dt;
             f.f = 1 - dt / prm.corr_time;
-            double y[NS];
-            phi_mv(f, Pc, y);
-            if (c < NS) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
+            for (int j = 0; j < CPL; ++j) {
+                const int cc = c + j * LANES;
+                double y[NS];
+                phi_mv(f, Pc[j], y);
+                if (cc < NS) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) sG[grp][cc * NS + i] = y[i];
+                }
+                phi_mv(f, Jc[j], y);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) Jc[j][i] = y[i];
             }
-            phi_mv(f, Jc, y);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) Jc[i] = y[i];
         }
         __syncthreads();
         if (act) {
             const double a = 0.5 * f.dt;
-            const int cl = c < NS ? c : 0;
-            double K[NS];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
-            if (c >= 3 && c < 6) {
-                K[3] = K[3] + a * Wv[c - 3];
-                K[4] = K[4] + a * Wv[3 + c - 3];
-                K[5] = K[5] + a * Wv[6 + c - 3];
+            for (int j = 0; j < CPL; ++j) {
+                const int ce = c + j * LANES;
+                const int cc = ce < NS ? ce : 0;
+                double K[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cc];
+                if (cc >= 3 && cc < 6) {
+                    K[3] = K[3] + a * Wv[cc - 3];
+                    K[4] = K[4] + a * Wv[3 + cc - 3];
+                    K[5] = K[5] + a * Wv[6 + cc - 3];
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i)
+                    if (i == cc) K[i] = K[i] + a * wd(i);
+                const int r3 = cc - 3, r6 = cc - 6;
+                double phr[NS];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    phr[3 + b] = (cc == b) ? f.dt : (cc == 3 + b ? 1.0 : 0.0);
+                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
+                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
+                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
+                    phr[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
+                    phr[9 + b] = (cc == 6 + b) ? -f.dt : (cc == 9 + b ? f.f : 0.0);
+                    phr[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (cc == 12 + b ? f.f : 0.0);
+                }
+                double y[NS];
+                phi_mv(f, K, y);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[j][i] = y[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    double u = Wv[3 * i] * phr[3];
+                    u = u + Wv[3 * i + 1] * phr[4];
+                    u = u + Wv[3 * i + 2] * phr[5];
+                    Pc[j][3 + i] = y[3 + i] + a * u;
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i) Pc[j][i] = y[i] + a * (wd(i) * phr[i]);
             }
-#pragma unroll
-            for (int i = 6; i < NS; ++i)
-                if (i == c) K[i] = K[i] + a * wd(i);
-            const int r3 = c - 3, r6 = c - 6;
-            double phr[NS];
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                phr[3 + b] = (c == b) ? f.dt : (c == 3 + b ? 1.0 : 0.0);
-                const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
-                const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
-                const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
-                phr[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
-                phr[9 + b] = (c == 6 + b) ? -f.dt : (c == 9 + b ? f.f : 0.0);
-                phr[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (c == 12 + b ? f.f : 0.0);
-            }
-            double y[NS];
-            phi_mv(f, K, y);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) Pc[i] = y[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                double u = Wv[3 * i] * phr[3];
-                u = u + Wv[3 * i + 1] * phr[4];
-                u = u + Wv[3 * i + 2] * phr[5];
-                Pc[3 + i] = y[3 + i] + a * u;
-            }
-#pragma unroll
-            for (int i = 6; i < NS; ++i) Pc[i] = y[i] + a * (wd(i) * phr[i]);
         }
     }
     if (!live) return;
     gvx_preint_result* o = out + seg;
-    if (c < NS) {
 #pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            o->jacobian[i * NS + c] = Jc[i];
-            o->covariance[c * NS + i] = Pc[i];
+    for (int j = 0; j < CPL; ++j) {
+        const int cc = c + j * LANES;
+        if (cc < NS) {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                o->jacobian[i * NS + cc] = Jc[j][i];
+                o->covariance[cc * NS + i] = Pc[j][i];
+            }
         }
     }
     if (c == 0)
@@ -838,8 +863,15 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                                (const PreG*)pre, qr, out);
             hipLaunchKernelGGL(preint_rot_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, seg_off,
                                state0, (const PreG*)pre, (const QRec*)qr, rr);
-            hipLaunchKernelGGL(preint_cov_kernel, dim3((n_seg + SPW - 1) / SPW), dim3(64), 0, c->stream, variant,
-                               prm, n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
+            // lanes per segment of the covariance pass (GVX_PREINT_COV_LANES = 8 or 16)
+            const char* el = getenv("GVX_PREINT_COV_LANES");
+            const int lanes = el && atoi(el) == 16 ? 16 : 8;
+            if (lanes == 16)
+                hipLaunchKernelGGL(preint_cov_kernel<16>, dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, variant,
+                                   prm, n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
+            else
+                hipLaunchKernelGGL(preint_cov_kernel<8>, dim3((n_seg + 7) / 8), dim3(64), 0, c->stream, variant,
+                                   prm, n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
             return hipGetLastError();
         }
     }
