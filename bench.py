@@ -541,10 +541,11 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     torch.cuda.synchronize()
 
     def step():
-        ctx.reproj_eval_dev(n_r, d_consts.data_ptr(), d_params.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(),
-                            d_jac.data_ptr())
-        ctx.preint_factor_eval_dev(n_p, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
-                                   d_params.data_ptr(), d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr())
+        # both factor kinds in one call (gvx_factor_batch_eval_dev: the preintegration
+        # launch beside the reprojection launch on a second stream)
+        ctx.factor_batch_eval_dev(n_r, d_consts.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(), d_jac.data_ptr(),
+                                  n_p, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(), d_poffs.data_ptr(),
+                                  d_pres.data_ptr(), d_pjac.data_ptr(), d_params.data_ptr())
 
     def integ():
         ctx.preint_integrate_dev(2, synth_ba.imu_params(), S, d_imu.data_ptr(), d_seg_off.data_ptr(),
@@ -578,10 +579,9 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     n_w = n_rp + (n_kf - 1)
 
     def window():
-        ctx.reproj_eval_dev(n_rp, d_consts.data_ptr(), d_params.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(),
-                            d_jac.data_ptr())
-        ctx.preint_factor_eval_dev(n_kf - 1, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
-                                   d_params.data_ptr(), d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr())
+        ctx.factor_batch_eval_dev(n_rp, d_consts.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(), d_jac.data_ptr(),
+                                  n_kf - 1, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
+                                  d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr(), d_params.data_ptr())
 
     k_w = max(50, steps)
     el_w, _ = timed(window, k_w)

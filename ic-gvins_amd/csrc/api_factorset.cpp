@@ -196,20 +196,12 @@ gvx_status gvx_factors_prepare(gvx_factor_set* s, int32_t with_jacobians) {
     double* pres = rjac + (size_t)RP_JAC * s->n_reproj;
     double* pjac = pres + (size_t)PF_RES * s->n_preint;
     const bool jac = with_jacobians != 0;
-    hipEvent_t ev{};
-    if (s->n_reproj > 0) {
-        prof_begin(c, "reproj", &ev);
-        e = launch_reproj(c, s->n_reproj, s->d_rc, s->d_params, s->d_roffs, rres, jac ? rjac : nullptr);
-        prof_end(c, "reproj", ev);
-        if (e != hipSuccess) return hip_err(c, e, "reproj kernel");
-    }
-    if (s->n_preint > 0) {
-        prof_begin(c, "preint_factor", &ev);
-        e = launch_preint_factor(c, s->n_preint, s->d_pre, s->d_pn, s->d_pn_off, s->d_params, s->d_poffs, pres,
-                                 jac ? pjac : nullptr);
-        prof_end(c, "preint_factor", ev);
-        if (e != hipSuccess) return hip_err(c, e, "preint factor kernel");
-    }
+    // both kinds in one call: the preintegration factors beside the reprojection
+    // launch on the context's side stream (gvx_factor_batch_eval_dev)
+    gvx_status st = gvx_factor_batch_eval_dev(c, s->n_reproj, s->d_rc, s->d_roffs, rres, jac ? rjac : nullptr,
+                                              s->n_preint, s->d_pre, s->d_pn, s->d_pn_off, s->d_poffs, pres,
+                                              jac ? pjac : nullptr, s->d_params);
+    if (st) return st;
     // one D2H of everything evaluated (the Jacobian regions only when computed)
     if (jac) {
         e = hipMemcpyAsync(s->h_out, s->d_out, sizeof(double) * s->out_doubles, hipMemcpyDeviceToHost, c->stream);

@@ -168,6 +168,7 @@ def _declare(L):
         "gvx_factor_read_reproj": (i32, [P, i32, P, P]),
         "gvx_factor_read_preint": (i32, [P, i32, P, P]),
         "gvx_reproj_eval_dev": (i32, [P, i32, P, P, P, P, P]),
+        "gvx_factor_batch_eval_dev": (i32, [P, i32, P, P, P, P, i32, P, P, P, P, P, P, P]),
         "gvx_detect_params_default": (None, [C.POINTER(DetectParams)]),
         "gvx_detect": (i32, [P, u64, P, i32, P, i32, i32, i32, C.POINTER(DetectParams), P, P, C.POINTER(i32)]),
         "gvx_clahe_params_default": (None, [C.POINTER(ClaheParams)]),
@@ -664,6 +665,14 @@ class Context:
         """Device-pointer PreintegrationFactor batch, async on the context stream."""
         self._check(self._L.gvx_preint_factor_eval_dev(self._h, n, d_pre, d_pn, d_pn_off, d_params, d_offs,
                                                        d_res, d_jac), "gvx_preint_factor_eval_dev")
+
+    def factor_batch_eval_dev(self, n_r, d_consts, d_roffs, d_rres, d_rjac, n_p, d_pre, d_pn, d_pn_off, d_poffs,
+                              d_pres, d_pjac, d_params):
+        """Both factor kinds over one parameter array, async on the context stream
+        (the preintegration launch beside the reprojection one on a second stream)."""
+        self._check(self._L.gvx_factor_batch_eval_dev(self._h, n_r, d_consts, d_roffs, d_rres, d_rjac, n_p, d_pre,
+                                                      d_pn, d_pn_off, d_poffs, d_pres, d_pjac, d_params),
+                    "gvx_factor_batch_eval_dev")
 
     def reproj_eval_dev(self, n, d_consts, d_params, d_offs, d_res, d_jac):
         """Device-pointer ReprojectionFactor batch, async on the context stream."""
