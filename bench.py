@@ -541,8 +541,7 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     torch.cuda.synchronize()
 
     def step():
-        # both factor kinds in one call (gvx_factor_batch_eval_dev: the preintegration
-        # launch beside the reprojection launch on a second stream)
+        # both factor kinds in one call (gvx_factor_batch_eval_dev)
         ctx.factor_batch_eval_dev(n_r, d_consts.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(), d_jac.data_ptr(),
                                   n_p, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(), d_poffs.data_ptr(),
                                   d_pres.data_ptr(), d_pjac.data_ptr(), d_params.data_ptr())

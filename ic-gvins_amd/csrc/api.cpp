@@ -112,35 +112,6 @@ void prof_drain(gvx_ctx* c) {
     c->pending.clear();
 }
 
-bool side_fork(gvx_ctx* c) {
-    if (c->capturing) return false;  // captures stay on one stream
-    static const bool off = [] {     // GVX_NO_SIDE_STREAM=1: everything on one stream (A/B)
-        const char* e = getenv("GVX_NO_SIDE_STREAM");
-        return e && atoi(e) != 0;
-    }();
-    if (off) return false;
-    if (!c->side) {
-        if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
-            c->side = nullptr;
-            return false;
-        }
-        if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) {
-            hipStreamDestroy(c->side);
-            c->side = nullptr;
-            return false;
-        }
-    }
-    return hipEventRecord(c->fork_ev, c->stream) == hipSuccess &&
-           hipStreamWaitEvent(c->side, c->fork_ev, 0) == hipSuccess;
-}
-
-hipError_t side_join(gvx_ctx* c) {
-    hipError_t e = hipEventRecord(c->join_ev, c->side);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->join_ev, 0);
-    return e;
-}
-
 }  // namespace gvx
 
 extern "C" {
@@ -193,12 +164,6 @@ void gvx_destroy(gvx_ctx* c) {
         hipEventDestroy(p.b);
     }
     for (auto e : c->event_pool) hipEventDestroy(e);
-    if (c->side) {
-        hipStreamSynchronize(c->side);
-        hipStreamDestroy(c->side);
-        hipEventDestroy(c->fork_ev);
-        hipEventDestroy(c->join_ev);
-    }
     hipStreamDestroy(c->stream);
     delete c;
 }

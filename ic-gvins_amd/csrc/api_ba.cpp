@@ -220,32 +220,23 @@ gvx_status gvx_factor_batch_eval_dev(gvx_ctx* c, int32_t n_reproj, const gvx_rep
     if (n_preint > 0 && (!d_pre || !d_poffs || !d_pres || !d_params))
         return set_err(c, GVX_ERR_INVALID, "null device pointer");
     hipSetDevice(c->device);
-    // the preintegration factors (a latency-bound launch of few waves) run on the
-    // side stream beside the HBM-bound reprojection launch
-    const bool two = n_reproj > 0 && n_preint > 0 && side_fork(c);
+    // one after the other on the context stream: the preintegration launch on a
+    // second stream beside the reprojection one measured slower (both kernels
+    // stretch: 0.162 -> 0.168 ms per configs[3] batch, r02 v17)
     hipEvent_t ev{};
     hipError_t e = hipSuccess;
-    if (n_preint > 0) {
-        if (two) {
-            SideScope side(c);
-            prof_begin(c, "preint_factor", &ev);
-            e = launch_preint_factor(c, n_preint, d_pre, d_pn, d_pn_off, d_params, d_poffs, d_pres, d_pjac);
-            prof_end(c, "preint_factor", ev);
-        } else {
-            prof_begin(c, "preint_factor", &ev);
-            e = launch_preint_factor(c, n_preint, d_pre, d_pn, d_pn_off, d_params, d_poffs, d_pres, d_pjac);
-            prof_end(c, "preint_factor", ev);
-        }
-        if (e != hipSuccess) return hip_err(c, e, "preint factor kernel");
-    }
     if (n_reproj > 0) {
         prof_begin(c, "reproj", &ev);
         e = launch_reproj(c, n_reproj, d_rc, d_params, d_roffs, d_rres, d_rjac);
         prof_end(c, "reproj", ev);
         if (e != hipSuccess) return hip_err(c, e, "reproj kernel");
     }
-    if (two) e = side_join(c);
-    return hip_err(c, e, "factor batch join");
+    if (n_preint > 0) {
+        prof_begin(c, "preint_factor", &ev);
+        e = launch_preint_factor(c, n_preint, d_pre, d_pn, d_pn_off, d_params, d_poffs, d_pres, d_pjac);
+        prof_end(c, "preint_factor", ev);
+    }
+    return hip_err(c, e, "preint factor kernel");
 }
 
 gvx_status gvx_preint_factor_eval_dev(gvx_ctx* c, int32_t n, const gvx_preint_result* d_pre,

@@ -196,8 +196,7 @@ gvx_status gvx_factors_prepare(gvx_factor_set* s, int32_t with_jacobians) {
     double* pres = rjac + (size_t)RP_JAC * s->n_reproj;
     double* pjac = pres + (size_t)PF_RES * s->n_preint;
     const bool jac = with_jacobians != 0;
-    // both kinds in one call: the preintegration factors beside the reprojection
-    // launch on the context's side stream (gvx_factor_batch_eval_dev)
+    // both kinds in one call (gvx_factor_batch_eval_dev)
     gvx_status st = gvx_factor_batch_eval_dev(c, s->n_reproj, s->d_rc, s->d_roffs, rres, jac ? rjac : nullptr,
                                               s->n_preint, s->d_pre, s->d_pn, s->d_pn_off, s->d_poffs, pres,
                                               jac ? pjac : nullptr, s->d_params);

@@ -80,10 +80,6 @@ struct gvx_ctx {
     };
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
-    // a second stream for independent launches that overlap the context
-    // stream's (fork / join below; created on first use)
-    hipStream_t side = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
 namespace gvx {
@@ -101,18 +97,6 @@ void prof_begin(gvx_ctx* c, const char* fam, hipEvent_t* a);
 void prof_end(gvx_ctx* c, const char* fam, hipEvent_t a);
 void prof_drain(gvx_ctx* c);
 
-// Fork: work queued on the side stream after side_fork starts after everything
-// already on the context stream; side_join makes the context stream wait for
-// the side stream.  Between the two, set c->stream = c->side to launch there
-// (SideScope does that).  false: no side stream (run on the context stream).
-bool side_fork(gvx_ctx* c);
-hipError_t side_join(gvx_ctx* c);
-struct SideScope {
-    gvx_ctx* c;
-    hipStream_t saved;
-    explicit SideScope(gvx_ctx* ctx) : c(ctx), saved(ctx->stream) { c->stream = c->side; }
-    ~SideScope() { c->stream = saved; }
-};
 
 // ---- kernel launchers (klt.hip) ----
 // Build pyramids for n_img images (h x w, row stride `stride` bytes, image i at

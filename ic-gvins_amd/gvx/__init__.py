@@ -668,8 +668,7 @@ class Context:
 
     def factor_batch_eval_dev(self, n_r, d_consts, d_roffs, d_rres, d_rjac, n_p, d_pre, d_pn, d_pn_off, d_poffs,
                               d_pres, d_pjac, d_params):
-        """Both factor kinds over one parameter array, async on the context stream
-        (the preintegration launch beside the reprojection one on a second stream)."""
+        """Both factor kinds over one parameter array, async on the context stream."""
         self._check(self._L.gvx_factor_batch_eval_dev(self._h, n_r, d_consts, d_roffs, d_rres, d_rjac, n_p, d_pre,
                                                       d_pn, d_pn_off, d_poffs, d_pres, d_pjac, d_params),
                     "gvx_factor_batch_eval_dev")

@@ -560,11 +560,9 @@ gvx_status gvx_reproj_eval(gvx_ctx* ctx, int32_t n, const gvx_reproj_const* c,
 gvx_status gvx_reproj_eval_dev(gvx_ctx* ctx, int32_t n, const gvx_reproj_const* d_c,
                                const double* d_params, const int32_t* d_offs,
                                double* d_residuals, double* d_jacobians);
-/* gvx_reproj_eval_dev and gvx_preint_factor_eval_dev over one parameter array in
-   one call (a window's two factor kinds, what gvx_factors_prepare evaluates): the
-   preintegration launch runs on a second stream beside the reprojection launch,
-   joined back into the context stream before return (async).  Results equal the
-   two separate calls'.  Either count may be 0. */
+/* gvx_reproj_eval_dev then gvx_preint_factor_eval_dev over one parameter array
+   in one call (a window's two factor kinds, what gvx_factors_prepare evaluates),
+   async on the context stream.  Either count may be 0. */
 gvx_status gvx_factor_batch_eval_dev(gvx_ctx* ctx, int32_t n_reproj, const gvx_reproj_const* d_rc,
                                      const int32_t* d_roffs, double* d_rres, double* d_rjac, int32_t n_preint,
                                      const gvx_preint_result* d_pre, const double* d_pn, const int32_t* d_pn_off,
