@@ -18,6 +18,8 @@
 //    the CPU restatement (oracle/klt.c), whose LK outputs are matched bit-exactly.
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include <cstdlib>
 
 #include "gvx_internal.h"
@@ -525,6 +527,11 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
         nextx -= halfw;
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
+        // the J rows of the last integer position: once the steps fall below a
+        // pixel the window stays on the same pixel grid and only the bilinear
+        // weights change, so the rows are reused instead of loaded again
+        int cinx = INT_MIN, ciny = INT_MIN;
+        uint32_t jr0[U][2], jr1[U][2];
         for (int j = 0; j < cfg.max_iter; ++j) {
             const float fnx = floorf(nextx), fny = floorf(nexty);
             const int inx = (int)fnx, iny = (int)fny;
@@ -535,16 +542,18 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             uint32_t J0, J1;
             weights(nextx - fnx, nexty - fny, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
-            {
+            if (inx != cinx || iny != ciny) {
                 const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
                 if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
 #pragma unroll
-                for (int s = 0; s < U; ++s) {
-                    uint32_t r0[2], r1[2];
-                    load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
-                    unit_get(ust, s, u[s]);
-                    match_unit<false>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
-                }
+                for (int s = 0; s < U; ++s) load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, jr0[s], jr1[s]);
+                cinx = inx;
+                ciny = iny;
+            }
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                unit_get(ust, s, u[s]);
+                match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
             }
             float fb1, fb2;
             group_sums_f32<G>(b1, b2, fb1, fb2);
