@@ -617,7 +617,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 // minimum waves per SIMD the register allocation must allow
 template <int PPW>
 constexpr int klt_occupancy() {
-    return PPW == 1 ? 7 : PPW == 2 ? 5 : 2;
+    return PPW == 1 ? 4 : PPW == 2 ? 5 : 2;
 }
 template <int PPW>
 __global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
@@ -724,7 +724,10 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 // Points per wavefront of the LK launch.  Batches that fill the chip take 2
 // (the per-point scalar work is shared; 0.47 vs 0.61 ms per 256 pairs); small
 // ones (one frame of a sequence: 150 points) take 1, which halves the work of
-// the slowest wave (41 vs 54 us per frame).  GVX_KLT_PPW (1, 2 or 4) forces it.
+// the slowest wave (41 vs 54 us per frame), built for 4 waves per SIMD (no
+// spills; at most 4 waves per SIMD below the threshold: 36.8 -> 35.8 us per
+// sequence frame, 50.3 -> 49.0 us per pair, r02 v18).  GVX_KLT_PPW (1, 2 or 4)
+// forces it.
 static int klt_ppw(int64_t total_points) {
     static const int forced = [] {
         const char* e = getenv("GVX_KLT_PPW");
@@ -732,7 +735,7 @@ static int klt_ppw(int64_t total_points) {
         return (p == 1 || p == 2 || p == 4) ? p : 0;
     }();
     if (forced) return forced;
-    return total_points < 8192 ? 1 : 2;
+    return total_points <= 4096 ? 1 : 2;
 }
 
 template <int PPW>

@@ -196,7 +196,7 @@ def test_frame_put_dev_matches_host_put(ctx, gvx_mod):
 
 @pytest.mark.parametrize("n_pairs,n_pts", [(64, 149), (3, 2731)])
 def test_batch_two_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
-    """Launches of >= 8192 points take the two-points-per-wave LK; odd point
+    """Launches of > 4096 points take the two-points-per-wave LK; odd point
     counts leave a spare lane group in each pair's last wave.  Border points
     included (the LDS tile gather runs per lane group)."""
     w, h = 320, 140
