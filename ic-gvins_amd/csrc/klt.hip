@@ -504,7 +504,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 a11 += t11;
                 a12 += t12;
                 a22 += t22;
-                unit_put(ust, s, u[s]);
+                if constexpr (PPW > 1) unit_put(ust, s, u[s]);  // one unit per lane: kept in registers
             }
         }
         float A11, A12;
@@ -552,7 +552,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             }
 #pragma unroll
             for (int s = 0; s < U; ++s) {
-                unit_get(ust, s, u[s]);
+                if constexpr (PPW > 1) unit_get(ust, s, u[s]);
                 match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
             }
             float fb1, fb2;
@@ -595,7 +595,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 for (int s = 0; s < U; ++s) {
                     uint32_t r0[2], r1[2];
                     load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
-                    unit_get(ust, s, u[s]);
+                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
                     match_unit<true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
                 }
             }
