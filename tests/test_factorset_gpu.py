@@ -151,3 +151,36 @@ def test_factor_set_rejects_bad_block_sizes(ctx, gvx_mod):
     rb[0, 3] = 0  # a 7-double pose where the inverse depth (1) belongs
     with pytest.raises(gvx_mod.GvxError):
         gvx_mod.FactorSet(ctx, w["blocks"], w["consts"], rb)
+
+
+def test_factor_batch_eval_dev_matches_batched(ctx, gvx_mod):
+    """gvx_factor_batch_eval_dev (both kinds over one device parameter array, the
+    configs[3] bench step) gives the separate batched calls' bits."""
+    import torch
+    w = _window(ctx, gvx_mod, seed=11)
+    params = _packed(w)
+    off = w["off"]
+    roffs = off[w["r_blocks"]].astype(np.int32)
+    poffs = off[w["p_blocks"]].astype(np.int32)
+    dev = torch.device("cuda", 0)
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    consts = w["consts"].astype(gvx_mod.REPROJ_DTYPE)
+    d_c, d_p, d_ro, d_po = t(consts.view(np.uint8)), t(params), t(roffs), t(poffs)
+    d_pre, d_pn, d_pno = t(w["pre"].view(np.uint8)), t(w["pn"]), t(w["pn_off"].astype(np.int32))
+    nr, npf = len(consts), len(w["pre"])
+    d_rr = torch.empty((nr, 2), dtype=torch.float64, device=dev)
+    d_rj = torch.empty((nr, 46), dtype=torch.float64, device=dev)
+    d_pr = torch.empty((npf, 15), dtype=torch.float64, device=dev)
+    d_pj = torch.empty((npf, 480), dtype=torch.float64, device=dev)
+    ctx.factor_batch_eval_dev(nr, d_c.data_ptr(), d_ro.data_ptr(), d_rr.data_ptr(), d_rj.data_ptr(), npf,
+                              d_pre.data_ptr(), d_pn.data_ptr(), d_pno.data_ptr(), d_po.data_ptr(), d_pr.data_ptr(),
+                              d_pj.data_ptr(), d_p.data_ptr())
+    ctx.sync()
+    rres, rjac, pres, pjac = _batched(ctx, gvx_mod, w)
+    assert np.array_equal(d_rr.cpu().numpy(), rres)
+    assert np.array_equal(d_rj.cpu().numpy(), rjac)
+    assert np.array_equal(d_pr.cpu().numpy(), pres)
+    assert np.array_equal(d_pj.cpu().numpy(), pjac)
