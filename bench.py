@@ -180,6 +180,9 @@ def main():
     ap.add_argument("--host-loop", action="store_true",
                     help="configs[4]: the per-frame loop with host round trips (SequenceTracker) instead of the "
                          "device-resident one-graph-per-frame loop")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="configs[4]: one graph per frame, frame t+1's CLAHE + pyramid after frame t's tracking "
+                         "(default: beside it, a preprocessing graph on a side stream)")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     args = ap.parse_args()
     world_env = os.environ.get("WORLD_SIZE")
@@ -824,7 +827,11 @@ def sequence_main(args):
         # the whole frame (pick frame t on the device, CLAHE + pyramid, LK fwd/bwd +
         # FB + compaction, detection top-up, record the track list) is one graph
         # launch: no host round trip, the host only enqueues
-        tracker = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=True, device=dev, frames=frames)
+        # pipelined (default): frame t+1's CLAHE + pyramid in a graph on the context's
+        # side stream beside frame t's tracking graph (the outputs are the same:
+        # tests/test_sequence_gpu.py); --no-pipeline: one graph per frame
+        tracker = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=True, device=dev, frames=frames,
+                                        pipeline=not args.no_pipeline)
 
         def frame(t):
             tracker.step()
@@ -856,6 +863,7 @@ def sequence_main(args):
         frame(t)
         t += 1
         timed += 1
+    t_enq = time.perf_counter() - t0  # host time to enqueue the timed frames
     if device_loop:
         ctx.sync()
         tracks[:] = tracker.rec_tracks.cpu().numpy()
@@ -913,7 +921,11 @@ def sequence_main(args):
             "config": {"workload": f"configs[4]: one {F}-frame sequence per GPU, {W}x{H} mono, {N} feat, maxLevel "
                                    f"{L}: per frame CLAHE + pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
                                    f"RCCL gather of all per-frame tracks to rank 0",
-                       "loop": ("device-resident: one captured hipGraph launch per frame (gvx_track_frame_dev)"
+                       "loop": (("device-resident: one captured hipGraph launch per frame (gvx_track_frame_dev)"
+                                 if args.no_pipeline else
+                                 "device-resident, pipelined: per frame t a tracking graph (gvx_track_frame_dev) on "
+                                 "the context stream beside a graph preprocessing frame t+1 on its side stream "
+                                 "(gvx_branch_begin/_end/_join), then the track record")
                                 if device_loop else "host loop: SequenceTracker, host round trips per frame"),
                        "parallelism": f"sequences sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
@@ -925,6 +937,7 @@ def sequence_main(args):
             "tracks_per_frame_mean": round(float(tr.mean()), 1),
             "detect_frames": stats["detect_frames"] if not device_loop else None,
             "host_overhead_frac": round(max(0.0, 1.0 - dev_ms / (elapsed / timed * 1e3)), 3) if dev_ms else None,
+            "host_enqueue_ms_per_frame": round(t_enq / timed * 1e3, 4),
             "gathered_ranks": len(gathered) if gathered else 0,
         }))
     if dist:

@@ -31,13 +31,19 @@ gvx_status hip_err(gvx_ctx* c, hipError_t e, const char* what) {
                    hipGetErrorString(e));
 }
 
+// both streams of the context (the side branch's too) before memory is freed
+static void sync_all(gvx_ctx* c) {
+    hipStreamSynchronize(c->main);
+    if (c->side) hipStreamSynchronize(c->side);
+}
+
 void* scratch(gvx_ctx* c, const std::string& name, size_t bytes) {
     DevBuf& b = c->dev[name];
     if (b.bytes >= bytes && b.p) return b.p;
     if (c->capturing) return nullptr;  // growing would synchronise the captured stream
     ++c->mem_gen;
     if (b.p) {
-        hipStreamSynchronize(c->stream);
+        sync_all(c);
         hipFree(b.p);
         b.p = nullptr;
         b.bytes = 0;
@@ -57,7 +63,7 @@ void* pinned(gvx_ctx* c, const std::string& name, size_t bytes) {
     if (c->capturing) return nullptr;
     ++c->mem_gen;
     if (b.p) {
-        hipStreamSynchronize(c->stream);
+        sync_all(c);
         hipHostFree(b.p);
         b.p = nullptr;
         b.bytes = 0;
@@ -148,6 +154,7 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
         delete c;
         return GVX_ERR_HIP;
     }
+    c->main = c->stream;
     *out = c;
     return GVX_OK;
 }
@@ -155,7 +162,8 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
 void gvx_destroy(gvx_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(c->main);
+    if (c->side) hipStreamSynchronize(c->side);
     for (auto& f : c->frames) hipFree(f.second.pyr);
     for (auto& b : c->dev) hipFree(b.second.p);
     for (auto& b : c->pinned) hipHostFree(b.second.p);
@@ -164,7 +172,13 @@ void gvx_destroy(gvx_ctx* c) {
         hipEventDestroy(p.b);
     }
     for (auto e : c->event_pool) hipEventDestroy(e);
-    hipStreamDestroy(c->stream);
+    if (c->side) {
+        hipStreamSynchronize(c->side);
+        hipStreamDestroy(c->side);
+    }
+    if (c->fork_ev) hipEventDestroy(c->fork_ev);
+    if (c->join_ev) hipEventDestroy(c->join_ev);
+    hipStreamDestroy(c->main);
     delete c;
 }
 
@@ -172,7 +186,11 @@ const char* gvx_last_error(const gvx_ctx* c) { return c ? c->err.c_str() : ""; }
 
 gvx_status gvx_sync(gvx_ctx* c) {
     if (!c) return GVX_ERR_INVALID;
-    return hip_err(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    if (c->side) {
+        const hipError_t e = hipStreamSynchronize(c->side);
+        if (e != hipSuccess) return hip_err(c, e, "hipStreamSynchronize");
+    }
+    return hip_err(c, hipStreamSynchronize(c->main), "hipStreamSynchronize");
 }
 
 void* gvx_get_stream(gvx_ctx* c) { return c ? (void*)c->stream : nullptr; }
@@ -248,7 +266,7 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
         }
         ++c->mem_gen;
         if (f.pyr) {
-            hipStreamSynchronize(c->stream);
+            sync_all(c);
             hipFree(f.pyr);
             f.pyr = nullptr;
         }
@@ -299,7 +317,7 @@ gvx_status gvx_frame_drop(gvx_ctx* c, uint64_t id) {
     if (it == c->frames.end()) return set_err(c, GVX_ERR_NOT_FOUND, "frame %llu", (unsigned long long)id);
     if (c->capturing) return set_err(c, GVX_ERR_INVALID, "gvx_frame_drop during a graph capture");
     ++c->mem_gen;
-    hipStreamSynchronize(c->stream);
+    sync_all(c);
     hipFree(it->second.pyr);
     c->frames.erase(it);
     return GVX_OK;
@@ -624,7 +642,7 @@ gvx_status frame_slot(gvx_ctx* c, uint64_t id, int32_t w, int32_t h, const gvx_k
         }
         ++c->mem_gen;
         if (f.pyr) {
-            hipStreamSynchronize(c->stream);
+            sync_all(c);
             hipFree(f.pyr);
             f.pyr = nullptr;
         }

@@ -20,6 +20,7 @@ struct gvx_graph {
 
 gvx_status gvx_capture_begin(gvx_ctx* c) {
     if (!c) return GVX_ERR_INVALID;
+    if (c->in_branch || c->branch_open) return set_err(c, GVX_ERR_INVALID, "join the open branch before capturing");
     // the profiling brackets record and query events on the host: not capturable
     if (c->prof) return set_err(c, GVX_ERR_INVALID, "disable profiling before capturing a graph");
     if (c->capturing) return set_err(c, GVX_ERR_INVALID, "a capture is already open");
@@ -37,6 +38,7 @@ gvx_status gvx_capture_end(gvx_ctx* c, gvx_graph** out) {
     *out = nullptr;
     hipSetDevice(c->device);
     if (!c->capturing) return set_err(c, GVX_ERR_INVALID, "no capture is open");
+    if (c->in_branch || c->branch_open) return set_err(c, GVX_ERR_INVALID, "join the open branch before ending the capture");
     c->capturing = false;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
@@ -89,4 +91,48 @@ gvx_status gvx_copy_dev(gvx_ctx* c, void* d_dst, const void* d_src, size_t bytes
     // a kernel, not hipMemcpyAsync: in a captured graph a memcpy node made the
     // one-pair replay slower than the eager calls (67 vs 60 us, r01)
     return hip_err(c, launch_copy(c, d_dst, d_src, bytes), "copy kernel");
+}
+
+// One side branch of the context (include/gvx.h): the calls between
+// gvx_branch_begin and gvx_branch_end run on a second stream that first waits
+// for everything enqueued before the branch; gvx_branch_join makes the context
+// stream wait for the branch.  Under a capture the event record / wait pairs
+// become graph edges, so the branch is a parallel path of the graph.
+gvx_status gvx_branch_begin(gvx_ctx* c) {
+    if (!c) return GVX_ERR_INVALID;
+    if (c->in_branch || c->branch_open) return set_err(c, GVX_ERR_INVALID, "a branch is already open");
+    if (c->prof) return set_err(c, GVX_ERR_INVALID, "disable profiling before branching");
+    hipSetDevice(c->device);
+    if (!c->side) {
+        if (c->capturing) return set_err(c, GVX_ERR_INVALID, "open a first branch outside a capture");
+        hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return hip_err(c, e, "branch stream");
+    }
+    hipError_t e = hipEventRecord(c->fork_ev, c->main);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->side, c->fork_ev, 0);
+    if (e != hipSuccess) return hip_err(c, e, "branch fork");
+    c->stream = c->side;
+    c->in_branch = true;
+    return GVX_OK;
+}
+
+gvx_status gvx_branch_end(gvx_ctx* c) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!c->in_branch) return set_err(c, GVX_ERR_INVALID, "no branch is open");
+    hipSetDevice(c->device);
+    c->stream = c->main;
+    c->in_branch = false;
+    c->branch_open = true;
+    return hip_err(c, hipEventRecord(c->join_ev, c->side), "branch end");
+}
+
+gvx_status gvx_branch_join(gvx_ctx* c) {
+    if (!c) return GVX_ERR_INVALID;
+    if (c->in_branch) return set_err(c, GVX_ERR_INVALID, "end the branch before joining it");
+    if (!c->branch_open) return GVX_OK;
+    hipSetDevice(c->device);
+    c->branch_open = false;
+    return hip_err(c, hipStreamWaitEvent(c->main, c->join_ev, 0), "branch join");
 }

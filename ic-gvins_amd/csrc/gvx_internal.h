@@ -58,6 +58,11 @@ struct gvx_ctx {
     int device = 0;
     int n_cu = 256;  // compute units (persistent-grid sizing)
     hipStream_t stream = nullptr;
+    // gvx_branch_begin / _end / _join: `stream` points at `side` inside a branch;
+    // `main` is the context's own stream (the one gvx_sync and captures use)
+    hipStream_t main = nullptr, side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    bool in_branch = false, branch_open = false;  // enqueuing on side / a recorded branch not yet joined
     std::string err;
     std::unordered_map<uint64_t, gvx::Frame> frames;
     // scratch (grown on demand, never shrunk)

@@ -215,6 +215,9 @@ def _declare(L):
         "gvx_graph_launch": (i32, [P, P]),
         "gvx_graph_destroy": (None, [P]),
         "gvx_copy_dev": (i32, [P, P, P, C.c_size_t]),
+        "gvx_branch_begin": (i32, [P]),
+        "gvx_branch_end": (i32, [P]),
+        "gvx_branch_join": (i32, [P]),
     }
     for name, (res, args) in sig.items():
         # an older build (a GVX_LIB variant timed against the tree) may lack newer
@@ -813,6 +816,18 @@ class Context:
     def copy_dev(self, d_dst: int, d_src: int, nbytes: int):
         """Device-to-device copy on the context stream (capturable)."""
         self._check(self._L.gvx_copy_dev(self._h, d_dst, d_src, nbytes), "gvx_copy_dev")
+
+    def branch_begin(self):
+        """Enqueue the following calls on a side branch (gvx_branch_begin)."""
+        self._check(self._L.gvx_branch_begin(self._h), "gvx_branch_begin")
+
+    def branch_end(self):
+        """Back to the context stream, the branch running beside it (gvx_branch_end)."""
+        self._check(self._L.gvx_branch_end(self._h), "gvx_branch_end")
+
+    def branch_join(self):
+        """The context stream waits for the branch (gvx_branch_join)."""
+        self._check(self._L.gvx_branch_join(self._h), "gvx_branch_join")
 
 
 class Graph:

@@ -84,7 +84,7 @@ class DeviceSequenceTracker:
 
     def __init__(self, ctx: Context, w: int, h: int, n_features: int = 150,
                  klt: Optional[KltParams] = None, detect: Optional[DetectParams] = None,
-                 ids=(0, 1), graph: bool = False, device=None, frames=None):
+                 ids=(0, 1), graph: bool = False, device=None, frames=None, pipeline: bool = False):
         import torch
         self.ctx, self.w, self.h, self.n = ctx, w, h, n_features
         self.kp = klt or KltParams.default()
@@ -101,13 +101,66 @@ class DeviceSequenceTracker:
         self.graphs = {}
         self.frames = frames
         self.stage = torch.empty((h, w), dtype=torch.uint8, device=dev) if (graph and frames is None) else None
+        # pipeline (HBM-resident sequences only): frame t+1's preprocessing
+        # (CLAHE + pyramid into a third frame slot) runs as a side branch beside
+        # frame t's tracking (gvx_branch_begin / _end / _join); the record that
+        # advances the frame index waits for the branch, which read the index.
+        # Frame t+1 is read at t = F - 1 too, so the sequence gets one spare frame.
+        self.pipeline = bool(pipeline) and frames is not None
+        self.src = frames
+        if self.pipeline:
+            if len(self.ids) < 3:
+                self.ids = tuple(self.ids) + (max(self.ids) + 1,)
+            self.src = torch.cat([frames, frames[-1:]])
         if frames is not None:
             F = frames.shape[0]
             self.index = torch.zeros(1, dtype=torch.int32, device=dev)
             self.rec_tracks = torch.zeros((F, n_features, 2), **f32)
             self.rec_counts = torch.zeros(F, dtype=torch.int32, device=dev)
 
+    def _pre_next(self, t: int):
+        # frame *index + 1 (the index still holds t: the record waits for the branch)
+        fb = self.w * self.h
+        self.ctx.frame_preprocess_indexed_dev(self.ids[(t + 1) % 3], self.src.data_ptr() + fb, fb,
+                                              self.index.data_ptr(), self.w, self.h, params=self.kp)
+
+    def _track_cur(self, t: int):
+        self.ctx.track_frame_dev(self.ids[(t - 1) % 3], self.ids[t % 3], t > 0, self.pts.data_ptr(),
+                                 self.vel.data_ptr(), self.init.data_ptr(), self.count.data_ptr(), self.n, self.w,
+                                 self.h, klt=self.kp, detect=self.dp)
+
+    def _graph(self, key, fn, t: int):
+        g = self.graphs.get(key)
+        if g is None:
+            self.ctx.capture_begin()
+            fn(t)
+            g = self.graphs[key] = self.ctx.capture_end()
+        return g
+
+    def _enqueue_pipelined(self, t: int, graphs: bool):
+        """Frame t+1's preprocessing on the context's side branch beside frame t's
+        tracking; the record (which advances the index the branch reads) after the
+        join.  With graphs, each half is its own captured graph (one per frame-slot
+        rotation), launched on its own stream: the branches of ONE captured graph
+        measured serialised (r02 v21)."""
+        ctx = self.ctx
+        if t == 0:
+            ctx.frame_preprocess_indexed_dev(self.ids[0], self.src.data_ptr(), self.w * self.h,
+                                             self.index.data_ptr(), self.w, self.h, params=self.kp)
+        if graphs:
+            ga = self._graph(("pre", t % 3), self._pre_next, t)
+            gb = self._graph(("trk", t % 3), self._track_cur, t)
+        ctx.branch_begin()
+        ctx.graph_launch(ga) if graphs else self._pre_next(t)
+        ctx.branch_end()
+        ctx.graph_launch(gb) if graphs else self._track_cur(t)
+        ctx.branch_join()
+        ctx.track_record_dev(self.pts.data_ptr(), self.count.data_ptr(), self.n, self.rec_tracks.data_ptr(),
+                             self.rec_counts.data_ptr(), self.index.data_ptr(), self.frames.shape[0])
+
     def _enqueue(self, d_frame: Optional[int], t: int):
+        if self.pipeline:
+            return self._enqueue_pipelined(t, False)
         ctx = self.ctx
         cur, prev = self.ids[t % 2], self.ids[(t - 1) % 2]
         if self.frames is not None:
@@ -134,14 +187,17 @@ class DeviceSequenceTracker:
         t = self.t
         if not self.graph or t < 3:
             self._enqueue(d_frame, t)  # the first frames also size every buffer
+        elif self.pipeline:
+            self._enqueue_pipelined(t, True)
         else:
             if self.frames is None:
                 self.ctx.copy_dev(self.stage.data_ptr(), d_frame, self.w * self.h)
-            g = self.graphs.get(t % 2)
+            key = t % 2  # the frame slots' rotation
+            g = self.graphs.get(key)
             if g is None:
                 self.ctx.capture_begin()
                 self._enqueue(None if self.frames is not None else self.stage.data_ptr(), t)
-                g = self.graphs[t % 2] = self.ctx.capture_end()
+                g = self.graphs[key] = self.ctx.capture_end()
             self.ctx.graph_launch(g)
         self.t += 1
 

@@ -74,6 +74,19 @@ void gvx_graph_destroy(gvx_graph* g);
    flow copied into next_xy before each replay).  A copy kernel on the compute
    queue (no DMA engine hand-off inside a graph). */
 gvx_status gvx_copy_dev(gvx_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
+/* One side branch of the context's stream: the *_dev calls between
+   gvx_branch_begin and gvx_branch_end are enqueued on a second stream that
+   first waits for everything enqueued before gvx_branch_begin; the calls after
+   gvx_branch_end go to the context stream again, concurrently with the branch,
+   until gvx_branch_join makes the context stream wait for the branch.  Inside a
+   capture the branch becomes a parallel path of the graph (the sequence replay
+   preprocesses frame t+1 beside frame t's tracking).  Work of the two paths
+   must not share scratch buffers or frame slots.  One branch at a time; the
+   first gvx_branch_begin of a context must not be inside a capture (it creates
+   the stream); a capture must not begin or end with a branch open. */
+gvx_status gvx_branch_begin(gvx_ctx* ctx);
+gvx_status gvx_branch_end(gvx_ctx* ctx);
+gvx_status gvx_branch_join(gvx_ctx* ctx);
 
 /* ------------------------------------------------------------------ KLT  */
 /* cv::calcOpticalFlowPyrLK arguments as used at tracking/tracking.cc:385-393:

@@ -80,12 +80,16 @@ def test_sequence_replay_bit_exact(ctx, orc, gvx_mod, n_frames):
     assert n_tracked > 100 * (n_frames - 1) and n_detect >= 2
 
 
-@pytest.mark.parametrize("graph,resident", [(False, False), (True, False), (True, True)])
-def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident):
+@pytest.mark.parametrize("graph,resident,pipeline", [(False, False, False), (True, False, False), (True, True, False),
+                                                     (False, True, True), (True, True, True)])
+def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident, pipeline):
     """gvx_track_frame_dev (the tracker state on the device, no host round trip;
     with graph=True one captured graph per frame parity replayed per frame)
     gives the same per-frame track list as SequenceTracker, whose every step the
-    test above holds bit-exact against the oracle."""
+    test above holds bit-exact against the oracle.  pipeline: frame t+1's
+    preprocessing runs as a side branch beside frame t's tracking (three frame
+    slots; with graphs, a preprocessing graph and a tracking graph per slot
+    rotation on two streams)."""
     import torch
     from gvx import synth
     from gvx.tracking import DeviceSequenceTracker, SequenceTracker
@@ -96,7 +100,7 @@ def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident):
     dp = gvx_mod.DetectParams.default(max_features=N)
     ref = SequenceTracker(ctx, W, H, N, klt=kp, detect=dp, ids=(10, 11))
     trk = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, ids=(20, 21), graph=graph, device=dev,
-                                frames=frames if resident else None)
+                                frames=frames if resident else None, pipeline=pipeline)
     try:
         wants = []
         for t in range(n_frames):
@@ -115,6 +119,6 @@ def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident):
             for t in range(n_frames):
                 assert np.array_equal(tracks[t, :counts[t]], wants[t]), f"frame {t}"
         if graph:
-            assert len(trk.graphs) == 2
+            assert len(trk.graphs) == (6 if pipeline else 2)
     finally:
         trk.close()
