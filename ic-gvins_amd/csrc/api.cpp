@@ -189,6 +189,7 @@ gvx_status gvx_sync(gvx_ctx* c) {
     if (c->side) {
         const hipError_t e = hipStreamSynchronize(c->side);
         if (e != hipSuccess) return hip_err(c, e, "hipStreamSynchronize");
+        if (!c->in_branch) c->branch_open = false;  // the branch's work is done: nothing left to join
     }
     return hip_err(c, hipStreamSynchronize(c->main), "hipStreamSynchronize");
 }

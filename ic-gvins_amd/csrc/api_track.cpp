@@ -278,3 +278,10 @@ extern "C" gvx_status gvx_track_record_dev(gvx_ctx* c, const float* d_pts, const
     return hip_err(c, launch_track_record(c, d_pts, d_n, capacity, d_tracks, d_counts, d_frame_index, max_frames),
                    "track record kernel");
 }
+
+gvx_status gvx_index_advance_dev(gvx_ctx* c, int32_t* d_index, int32_t delta) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!d_index) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    return hip_err(c, launch_index_advance(c, d_index, delta), "index advance kernel");
+}

@@ -285,6 +285,7 @@ hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d);
 // ---- track.hip (gvx_track_frame_dev, gvx_copy_dev) ----
 hipError_t launch_copy(gvx_ctx* c, void* dst, const void* src, size_t bytes);
 hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index);
+hipError_t launch_index_advance(gvx_ctx* c, int32_t* index, int32_t delta);
 hipError_t launch_track_record(gvx_ctx* c, const float* pts, const int32_t* n, int cap, float* tracks,
                                int32_t* counts, int32_t* frame, int max_frames);
 // the device tracker state after the forward/backward LK: keep-flag compaction,

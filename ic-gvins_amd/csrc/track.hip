@@ -246,6 +246,16 @@ __global__ void __launch_bounds__(256) track_record_kernel(const float2* __restr
 
 }  // namespace
 
+// *index += delta (a frame counter a graph advances for itself)
+__global__ void __launch_bounds__(64) index_advance_kernel(int32_t* __restrict__ index, int32_t delta) {
+    if (threadIdx.x == 0) index[0] += delta;
+}
+
+hipError_t launch_index_advance(gvx_ctx* c, int32_t* index, int32_t delta) {
+    index_advance_kernel<<<1, 64, 0, c->stream>>>(index, delta);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index) {
     const size_t units = (bytes + 15) / 16;
     const unsigned blocks = (unsigned)std::min<size_t>((units + 255) / 256, 4096);

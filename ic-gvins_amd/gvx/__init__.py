@@ -218,6 +218,7 @@ def _declare(L):
         "gvx_branch_begin": (i32, [P]),
         "gvx_branch_end": (i32, [P]),
         "gvx_branch_join": (i32, [P]),
+        "gvx_index_advance_dev": (i32, [P, P, i32]),
     }
     for name, (res, args) in sig.items():
         # an older build (a GVX_LIB variant timed against the tree) may lack newer
@@ -414,6 +415,10 @@ class Context:
                          d_frame_index: int, max_frames: int):
         self._check(self._L.gvx_track_record_dev(self._h, d_pts, d_n, capacity, d_tracks, d_counts, d_frame_index,
                                                  max_frames), "gvx_track_record_dev")
+
+    def index_advance_dev(self, d_index: int, delta: int = 1):
+        """*d_index += delta on the context stream (gvx_index_advance_dev)."""
+        self._check(self._L.gvx_index_advance_dev(self._h, d_index, delta), "gvx_index_advance_dev")
 
     def find_fundamental_ransac(self, sets, thresh=1.5, confidence=0.99, max_iters=1000):
         """cv::findFundamentalMat(p1, p2, FM_RANSAC, thresh, confidence, mask) per

@@ -103,15 +103,16 @@ class DeviceSequenceTracker:
         self.stage = torch.empty((h, w), dtype=torch.uint8, device=dev) if (graph and frames is None) else None
         # pipeline (HBM-resident sequences only): frame t+1's preprocessing
         # (CLAHE + pyramid into a third frame slot) runs as a side branch beside
-        # frame t's tracking (gvx_branch_begin / _end / _join); the record that
-        # advances the frame index waits for the branch, which read the index.
-        # Frame t+1 is read at t = F - 1 too, so the sequence gets one spare frame.
+        # frame t's tracking (gvx_branch_begin / _end / _join), reading the frame
+        # at its own device counter.  Frame t+1 is read at t = F - 1 too, so the
+        # sequence gets one spare frame.
         self.pipeline = bool(pipeline) and frames is not None
         self.src = frames
         if self.pipeline:
             if len(self.ids) < 3:
                 self.ids = tuple(self.ids) + (max(self.ids) + 1,)
             self.src = torch.cat([frames, frames[-1:]])
+            self.pindex = torch.ones(1, dtype=torch.int32, device=dev)
         if frames is not None:
             F = frames.shape[0]
             self.index = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -119,15 +120,17 @@ class DeviceSequenceTracker:
             self.rec_counts = torch.zeros(F, dtype=torch.int32, device=dev)
 
     def _pre_next(self, t: int):
-        # frame *index + 1 (the index still holds t: the record waits for the branch)
-        fb = self.w * self.h
-        self.ctx.frame_preprocess_indexed_dev(self.ids[(t + 1) % 3], self.src.data_ptr() + fb, fb,
-                                              self.index.data_ptr(), self.w, self.h, params=self.kp)
+        # frame *pindex (= t + 1) into the slot of frame t+1; the branch advances its
+        # own counter, so it never reads the index the tracking graph's record advances
+        self.ctx.frame_preprocess_indexed_dev(self.ids[(t + 1) % 3], self.src.data_ptr(), self.w * self.h,
+                                              self.pindex.data_ptr(), self.w, self.h, params=self.kp)
+        self.ctx.index_advance_dev(self.pindex.data_ptr(), 1)
 
     def _track_cur(self, t: int):
-        self.ctx.track_frame_dev(self.ids[(t - 1) % 3], self.ids[t % 3], t > 0, self.pts.data_ptr(),
-                                 self.vel.data_ptr(), self.init.data_ptr(), self.count.data_ptr(), self.n, self.w,
-                                 self.h, klt=self.kp, detect=self.dp)
+        self.ctx.track_frame_record_dev(self.ids[(t - 1) % 3], self.ids[t % 3], t > 0, self.pts.data_ptr(),
+                                        self.vel.data_ptr(), self.init.data_ptr(), self.count.data_ptr(), self.n,
+                                        self.w, self.h, self.rec_tracks.data_ptr(), self.rec_counts.data_ptr(),
+                                        self.index.data_ptr(), self.frames.shape[0], klt=self.kp, detect=self.dp)
 
     def _graph(self, key, fn, t: int):
         g = self.graphs.get(key)
@@ -139,14 +142,17 @@ class DeviceSequenceTracker:
 
     def _enqueue_pipelined(self, t: int, graphs: bool):
         """Frame t+1's preprocessing on the context's side branch beside frame t's
-        tracking; the record (which advances the index the branch reads) after the
-        join.  With graphs, each half is its own captured graph (one per frame-slot
+        tracking (+ its record).  Frame t's tracking waits for frame t's
+        preprocessing (the join at the top); frame t+1's preprocessing waits for
+        frame t-1's tracking, the last reader of the slot it writes (the fork).
+        With graphs, each half is its own captured graph (one per frame-slot
         rotation), launched on its own stream: the branches of ONE captured graph
         measured serialised (r02 v21)."""
         ctx = self.ctx
         if t == 0:
             ctx.frame_preprocess_indexed_dev(self.ids[0], self.src.data_ptr(), self.w * self.h,
                                              self.index.data_ptr(), self.w, self.h, params=self.kp)
+        ctx.branch_join()
         if graphs:
             ga = self._graph(("pre", t % 3), self._pre_next, t)
             gb = self._graph(("trk", t % 3), self._track_cur, t)
@@ -154,9 +160,6 @@ class DeviceSequenceTracker:
         ctx.graph_launch(ga) if graphs else self._pre_next(t)
         ctx.branch_end()
         ctx.graph_launch(gb) if graphs else self._track_cur(t)
-        ctx.branch_join()
-        ctx.track_record_dev(self.pts.data_ptr(), self.count.data_ptr(), self.n, self.rec_tracks.data_ptr(),
-                             self.rec_counts.data_ptr(), self.index.data_ptr(), self.frames.shape[0])
 
     def _enqueue(self, d_frame: Optional[int], t: int):
         if self.pipeline:
@@ -208,6 +211,8 @@ class DeviceSequenceTracker:
         return self.pts[:n].cpu().numpy()
 
     def close(self):
+        if self.pipeline:
+            self.ctx.branch_join()  # the last frame's preprocessing branch
         for g in self.graphs.values():
             g.destroy()
         self.graphs = {}

@@ -83,7 +83,8 @@ gvx_status gvx_copy_dev(gvx_ctx* ctx, void* d_dst, const void* d_src, size_t byt
    preprocesses frame t+1 beside frame t's tracking).  Work of the two paths
    must not share scratch buffers or frame slots.  One branch at a time; the
    first gvx_branch_begin of a context must not be inside a capture (it creates
-   the stream); a capture must not begin or end with a branch open. */
+   the stream); a capture must not begin or end with a branch open (gvx_sync
+   also completes an ended branch). */
 gvx_status gvx_branch_begin(gvx_ctx* ctx);
 gvx_status gvx_branch_end(gvx_ctx* ctx);
 gvx_status gvx_branch_join(gvx_ctx* ctx);
@@ -363,6 +364,9 @@ gvx_status gvx_copy_indexed_dev(gvx_ctx* ctx, void* d_dst, const void* d_src_bas
                                 const int32_t* d_index);
 gvx_status gvx_track_record_dev(gvx_ctx* ctx, const float* d_pts, const int32_t* d_n, int32_t capacity,
                                 float* d_tracks, int32_t* d_counts, int32_t* d_frame_index, int32_t max_frames);
+/* *d_index += delta on the context stream (a frame counter that a captured
+   graph advances for itself, e.g. the pipelined replay's preprocessing branch). */
+gvx_status gvx_index_advance_dev(gvx_ctx* ctx, int32_t* d_index, int32_t delta);
 
 
 /* --------------------------------------------------- IMU preintegration */
