@@ -145,7 +145,7 @@ __device__ __forceinline__ uint32_t hibytes(uint32_t lo, uint32_t hi) {
 //    Levels narrower or shorter than RING_MIN take their ring from ring_kernel.
 constexpr int ST_COLS = 480;  // source columns owned per strip
 #ifndef STREAM_BAND
-#define STREAM_BAND 32
+#define STREAM_BAND 40
 #endif
 constexpr int BAND = STREAM_BAND;  // level-1 rows owned per band (level k: BAND >> (k-1))
 
@@ -573,7 +573,7 @@ __host__ __device__ inline bool pass_writes_sides(int w, int h) { return w >= RI
 // less latency for more halo work on an otherwise idle GPU
 inline int stream_band(int n_strips, int h1, int n_img, int n_cu) {
     int band = BAND;
-    while (band > 4 && n_strips * ((h1 + band - 1) / band) * n_img < 4 * n_cu) band >>= 1;
+    while (band > 4 && n_strips * ((h1 + band - 1) / band) * n_img < 4 * n_cu) band = std::max(4, (band >> 1) & ~3);
     // the same number of bands, balanced (a multiple of 4 rows each)
     const int n_bands = (h1 + band - 1) / band;
     return std::min(band, ((h1 + n_bands - 1) / n_bands + 3) / 4 * 4);
