@@ -93,3 +93,49 @@ def test_stale_graph_refused(gvx_mod):
         g.launch()
     g.destroy()
     ctx.close()
+
+
+def test_branch_order_and_misuse(gvx_mod):
+    """gvx_branch_begin / _end / _join: the branch sees everything enqueued before
+    it, the context stream after gvx_branch_join sees the branch's writes, index
+    advance is a device-side += , and misuse is refused (nested branches, ending
+    without a branch, capturing with a branch open).  A private context."""
+    import torch
+    ctx = gvx_mod.Context(0)
+    dev = torch.device("cuda", 0)
+    n = 1 << 20
+    src = torch.arange(n, dtype=torch.int32, device=dev)
+    a, b, c = (torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(3))
+    idx = torch.full((1,), 5, dtype=torch.int32, device=dev)
+    nb = n * 4
+    try:
+        torch.cuda.synchronize()
+        with pytest.raises(gvx_mod.GvxError):
+            ctx.branch_end()  # no branch open
+        for _ in range(3):
+            ctx.copy_dev(a.data_ptr(), src.data_ptr(), nb)        # context stream
+            ctx.branch_begin()
+            with pytest.raises(gvx_mod.GvxError):
+                ctx.branch_begin()                                 # one branch at a time
+            ctx.copy_dev(b.data_ptr(), a.data_ptr(), nb)           # branch: after the first copy
+            ctx.index_advance_dev(idx.data_ptr(), 2)
+            ctx.branch_end()
+            with pytest.raises(gvx_mod.GvxError):
+                ctx.capture_begin()                                # an ended branch is still open
+            ctx.branch_join()
+            ctx.copy_dev(c.data_ptr(), b.data_ptr(), nb)           # after the join
+            ctx.sync()
+            assert torch.equal(c, src)
+            a.zero_(), b.zero_(), c.zero_()
+            torch.cuda.synchronize()
+        assert int(idx.cpu()[0]) == 5 + 2 * 3
+        # gvx_sync completes an ended branch: a capture may begin afterwards
+        ctx.branch_begin()
+        ctx.branch_end()
+        ctx.sync()
+        ctx.capture_begin()
+        ctx.copy_dev(a.data_ptr(), src.data_ptr(), nb)
+        g = ctx.capture_end()
+        g.destroy()
+    finally:
+        ctx.close()
