@@ -227,10 +227,13 @@ void gvx_klt_params_default(gvx_klt_params* p) {
     p->eps = 0.01;
     p->use_initial_flow = 1;
     p->min_eig = 1e-4f;
+    p->accum = GVX_LK_ACCUM_EXACT;
 }
 
 static gvx_status check_klt_params(gvx_ctx* c, const gvx_klt_params* p) {
     if (!p) return set_err(c, GVX_ERR_INVALID, "null klt params");
+    if (p->accum < GVX_LK_ACCUM_EXACT || p->accum > GVX_LK_ACCUM_F32_SIMD4)
+        return set_err(c, GVX_ERR_INVALID, "unknown LK accumulation order %d", p->accum);
     if (p->win != WIN)
         return set_err(c, GVX_ERR_UNSUPPORTED, "device LK supports win=21 only (got %d)", p->win);
     if (p->max_level < 0 || p->max_level >= MAX_LEVELS)
@@ -247,6 +250,7 @@ static KltArgs klt_args(const gvx_klt_params* p) {
     a.crit_eps = e * e;
     a.min_eig = p->min_eig;
     a.use_initial_flow = p->use_initial_flow;
+    a.accum = p->accum;
     return a;
 }
 

@@ -24,6 +24,8 @@ static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, in
     if (!d_pts || !d_vel || !d_init || !d_n) return set_err(c, GVX_ERR_INVALID, "null tracker state");
     if (cap <= 0 || cap < dp->max_features) return set_err(c, GVX_ERR_INVALID, "capacity %d < max_features", cap);
     if (kp->win != WIN) return set_err(c, GVX_ERR_UNSUPPORTED, "device LK supports win=21 only (got %d)", kp->win);
+    if (kp->accum < GVX_LK_ACCUM_EXACT || kp->accum > GVX_LK_ACCUM_F32_SIMD4)
+        return set_err(c, GVX_ERR_INVALID, "unknown LK accumulation order %d", kp->accum);
     if (dp->subpix_win != 5) return set_err(c, GVX_ERR_UNSUPPORTED, "cornerSubPix win must be 5 (tracking.cc:623)");
     auto in = c->frames.find(next_id);
     if (in == c->frames.end()) return set_err(c, GVX_ERR_NOT_FOUND, "frame %llu", (unsigned long long)next_id);
@@ -141,6 +143,7 @@ static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, in
         const double ce = kp->eps < 0 ? 0.0 : (kp->eps > 10.0 ? 10.0 : kp->eps);
         a.crit_eps = ce * ce;
         a.min_eig = kp->min_eig;
+        a.accum = kp->accum;
         a.use_initial_flow = 1;  // pts + vel, as SequenceTracker / Tracking::track
         a.n_pairs = 1;
         a.n_pts = cap;

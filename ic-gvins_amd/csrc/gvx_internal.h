@@ -130,6 +130,7 @@ struct KltArgs {
     double crit_eps;         // eps*eps (double, like OpenCV criteria.epsilon)
     float min_eig;
     int32_t use_initial_flow;
+    int32_t accum;           // GVX_LK_ACCUM_*
     int32_t mode;            // 0: single LK, 1: fwd + bwd + FB
     double fb_thresh, border;
     int32_t cam_w, cam_h;

@@ -20,8 +20,6 @@
 
 #include <climits>
 
-#include <cstdlib>
-
 #include "gvx_internal.h"
 
 namespace gvx {
@@ -51,6 +49,8 @@ __device__ __forceinline__ int dot2k(uint32_t a, uint32_t b, int k) {
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) {
     return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
 }
+// signed int16 half `hi` of a packed pair
+__device__ __forceinline__ int half16(uint32_t v, int hi) { return hi ? ((int)v >> 16) : (int)(short)(v & 0xffffu); }
 // bytes (b[t], b[t+1]) of the 8-byte value {d1:d0} zero-extended to int16 halves
 template <int T>
 __device__ __forceinline__ uint32_t byte_pair(uint32_t d0, uint32_t d1) {
@@ -339,6 +339,25 @@ __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2
     }
 }
 
+// match_unit's products for the fp32 orders: p1[t] = (float)(diff*Ix),
+// p2[t] = (float)(diff*Iy) of the unit's 7 pixels (OpenCV converts the int32
+// products, `ib1 += (itemtype)(diff*dIptr[0])`; |diff*Ix| < 2^25, round to
+// nearest even like the CPU's int -> float conversion).
+__device__ __forceinline__ uint32_t bp2(const uint32_t (&r)[2], int T) {
+    return __builtin_amdgcn_perm(r[1], r[0], 0x0c000c00u | ((uint32_t)(T + 1) << 16) | (uint32_t)T);
+}
+__device__ __forceinline__ void match_unit_f32(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
+                                               uint32_t W0, uint32_t W1, float (&p1)[7], float (&p2)[7]) {
+    constexpr int RND = 1 << (W_BITS - 6);
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        const int jv = dot2(bp2(r1, t), W1, dot2k(bp2(r0, t), W0, RND)) >> (W_BITS - 5);
+        const int d = jv - half16(u.iv[t >> 1], t & 1);
+        p1[t] = (float)__mul24(d, half16(u.ix[t >> 1], t & 1));
+        p2[t] = (float)__mul24(d, half16(u.iy[t >> 1], t & 1));
+    }
+}
+
 // Exact sums over a point's lane group (G = 16, 32 or 64 lanes, aligned):
 // a butterfly, so every lane of the group ends with the group total --
 // DPP quad / row mirrors inside 16-lane rows, then v_permlane16_swap /
@@ -374,6 +393,102 @@ template <int G>
 __device__ __forceinline__ float group_sum_f32(int v) {
     const int h = group_sum<G>(v >> 10), l = group_sum<G>(v & 1023);
     return (float)__builtin_fma((double)h, 1024.0, (double)l);
+}
+
+// ---- OpenCV's fp32 window-sum orders (gvx_klt_params.accum, oracle/klt.c
+// ORC_ACC_F32 / ORC_ACC_F32X4) ----
+// The products of one window sum are computed lane-parallel like the exact
+// path, staged in the point group's LDS region, and summed in OpenCV's order
+// by one lane per fp32 accumulator (a dependent chain: 441 adds for the scalar
+// loop, at most 105 for the CV_SIMD128 lanes and the scalar tail); the finished
+// accumulators are combined in OpenCV's reduction order by every lane.
+// Region layout (floats), two arrays k = 0, 1 (two sums at once):
+//  ACC 1 (scalar): array k at 512k; unit q's 7 pixels at 8q .. 8q+6 (window
+//    pixel (y, x) is unit 3y + x/7, slot x%7: row-major order is unit order);
+//    accumulator lane gl = k walks q = 0..62.
+//  ACC 2 (SIMD4): array k at 540k; lane m = 0..3 (pixels x = m, m+4, m+8, m+12
+//    of every row, index 4y + x/4) at 108m, the scalar tail (x = 16..20, index
+//    5y + x - 16) at 432; zero padded to 108 per accumulator (adding +0 is
+//    exact: no partial sum is -0); accumulator lane gl = 5k + m.
+//  Accumulator results at ACC_RES + gl.
+constexpr int ACC_RES = 1080, ACC_FLOATS = 1092;
+template <int ACC>
+constexpr int acc_chains() {
+    return ACC == 1 ? 2 : 10;
+}
+
+// unit q's 7 values into array k
+template <int ACC>
+__device__ __forceinline__ void acc_put(float* scr, int k, int q, const float (&v)[7]) {
+    if constexpr (ACC == 1) {
+        float4* p = reinterpret_cast<float4*>(scr + 512 * k + 8 * q);
+        p[0] = float4{v[0], v[1], v[2], v[3]};
+        p[1] = float4{v[4], v[5], v[6], 0.f};
+    } else {
+        const int y = q / 3, x0 = 7 * (q - 3 * y);
+        float* a = scr + 540 * k;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int x = x0 + t;
+            const int idx = x < 16 ? (x & 3) * 108 + 4 * y + (x >> 2) : 432 + 5 * y + (x - 16);
+            a[idx] = v[t];
+        }
+    }
+}
+// zero the region once per wave (the SIMD4 pads are never written again)
+template <int ACC, int G>
+__device__ __forceinline__ void acc_clear(float* scr, int gl) {
+    if constexpr (ACC != 0) {
+        float4* p = reinterpret_cast<float4*>(scr);
+        for (int i = gl; i < ACC_FLOATS / 4; i += G) p[i] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+// the accumulator lanes' sequential sums; every lane of the group ends with
+// the region's accumulators published at ACC_RES
+template <int ACC>
+__device__ __forceinline__ void acc_chains_run(float* scr, int gl) {
+    wave_lds_sync();  // the products are in place
+    float s = 0.f;
+    if constexpr (ACC == 1) {
+        const float4* p = reinterpret_cast<const float4*>(scr + 512 * (gl & 1));
+#pragma unroll 9
+        for (int q = 0; q < 63; ++q) {
+            const float4 a = p[2 * q], b = p[2 * q + 1];
+            s += a.x;
+            s += a.y;
+            s += a.z;
+            s += a.w;
+            s += b.x;
+            s += b.y;
+            s += b.z;
+        }
+    } else {
+        const int c = gl < 10 ? gl : 9, k = c >= 5 ? 1 : 0, m = c - 5 * k;
+        const float4* p = reinterpret_cast<const float4*>(scr + 540 * k + 108 * m);
+#pragma unroll 9
+        for (int i = 0; i < 27; ++i) {
+            const float4 a = p[i];
+            s += a.x;
+            s += a.y;
+            s += a.z;
+            s += a.w;
+        }
+    }
+    if (gl < acc_chains<ACC>()) scr[ACC_RES + gl] = s;
+    wave_lds_sync();
+}
+// sum k of the region in OpenCV's reduction order (after acc_chains_run).
+// A (qA..: lane x mod 4): tail + ((l0 + l1) + (l2 + l3)) (v_reduce_sum);
+// b (qb0 = (b1, b2) of x%4 = 0, 1; qb1 of x%4 = 2, 3): tail + ((l0 + l2) + (l1 + l3))
+// (v_interleave_pairs(qb0 + qb1), then the two-lane v_reduce_sum).
+template <int ACC, bool B>
+__device__ __forceinline__ float acc_result(const float* scr, int k) {
+    if constexpr (ACC == 1) {
+        return scr[ACC_RES + k];
+    } else {
+        const float* r = scr + ACC_RES + 5 * k;
+        return B ? r[4] + ((r[0] + r[2]) + (r[1] + r[3])) : r[4] + ((r[0] + r[1]) + (r[2] + r[3]));
+    }
 }
 
 // Window rows of a point's units: 4 rows x 12 bytes of I per unit for the
@@ -430,11 +545,13 @@ struct L0Planes {
 // issued once for PPW points.  I/J: padded pyramids of the prev / next image
 // (levels >= 1); level 0 from `p0`.  Every per-point value below is uniform
 // over the point's group; control flow diverges only between groups.
-template <int PPW>
+// ACC: the window-sum order (0 exact, 1 / 2 OpenCV's fp32 scalar / SIMD4
+// orders through the group's LDS region `acc`).
+template <int PPW, int ACC>
 __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
                                          const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
                                          float p0y, float& nx, float& ny, int& status, float& err, int gl,
-                                         uint32_t* win, v4u* ust) {
+                                         uint32_t* win, v4u* ust, float* acc) {
     constexpr int G = 64 / PPW, U = PPW;
     Unit u[U];
 #pragma unroll
@@ -507,11 +624,47 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 if constexpr (PPW > 1) unit_put(ust, s, u[s]);  // one unit per lane: kept in registers
             }
         }
-        float A11, A12;
-        group_sums_f32<G>(a11, a12, A11, A12);
+        float A11, A12, A22;
+        if constexpr (ACC == 0) {
+            group_sums_f32<G>(a11, a12, A11, A12);
+            A22 = group_sum_f32<G>(a22);
+        } else {
+            // Ix*Ix and Ix*Iy first, then Iy*Iy (exact int products < 2^24: the
+            // float conversion is exact, as OpenCV's fx*fx of converted values)
+            wave_lds_sync();  // the previous readers of the region are done
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                if (!u[s].valid) continue;
+                float v0[7], v1[7];
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const int x = half16(u[s].ix[t >> 1], t & 1), y = half16(u[s].iy[t >> 1], t & 1);
+                    v0[t] = (float)__mul24(x, x);
+                    v1[t] = (float)__mul24(x, y);
+                }
+                acc_put<ACC>(acc, 0, gl + s * G, v0);
+                acc_put<ACC>(acc, 1, gl + s * G, v1);
+            }
+            acc_chains_run<ACC>(acc, gl);
+            A11 = acc_result<ACC, false>(acc, 0);
+            A12 = acc_result<ACC, false>(acc, 1);
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                if (!u[s].valid) continue;
+                float v0[7];
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const int y = half16(u[s].iy[t >> 1], t & 1);
+                    v0[t] = (float)__mul24(y, y);
+                }
+                acc_put<ACC>(acc, 0, gl + s * G, v0);
+            }
+            acc_chains_run<ACC>(acc, gl);
+            A22 = acc_result<ACC, false>(acc, 0);
+        }
         A11 *= FLT_SCALE;
         A12 *= FLT_SCALE;
-        const float A22 = group_sum_f32<G>(a22) * FLT_SCALE;
+        A22 *= FLT_SCALE;
         float D = A11 * A22 - A12 * A12;
         const float minEig =
             __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12), (float)(2 * WIN * WIN));
@@ -550,13 +703,30 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 cinx = inx;
                 ciny = iny;
             }
-#pragma unroll
-            for (int s = 0; s < U; ++s) {
-                if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
-            }
             float fb1, fb2;
-            group_sums_f32<G>(b1, b2, fb1, fb2);
+            if constexpr (ACC == 0) {
+#pragma unroll
+                for (int s = 0; s < U; ++s) {
+                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                    match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                }
+                group_sums_f32<G>(b1, b2, fb1, fb2);
+            } else {
+                wave_lds_sync();  // the previous readers of the region are done
+#pragma unroll
+                for (int s = 0; s < U; ++s) {
+                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                    float p1[7], p2[7];
+                    match_unit_f32(u[s], jr0[s], jr1[s], J0, J1, p1, p2);
+                    if (u[s].valid) {
+                        acc_put<ACC>(acc, 0, gl + s * G, p1);
+                        acc_put<ACC>(acc, 1, gl + s * G, p2);
+                    }
+                }
+                acc_chains_run<ACC>(acc, gl);
+                fb1 = acc_result<ACC, true>(acc, 0);
+                fb2 = acc_result<ACC, true>(acc, 1);
+            }
             fb1 *= FLT_SCALE;
             fb2 *= FLT_SCALE;
             const float dx = (A12 * fb2 - A22 * fb1) * D;
@@ -615,12 +785,13 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 #define KLT_WPB 1
 #endif
 // minimum waves per SIMD the register allocation must allow
-template <int PPW>
+// (the fp32-order instances are LDS-limited: 16 KB per two-point wave)
+template <int PPW, int ACC>
 constexpr int klt_occupancy() {
-    return PPW == 1 ? 4 : PPW == 2 ? 5 : 2;
+    return PPW == 1 ? 4 : ACC ? 2 : 5;
 }
-template <int PPW>
-__global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
+template <int PPW, int ACC>
+__global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
                                                   const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
                                                   int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
                                                   float* __restrict__ next_xy, float* __restrict__ back_xy,
@@ -628,11 +799,14 @@ __global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel
     constexpr int G = 64 / PPW;
     __shared__ uint32_t wins[KLT_WPB * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
     __shared__ v4u units[KLT_WPB][3 * PPW * 64];                  // per-lane window values
+    // fp32-order window sums: one region per point group
+    __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC ? ACC_FLOATS : 4];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp = lane / G, gl = lane & (G - 1);
     uint32_t* win = wins[wv * PPW + grp];
     v4u* ust = &units[wv][lane];
+    float* acc = accs[ACC ? wv * PPW + grp : 0];
     const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair (launch capacity)
     const int n_waves = a.n_pairs * wpp;
     const int nb = (n_waves + KLT_WPB - 1) / KLT_WPB;
@@ -657,7 +831,8 @@ __global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel
     float nx = init_xy[2 * gp], ny = init_xy[2 * gp + 1];
     int st = 1;
     float e = 0.f;
-    lk_group<PPW>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, gl, win, ust);
+    acc_clear<ACC, G>(acc, gl);
+    lk_group<PPW, ACC>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, gl, win, ust, acc);
     if (a.mode == 0) {
         if (writer) {
             next_xy[2 * gp] = nx;
@@ -673,7 +848,7 @@ __global__ void __launch_bounds__(64 * KLT_WPB, klt_occupancy<PPW>()) klt_kernel
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
     cfg.want_err = 0;  // the backward error is not reported
-    lk_group<PPW>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, gl, win, ust);
+    lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, gl, win, ust, acc);
     if (writer) {
         const double B = a.border;
         const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
@@ -726,27 +901,31 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 // ones (one frame of a sequence: 150 points) take 1, which halves the work of
 // the slowest wave (41 vs 54 us per frame), built for 4 waves per SIMD (no
 // spills; at most 4 waves per SIMD below the threshold: 36.8 -> 35.8 us per
-// sequence frame, 50.3 -> 49.0 us per pair, r02 v18).  GVX_KLT_PPW (1, 2 or 4)
-// forces it.
-static int klt_ppw(int64_t total_points) {
-    static const int forced = [] {
-        const char* e = getenv("GVX_KLT_PPW");
-        const int p = e ? atoi(e) : 0;
-        return (p == 1 || p == 2 || p == 4) ? p : 0;
-    }();
-    if (forced) return forced;
-    return total_points <= 4096 ? 1 : 2;
-}
+// sequence frame, 50.3 -> 49.0 us per pair, r02 v18).
+static int klt_ppw(int64_t total_points) { return total_points <= 4096 ? 1 : 2; }
 
-template <int PPW>
+template <int PPW, int ACC>
 static void launch_klt_ppw(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
                            const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
                            const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
                            float* err) {
     const int n_waves = a.n_pairs * ((a.n_pts + PPW - 1) / PPW);
     dim3 grid((unsigned)(N_XCD * xcd_per((n_waves + KLT_WPB - 1) / KLT_WPB)));
-    hipLaunchKernelGGL(klt_kernel<PPW>, grid, dim3(64 * KLT_WPB), 0, c->stream, a, lay, pyr_prev, pyr_next, prev_pair_stride,
-                       next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
+    hipLaunchKernelGGL((klt_kernel<PPW, ACC>), grid, dim3(64 * KLT_WPB), 0, c->stream, a, lay, pyr_prev, pyr_next,
+                       prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
+}
+
+template <int ACC>
+static void launch_klt_acc(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                           const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                           const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                           float* err) {
+    if (klt_ppw((int64_t)a.n_pairs * a.n_pts) == 1)
+        launch_klt_ppw<1, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                               next_xy, back_xy, flags, err);
+    else
+        launch_klt_ppw<2, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                               next_xy, back_xy, flags, err);
 }
 
 hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
@@ -756,18 +935,21 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
     const int64_t total = (int64_t)a.n_pairs * a.n_pts;
     if (total <= 0) return hipSuccess;
     if (total > (int64_t)1 << 30) return hipErrorInvalidValue;  // wave indices are int32
-    switch (klt_ppw(total)) {
-        case 1:
-            launch_klt_ppw<1>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+    switch (a.accum) {
+        case GVX_LK_ACCUM_EXACT:
+            launch_klt_acc<0>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
                               back_xy, flags, err);
             break;
-        case 4:
-            launch_klt_ppw<4>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+        case GVX_LK_ACCUM_F32_SCALAR:
+            launch_klt_acc<1>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+            break;
+        case GVX_LK_ACCUM_F32_SIMD4:
+            launch_klt_acc<2>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
                               back_xy, flags, err);
             break;
         default:
-            launch_klt_ppw<2>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
-                              back_xy, flags, err);
+            return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

@@ -31,13 +31,18 @@ class GvxError(RuntimeError):
     pass
 
 
+# gvx_klt_params.accum (include/gvx.h GVX_LK_ACCUM_*): LK's window-sum order
+LK_ACCUM_EXACT, LK_ACCUM_F32_SCALAR, LK_ACCUM_F32_SIMD4 = 0, 1, 2
+
+
 class KltParams(C.Structure):
     _fields_ = [("win", C.c_int32), ("max_level", C.c_int32), ("max_iter", C.c_int32),
-                ("eps", C.c_double), ("use_initial_flow", C.c_int32), ("min_eig", C.c_float)]
+                ("eps", C.c_double), ("use_initial_flow", C.c_int32), ("min_eig", C.c_float),
+                ("accum", C.c_int32)]
 
     @classmethod
     def default(cls, **kw) -> "KltParams":
-        p = cls(21, 3, 30, 0.01, 1, 1e-4)
+        p = cls(21, 3, 30, 0.01, 1, 1e-4, LK_ACCUM_EXACT)
         for k, v in kw.items():
             setattr(p, k, v)
         return p

@@ -100,7 +100,22 @@ typedef struct {
     double eps;               /* TermCriteria EPS (squared internally) */
     int32_t use_initial_flow; /* OPTFLOW_USE_INITIAL_FLOW */
     float min_eig;            /* minEigThreshold */
+    int32_t accum;            /* GVX_LK_ACCUM_*: order of the 21x21 window sums */
 } gvx_klt_params;
+/* Window-sum order of LK's structure tensor A and mismatch vector b
+   (LKTrackerInvoker::operator()):
+   EXACT      exact integer sums rounded once to fp32 (default; machine
+              independent, the restatement's documented order);
+   F32_SCALAR OpenCV 4.x's scalar loop: one fp32 accumulator per sum, each
+              int32 product converted to float and added in row-major order
+              (non-SIMD builds);
+   F32_SIMD4  OpenCV 4.x's CV_SIMD128 path (x86 builds): pixels 0..15 of each
+              row in 4-lane fp32 accumulators (lane x mod 4), pixels 16..20 in
+              the scalar accumulator, the lanes reduced and added last.
+   All three are bit-exact against oracle/klt.c's orc_set_lk_accum modes. */
+#define GVX_LK_ACCUM_EXACT 0
+#define GVX_LK_ACCUM_F32_SCALAR 1
+#define GVX_LK_ACCUM_F32_SIMD4 2
 void gvx_klt_params_default(gvx_klt_params* p);
 
 /* Upload one gray u8 frame (Frame::image() after CLAHE, tracking/frame.h:62-64)

@@ -4,8 +4,10 @@ DESIGN.md section 2.)  The restatement and the GPU sum the 21x21 window products
 exactly (int64); OpenCV 4.x sums them in fp32, in its scalar-loop order or in
 its 4-lane CV_SIMD128 order.  This runs the oracle's klt_fb (fwd + bwd LK + FB +
 border) in all three orders on the configs[1] and configs[2] synthetic inputs
-and reports status / keep flips and the max |dnext| over points whose status
-and keep agree.  CPU only.
+and reports status / keep flips, the max |dnext| over points whose status
+and keep agree and how many of them move by more than the north_star's 1e-4 px
+-- each fp32 order against the exact one, and the two fp32 orders (two OpenCV
+builds) against each other.  CPU only.
 
     python tools/accum_flips.py [--pairs1 64] [--pairs2 8] [--json out.json]
 """
@@ -23,6 +25,9 @@ import oracle as orc  # noqa: E402
 from gvx import synth  # noqa: E402
 
 
+TOL_PX = 1e-4
+
+
 def compare(w, h, n, level, pairs, seed0, threads):
     p = orc.KltParams.default(max_level=level)
     res = {}
@@ -34,11 +39,13 @@ def compare(w, h, n, level, pairs, seed0, threads):
         for m in runs:
             with orc.lk_accum(m):
                 runs[m].append(orc.klt_fb(I, J, P, Q, params=p, nthreads=threads))
-    for m, name in ((orc.ACC_F32, "f32_scalar"), (orc.ACC_F32X4, "f32_simd4")):
+    pairs_cmp = ((orc.ACC_EXACT, orc.ACC_F32, "f32_scalar"), (orc.ACC_EXACT, orc.ACC_F32X4, "f32_simd4"),
+                 (orc.ACC_F32, orc.ACC_F32X4, "f32_scalar_vs_f32_simd4"))
+    for m0, m, name in pairs_cmp:
         st_flips = keep_flips = 0
         dmax_f = dmax_b = 0.0
-        n_diff = 0
-        for e, f in zip(runs[orc.ACC_EXACT], runs[m]):
+        n_diff = n_over_f = n_over_b = 0
+        for e, f in zip(runs[m0], runs[m]):
             st_flips += int(np.sum(e["st_f"] != f["st_f"])) + int(np.sum(e["st_b"] != f["st_b"]))
             keep_flips += int(np.sum(e["keep"] != f["keep"]))
             same = (e["st_f"] == f["st_f"]) & (e["st_b"] == f["st_b"]) & (e["keep"] == f["keep"]) & (e["st_f"] > 0)
@@ -46,10 +53,14 @@ def compare(w, h, n, level, pairs, seed0, threads):
             sb = same & (e["st_b"] > 0)
             db = np.abs(e["back"][sb] - f["back"][sb]).max(initial=0.0)
             n_diff += int(np.sum(np.any(e["next"][same] != f["next"][same], axis=1)))
+            # points past the north_star's 1e-4 px (per coordinate)
+            n_over_f += int(np.sum(np.abs(e["next"][same] - f["next"][same]).max(axis=1, initial=0.0) > TOL_PX))
+            n_over_b += int(np.sum(np.abs(e["back"][sb] - f["back"][sb]).max(axis=1, initial=0.0) > TOL_PX))
             dmax_f, dmax_b = max(dmax_f, float(df)), max(dmax_b, float(db))
         res[name] = {"status_flips": st_flips, "keep_flips": keep_flips, "points": tot,
                      "max_abs_dnext_px": dmax_f, "max_abs_dback_px": dmax_b,
-                     "points_with_any_dnext": n_diff}
+                     "points_with_any_dnext": n_diff, "points_dnext_over_1e-4px": n_over_f,
+                     "points_dback_over_1e-4px": n_over_b}
     return res
 
 
