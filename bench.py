@@ -153,6 +153,9 @@ def host_threads():
     return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
+ACCUM_MODES = {"exact": 0, "f32_scalar": 1, "f32_simd4": 2}  # include/gvx.h GVX_LK_ACCUM_*
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,6 +187,9 @@ def main():
                     help="configs[4]: one graph per frame, frame t+1's CLAHE + pyramid after frame t's tracking "
                          "(default: beside it, a preprocessing graph on a side stream)")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
+    ap.add_argument("--accum", default="exact", choices=tuple(ACCUM_MODES),
+                    help="LK window-sum order (gvx_klt_params.accum): exact integer sums (default), or "
+                         "OpenCV 4.x's fp32 scalar-loop / CV_SIMD128 orders")
     args = ap.parse_args()
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
@@ -233,13 +239,13 @@ def main():
 
     ctx = gvx.Context(local)
     stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
-    params = gvx.KltParams.default(max_level=L)
+    params = gvx.KltParams.default(max_level=L, accum=ACCUM_MODES[args.accum])
 
-    def step():
+    def step(p=params):
         # initial flow (the predictions) read from dQ, tracked points out to dN
         ctx.klt_fb_batch_init_dev(Pn, W, H, dI.data_ptr(), dJ.data_ptr(), N, dP.data_ptr(), dQ.data_ptr(),
                                   dN.data_ptr(), dB.data_ptr(), dF.data_ptr(), dK.data_ptr(), dNK.data_ptr(),
-                                  params=params)
+                                  params=p)
 
     gathered = [torch.empty_like(dNK) for _ in range(world)] if world > 1 else None
 
@@ -269,6 +275,9 @@ def main():
     fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact")}
     ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
+    # LK device time of each window-sum order on the same batch (after the timed region)
+    accum_cost = accum_leg(ctx, step, gvx, L, steps=max(5, args.steps // 4)) if world == 1 and not args.no_pre \
+        else None
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if not args.no_pre else None
     single = single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps=max(200, 5 * args.steps)) \
         if world == 1 and not args.no_pre else None
@@ -348,6 +357,8 @@ def main():
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
+            "lk_accum": args.accum,
+            "lk_accum_cost": accum_cost,
             "preprocess": pre,
             "single_pair": single,
             "host_buffers": pcie,
@@ -357,6 +368,28 @@ def main():
     if dist:
         dist.destroy_process_group()
     ctx.close()
+
+
+def accum_leg(ctx, step, gvx, L, steps):
+    """LK device ms per step in each window-sum order (gvx_klt_params.accum):
+    the exact integer order and OpenCV 4.x's fp32 scalar / CV_SIMD128 orders,
+    which the device reproduces bit-exactly (tests/test_klt_accum_gpu.py)."""
+    out = {}
+    for name, mode in ACCUM_MODES.items():
+        p = gvx.KltParams.default(max_level=L, accum=mode)
+        for _ in range(3):
+            step(p)
+        ctx.sync()
+        ctx.profile_reset()
+        ctx.profile(True)
+        for _ in range(steps):
+            step(p)
+        ctx.sync()
+        out[name] = round(ctx.profile_read("klt")[0] / steps, 4)
+        ctx.profile(False)
+    out["unit"] = "LK device ms per step"
+    out["steps"] = steps
+    return out
 
 
 def single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps):

@@ -40,7 +40,10 @@ static void sync_all(gvx_ctx* c) {
 void* scratch(gvx_ctx* c, const std::string& name, size_t bytes) {
     DevBuf& b = c->dev[name];
     if (b.bytes >= bytes && b.p) return b.p;
-    if (c->capturing) return nullptr;  // growing would synchronise the captured stream
+    if (c->capturing) {  // growing would synchronise the captured stream
+        c->capture_failed = true;
+        return nullptr;
+    }
     ++c->mem_gen;
     if (b.p) {
         sync_all(c);
@@ -60,7 +63,10 @@ void* scratch(gvx_ctx* c, const std::string& name, size_t bytes) {
 void* pinned(gvx_ctx* c, const std::string& name, size_t bytes) {
     DevBuf& b = c->pinned[name];
     if (b.bytes >= bytes && b.p) return b.p;
-    if (c->capturing) return nullptr;
+    if (c->capturing) {
+        c->capture_failed = true;
+        return nullptr;
+    }
     ++c->mem_gen;
     if (b.p) {
         sync_all(c);
@@ -266,6 +272,7 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
     if (!f.pyr || f.lay.bytes < lay.bytes) {
         if (c->capturing) {
             if (!f.pyr) c->frames.erase(id);
+            c->capture_failed = true;
             return set_err(c, GVX_ERR_INVALID, "frame %llu needs a (re)allocation during a graph capture",
                            (unsigned long long)id);
         }
@@ -642,6 +649,7 @@ gvx_status frame_slot(gvx_ctx* c, uint64_t id, int32_t w, int32_t h, const gvx_k
     if (!f.pyr || f.lay.bytes < lay.bytes) {
         if (c->capturing) {
             if (!f.pyr) c->frames.erase(id);
+            c->capture_failed = true;
             return set_err(c, GVX_ERR_INVALID, "frame %llu needs a (re)allocation during a graph capture",
                            (unsigned long long)id);
         }

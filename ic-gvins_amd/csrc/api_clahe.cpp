@@ -30,7 +30,7 @@ static gvx_status check_clahe(gvx_ctx* c, int w, int h, const gvx_clahe_params* 
 static gvx_status clahe_enqueue(gvx_ctx* c, int n, int w, int h, const uint8_t* src, int64_t img_stride,
                                 int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride,
                                 const gvx_clahe_params* cp, double* d_mean, const int32_t* src_index = nullptr,
-                                int ring = 0) {
+                                int n_src = 0, int ring = 0) {
     const ClaheGeom g = clahe_geometry(w, h, cp->clip_limit, cp->tiles_x, cp->tiles_y);
     uint8_t* lut = (uint8_t*)scratch(c, "clahe_lut", (size_t)n * g.tiles_x * g.tiles_y * 256);
     uint32_t* hist = d_mean ? (uint32_t*)scratch(c, "clahe_hist", (size_t)n * 256 * sizeof(uint32_t)) : nullptr;
@@ -38,7 +38,7 @@ static gvx_status clahe_enqueue(gvx_ctx* c, int n, int w, int h, const uint8_t* 
     hipEvent_t ev{};
     prof_begin(c, "clahe", &ev);
     hipError_t e = launch_clahe(c, n, g, src, img_stride, stride, dst, dst_img_stride, dst_stride, lut, hist, d_mean,
-                                src_index, ring);
+                                src_index, n_src, ring);
     prof_end(c, "clahe", ev);
     return hip_err(c, e, "CLAHE kernels");
 }
@@ -91,7 +91,7 @@ gvx_status gvx_clahe(gvx_ctx* c, int32_t w, int32_t h, const uint8_t* src, int32
 // levels >= 1 from that slot: no level-0 copy pass.  src_index: the frame is
 // d_gray + (*src_index) * img_stride, picked on the device.
 static gvx_status preprocess_into_slot(gvx_ctx* c, uint64_t id, const uint8_t* d_gray, int64_t img_stride,
-                                       const int32_t* src_index, int32_t w, int32_t h, int32_t stride,
+                                       const int32_t* src_index, int32_t n_src, int32_t w, int32_t h, int32_t stride,
                                        const gvx_clahe_params* cp, const gvx_klt_params* p, double* d_hist_mean) {
     Frame* f = nullptr;
     gvx_status s = frame_slot(c, id, w, h, p, &f);
@@ -99,7 +99,7 @@ static gvx_status preprocess_into_slot(gvx_ctx* c, uint64_t id, const uint8_t* d
     const PyrLayout& lay = f->lay;
     uint8_t* slot0 = f->pyr + lay.off[0] + (int64_t)PAD * lay.pitch[0] + PAD;
     s = clahe_enqueue(c, 1, w, h, d_gray, img_stride, stride, slot0, lay.bytes, lay.pitch[0], cp, d_hist_mean,
-                      src_index, 1);
+                      src_index, n_src, 1);
     if (s) return s;
     hipEvent_t ev{};
     prof_begin(c, "pyramid", &ev);
@@ -110,17 +110,19 @@ static gvx_status preprocess_into_slot(gvx_ctx* c, uint64_t id, const uint8_t* d
 static bool ring_in_apply(int w, int h) { return w >= 2 * PAD + 2 && h >= 2 * PAD + 2; }
 
 gvx_status gvx_frame_preprocess_indexed_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_frames,
-                                            int64_t frame_stride, const int32_t* d_index, int32_t w, int32_t h,
+                                            int64_t frame_stride, const int32_t* d_index, int32_t n_frames,
+                                            int32_t w, int32_t h,
                                             int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
                                             double* d_hist_mean) {
     if (!c) return GVX_ERR_INVALID;
-    if (!d_frames || !d_index || w <= 0 || h <= 0 || stride < w || frame_stride < (int64_t)stride * (h - 1) + w)
+    if (!d_frames || !d_index || n_frames <= 0 || w <= 0 || h <= 0 || stride < w ||
+        frame_stride < (int64_t)stride * (h - 1) + w)
         return set_err(c, GVX_ERR_INVALID, "bad frame sequence");
     if (!ring_in_apply(w, h)) return set_err(c, GVX_ERR_INVALID, "indexed preprocessing needs frames >= 66 x 66");
     gvx_status s = check_clahe(c, w, h, cp);
     if (s) return s;
     hipSetDevice(c->device);
-    return preprocess_into_slot(c, id, d_frames, frame_stride, d_index, w, h, stride, cp, p, d_hist_mean);
+    return preprocess_into_slot(c, id, d_frames, frame_stride, d_index, n_frames, w, h, stride, cp, p, d_hist_mean);
 }
 
 gvx_status gvx_frame_preprocess_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_gray, int32_t w, int32_t h,
@@ -132,7 +134,8 @@ gvx_status gvx_frame_preprocess_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_gr
     if (s) return s;
     hipSetDevice(c->device);
     if (!d_clahe_out && ring_in_apply(w, h))
-        return preprocess_into_slot(c, id, d_gray, (int64_t)h * stride, nullptr, w, h, stride, cp, p, d_hist_mean);
+        return preprocess_into_slot(c, id, d_gray, (int64_t)h * stride, nullptr, 0, w, h, stride, cp, p,
+                                    d_hist_mean);
     const size_t nb = (size_t)w * h;
     uint8_t* eq = d_clahe_out ? d_clahe_out : (uint8_t*)scratch(c, "preproc_eq", nb);
     if (!eq) return set_err(c, GVX_ERR_OOM, "preprocess scratch");

@@ -28,9 +28,26 @@ gvx_status gvx_capture_begin(gvx_ctx* c) {
     gvx_status s = hip_err(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
     if (s == GVX_OK) {
         c->capturing = true;
+        c->capture_failed = false;
         c->capture_gen = c->mem_gen;
     }
     return s;
+}
+
+gvx_status gvx_capture_abort(gvx_ctx* c) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!c->capturing) return GVX_OK;
+    hipSetDevice(c->device);
+    // close an open branch first: the capture cannot end with the side stream unjoined
+    if (c->in_branch) gvx_branch_end(c);
+    if (c->branch_open) gvx_branch_join(c);
+    c->capturing = false;
+    c->capture_failed = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (g) hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return e == hipSuccess ? GVX_OK : hip_err(c, e, "hipStreamEndCapture (abort)");
 }
 
 gvx_status gvx_capture_end(gvx_ctx* c, gvx_graph** out) {
@@ -46,6 +63,12 @@ gvx_status gvx_capture_end(gvx_ctx* c, gvx_graph** out) {
     if (c->mem_gen != c->capture_gen) {
         hipGraphDestroy(g);
         return set_err(c, GVX_ERR_INVALID, "device buffers moved during the capture");
+    }
+    if (c->capture_failed) {
+        c->capture_failed = false;
+        hipGraphDestroy(g);
+        return set_err(c, GVX_ERR_INVALID, "a call inside the capture needed a device allocation; run it once "
+                                           "uncaptured first");
     }
     hipGraphExec_t x = nullptr;
     e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);

@@ -85,10 +85,18 @@ static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, in
     void* sb = scratch(c, "trk_static", sc.bytes());
     if (!sb) return set_err(c, GVX_ERR_OOM, "track constants");
     sc.bind(sb);
-    const uint64_t key = ((uint64_t)W << 40) ^ ((uint64_t)H << 24) ^ ((uint64_t)dp->max_features << 8) ^
-                         (uint64_t)std::lround(dp->block_size) ^ (c->mem_gen << 52);
-    if (c->track_static_key != key) {
-        if (c->capturing) return set_err(c, GVX_ERR_INVALID, "detection constants not uploaded before the capture");
+    gvx_ctx::TrackStatic key;
+    key.buf = sb;
+    key.bytes = sc.bytes();
+    key.w = W;
+    key.h = H;
+    key.max_features = dp->max_features;
+    key.block_size = std::lround(dp->block_size);
+    if (!(c->track_static == key)) {
+        if (c->capturing) {
+            c->capture_failed = true;
+            return set_err(c, GVX_ERR_INVALID, "detection constants not uploaded before the capture");
+        }
         std::vector<int4> r(bcnt);
         for (int k = 0; k < bcnt; ++k) {
             const int bc = k % bcols, br = k / bcols;
@@ -128,7 +136,7 @@ static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, in
         if (e == hipSuccess) e = hipMemcpyAsync(gm, g, sizeof g, hipMemcpyHostToDevice, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // pageable sources
         if (e != hipSuccess) return hip_err(c, e, "track constants upload");
-        c->track_static_key = key;
+        c->track_static = key;
     }
     hipEvent_t ev{};
     hipError_t e = hipSuccess;
@@ -263,12 +271,13 @@ extern "C" gvx_status gvx_track_frame_record_dev(gvx_ctx* c, uint64_t prev_id, u
 }
 
 extern "C" gvx_status gvx_copy_indexed_dev(gvx_ctx* c, void* d_dst, const void* d_src_base, size_t bytes,
-                                           const int32_t* d_index) {
+                                           const int32_t* d_index, int32_t n_src) {
     if (!c) return GVX_ERR_INVALID;
     if (bytes == 0) return GVX_OK;
     if (!d_dst || !d_src_base || !d_index) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    if (n_src <= 0) return set_err(c, GVX_ERR_INVALID, "n_src must be positive");
     hipSetDevice(c->device);
-    return hip_err(c, launch_copy_indexed(c, d_dst, d_src_base, bytes, d_index), "indexed copy kernel");
+    return hip_err(c, launch_copy_indexed(c, d_dst, d_src_base, bytes, d_index, n_src), "indexed copy kernel");
 }
 
 extern "C" gvx_status gvx_track_record_dev(gvx_ctx* c, const float* d_pts, const int32_t* d_n, int32_t capacity,

@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
                                                           int stride, ClaheGeom g, int vec8, int tpw,
                                                           uint8_t* __restrict__ lut,
                                                           uint32_t* __restrict__ hist_img,
-                                                          const int32_t* __restrict__ src_index) {
+                                                          const int32_t* __restrict__ src_index, int n_src) {
     extern __shared__ uint32_t hs[];  // tpw histograms of 256 bins, HROW dwords apart
     const int ngrp = (g.tiles_x + tpw - 1) / tpw;
     const int img = blockIdx.x / (g.tiles_y * ngrp);
@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
     for (int i = t; i < nbins; i += LUT_THREADS) hs[i] = 0;
     __syncthreads();
     // src_index (one image): the source image is picked on the device
-    const uint8_t* s = src + (src_index ? (int64_t)*src_index : (int64_t)img) * img_stride;
+    const uint8_t* s = src + (src_index ? (int64_t)min(max(*src_index, 0), n_src - 1) : (int64_t)img) * img_stride;
     const int y0 = ty * g.th;
     const int rows_in = max(0, min(y0 + g.th, g.h) - y0);
     const float inv_tw = 1.0f / g.tw;
@@ -220,7 +220,7 @@ __device__ __forceinline__ int first_row(int k, const ClaheGeom& g, float inv_th
 __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t img_stride, int stride,
                                                      uint8_t* dst, int64_t dst_img_stride, int dst_stride,
                                                      ClaheGeom g, const uint8_t* __restrict__ lut, int nsplit,
-                                                     int vec8, const int32_t* __restrict__ src_index, int ring) {
+                                                     int vec8, const int32_t* __restrict__ src_index, int n_src, int ring) {
     extern __shared__ uint32_t tab[];  // (tiles_x + 1) * TROW dwords
     const int nb = g.tiles_y + 1;
     const int img = blockIdx.x / (nb * nsplit);
@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t
         }
     }
     __syncthreads();
-    const uint8_t* s = src + (src_index ? (int64_t)*src_index : (int64_t)img) * img_stride;
+    const uint8_t* s = src + (src_index ? (int64_t)min(max(*src_index, 0), n_src - 1) : (int64_t)img) * img_stride;
     uint8_t* dd = dst + img * dst_img_stride;
     for (int x0 = PPT * threadIdx.x; x0 < g.w; x0 += PPT * blockDim.x) {
         // column terms of CLAHE_Interpolation_Body's constructor, once per thread
@@ -387,7 +387,7 @@ ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles
 
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
-                        uint32_t* hist_img, double* hist_mean, const int32_t* src_index, int ring) {
+                        uint32_t* hist_img, double* hist_mean, const int32_t* src_index, int n_src, int ring) {
     if (n <= 0) return hipSuccess;
     if (hist_img) {
         hipError_t e = hipMemsetAsync(hist_img, 0, (size_t)n * 256 * sizeof(uint32_t), c->stream);
@@ -402,17 +402,12 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const int tpw = (g.tiles_x + ngrp - 1) / ngrp;
     ngrp = (g.tiles_x + tpw - 1) / tpw;
     hipLaunchKernelGGL(lut_kernel, dim3(n * g.tiles_y * ngrp), dim3(LUT_THREADS), (size_t)tpw * HROW * 4, c->stream,
-                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index);
+                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index, n_src);
     // bands of rows sharing one pair of LUT rows, split to fill the chip
     const int nb = g.tiles_y + 1;
-    // workgroups wanted for the apply pass (GVX_CLAHE_APPLY_WG overrides; the
-    // sequence replay's single frames measured 17.5 us at 1,024 against 19.9 at
-    // 128, r02 v16)
-    static const int apply_wg = [] {
-        const char* e = getenv("GVX_CLAHE_APPLY_WG");
-        return e ? atoi(e) : 0;
-    }();
-    const int64_t want_wg = apply_wg > 0 ? apply_wg : 4LL * c->n_cu;
+    // workgroups wanted for the apply pass (the sequence replay's single frames
+    // measured 17.5 us at 1,024 against 19.9 at 128, r02 v16)
+    const int64_t want_wg = 4LL * c->n_cu;
     int nsplit = 1;
     while ((int64_t)n * nb * nsplit < want_wg && nsplit < g.th) nsplit *= 2;
     const int cols = (g.w + PPT - 1) / PPT;
@@ -420,7 +415,7 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const size_t lds = (size_t)(g.tiles_x + 1) * TROW * 4;
     hipLaunchKernelGGL(apply_kernel, dim3(n * nb * nsplit), dim3(threads), lds, c->stream, src, img_stride, stride,
                        dst, dst_img_stride, dst_stride, g, (const uint8_t*)lut, nsplit, (int)(src8 && dst8), src_index,
-                       ring);
+                       n_src, ring);
     if (hist_img && hist_mean)
         hipLaunchKernelGGL(mean_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, (const uint32_t*)hist_img, n,
                            g.w, g.h, hist_mean);

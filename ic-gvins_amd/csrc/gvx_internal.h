@@ -74,8 +74,20 @@ struct gvx_ctx {
     uint64_t mem_gen = 0;
     bool capturing = false;
     uint64_t capture_gen = 0;
-    // gvx_track_frame_dev: key of the detection constants uploaded to "trk_static"
-    uint64_t track_static_key = 0;
+    // a call inside the open capture failed for want of a (re)allocation:
+    // gvx_capture_end refuses the graph
+    bool capture_failed = false;
+    // gvx_track_frame_dev: what the detection constants in "trk_static" were
+    // built for (the buffer itself and the geometry)
+    struct TrackStatic {
+        const void* buf = nullptr;
+        size_t bytes = 0;
+        int64_t w = 0, h = 0, max_features = 0, block_size = 0;
+        bool operator==(const TrackStatic& o) const {
+            return buf == o.buf && bytes == o.bytes && w == o.w && h == o.h && max_features == o.max_features &&
+                   block_size == o.block_size;
+        }
+    } track_static;
     // profiling
     bool prof = false;
     std::map<std::string, gvx::ProfEntry> prof_acc;
@@ -173,11 +185,12 @@ ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles
 // n images; lut: n*tiles*256 bytes scratch; hist_img (nullable): n*256 u32
 // scratch for the histogram check, whose means go to hist_mean (device).
 // src_index (n == 1): the source is src + (*src_index) * img_stride, picked on the
-// device; ring: dst is pixel (0,0) of a padded level (PAD ring written too)
+// device, the index clamped to [0, n_src - 1]; ring: dst is pixel (0,0) of a
+// padded level (PAD ring written too)
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean, const int32_t* src_index = nullptr,
-                        int ring = 0);
+                        int n_src = 0, int ring = 0);
 
 // ---- aux_factors.hip ----
 // residuals of a small factor kind (0: unknown kind); *P block size, *NC constants per factor
@@ -285,7 +298,8 @@ hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d);
 
 // ---- track.hip (gvx_track_frame_dev, gvx_copy_dev) ----
 hipError_t launch_copy(gvx_ctx* c, void* dst, const void* src, size_t bytes);
-hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index);
+hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index,
+                               int n_src);
 hipError_t launch_index_advance(gvx_ctx* c, int32_t* index, int32_t delta);
 hipError_t launch_track_record(gvx_ctx* c, const float* pts, const int32_t* n, int cap, float* tracks,
                                int32_t* counts, int32_t* frame, int max_frames);

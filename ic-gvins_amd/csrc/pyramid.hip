@@ -580,7 +580,7 @@ inline int stream_band(int n_strips, int h1, int n_img, int n_cu) {
 }
 
 template <int NL>
-void launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
+hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
     DownLevels D{};
     for (int k = 0; k < NL; ++k) {
         D.off[k] = lay.off[l0 + 1 + k];
@@ -594,9 +594,13 @@ void launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrLayout&
     const int n_bands = (D.h[0] + band - 1) / band;
     const int n_units = n_strips * n_bands * n_img;
     const int nblk = (n_units + 3) / 4;
+    // the lanes without an output store to their wave's trash line: the kernel
+    // must not run without it (a scratch buffer cannot grow inside a capture)
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
+    if (!trash) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, dst, lay.bytes,
                        D, n_strips, n_bands, n_units, band, trash);
+    return hipSuccess;
 }
 
 
@@ -760,12 +764,10 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         s.w = lay.w[l];
         s.h = lay.h[l];
         s.raw = l == 0 && raw;
-        if (nl == 3)
-            launch_stream<3>(c, s, n_img, lay, l, dst);
-        else if (nl == 2)
-            launch_stream<2>(c, s, n_img, lay, l, dst);
-        else
-            launch_stream<1>(c, s, n_img, lay, l, dst);
+        const hipError_t e = nl == 3   ? launch_stream<3>(c, s, n_img, lay, l, dst)
+                             : nl == 2 ? launch_stream<2>(c, s, n_img, lay, l, dst)
+                                       : launch_stream<1>(c, s, n_img, lay, l, dst);
+        if (e != hipSuccess) return e;
         launch_rings(c, n_img, lay, l + 1, l + nl, dst);
         l += nl;
     }

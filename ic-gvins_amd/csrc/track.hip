@@ -214,8 +214,8 @@ __global__ void __launch_bounds__(256) copy_kernel(uint8_t* __restrict__ dst, co
 // dst <- src_base + (*index) * bytes: a copy whose source is chosen on the device
 __global__ void __launch_bounds__(256) copy_indexed_kernel(uint8_t* __restrict__ dst,
                                                            const uint8_t* __restrict__ src_base, size_t bytes,
-                                                           const int32_t* __restrict__ index) {
-    const uint8_t* src = src_base + (size_t)(*index) * bytes;
+                                                           const int32_t* __restrict__ index, int n_src) {
+    const uint8_t* src = src_base + (size_t)min(max(*index, 0), n_src - 1) * bytes;
     const size_t stride = (size_t)gridDim.x * 256;
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
@@ -256,12 +256,13 @@ hipError_t launch_index_advance(gvx_ctx* c, int32_t* index, int32_t delta) {
     return hipGetLastError();
 }
 
-hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index) {
+hipError_t launch_copy_indexed(gvx_ctx* c, void* dst, const void* src_base, size_t bytes, const int32_t* index,
+                               int n_src) {
     const size_t units = (bytes + 15) / 16;
     const unsigned blocks = (unsigned)std::min<size_t>((units + 255) / 256, 4096);
     copy_indexed_kernel<<<blocks ? blocks : 1, 256, 0, c->stream>>>(static_cast<uint8_t*>(dst),
                                                                     static_cast<const uint8_t*>(src_base), bytes,
-                                                                    index);
+                                                                    index, n_src);
     return hipGetLastError();
 }
 

@@ -164,6 +164,7 @@ def _declare(L):
         "gvx_preint_integrate": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
         "gvx_preint_integrate_dev": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
         "gvx_earth_iewn": (None, [P, P, P]),
+        "gvx_preint_sqrt_info": (i32, [P, i32, P]),
         "gvx_preint_factor_eval": (i32, [P, i32, P, P, i32, P, P, i32, P, P, P]),
         "gvx_preint_factor_eval_dev": (i32, [P, i32, P, P, P, P, P, P, P]),
         "gvx_reproj_eval": (i32, [P, i32, P, P, i32, P, P, P]),
@@ -195,7 +196,7 @@ def _declare(L):
                                        P, P]),
         "gvx_frame_preprocess_dev": (i32, [P, u64, P, i32, i32, i32, C.POINTER(ClaheParams),
                                            C.POINTER(KltParams), P, P]),
-        "gvx_frame_preprocess_indexed_dev": (i32, [P, u64, P, i64, P, i32, i32, i32, C.POINTER(ClaheParams),
+        "gvx_frame_preprocess_indexed_dev": (i32, [P, u64, P, i64, P, i32, i32, i32, i32, C.POINTER(ClaheParams),
                                                    C.POINTER(KltParams), P]),
         "gvx_ins_propagate": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
         "gvx_ins_propagate_dev": (i32, [P, C.POINTER(InsConfig), i32, P, P, P, P]),
@@ -208,7 +209,7 @@ def _declare(L):
         "gvx_marginalize_dev": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
         "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
         "gvx_find_fundamental_ransac": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
-        "gvx_copy_indexed_dev": (i32, [P, P, P, C.c_size_t, P]),
+        "gvx_copy_indexed_dev": (i32, [P, P, P, C.c_size_t, P, i32]),
         "gvx_track_record_dev": (i32, [P, P, P, i32, P, P, P, i32]),
         "gvx_track_frame_dev": (i32, [P, u64, u64, i32, P, P, P, P, i32, i32, i32, f64, f64, C.POINTER(KltParams),
                                       C.POINTER(DetectParams), P, P, P]),
@@ -217,6 +218,7 @@ def _declare(L):
         "gvx_find_fundamental_ransac_dev": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
         "gvx_capture_begin": (i32, [P]),
         "gvx_capture_end": (i32, [P, C.POINTER(P)]),
+        "gvx_capture_abort": (i32, [P]),
         "gvx_graph_launch": (i32, [P, P]),
         "gvx_graph_destroy": (None, [P]),
         "gvx_copy_dev": (i32, [P, P, P, C.c_size_t]),
@@ -378,11 +380,13 @@ class Context:
                                                      C.byref(params or KltParams.default()), d_hist_mean,
                                                      d_clahe_out), "frame_preprocess_dev")
 
-    def frame_preprocess_indexed_dev(self, fid: int, d_frames: int, frame_stride: int, d_index: int, w: int,
-                                     h: int, stride: Optional[int] = None, clahe: Optional[ClaheParams] = None,
+    def frame_preprocess_indexed_dev(self, fid: int, d_frames: int, frame_stride: int, d_index: int, n_frames: int,
+                                     w: int, h: int, stride: Optional[int] = None, clahe: Optional[ClaheParams] = None,
                                      params: Optional[KltParams] = None, d_hist_mean=None):
-        """Preprocess frame *d_index of an HBM-resident sequence (index read on the device)."""
-        self._check(self._L.gvx_frame_preprocess_indexed_dev(self._h, fid, d_frames, frame_stride, d_index, w, h,
+        """Preprocess frame *d_index (clamped to [0, n_frames - 1]) of an HBM-resident
+        sequence (index read on the device)."""
+        self._check(self._L.gvx_frame_preprocess_indexed_dev(self._h, fid, d_frames, frame_stride, d_index,
+                                                             n_frames, w, h,
                                                              stride or w, C.byref(clahe or ClaheParams.default()),
                                                              C.byref(params or KltParams.default()), d_hist_mean),
                     "frame_preprocess_indexed_dev")
@@ -413,8 +417,9 @@ class Context:
                                                        C.byref(kp), C.byref(dp), d_tracks, d_counts, d_frame_index,
                                                        max_frames), "gvx_track_frame_record_dev")
 
-    def copy_indexed_dev(self, d_dst: int, d_src_base: int, nbytes: int, d_index: int):
-        self._check(self._L.gvx_copy_indexed_dev(self._h, d_dst, d_src_base, nbytes, d_index), "gvx_copy_indexed_dev")
+    def copy_indexed_dev(self, d_dst: int, d_src_base: int, nbytes: int, d_index: int, n_src: int):
+        self._check(self._L.gvx_copy_indexed_dev(self._h, d_dst, d_src_base, nbytes, d_index, n_src),
+                    "gvx_copy_indexed_dev")
 
     def track_record_dev(self, d_pts: int, d_n: int, capacity: int, d_tracks: int, d_counts: int,
                          d_frame_index: int, max_frames: int):
@@ -612,6 +617,13 @@ class Context:
         self._check(self._L.gvx_preint_integrate(self._h, variant, C.byref(p), n, _ptr(imu), _ptr(off), _ptr(st),
                                                  _ptr(iw), _ptr(out), _ptr(pn)), "gvx_preint_integrate")
         return out, pn[:int(off[-1]) - n], pn_off
+
+    def preint_sqrt_info(self, pre):
+        """Fill pre[i].sqrt_info = LLT(covariance^-1).matrixL()^T (gvx_preint_sqrt_info)
+        for preintegration results formed elsewhere; returns the updated copy."""
+        out = np.ascontiguousarray(pre, dtype=PREINT_DTYPE).copy()
+        self._check(self._L.gvx_preint_sqrt_info(self._h, out.shape[0], _ptr(out)), "gvx_preint_sqrt_info")
+        return out
 
     def preint_factor_eval(self, pre, pn, pn_off, params, offs, jacobians=True):
         """PreintegrationFactor::Evaluate batch -> (residuals [n,15], jacobians [n,480] or None)."""
@@ -819,6 +831,21 @@ class Context:
         g = C.c_void_p()
         self._check(self._L.gvx_capture_end(self._h, C.byref(g)), "gvx_capture_end")
         return Graph(self, g)
+
+    def capture_abort(self):
+        """Discard an open capture (gvx_capture_abort)."""
+        self._check(self._L.gvx_capture_abort(self._h), "gvx_capture_abort")
+
+    def capture(self, fn, *args) -> "Graph":
+        """Capture what fn(*args) enqueues into a graph; if fn raises, the capture
+        is aborted (the context stays usable) and the error propagates."""
+        self.capture_begin()
+        try:
+            fn(*args)
+        except BaseException:
+            self.capture_abort()
+            raise
+        return self.capture_end()
 
     def graph_launch(self, g: "Graph"):
         self._check(self._L.gvx_graph_launch(self._h, g.handle), "gvx_graph_launch")

@@ -104,14 +104,12 @@ class DeviceSequenceTracker:
         # pipeline (HBM-resident sequences only): frame t+1's preprocessing
         # (CLAHE + pyramid into a third frame slot) runs as a side branch beside
         # frame t's tracking (gvx_branch_begin / _end / _join), reading the frame
-        # at its own device counter.  Frame t+1 is read at t = F - 1 too, so the
-        # sequence gets one spare frame.
+        # at its own device counter.  At t = F - 1 that counter is past the last
+        # frame: the device clamps it (the spare preprocessing is never tracked).
         self.pipeline = bool(pipeline) and frames is not None
-        self.src = frames
         if self.pipeline:
             if len(self.ids) < 3:
                 self.ids = tuple(self.ids) + (max(self.ids) + 1,)
-            self.src = torch.cat([frames, frames[-1:]])
             self.pindex = torch.ones(1, dtype=torch.int32, device=dev)
         if frames is not None:
             F = frames.shape[0]
@@ -122,8 +120,9 @@ class DeviceSequenceTracker:
     def _pre_next(self, t: int):
         # frame *pindex (= t + 1) into the slot of frame t+1; the branch advances its
         # own counter, so it never reads the index the tracking graph's record advances
-        self.ctx.frame_preprocess_indexed_dev(self.ids[(t + 1) % 3], self.src.data_ptr(), self.w * self.h,
-                                              self.pindex.data_ptr(), self.w, self.h, params=self.kp)
+        self.ctx.frame_preprocess_indexed_dev(self.ids[(t + 1) % 3], self.frames.data_ptr(), self.w * self.h,
+                                              self.pindex.data_ptr(), self.frames.shape[0], self.w, self.h,
+                                              params=self.kp)
         self.ctx.index_advance_dev(self.pindex.data_ptr(), 1)
 
     def _track_cur(self, t: int):
@@ -135,9 +134,7 @@ class DeviceSequenceTracker:
     def _graph(self, key, fn, t: int):
         g = self.graphs.get(key)
         if g is None:
-            self.ctx.capture_begin()
-            fn(t)
-            g = self.graphs[key] = self.ctx.capture_end()
+            g = self.graphs[key] = self.ctx.capture(fn, t)
         return g
 
     def _enqueue_pipelined(self, t: int, graphs: bool):
@@ -150,8 +147,9 @@ class DeviceSequenceTracker:
         measured serialised (r02 v21)."""
         ctx = self.ctx
         if t == 0:
-            ctx.frame_preprocess_indexed_dev(self.ids[0], self.src.data_ptr(), self.w * self.h,
-                                             self.index.data_ptr(), self.w, self.h, params=self.kp)
+            ctx.frame_preprocess_indexed_dev(self.ids[0], self.frames.data_ptr(), self.w * self.h,
+                                             self.index.data_ptr(), self.frames.shape[0], self.w, self.h,
+                                             params=self.kp)
         ctx.branch_join()
         if graphs:
             ga = self._graph(("pre", t % 3), self._pre_next, t)
@@ -170,7 +168,7 @@ class DeviceSequenceTracker:
             # frame *index of the HBM-resident sequence, equalised straight into the
             # frame cache (no staging copy)
             ctx.frame_preprocess_indexed_dev(cur, self.frames.data_ptr(), self.w * self.h, self.index.data_ptr(),
-                                             self.w, self.h, params=self.kp)
+                                             self.frames.shape[0], self.w, self.h, params=self.kp)
         else:
             ctx.frame_preprocess_dev(cur, d_frame, self.w, self.h, None, params=self.kp)
         if self.frames is not None:
@@ -188,6 +186,10 @@ class DeviceSequenceTracker:
         """Enqueue one frame (nothing waits); the tracks are
         self.pts[:self.count] once the stream has run it."""
         t = self.t
+        if self.frames is not None and t >= self.frames.shape[0]:
+            raise IndexError(f"step {t}: the resident sequence has {self.frames.shape[0]} frames")
+        if self.frames is None and d_frame is None:
+            raise ValueError("step() needs the frame's device pointer when no sequence is resident")
         if not self.graph or t < 3:
             self._enqueue(d_frame, t)  # the first frames also size every buffer
         elif self.pipeline:
@@ -198,9 +200,8 @@ class DeviceSequenceTracker:
             key = t % 2  # the frame slots' rotation
             g = self.graphs.get(key)
             if g is None:
-                self.ctx.capture_begin()
-                self._enqueue(None if self.frames is not None else self.stage.data_ptr(), t)
-                g = self.graphs[key] = self.ctx.capture_end()
+                src = None if self.frames is not None else self.stage.data_ptr()
+                g = self.graphs[key] = self.ctx.capture(lambda tt: self._enqueue(src, tt), t)
             self.ctx.graph_launch(g)
         self.t += 1
 

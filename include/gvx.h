@@ -68,6 +68,10 @@ gvx_status gvx_profile_reset(gvx_ctx* ctx);
 typedef struct gvx_graph gvx_graph;
 gvx_status gvx_capture_begin(gvx_ctx* ctx);
 gvx_status gvx_capture_end(gvx_ctx* ctx, gvx_graph** out);
+/* End an open capture and discard it (a call inside it failed): closes an open
+   branch, ends the stream capture and destroys the partial graph, so the context
+   is usable again.  A no-op when no capture is open. */
+gvx_status gvx_capture_abort(gvx_ctx* ctx);
 gvx_status gvx_graph_launch(gvx_ctx* ctx, const gvx_graph* g);
 void gvx_graph_destroy(gvx_graph* g);
 /* Device-to-device copy on the context stream (capturable: e.g. the initial
@@ -245,11 +249,13 @@ gvx_status gvx_frame_preprocess_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_
                                     int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
                                     double* d_hist_mean, uint8_t* d_clahe_out);
 /* The same for frame *d_index of a sequence resident in HBM (frame f at
-   d_frames + f * frame_stride, rows `stride` bytes apart), the index read on the
-   device: a captured per-frame graph picks its frame without a host round trip
-   (bench.py --config 5).  Frames of at least 66 x 66 px. */
+   d_frames + f * frame_stride, rows `stride` bytes apart, n_frames of them), the
+   index read on the device and clamped to [0, n_frames - 1]: a captured
+   per-frame graph picks its frame without a host round trip (bench.py
+   --config 5).  Frames of at least 66 x 66 px. */
 gvx_status gvx_frame_preprocess_indexed_dev(gvx_ctx* ctx, uint64_t id, const uint8_t* d_frames,
-                                            int64_t frame_stride, const int32_t* d_index, int32_t w, int32_t h,
+                                            int64_t frame_stride, const int32_t* d_index, int32_t n_frames,
+                                            int32_t w, int32_t h,
                                             int32_t stride, const gvx_clahe_params* cp, const gvx_klt_params* p,
                                             double* d_hist_mean);
 
@@ -372,11 +378,11 @@ gvx_status gvx_track_frame_record_dev(gvx_ctx* ctx, uint64_t prev_frame, uint64_
                                       int32_t* d_counts, int32_t* d_frame_index, int32_t max_frames);
 /* Helpers that keep a replay loop inside one captured graph per frame: copy
    bytes from d_src_base + (*d_index) * bytes (e.g. frame *d_index of a sequence
-   resident in HBM), and append the current track list (*d_n points of d_pts) to
+   resident in HBM; the index clamped to [0, n_src - 1]), and append the current track list (*d_n points of d_pts) to
    d_tracks[*d_frame_index * capacity ..] / d_counts[*d_frame_index], then
    advance *d_frame_index (frames >= max_frames are not stored). */
 gvx_status gvx_copy_indexed_dev(gvx_ctx* ctx, void* d_dst, const void* d_src_base, size_t bytes,
-                                const int32_t* d_index);
+                                const int32_t* d_index, int32_t n_src);
 gvx_status gvx_track_record_dev(gvx_ctx* ctx, const float* d_pts, const int32_t* d_n, int32_t capacity,
                                 float* d_tracks, int32_t* d_counts, int32_t* d_frame_index, int32_t max_frames);
 /* *d_index += delta on the context stream (a frame counter that a captured

@@ -103,9 +103,12 @@ def test_frame_preprocess_into_slot_with_rings(ctx, orc, gvx_mod, w, h):
     p = gvx_mod.KltParams.default(max_level=3)
     ctx.frame_preprocess_dev(12, d_seq[2].data_ptr(), w, h, params=p)
     idx = torch.tensor([2], dtype=torch.int32, device="cuda")
-    ctx.frame_preprocess_indexed_dev(13, d_seq.data_ptr(), w * h, idx.data_ptr(), w, h, params=p)
+    ctx.frame_preprocess_indexed_dev(13, d_seq.data_ptr(), w * h, idx.data_ptr(), 3, w, h, params=p)
+    # an index past the sequence is clamped to its last frame (never read past it)
+    idx_past = torch.tensor([7], dtype=torch.int32, device="cuda")
+    ctx.frame_preprocess_indexed_dev(14, d_seq.data_ptr(), w * h, idx_past.data_ptr(), 3, w, h, params=p)
     ctx.sync()
-    for fid in (12, 13):
+    for fid in (12, 13, 14):
         for l, r in enumerate(levels):
             _same(ctx.frame_level_padded(fid, l, 32), r, f"frame {fid} padded level {l}")
         ctx.frame_drop(fid)

@@ -1,6 +1,7 @@
 """hipGraph capture of one frame pair (gvx_capture_begin / gvx_capture_end /
 gvx_graph_launch): replaying the captured initial-flow copy
 + pyramid + LK + compaction gives the eager call's outputs bit for bit."""
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -136,6 +137,62 @@ def test_branch_order_and_misuse(gvx_mod):
         ctx.capture_begin()
         ctx.copy_dev(a.data_ptr(), src.data_ptr(), nb)
         g = ctx.capture_end()
+        g.destroy()
+    finally:
+        ctx.close()
+
+
+def test_capture_needing_scratch_growth_refused(gvx_mod):
+    """a captured gvx_build_pyramids_dev with more strip / band units
+    than any earlier uncaptured call needs its scratch to grow, which cannot
+    happen inside a capture: the call fails (no kernel with a null scratch
+    pointer is captured) and gvx_capture_end refuses the graph; the context is
+    usable afterwards."""
+    import torch
+    from gvx import synth
+    ctx = gvx_mod.Context(0)
+    try:
+        W, H, L = 320, 140, 3
+        lay = gvx_mod.pyramid_layout(W, H, L)
+        dev = torch.device("cuda", 0)
+        imgs = torch.from_numpy(np.stack([synth.make_image(W, H, np.random.default_rng(i)) for i in range(64)])).to(dev)
+        out = torch.empty(64 * lay["bytes"], dtype=torch.uint8, device=dev)
+        ctx.build_pyramids_dev(1, W, H, imgs.data_ptr(), W * H, W, L, out.data_ptr())  # sizes for one image
+        ctx.sync()
+        ctx.capture_begin()
+        with pytest.raises(gvx_mod.GvxError):
+            ctx.build_pyramids_dev(64, W, H, imgs.data_ptr(), W * H, W, L, out.data_ptr())
+        with pytest.raises(gvx_mod.GvxError):
+            ctx.capture_end()
+        # the same call uncaptured now works, and so does a capture of it
+        ctx.build_pyramids_dev(64, W, H, imgs.data_ptr(), W * H, W, L, out.data_ptr())
+        ctx.sync()
+        g = ctx.capture(ctx.build_pyramids_dev, 64, W, H, imgs.data_ptr(), W * H, W, L, out.data_ptr())
+        g.launch()
+        ctx.sync()
+        g.destroy()
+    finally:
+        ctx.close()
+
+
+def test_capture_abort_after_failed_call(gvx_mod):
+    """A call that raises inside Context.capture aborts the capture
+    (gvx_capture_abort): the context is not left capturing."""
+    import torch
+    ctx = gvx_mod.Context(0)
+    try:
+        def bad():
+            ctx.frame_drop(12345)  # refused during a capture
+        with pytest.raises(gvx_mod.GvxError):
+            ctx.capture(bad)
+        ctx.capture_abort()  # no capture open: a no-op
+        # the context works and can capture again
+        buf = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+        src = torch.full((1024,), 9, dtype=torch.uint8, device="cuda")
+        g = ctx.capture(ctx.copy_dev, buf.data_ptr(), src.data_ptr(), 1024)
+        g.launch()
+        ctx.sync()
+        assert int(buf.sum().item()) == 9 * 1024
         g.destroy()
     finally:
         ctx.close()
