@@ -155,6 +155,17 @@ __device__ __forceinline__ void read_win(const uint32_t* win, int row, int byteo
     for (int k = 0; k < NDW; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
 }
 
+// The lane id, recomputed where it is used (volatile: never hoisted or kept
+// live): everything lane-derived (the lane group, the window units, LDS slots,
+// the point index) is rebuilt from it inside each LK pass, so nothing per-lane
+// stays live across the forward and backward passes (where the register
+// allocator spilled such values to scratch: 45 MB of writes per 256 pairs, r02).
+__device__ __forceinline__ int lane_v() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // cvRound((1-a)(1-b) 2^14) ... in fp32 (LKTrackerInvoker), packed as int16 pairs
 // W0 = (w00, w01), W1 = (w10, w11).  p*2^14 is exact, so fma(p, 2^14, 1.5*2^23)
 // is 1.5*2^23 + cvRound(p*2^14) (round to nearest even, 0 <= p*2^14 <= 2^14)
@@ -547,12 +558,18 @@ struct L0Planes {
 // over the point's group; control flow diverges only between groups.
 // ACC: the window-sum order (0 exact, 1 / 2 OpenCV's fp32 scalar / SIMD4
 // orders through the group's LDS region `acc`).
+// wins / units / accs: the wave's LDS bases (wave-uniform); the lane's slots
+// are derived from lane_v() here.
 template <int PPW, int ACC>
 __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
                                          const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
-                                         float p0y, float& nx, float& ny, int& status, float& err, int gl,
-                                         uint32_t* win, v4u* ust, float* acc) {
+                                         float p0y, float& nx, float& ny, int& status, float& err,
+                                         uint32_t (*wins)[(WIN + 3) * WIN_DW], v4u* units, float (*accs)[ACC_FLOATS]) {
     constexpr int G = 64 / PPW, U = PPW;
+    const int lane = lane_v(), grp = lane / G, gl = lane & (G - 1);
+    uint32_t* win = wins[grp];
+    v4u* ust = units + lane;
+    float* acc = ACC ? accs[grp] : nullptr;
     Unit u[U];
 #pragma unroll
     for (int s = 0; s < U; ++s) {
@@ -800,40 +817,51 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
     __shared__ uint32_t wins[KLT_WPB * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
     __shared__ v4u units[KLT_WPB][3 * PPW * 64];                  // per-lane window values
     // fp32-order window sums: one region per point group
-    __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC ? ACC_FLOATS : 4];
-    const int lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC_FLOATS];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int grp = lane / G, gl = lane & (G - 1);
-    uint32_t* win = wins[wv * PPW + grp];
-    v4u* ust = &units[wv][lane];
-    float* acc = accs[ACC ? wv * PPW + grp : 0];
     const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair (launch capacity)
     const int n_waves = a.n_pairs * wpp;
     const int nb = (n_waves + KLT_WPB - 1) / KLT_WPB;
     const int wg = xcd_swizzle(blockIdx.x, nb) * KLT_WPB + wv;
     if (wg >= n_waves) return;
     const int pair = wg / wpp;
-    const int pt_raw = (wg - pair * wpp) * PPW + grp;
     // device-resident count (the per-frame loop without host round trips)
     const int npt = a.n_dev ? min(a.n_pts, *a.n_dev) : a.n_pts;
     if ((wg - pair * wpp) * PPW >= npt) return;  // the whole wave is past the count
-    const bool own = pt_raw < npt;
-    const int64_t gp = (int64_t)pair * a.n_pts + (own ? pt_raw : npt - 1);
-    const bool writer = own && gl == 0;
+    // the group's point (a spare group of a pair's last wave recomputes the last
+    // point); rebuilt from the lane id where needed
+    auto point = [&](bool& writer) -> int64_t {
+        const int lane = lane_v(), pt_raw = (wg - pair * wpp) * PPW + lane / G;
+        writer = pt_raw < npt && (lane & (G - 1)) == 0;
+        return (int64_t)pair * a.n_pts + (pt_raw < npt ? pt_raw : npt - 1);
+    };
+    uint32_t(*wv_wins)[(WIN + 3) * WIN_DW] = wins + wv * PPW;
+    v4u* wv_units = units[wv];
+    float(*wv_accs)[ACC_FLOATS] = accs + (ACC ? wv * PPW : 0);
     const uint8_t* I = pyr_prev + pair * prev_stride;
     const uint8_t* J = pyr_next + pair * next_stride;
     const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.o0, l0.pitch,
                       l0.raw != 0};
     const L0Planes pb{pf.j, pf.i, pf.o0, pf.pitch, pf.raw};
     LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow, err_out != nullptr};
-    const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
-    const float* init_xy = a.init_xy ? a.init_xy : next_xy;
-    float nx = init_xy[2 * gp], ny = init_xy[2 * gp + 1];
+    bool writer;
+    int64_t gp = point(writer);
+    float nx = 0.f, ny = 0.f;
     int st = 1;
     float e = 0.f;
-    acc_clear<ACC, G>(acc, gl);
-    lk_group<PPW, ACC>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, gl, win, ust, acc);
+    {
+        const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
+        const float* init_xy = a.init_xy ? a.init_xy : next_xy;
+        nx = init_xy[2 * gp];
+        ny = init_xy[2 * gp + 1];
+        if constexpr (ACC != 0) {
+            const int lane = lane_v();
+            acc_clear<ACC, G>(wv_accs[lane / G], lane & (G - 1));
+        }
+        lk_group<PPW, ACC>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, wv_wins, wv_units, wv_accs);
+    }
     if (a.mode == 0) {
+        gp = point(writer);
         if (writer) {
             next_xy[2 * gp] = nx;
             next_xy[2 * gp + 1] = ny;
@@ -843,13 +871,20 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
         return;
     }
     // backward: prevPts = forward result, initial flow = original prev points
-    float bx = p0x, by = p0y;
+    // (re-read: an opaque copy of the pointer keeps the compiler from holding
+    // the first load's values live across the forward pass)
+    const float* pxy = prev_xy;
+    asm volatile("" : "+s"(pxy));
+    gp = point(writer);
+    float bx = pxy[2 * gp], by = pxy[2 * gp + 1];
     int st2 = 1;
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
     cfg.want_err = 0;  // the backward error is not reported
-    lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, gl, win, ust, acc);
+    lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, wv_wins, wv_units, wv_accs);
+    gp = point(writer);
     if (writer) {
+        const float p0x = pxy[2 * gp], p0y = pxy[2 * gp + 1];
         const double B = a.border;
         const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
         const double ddx = (double)(bx - p0x), ddy = (double)(by - p0y);

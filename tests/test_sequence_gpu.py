@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 W, H, N, L = 1280, 560, 150, 3
 
 
-def _oracle_sequence(orc, frames, kp, dp):
+def _oracle_sequence(orc, frames, kp, dp, nthreads=1):
     pts, vel = np.zeros((0, 2), np.float32), np.zeros((0, 2), np.float32)
     prev_eq = None
     out = []
@@ -26,7 +26,8 @@ def _oracle_sequence(orc, frames, kp, dp):
         eq = orc.clahe(f)
         rec = {}
         if t > 0 and pts.shape[0]:
-            r = orc.klt_fb(prev_eq, eq, pts, pts + vel, params=kp)
+            # each pyramid built once (bit-identical to OpenCV's per-call rebuild)
+            r = orc.klt_fb(prev_eq, eq, pts, pts + vel, params=kp, reuse_pyramids=nthreads > 1, nthreads=nthreads)
             k = r["kept_idx"]
             nxt = r["next"][k]
             vel = nxt - pts[k]
@@ -120,5 +121,73 @@ def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident, pipelin
                 assert np.array_equal(tracks[t, :counts[t]], wants[t]), f"frame {t}"
         if graph:
             assert len(trk.graphs) == (6 if pipeline else 2)
+    finally:
+        trk.close()
+
+
+LONG = 300
+
+
+@pytest.fixture(scope="module")
+def long_sequence(orc, gvx_mod):
+    """A 300-frame configs[4] sequence rendered on the device and the oracle's
+    per-frame loop over it (host copy), computed once for the tests below."""
+    import torch
+    from gvx import synth
+    dev = torch.device("cuda", 0)
+    frames, _ = synth.make_sequence(W, H, LONG, dev, seed=synth.SEED + 2)
+    ref = _oracle_sequence(orc, frames.cpu().numpy(), orc.KltParams.default(max_level=L), orc.DetectParams.default(),
+                           nthreads=8)
+    return frames, ref
+
+
+def test_long_sequence_bit_exact(ctx, orc, gvx_mod, long_sequence):
+    """300 frames of the host loop, every frame's forward /
+    backward flow, status, keep flags, kept indices, detected corners and track
+    list bit-exact against the oracle loop -- dozens of detection top-ups."""
+    from gvx.tracking import SequenceTracker
+    frames, ref = long_sequence
+    tr = SequenceTracker(ctx, W, H, N, klt=gvx_mod.KltParams.default(max_level=L),
+                         detect=gvx_mod.DetectParams.default(max_features=N), ids=(30, 31))
+    n_detect = 0
+    for t in range(LONG):
+        pts = tr.step(frames[t].data_ptr())
+        g, o = tr.last, ref[t]
+        assert ("track" in g) == ("track" in o), f"frame {t}: tracking ran on one side only"
+        if "track" in g:
+            for k in ("next", "back", "st_f", "st_b", "keep", "kept_idx"):
+                assert np.array_equal(g["track"][k], o["track"][k]), f"frame {t}: {k}"
+        assert ("corners" in g) == ("corners" in o), f"frame {t}: detection ran on one side only"
+        if "corners" in g and g["corners"] is not None:
+            assert np.array_equal(g["corners"], o["corners"]), f"frame {t}: corners"
+            n_detect += g["corners"].shape[0] > 0
+        assert np.array_equal(pts, o["pts"]), f"frame {t}: track list"
+    assert n_detect >= 10, n_detect
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline):
+    """The bench's loop over the same 300 frames: the HBM-resident sequence, one
+    captured graph per frame-slot rotation replayed per frame (pipelined: frame
+    t+1's CLAHE + pyramid graph on the side stream beside frame t's tracking
+    graph, three slots rotating 100 times), the per-frame track records written
+    on the device -- every record bit-exact against the oracle loop's track list."""
+    from gvx.tracking import DeviceSequenceTracker
+    frames, ref = long_sequence
+    trk = DeviceSequenceTracker(ctx, W, H, N, klt=gvx_mod.KltParams.default(max_level=L),
+                                detect=gvx_mod.DetectParams.default(max_features=N), ids=(40, 41), graph=True,
+                                frames=frames, pipeline=pipeline)
+    try:
+        for _ in range(LONG):
+            trk.step()
+        with pytest.raises(IndexError):
+            trk.step()  # past the resident sequence
+        ctx.sync()
+        assert int(trk.index.cpu()[0]) == LONG
+        counts = trk.rec_counts.cpu().numpy()
+        tracks = trk.rec_tracks.cpu().numpy()
+        for t in range(LONG):
+            assert np.array_equal(tracks[t, :counts[t]], ref[t]["pts"]), f"frame {t}"
+        assert len(trk.graphs) == (6 if pipeline else 2)
     finally:
         trk.close()
