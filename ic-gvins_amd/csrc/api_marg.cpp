@@ -153,8 +153,8 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     const size_t nl = d_loss ? (size_t)n_fac : 0;
     lists.add(nl, &d_nres, &h_nres);
     lists.add(nl, &d_roff, &h_roff);
-    double *H0, *b0, *V1, *w1, *Hi, *T, *Hp, *bp, *V2, *w2, *hc, *sr, *J0, *e0;
-    int32_t* info;
+    double *H0, *b0, *V1, *w1, *Hi, *T, *Hp, *bp, *V2, *w2, *hc, *sr, *J0, *e0, *Lm, *Lp, *X;
+    int32_t *info, *chol;
     Staging work;
     work.add((size_t)L * L, &H0);
     work.add((size_t)L, &b0);
@@ -171,6 +171,11 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     work.add((size_t)r * r, &J0);
     work.add((size_t)r, &e0);
     work.add(2, &info);
+    const bool fast = c->marg_solver == GVX_MARG_SOLVER_FAST;
+    work.add(fast ? (size_t)m * m : 0, &Lm);
+    work.add(fast ? (size_t)r * r : 0, &Lp);
+    work.add(fast ? (size_t)m * (r + 1) : 0, &X);
+    work.add(2, &chol);
     // the pinned list buffer may still feed an earlier call's upload
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_err(c, e, "marginalisation: stream");
@@ -190,6 +195,8 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     if (e != hipSuccess) return hip_err(c, e, "marginalisation: list upload");
     if ((e = hipMemsetAsync(info, 0, 2 * sizeof(int32_t), c->stream)) != hipSuccess)
         return hip_err(c, e, "marginalisation: info");
+    if ((e = hipMemsetAsync(chol, 0, 2 * sizeof(int32_t), c->stream)) != hipSuccess)
+        return hip_err(c, e, "marginalisation: flags");
     MargLaunch p{};
     p.n_pairs = ls.n_pairs;
     p.n_bvec = ls.n_bvec;
@@ -217,6 +224,11 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     p.info = o.info ? o.info : info;
     p.J0 = o.J0 ? o.J0 : J0;
     p.e0 = o.e0 ? o.e0 : e0;
+    p.solver = c->marg_solver;
+    p.Lm = Lm;
+    p.Lp = Lp;
+    p.X = X;
+    p.chol = chol;
     if (o.info) {
         if ((e = hipMemsetAsync(o.info, 0, 2 * sizeof(int32_t), c->stream)) != hipSuccess)
             return hip_err(c, e, "marginalisation: info");
@@ -289,6 +301,14 @@ gvx_status gvx_marginalize(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const
     if (bp) std::memcpy(bp, h_bp, sizeof(double) * (size_t)r);
     if (eval) std::memcpy(eval, h_ev, sizeof(double) * (size_t)r);
     if (info) std::memcpy(info, h_info, sizeof(int32_t) * 2);
+    return GVX_OK;
+}
+
+gvx_status gvx_set_marg_solver(gvx_ctx* c, int32_t solver) {
+    if (!c) return GVX_ERR_INVALID;
+    if (solver != GVX_MARG_SOLVER_EXACT && solver != GVX_MARG_SOLVER_FAST)
+        return set_err(c, GVX_ERR_INVALID, "unknown marginalisation solver %d", solver);
+    c->marg_solver = solver;
     return GVX_OK;
 }
 

@@ -77,6 +77,8 @@ struct gvx_ctx {
     // a call inside the open capture failed for want of a (re)allocation:
     // gvx_capture_end refuses the graph
     bool capture_failed = false;
+    // gvx_set_marg_solver
+    int32_t marg_solver = GVX_MARG_SOLVER_FAST;
     // gvx_track_frame_dev: what the detection constants in "trk_static" were
     // built for (the buffer itself and the geometry)
     struct TrackStatic {
@@ -222,8 +224,21 @@ struct MargLaunch {
     double *H0, *b0, *V1, *w1, *Hinv, *T, *Hp, *bp, *V2, *w2, *hc;
     int* info;                        // device [2]: Hmm and Hp eigen-solver status
     double *J0, *e0;
+    // GVX_MARG_SOLVER_*; FAST: Cholesky factors Lm (m x m), Lp (r x r), X = Lm^-1
+    // [Hmr | bm] (m x (r + 1) row-major) and the two check flags chol[2] (device)
+    int solver;
+    double *Lm, *Lp, *X;
+    int* chol;
 };
 hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p);
+// ---- dense.hip (fp64 Cholesky kernels; gate: skipped unless *gate == 0) ----
+hipError_t launch_potrf(gvx_ctx* c, int n, const double* A, int lda, double shift, double* L, int* fail,
+                        const int* gate);
+hipError_t launch_trsv(gvx_ctx* c, int n, const double* L, int nrhs, const double* B, long ldb, double* X, int ldx,
+                       bool neg, const int* gate);
+hipError_t launch_schur_chol(gvx_ctx* c, int L, int m, const double* H0, const double* b0, const double* X,
+                             double* Hp, double* bp, const int* gate);
+hipError_t launch_lin_chol(gvx_ctx* c, int r, const double* Lp, double* J0, double* eval, const int* gate);
 // SelfAdjointEigenSolver of the lower triangle of src (ld lds): V n x n, w n, hc n scratch, info 1 int;
 // ts (nullable, diagnostics): 7 u64, wall-clock stamps (100 MHz) of the solver's phases + QR iterations
 hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc,

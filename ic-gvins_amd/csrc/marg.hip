@@ -299,8 +299,10 @@ __device__ void qr_produce(EigShared& S, QrState& st, int n, int b, int lane) {
 __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const double* __restrict__ src, int lds,
                                                                 double* __restrict__ A, double* __restrict__ w,
                                                                 double* __restrict__ hc, int* __restrict__ info,
-                                                                unsigned long long* __restrict__ ts) {
+                                                                unsigned long long* __restrict__ ts,
+                                                                const int* __restrict__ run_if) {
     __shared__ EigShared S;
+    if (run_if && *run_if == 0) return;  // the Cholesky path (dense.hip) succeeded
     // ts (nullable, diagnostics): wall clock (100 MHz) at the phase boundaries
 #define EIG_STAMP(k) \
     if (ts && tid == 0) ts[k] = wall_clock64()
@@ -626,8 +628,11 @@ __global__ void __launch_bounds__(EIG_THREADS) sym_eigen_kernel(int n, const dou
 
 // ------------------------------------------------------------ Schur complement
 // Hmm_inv(a, b) = sum_k (V(a, k) d_k) V(b, k), d_k = 1/w_k masked at EPS
+// run_if (nullable): the eigen-solver path only runs where the Cholesky path's
+// check failed (*run_if != 0)
 __global__ void __launch_bounds__(256) hinv_kernel(int m, const double* __restrict__ V, const double* __restrict__ w,
-                                                   double* __restrict__ Hi) {
+                                                   double* __restrict__ Hi, const int* __restrict__ run_if) {
+    if (run_if && *run_if == 0) return;
     const int a = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
     if (a >= m) return;
     double acc = 0.0;
@@ -640,7 +645,9 @@ __global__ void __launch_bounds__(256) hinv_kernel(int m, const double* __restri
 
 // T = Hrm Hmm_inv (r x m), Hrm = H0(m.., 0..m)
 __global__ void __launch_bounds__(256) schur_t_kernel(int L, int m, const double* __restrict__ H0,
-                                                      const double* __restrict__ Hi, double* __restrict__ T) {
+                                                      const double* __restrict__ Hi, double* __restrict__ T,
+                                                      const int* __restrict__ run_if) {
+    if (run_if && *run_if == 0) return;
     const int r = L - m;
     const int a = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
     if (a >= r) return;
@@ -654,7 +661,9 @@ __global__ void __launch_bounds__(256) schur_t_kernel(int L, int m, const double
 // Hp = Hrr - T Hmr (column b < r), bp = brr - T bmm (column b == r)
 __global__ void __launch_bounds__(256) schur_p_kernel(int L, int m, const double* __restrict__ H0,
                                                       const double* __restrict__ b0, const double* __restrict__ T,
-                                                      double* __restrict__ Hp, double* __restrict__ bp) {
+                                                      double* __restrict__ Hp, double* __restrict__ bp,
+                                                      const int* __restrict__ run_if) {
+    if (run_if && *run_if == 0) return;
     const int r = L - m;
     const int a = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
     if (a >= r) return;
@@ -670,7 +679,9 @@ __global__ void __launch_bounds__(256) schur_p_kernel(int L, int m, const double
 // J0 = S^1/2 V^T, e0 = (S^-1/2 V^T) (-bp), S masked at EPS
 __global__ void __launch_bounds__(256) linearize_kernel(int r, const double* __restrict__ V,
                                                         const double* __restrict__ w, const double* __restrict__ bp,
-                                                        double* __restrict__ J0, double* __restrict__ e0) {
+                                                        double* __restrict__ J0, double* __restrict__ e0,
+                                                        const int* __restrict__ run_if) {
+    if (run_if && *run_if == 0) return;
     const int i = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;  // J0(i, j) = sqrt(S_i) V(j, i)
     if (i >= r) return;
     const double wi = w[i];
@@ -686,9 +697,9 @@ __global__ void __launch_bounds__(256) linearize_kernel(int r, const double* __r
 }
 
 hipError_t launch_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc, int* info,
-                        unsigned long long* ts = nullptr) {
+                        unsigned long long* ts = nullptr, const int* run_if = nullptr) {
     if (n <= 0) return hipSuccess;
-    sym_eigen_kernel<<<1, EIG_THREADS, 0, c->stream>>>(n, src, lds, V, w, hc, info, ts);
+    sym_eigen_kernel<<<1, EIG_THREADS, 0, c->stream>>>(n, src, lds, V, w, hc, info, ts, run_if);
     return hipGetLastError();
 }
 
@@ -701,6 +712,7 @@ hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, doubl
 
 hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p) {
     const int r = p.L - p.m;
+    const bool fast = p.solver == GVX_MARG_SOLVER_FAST;
     hipError_t e = hipMemsetAsync(p.H0, 0, sizeof(double) * (size_t)p.L * p.L, c->stream);
     if (e != hipSuccess) return e;
     if (p.loss) {
@@ -712,22 +724,50 @@ hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p) {
                                                                        p.loss ? p.sr : nullptr, p.L, p.H0, p.b0);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    // FAST: Cholesky path where Hmm - EPS*I (then Hp - EPS*I) is positive definite
+    // (dense.hip), the eigen-solver path below only where that check failed;
+    // chol[k] != 0 marks the failure, read by the kernels on the device
+    const int* gate_m = fast ? p.chol : nullptr;
+    const int* gate_r = fast ? p.chol + 1 : nullptr;
+    if (fast && p.m > 0) {
+        if ((e = launch_potrf(c, p.m, p.H0, p.L, MARG_EPS, p.Lm, p.chol, nullptr)) != hipSuccess) return e;
+        if ((e = launch_potrf(c, p.m, p.H0, p.L, 0.0, p.Lm, p.chol, p.chol)) != hipSuccess) return e;
+    }
     // Hmm = 0.5 (H0mm + H0mm^T) is H0mm itself: h0_kernel writes both triangles alike
-    if ((e = launch_eigen(c, p.m, p.H0, p.L, p.V1, p.w1, p.hc, p.info)) != hipSuccess) return e;
+    if ((e = launch_eigen(c, p.m, p.H0, p.L, p.V1, p.w1, p.hc, p.info, nullptr, gate_m)) != hipSuccess) return e;
     if (p.m > 0) {
-        hinv_kernel<<<dim3((p.m + 255) / 256, p.m), 256, 0, c->stream>>>(p.m, p.V1, p.w1, p.Hinv);
+        hinv_kernel<<<dim3((p.m + 255) / 256, p.m), 256, 0, c->stream>>>(p.m, p.V1, p.w1, p.Hinv, gate_m);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (r <= 0) return hipSuccess;
     if (p.m > 0) {
-        schur_t_kernel<<<dim3((r + 255) / 256, p.m), 256, 0, c->stream>>>(p.L, p.m, p.H0, p.Hinv, p.T);
+        schur_t_kernel<<<dim3((r + 255) / 256, p.m), 256, 0, c->stream>>>(p.L, p.m, p.H0, p.Hinv, p.T, gate_m);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    schur_p_kernel<<<dim3((r + 255) / 256, r + 1), 256, 0, c->stream>>>(p.L, p.m, p.H0, p.b0, p.T, p.Hp, p.bp);
+    schur_p_kernel<<<dim3((r + 255) / 256, r + 1), 256, 0, c->stream>>>(p.L, p.m, p.H0, p.b0, p.T, p.Hp, p.bp,
+                                                                         gate_m);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_eigen(c, r, p.Hp, r, p.V2, p.w2, p.hc, p.info + 1)) != hipSuccess) return e;
-    linearize_kernel<<<dim3((r + 255) / 256, r), 256, 0, c->stream>>>(r, p.V2, p.w2, p.bp, p.J0, p.e0);
-    return hipGetLastError();
+    if (fast) {
+        if (p.m > 0) {
+            // X = Lm^-1 [Hmr | bm] (row-major m x (r + 1)), then Hp, bp
+            if ((e = launch_trsv(c, p.m, p.Lm, r, p.H0 + (size_t)p.m * p.L, p.L, p.X, r + 1, false, p.chol)) !=
+                hipSuccess)
+                return e;
+            if ((e = launch_trsv(c, p.m, p.Lm, 1, p.b0, p.m, p.X + r, r + 1, false, p.chol)) != hipSuccess) return e;
+            if ((e = launch_schur_chol(c, p.L, p.m, p.H0, p.b0, p.X, p.Hp, p.bp, p.chol)) != hipSuccess) return e;
+        }
+        if ((e = launch_potrf(c, r, p.Hp, r, MARG_EPS, p.Lp, p.chol + 1, nullptr)) != hipSuccess) return e;
+        if ((e = launch_potrf(c, r, p.Hp, r, 0.0, p.Lp, p.chol + 1, p.chol + 1)) != hipSuccess) return e;
+    }
+    if ((e = launch_eigen(c, r, p.Hp, r, p.V2, p.w2, p.hc, p.info + 1, nullptr, gate_r)) != hipSuccess) return e;
+    linearize_kernel<<<dim3((r + 255) / 256, r), 256, 0, c->stream>>>(r, p.V2, p.w2, p.bp, p.J0, p.e0, gate_r);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (fast) {
+        // J0 = Lp^T, e0 = -Lp^-1 bp
+        if ((e = launch_lin_chol(c, r, p.Lp, p.J0, p.w2, p.chol + 1)) != hipSuccess) return e;
+        if ((e = launch_trsv(c, r, p.Lp, 1, p.bp, r, p.e0, 1, true, p.chol + 1)) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace gvx

@@ -508,13 +508,29 @@ gvx_status gvx_marg_factor_eval(gvx_ctx* ctx, int32_t r, int32_t nb, const int32
    blocks first); m = marginalizedSize() > 0, L = local size, r = L - m; m and r
    at most 512.  Outputs: J0 (r x r column-major, linearizedJacobians()), e0 [r]
    (linearizedResiduals()); optional Hp (r x r column-major), bp [r], eval [r]
-   (Hp's eigenvalues, ascending) and info [2] (the two eigen solves: 0 =
-   Success, 1 = NoConvergence, which the reference does not check either). */
+   (Hp's eigenvalues, ascending; NaN where the FAST solver's Cholesky path ran,
+   gvx_set_marg_solver below) and info [2] (the two eigen solves: 0 = Success,
+   1 = NoConvergence, which the reference does not check either). */
 gvx_status gvx_marginalize(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
                            const int32_t* blk, const int64_t* res_off, const int64_t* jac_off, const double* data,
                            int64_t n_data, const double* loss, int32_t nb, const int32_t* size, const int32_t* index,
                            int32_t m, int32_t L, double* J0, double* e0, double* Hp, double* bp, double* eval,
                            int32_t* info);
+/* The solver of schurElimination / linearization (per context, default FAST):
+   EXACT  Eigen's SelfAdjointEigenSolver for both Hmm^-1 and Hp's factor, bit-exact
+          against the restatement (oracle/marg.c) -- the reference's arithmetic;
+   FAST   where Hmm - 1e-8*I (resp. Hp - 1e-8*I) is positive definite, i.e. no
+          eigenvalue is dropped, Cholesky factors instead: Hp = Hrr - X^T X with
+          X = Lm^-1 Hmr, J0 = Lp^T, e0 = -Lp^-1 bp.  Hp and bp are the same matrix
+          and vector (to rounding; Hmm's conditioning bounds the difference), and
+          J0^T J0 = Hp, J0^T e0 = -bp as in the reference, so the marginalisation
+          prior ||e0 + J0 dx||^2 is the same function; J0 / e0 themselves differ
+          by an orthogonal transform, and eval is NaN.  Where the check fails
+          (an eigenvalue <= 1e-8) that step runs the EXACT solver.  The check is
+          decided on the device (no host round trip). */
+#define GVX_MARG_SOLVER_EXACT 0
+#define GVX_MARG_SOLVER_FAST 1
+gvx_status gvx_set_marg_solver(gvx_ctx* ctx, int32_t solver);
 /* The same with data, loss and every output as device pointers (d_info: 2 ints,
    nullable), enqueued on the context stream; the structure arrays stay host
    arrays (the host turns them into the per-pair contribution lists).  Waits
