@@ -102,11 +102,26 @@ __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, 
     reinterpret_cast<uint32_t*>(out)[lane] = packed;
 }
 
+// cv::cvtColor(COLOR_BGR2GRAY), 8-bit (OpenCV 4.x RGB2Gray<uchar>, tracking.cc:111-113)
+__device__ __forceinline__ uint32_t bgr_gray(uint32_t b, uint32_t g, uint32_t r) {
+    return (b * 1868u + g * 9617u + r * 4899u + 8192u) >> 14;
+}
+// byte k of the 24-byte value {c:b:a} (k constant after unrolling)
+__device__ __forceinline__ uint32_t byte24(const uint2& a, const uint2& b, const uint2& c, int k) {
+    const uint32_t d[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    return (d[k >> 2] >> (8 * (k & 3))) & 255u;
+}
+
+// chan 3: the source is BGR8 (3 bytes per pixel, strides in bytes); each pixel
+// is converted to gray as it is read, and the in-image gray pixels are written
+// to gray (image i at gray + i*gray_img, rows gray_pitch apart) for the apply pass.
 __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
                                                           int stride, ClaheGeom g, int vec8, int tpw,
                                                           uint8_t* __restrict__ lut,
                                                           uint32_t* __restrict__ hist_img,
-                                                          const int32_t* __restrict__ src_index, int n_src) {
+                                                          const int32_t* __restrict__ src_index, int n_src, int chan,
+                                                          uint8_t* __restrict__ gray, int64_t gray_img,
+                                                          int gray_pitch) {
     extern __shared__ uint32_t hs[];  // tpw histograms of 256 bins, HROW dwords apart
     const int ngrp = (g.tiles_x + tpw - 1) / tpw;
     const int img = blockIdx.x / (g.tiles_y * ngrp);
@@ -123,8 +138,51 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
     const int rows_in = max(0, min(y0 + g.th, g.h) - y0);
     const float inv_tw = 1.0f / g.tw;
     const int xlo = txa0 * g.tw, xhi_ext = txa1 * g.tw, xhi = min(xhi_ext, g.w);  // in-image columns [xlo, xhi)
+    // the gray value of in-image pixel (x, y)
+    auto pixel = [&](int y, int x) -> uint32_t {
+        const uint8_t* p = s + (int64_t)y * stride;
+        return chan == 3 ? bgr_gray(p[3 * x], p[3 * x + 1], p[3 * x + 2]) : p[x];
+    };
+    uint8_t* gimg = chan == 3 ? gray + img * gray_img : nullptr;
     // ---- in-image pixels ----
-    if (vec8) {
+    if (vec8 && chan == 3) {
+        // 8 pixels = 24 bytes per chunk; the chunk's gray bytes are stored whole (a
+        // chunk shared with the neighbouring group is written with the same bytes)
+        const int c8lo = xlo >> 3, n8 = ((xhi + 7) >> 3) - c8lo;
+        const int total = rows_in * max(n8, 0);
+        for (int base = t; base < total; base += LUT_UNROLL * LUT_THREADS) {
+            uint2 v[LUT_UNROLL][3];
+            int x0[LUT_UNROLL], yr[LUT_UNROLL];
+#pragma unroll
+            for (int k = 0; k < LUT_UNROLL; ++k) {
+                const int i = base + k * LUT_THREADS;
+                const int r = i / n8, c8 = c8lo + (i - r * n8);
+                x0[k] = 8 * c8;
+                yr[k] = y0 + r;
+                const uint2* p = reinterpret_cast<const uint2*>(s + (int64_t)(y0 + r) * stride + 24 * c8);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) v[k][q] = i < total ? p[q] : uint2{0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < LUT_UNROLL; ++k) {
+                if (base + k * LUT_THREADS >= total) break;
+                const int txa = div_small(max(x0[k], xlo), g.tw, inv_tw);
+                const int xb = (txa + 1) * g.tw;
+                uint32_t gw[2] = {0, 0};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t b = bgr_gray(byte24(v[k][0], v[k][1], v[k][2], 3 * j),
+                                                byte24(v[k][0], v[k][1], v[k][2], 3 * j + 1),
+                                                byte24(v[k][0], v[k][1], v[k][2], 3 * j + 2));
+                    gw[j >> 2] |= b << (8 * (j & 3));
+                    const int x = x0[k] + j;
+                    const int tx = x < xb ? txa : (x < xb + g.tw ? txa + 1 : div_small(x, g.tw, inv_tw));
+                    if (x >= xlo && x < xhi) atomicAdd(&hs[(tx - txa0) * HROW + b], 1u);
+                }
+                *reinterpret_cast<uint2*>(gimg + (int64_t)yr[k] * gray_pitch + x0[k]) = uint2{gw[0], gw[1]};
+            }
+        }
+    } else if (vec8) {
         const int c8lo = xlo >> 3, n8 = ((xhi + 7) >> 3) - c8lo;  // w % 8 == 0: chunks stay in the row
         const int total = rows_in * max(n8, 0);
         for (int base = t; base < total; base += LUT_UNROLL * LUT_THREADS) {
@@ -157,7 +215,9 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
         const int total = rows_in * max(cw, 0);
         for (int i = t; i < total; i += LUT_THREADS) {
             const int r = i / cw, x = xlo + (i - r * cw);
-            atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + s[(int64_t)(y0 + r) * stride + x]], 1u);
+            const uint32_t b = pixel(y0 + r, x);
+            if (gimg) gimg[(int64_t)(y0 + r) * gray_pitch + x] = (uint8_t)b;
+            atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + b], 1u);
         }
     }
     if (hist_img) {
@@ -173,15 +233,14 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
         const int pxlo = max(g.w, xlo), pc = xhi_ext - pxlo;
         for (int i = t; i < rows_in * pc; i += LUT_THREADS) {
             const int r = i / pc, x = pxlo + (i - r * pc);
-            atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + s[(int64_t)(y0 + r) * stride + refl101(x, g.w)]],
-                      1u);
+            atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + pixel(y0 + r, refl101(x, g.w))], 1u);
         }
     }
     const int pr = g.th - rows_in, ecw = xhi_ext - xlo;  // pad rows (reflected source rows), this group's columns
     for (int i = t; i < pr * ecw; i += LUT_THREADS) {
         const int r = i / ecw, x = xlo + (i - r * ecw);
         const int sy = refl101(y0 + rows_in + r, g.h);
-        atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + s[(int64_t)sy * stride + refl101(x, g.w)]], 1u);
+        atomicAdd(&hs[(div_small(x, g.tw, inv_tw) - txa0) * HROW + pixel(sy, refl101(x, g.w))], 1u);
     }
     __syncthreads();
     for (int tx = txa0 + wave; tx < txa1; tx += LUT_THREADS / 64)
@@ -387,8 +446,11 @@ ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles
 
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
-                        uint32_t* hist_img, double* hist_mean, const int32_t* src_index, int n_src, int ring) {
+                        uint32_t* hist_img, double* hist_mean, const int32_t* src_index, int n_src, int ring,
+                        int chan, uint8_t* gray) {
     if (n <= 0) return hipSuccess;
+    if (chan == 3 && !gray) return hipErrorInvalidValue;
+    const int gray_pitch = (g.w + 63) & ~63;
     if (hist_img) {
         hipError_t e = hipMemsetAsync(hist_img, 0, (size_t)n * 256 * sizeof(uint32_t), c->stream);
         if (e != hipSuccess) return e;
@@ -402,7 +464,16 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const int tpw = (g.tiles_x + ngrp - 1) / ngrp;
     ngrp = (g.tiles_x + tpw - 1) / tpw;
     hipLaunchKernelGGL(lut_kernel, dim3(n * g.tiles_y * ngrp), dim3(LUT_THREADS), (size_t)tpw * HROW * 4, c->stream,
-                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index, n_src);
+                       src, img_stride, stride, g, lut_vec8, tpw, lut, hist_img, src_index, n_src, chan, gray,
+                       (int64_t)gray_pitch * g.h, gray_pitch);
+    if (chan == 3) {
+        // the apply pass reads the gray frames the LUT pass wrote
+        src = gray;
+        img_stride = (int64_t)gray_pitch * g.h;
+        stride = gray_pitch;
+        src_index = nullptr;
+    }
+    const bool asrc8 = (uintptr_t)src % 8 == 0 && stride % 8 == 0 && img_stride % 8 == 0;
     // bands of rows sharing one pair of LUT rows, split to fill the chip
     const int nb = g.tiles_y + 1;
     // workgroups wanted for the apply pass (the sequence replay's single frames
@@ -414,7 +485,7 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     const int threads = std::min(1024, (cols + 63) / 64 * 64);
     const size_t lds = (size_t)(g.tiles_x + 1) * TROW * 4;
     hipLaunchKernelGGL(apply_kernel, dim3(n * nb * nsplit), dim3(threads), lds, c->stream, src, img_stride, stride,
-                       dst, dst_img_stride, dst_stride, g, (const uint8_t*)lut, nsplit, (int)(src8 && dst8), src_index,
+                       dst, dst_img_stride, dst_stride, g, (const uint8_t*)lut, nsplit, (int)(asrc8 && dst8), src_index,
                        n_src, ring);
     if (hist_img && hist_mean)
         hipLaunchKernelGGL(mean_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, (const uint32_t*)hist_img, n,

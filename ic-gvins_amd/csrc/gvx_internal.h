@@ -192,7 +192,9 @@ ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean, const int32_t* src_index = nullptr,
-                        int n_src = 0, int ring = 0);
+                        int n_src = 0, int ring = 0, int chan = 1, uint8_t* gray = nullptr);
+// gray scratch of launch_clahe for chan 3: n images of clahe_gray_pitch(w) x h bytes
+inline int clahe_gray_pitch(int w) { return (w + 63) & ~63; }
 
 // ---- aux_factors.hip ----
 // residuals of a small factor kind (0: unknown kind); *P block size, *NC constants per factor

@@ -83,14 +83,30 @@ class DetectParams(C.Structure):
 
 class ClaheParams(C.Structure):
     """cv::createCLAHE(clipLimit, tileGridSize) -- tracking.cc:63 uses (3.0, (21, 21))."""
-    _fields_ = [("clip_limit", C.c_double), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32)]
+    _fields_ = [("clip_limit", C.c_double), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32),
+                ("channels", C.c_int32)]
 
     @classmethod
     def default(cls, **kw) -> "ClaheParams":
-        p = cls(3.0, 21, 21)
+        p = cls(3.0, 21, 21, 1)
         for k, v in kw.items():
             setattr(p, k, v)
         return p
+
+
+def _frame_and_params(img, params):
+    """A MONO8 (h x w) or BGR8 (h x w x 3) frame and CLAHE params whose channels
+    field says which (gvx_clahe_params.channels)."""
+    g = np.ascontiguousarray(img, dtype=np.uint8)
+    if g.ndim == 3 and g.shape[2] == 3:
+        ch = 3
+    elif g.ndim == 2:
+        ch = 1
+    else:
+        raise ValueError("frame must be h x w (MONO8) or h x w x 3 (BGR8) u8")
+    p = params or ClaheParams.default()
+    p = ClaheParams(p.clip_limit, p.tiles_x, p.tiles_y, ch)
+    return g, p
 
 
 class Camera(C.Structure):
@@ -342,14 +358,13 @@ class Context:
     # -------------------------------------------------------- preprocessing
     def clahe(self, gray: np.ndarray, params: Optional[ClaheParams] = None, hist_mean: bool = False):
         """clahe_->apply(image, image) (tracking.cc:139); with hist_mean also
-        calculateHistigram of the input (tracking.cc:88-105) -> (image, mean)."""
-        g = np.ascontiguousarray(gray, dtype=np.uint8)
-        if g.ndim != 2:
-            raise ValueError("gray image must be 2-D u8")
-        h, w = g.shape
-        out = np.empty_like(g)
+        calculateHistigram of the input (tracking.cc:88-105) -> (image, mean).
+        An h x w x 3 input is BGR8: converted to gray first (tracking.cc:111-113)."""
+        g, p = _frame_and_params(gray, params)
+        h, w = g.shape[:2]
+        out = np.empty((h, w), np.uint8)
         m = C.c_double()
-        self._check(self._L.gvx_clahe(self._h, w, h, _ptr(g), w, _ptr(out), w, C.byref(params or ClaheParams.default()),
+        self._check(self._L.gvx_clahe(self._h, w, h, _ptr(g), w * p.channels, _ptr(out), w, C.byref(p),
                                       C.byref(m) if hist_mean else None), "clahe")
         return (out, m.value) if hist_mean else out
 
@@ -363,15 +378,12 @@ class Context:
     def frame_preprocess(self, fid: int, gray: np.ndarray, clahe: Optional[ClaheParams] = None,
                          params: Optional[KltParams] = None, hist_mean: bool = False):
         """Tracking::preprocessing (tracking.cc:107-141) into the frame cache:
-        -> (equalised image, histogram mean or None)."""
-        g = np.ascontiguousarray(gray, dtype=np.uint8)
-        if g.ndim != 2:
-            raise ValueError("gray image must be 2-D u8")
-        h, w = g.shape
-        out = np.empty_like(g)
+        -> (equalised image, histogram mean or None).  An h x w x 3 input is BGR8."""
+        g, cp = _frame_and_params(gray, clahe)
+        h, w = g.shape[:2]
+        out = np.empty((h, w), np.uint8)
         m = C.c_double()
-        self._check(self._L.gvx_frame_preprocess(self._h, fid, _ptr(g), w, h, w,
-                                                 C.byref(clahe or ClaheParams.default()),
+        self._check(self._L.gvx_frame_preprocess(self._h, fid, _ptr(g), w, h, w * cp.channels, C.byref(cp),
                                                  C.byref(params or KltParams.default()),
                                                  C.byref(m) if hist_mean else None, _ptr(out)), "frame_preprocess")
         return out, (m.value if hist_mean else None)

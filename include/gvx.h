@@ -221,6 +221,12 @@ gvx_status gvx_build_pyramids_dev(gvx_ctx* ctx, int32_t n_img, int32_t w, int32_
 typedef struct {
     double clip_limit;         /* 3.0 */
     int32_t tiles_x, tiles_y;  /* tileGridSize = (21, 21), each in [1, GVX_CLAHE_MAX_TILES] */
+    int32_t channels;          /* source format: 1 = MONO8 (default), 3 = BGR8 -- converted
+                                  first as cv::cvtColor(COLOR_BGR2GRAY) (tracking.cc:111-113):
+                                  (B*1868 + G*9617 + R*4899 + 8192) >> 14, folded into the
+                                  CLAHE histogram pass (which writes the gray frame once);
+                                  strides stay in bytes (>= 3 w), the histogram check and
+                                  the outputs are of the gray frame */
 } gvx_clahe_params;
 void gvx_clahe_params_default(gvx_clahe_params* p);
 

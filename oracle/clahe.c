@@ -146,3 +146,15 @@ double orc_hist_mean(const uint8_t* src, int w, int h, int stride) {
     for (int k = 0; k < 256; ++k) m += (double)((float)hist[k] * (float)k) / 256.0;
     return m / (w * h);
 }
+
+/* RGB2Gray<uchar> (imgproc/src/color_rgb.simd.hpp, OpenCV 4.x) with blueIdx = 0:
+   tab[i] = i*B2Y, tab[256+i] = i*G2Y, tab[512+i] = i*R2Y + (1 << 13), yuv_shift 14,
+   R2Y = 4899, G2Y = 9617, B2Y = 1868 -- the integer sum, whatever the SIMD path. */
+void orc_bgr2gray(const uint8_t* bgr, int w, int h, int stride, uint8_t* gray, int gray_stride) {
+    for (int y = 0; y < h; y++) {
+        const uint8_t* s = bgr + (size_t)y * stride;
+        uint8_t* d = gray + (size_t)y * gray_stride;
+        for (int x = 0; x < w; x++)
+            d[x] = (uint8_t)((s[3 * x] * 1868 + s[3 * x + 1] * 9617 + s[3 * x + 2] * 4899 + (1 << 13)) >> 14);
+    }
+}

@@ -272,6 +272,10 @@ void orc_pose_plus(const double* x, const double* delta, double* x_plus_delta);
 /* ------------------------------------------------------------------------- */
 /* Preprocessing: CLAHE and the histogram check (clahe.c)                     */
 /* ------------------------------------------------------------------------- */
+/* cv::cvtColor(src, dst, COLOR_BGR2GRAY) for 8-bit BGR (OpenCV 4.x RGB2Gray<uchar>:
+   (B*1868 + G*9617 + R*4899 + (1 << 13)) >> 14); the reference converts BGR8
+   frames this way first (tracking.cc:111-113). */
+void orc_bgr2gray(const uint8_t* bgr, int w, int h, int stride, uint8_t* gray, int gray_stride);
 void orc_clahe_geometry(int w, int h, int tiles_x, int tiles_y, int* tw, int* th, int* ext_w, int* ext_h);
 void orc_clahe_luts(const uint8_t* src, int w, int h, int stride, double clip_limit, int tiles_x,
                     int tiles_y, uint8_t* lut);

@@ -150,6 +150,7 @@ def lib():
         L.orc_pose_plus.argtypes = [P, P, P]
         L.orc_clahe_luts.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, P]
         L.orc_clahe.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, P, C.c_int]
+        L.orc_bgr2gray.argtypes = [P, C.c_int, C.c_int, C.c_int, P, C.c_int]
         L.orc_hist_mean.argtypes = [P, C.c_int, C.c_int, C.c_int]
         L.orc_hist_mean.restype = C.c_double
         IC = C.POINTER(InsConfig)
@@ -479,6 +480,15 @@ def preint_factor_eval_batch(segs, params, offs, jacobians=True, nthreads=1):
 
 
 # ------------------------------------------------------------------ preprocessing
+def bgr2gray(bgr: np.ndarray) -> np.ndarray:
+    """cv::cvtColor(COLOR_BGR2GRAY) of an h x w x 3 u8 image (clahe.c)."""
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    h, w = bgr.shape[:2]
+    out = np.zeros((h, w), np.uint8)
+    lib().orc_bgr2gray(_p(bgr), w, h, 3 * w, _p(out), w)
+    return out
+
+
 def clahe(img: np.ndarray, clip_limit=3.0, tiles=(21, 21)) -> np.ndarray:
     """cv::createCLAHE(clip_limit, Size(tiles))->apply(img) (tracking.cc:63, :139)."""
     img = np.ascontiguousarray(img, np.uint8)

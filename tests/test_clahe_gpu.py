@@ -120,3 +120,85 @@ def test_clahe_rejects_bad_grids(ctx, gvx_mod):
               gvx_mod.ClaheParams.default(tiles_x=65), gvx_mod.ClaheParams.default(tiles_x=21, tiles_y=41)):
         with pytest.raises(gvx_mod.GvxError):
             ctx.clahe(img, p)
+
+
+# ---- BGR8 frames (Tracking::preprocessing's cv::cvtColor(COLOR_BGR2GRAY),
+# tracking.cc:111-113, folded into the CLAHE histogram pass) ----
+
+def _bgr(w, h, seed):
+    rng = np.random.default_rng(seed)
+    return np.stack([synth.make_image(w, h, rng) for _ in range(3)], axis=-1)
+
+
+@pytest.mark.parametrize("w,h", [(1280, 560), (333, 149), (210, 147), (47, 33)])
+def test_clahe_bgr_bit_exact(ctx, orc, gvx_mod, w, h):
+    """BGR8 in, the CLAHE of its gray conversion out (8-byte path at widths that
+    are multiples of 8, the byte path otherwise), the histogram check of the gray
+    frame: bit-exact against oracle bgr2gray + clahe."""
+    bgr = _bgr(w, h, w + h)
+    gray = orc.bgr2gray(bgr)
+    out, m = ctx.clahe(bgr, hist_mean=True)
+    _same(out, orc.clahe(gray), "clahe of the gray frame")
+    assert m == orc.hist_mean(gray)
+
+
+def test_bgr_extremes(ctx, orc, gvx_mod):
+    """Pure channels and white: the fixed-point weights themselves."""
+    for col in ((255, 0, 0), (0, 255, 0), (0, 0, 255), (255, 255, 255), (1, 2, 3)):
+        bgr = np.zeros((64, 96, 3), np.uint8)
+        bgr[:, 48:] = col
+        _same(ctx.clahe(bgr), orc.clahe(orc.bgr2gray(bgr)), f"colour {col}")
+
+
+def test_clahe_batch_dev_bgr(ctx, orc, gvx_mod):
+    import torch
+    w, h, n = 1280, 560, 3
+    imgs = [_bgr(w, h, 50 + i) for i in range(n)]
+    src = torch.from_numpy(np.stack(imgs)).cuda()
+    dst = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
+    means = torch.zeros(n, dtype=torch.float64, device="cuda")
+    p = gvx_mod.ClaheParams.default(channels=3)
+    ctx.clahe_batch_dev(n, w, h, src.data_ptr(), dst.data_ptr(), params=p, d_hist_mean=means.data_ptr(),
+                        src_img_stride=3 * w * h, src_stride=3 * w)
+    ctx.sync()
+    out, mv = dst.cpu().numpy(), means.cpu().numpy()
+    for i in range(n):
+        g = orc.bgr2gray(imgs[i])
+        _same(out[i], orc.clahe(g), f"image {i}")
+        assert mv[i] == orc.hist_mean(g)
+
+
+def test_frame_preprocess_bgr_feeds_pyramid(ctx, orc, gvx_mod):
+    """A BGR8 frame through the whole preprocessing into the frame cache (host
+    entry and the HBM-resident indexed entry): every pyramid level is the
+    oracle's pyramid of clahe(bgr2gray(frame))."""
+    import torch
+    w, h = 1280, 560
+    seq = np.stack([_bgr(w, h, 70 + i) for i in range(2)])
+    ref = orc.clahe(orc.bgr2gray(seq[1]))
+    eq, m = ctx.frame_preprocess(15, seq[1], hist_mean=True)
+    _same(eq, ref, "equalised frame")
+    assert m == orc.hist_mean(orc.bgr2gray(seq[1]))
+    d_seq = torch.from_numpy(seq).cuda()
+    idx = torch.tensor([1], dtype=torch.int32, device="cuda")
+    ctx.frame_preprocess_indexed_dev(16, d_seq.data_ptr(), 3 * w * h, idx.data_ptr(), 2, w, h, stride=3 * w,
+                                     clahe=gvx_mod.ClaheParams.default(channels=3),
+                                     params=gvx_mod.KltParams.default(max_level=3))
+    ctx.sync()
+    for l, r in enumerate(orc.build_pyramid(ref, 3)):
+        _same(ctx.frame_level(15, l), r, f"level {l}")
+        _same(ctx.frame_level_padded(16, l, 32), np.pad(r, 32, mode="reflect"), f"indexed padded level {l}")
+    ctx.frame_drop(15)
+    ctx.frame_drop(16)
+
+
+def test_bad_channels_refused(ctx, gvx_mod):
+    import torch
+    buf = torch.zeros(3 * 64 * 40, dtype=torch.uint8, device="cuda")
+    ctx.clahe_batch_dev(1, 64, 40, buf.data_ptr(), buf.data_ptr())  # MONO8: fine
+    with pytest.raises(gvx_mod.GvxError):
+        ctx.clahe_batch_dev(1, 64, 40, buf.data_ptr(), buf.data_ptr(), params=gvx_mod.ClaheParams.default(channels=2))
+    with pytest.raises(gvx_mod.GvxError):  # BGR8 rows need 3 w bytes
+        ctx.clahe_batch_dev(1, 64, 40, buf.data_ptr(), buf.data_ptr(), params=gvx_mod.ClaheParams.default(channels=3),
+                            src_stride=64)
+    ctx.sync()

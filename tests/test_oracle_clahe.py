@@ -115,3 +115,15 @@ def test_hist_mean_known_answer():
     h = np.bincount(_img(60, 70, 3).ravel(), minlength=256)
     m = sum(float(F32(h[k]) * F32(k)) / 256.0 for k in range(256)) / (60 * 70)
     assert orc.hist_mean(_img(60, 70, 3)) == m
+
+
+def test_bgr2gray_known_answers(orc):
+    """cv::cvtColor(COLOR_BGR2GRAY), 8-bit: (B*1868 + G*9617 + R*4899 + 8192) >> 14
+    (OpenCV 4.x RGB2Gray<uchar>, yuv_shift 14; BGR channel order)."""
+    rng = np.random.default_rng(3)
+    bgr = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    b, g, r = (bgr[..., k].astype(np.int64) for k in range(3))
+    assert np.array_equal(orc.bgr2gray(bgr), ((b * 1868 + g * 9617 + r * 4899 + 8192) >> 14).astype(np.uint8))
+    px = np.array([[[255, 255, 255], [0, 0, 0], [255, 0, 0], [0, 255, 0], [0, 0, 255]]], np.uint8)
+    # white stays 255 (the weights sum to 2^14); pure B / G / R: 29, 150, 76
+    assert orc.bgr2gray(px).tolist() == [[255, 0, 29, 150, 76]]
