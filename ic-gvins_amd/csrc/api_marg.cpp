@@ -27,7 +27,32 @@ struct Lists {
     std::vector<MargPairRec> recs;  // H0 pairs, then b0 blocks
     std::vector<int4> contrib;
     int n_pairs = 0, n_bvec = 0;
+    // contribution chunks of at most H0_CHUNK (chunked H0 build, MargLaunch)
+    std::vector<int4> chunks;
+    std::vector<int2> recpart;
+    int64_t n_part = 0;
 };
+constexpr int H0_CHUNK = 32;
+
+void make_chunks(Lists& ls) {
+    ls.chunks.clear();
+    ls.recpart.resize(ls.recs.size());
+    int64_t part = 0;
+    for (size_t k = 0; k < ls.recs.size(); ++k) {
+        const MargPairRec& r = ls.recs[k];
+        const int n_ent = r.lp * r.lq;
+        int nch = 0;
+        int c0 = r.c0;
+        do {  // at least one chunk per record (an empty one sums to 0)
+            ls.chunks.push_back(make_int4((int)k, c0, std::min(c0 + H0_CHUNK, r.c1), (int)(part + (int64_t)nch * n_ent)));
+            ++nch;
+            c0 += H0_CHUNK;
+        } while (c0 < r.c1);
+        ls.recpart[k] = make_int2((int)part, nch);
+        part += (int64_t)nch * n_ent;
+    }
+    ls.n_part = part;
+}
 
 // Validates the problem and builds the contribution lists.  Returns GVX_OK or
 // an error with the message set.
@@ -153,6 +178,13 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     const size_t nl = d_loss ? (size_t)n_fac : 0;
     lists.add(nl, &d_nres, &h_nres);
     lists.add(nl, &d_roff, &h_roff);
+    const bool fast = c->marg_solver == GVX_MARG_SOLVER_FAST;
+    int4 *d_chk = nullptr, *h_chk = nullptr;
+    int2 *d_rpart = nullptr, *h_rpart = nullptr;
+    if (fast) {
+        lists.add(ls.chunks.size(), &d_chk, &h_chk);
+        lists.add(ls.recpart.size(), &d_rpart, &h_rpart);
+    }
     double *H0, *b0, *V1, *w1, *Hi, *T, *Hp, *bp, *V2, *w2, *hc, *sr, *J0, *e0, *Lm, *Lp, *X;
     int32_t *info, *chol;
     Staging work;
@@ -171,7 +203,8 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     work.add((size_t)r * r, &J0);
     work.add((size_t)r, &e0);
     work.add(2, &info);
-    const bool fast = c->marg_solver == GVX_MARG_SOLVER_FAST;
+    double* part = nullptr;
+    if (fast) work.add((size_t)ls.n_part, &part);
     work.add(fast ? (size_t)m * m : 0, &Lm);
     work.add(fast ? (size_t)r * r : 0, &Lp);
     work.add(fast ? (size_t)m * (r + 1) : 0, &X);
@@ -190,6 +223,10 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     if (nl) {
         std::memcpy(h_nres, nres, sizeof(int32_t) * nl);
         std::memcpy(h_roff, res_off, sizeof(int64_t) * nl);
+    }
+    if (fast) {
+        std::memcpy(h_chk, ls.chunks.data(), sizeof(int4) * ls.chunks.size());
+        std::memcpy(h_rpart, ls.recpart.data(), sizeof(int2) * ls.recpart.size());
     }
     e = hipMemcpyAsync(db, hb, lists.bytes(), hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "marginalisation: list upload");
@@ -229,6 +266,10 @@ gvx_status run(gvx_ctx* c, const Lists& ls, int n_fac, const int32_t* nres, cons
     p.Lp = Lp;
     p.X = X;
     p.chol = chol;
+    p.n_chunks = fast ? (int)ls.chunks.size() : 0;
+    p.chunks = d_chk;
+    p.recpart = d_rpart;
+    p.part = part;
     if (o.info) {
         if ((e = hipMemsetAsync(o.info, 0, 2 * sizeof(int32_t), c->stream)) != hipSuccess)
             return hip_err(c, e, "marginalisation: info");
@@ -253,6 +294,7 @@ gvx_status gvx_marginalize_dev(gvx_ctx* c, int32_t n_fac, const int32_t* nres, c
     Lists ls;
     gvx_status s = build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls);
     if (s) return s;
+    if (c->marg_solver == GVX_MARG_SOLVER_FAST) make_chunks(ls);
     return run(c, ls, n_fac, nres, res_off, d_data, d_loss, m, L, DevOut{d_J0, d_e0, d_Hp, d_bp, d_eval, d_info});
 }
 
@@ -266,6 +308,7 @@ gvx_status gvx_marginalize(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const
     Lists ls;
     gvx_status s = build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls);
     if (s) return s;
+    if (c->marg_solver == GVX_MARG_SOLVER_FAST) make_chunks(ls);
     const int r = L - m;
     // inputs and outputs through one pinned arena laid out like the device one
     double *d_in, *h_in, *d_loss, *h_loss, *d_J0, *h_J0, *d_e0, *h_e0, *d_Hp, *h_Hp, *d_bp, *h_bp, *d_ev, *h_ev;
@@ -300,6 +343,132 @@ gvx_status gvx_marginalize(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const
     if (Hp) std::memcpy(Hp, h_Hp, sizeof(double) * (size_t)r * r);
     if (bp) std::memcpy(bp, h_bp, sizeof(double) * (size_t)r);
     if (eval) std::memcpy(eval, h_ev, sizeof(double) * (size_t)r);
+    if (info) std::memcpy(info, h_info, sizeof(int32_t) * 2);
+    return GVX_OK;
+}
+
+// ---------------------------------------------------- LM step (DENSE_SCHUR)
+namespace {
+
+gvx_status run_lm(gvx_ctx* c, Lists& ls, const double* d_data, const double* d_D, int m, int L, double* d_delta,
+                  double* d_S, int32_t* d_info) {
+    const int r = L - m;
+    make_chunks(ls);
+    MargPairRec *d_rec, *h_rec;
+    int4 *d_con, *h_con, *d_chk, *h_chk;
+    int2 *d_rpart, *h_rpart;
+    Staging lists;
+    lists.add(ls.recs.size(), &d_rec, &h_rec);
+    lists.add(ls.contrib.size(), &d_con, &h_con);
+    lists.add(ls.chunks.size(), &d_chk, &h_chk);
+    lists.add(ls.recpart.size(), &d_rpart, &h_rpart);
+    double *H0, *b0, *Lm, *Lp, *X, *part, *S, *bs, *tmp;
+    int32_t* chol;
+    Staging work;
+    work.add((size_t)L * L, &H0);
+    work.add((size_t)L, &b0);
+    work.add((size_t)m * m, &Lm);
+    work.add((size_t)r * r, &Lp);
+    work.add((size_t)m * (r + 1), &X);
+    work.add((size_t)ls.n_part, &part);
+    work.add((size_t)r * r, &S);
+    work.add((size_t)r, &bs);
+    work.add((size_t)(2 * m + r), &tmp);
+    work.add(2, &chol);
+    hipError_t e = hipStreamSynchronize(c->stream);  // the pinned list staging may feed an earlier call
+    if (e != hipSuccess) return hip_err(c, e, "schur solve: stream");
+    void* hb = pinned(c, "lm_lists", lists.bytes());
+    void* db = scratch(c, "lm_lists", lists.bytes());
+    void* wb = scratch(c, "lm_work", work.bytes());
+    if (!hb || !db || !wb) return set_err(c, GVX_ERR_OOM, "schur solve staging");
+    lists.bind(db, hb);
+    work.bind(wb);
+    std::memcpy(h_rec, ls.recs.data(), sizeof(MargPairRec) * ls.recs.size());
+    if (!ls.contrib.empty()) std::memcpy(h_con, ls.contrib.data(), sizeof(int4) * ls.contrib.size());
+    std::memcpy(h_chk, ls.chunks.data(), sizeof(int4) * ls.chunks.size());
+    std::memcpy(h_rpart, ls.recpart.data(), sizeof(int2) * ls.recpart.size());
+    e = hipMemcpyAsync(db, hb, lists.bytes(), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(chol, 0, 2 * sizeof(int32_t), c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "schur solve: upload");
+    MargLaunch p{};
+    p.n_pairs = ls.n_pairs;
+    p.n_bvec = ls.n_bvec;
+    p.pairs = d_rec;
+    p.contrib = d_con;
+    p.data = d_data;
+    p.L = L;
+    p.m = m;
+    p.H0 = H0;
+    p.b0 = b0;
+    p.Lm = Lm;
+    p.Lp = Lp;
+    p.X = X;
+    p.chol = chol;
+    p.n_chunks = (int)ls.chunks.size();
+    p.chunks = d_chk;
+    p.recpart = d_rpart;
+    p.part = part;
+    hipEvent_t ev{};
+    prof_begin(c, "lm_step", &ev);
+    e = launch_lm_step(c, p, d_D, d_delta, d_S ? d_S : S, bs, tmp);
+    if (e == hipSuccess && d_info) e = hipMemcpyAsync(d_info, chol, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream);
+    prof_end(c, "lm_step", ev);
+    return hip_err(c, e, "schur solve kernels");
+}
+
+}  // namespace
+
+gvx_status gvx_schur_solve_dev(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
+                               const int32_t* blk, const int64_t* res_off, const int64_t* jac_off,
+                               const double* d_data, int64_t n_data, int32_t nb, const int32_t* size,
+                               const int32_t* index, int32_t m, int32_t L, const double* d_D, double* d_delta,
+                               double* d_S, int32_t* d_info) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!d_delta || (n_fac && !d_data)) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    hipSetDevice(c->device);
+    Lists ls;
+    gvx_status s = build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls);
+    if (s) return s;
+    return run_lm(c, ls, d_data, d_D, m, L, d_delta, d_S, d_info);
+}
+
+gvx_status gvx_schur_solve(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const int32_t* blk_off, const int32_t* blk,
+                           const int64_t* res_off, const int64_t* jac_off, const double* data, int64_t n_data,
+                           int32_t nb, const int32_t* size, const int32_t* index, int32_t m, int32_t L,
+                           const double* D, double* delta, double* S, int32_t* info) {
+    if (!c) return GVX_ERR_INVALID;
+    if (!delta || (n_fac && !data)) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    hipSetDevice(c->device);
+    Lists ls;
+    gvx_status s = build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls);
+    if (s) return s;
+    const int r = L - m;
+    double *d_in, *h_in, *d_D, *h_D, *d_delta, *h_delta, *d_S, *h_S;
+    int32_t *d_info, *h_info;
+    Staging st;
+    st.add((size_t)n_data, &d_in, &h_in);
+    st.add(D ? (size_t)L : 0, &d_D, &h_D);
+    st.add((size_t)L, &d_delta, &h_delta);
+    st.add((size_t)r * r, &d_S, &h_S);
+    st.add(2, &d_info, &h_info);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "schur solve: stream");
+    void* hb = pinned(c, "lm_io", st.bytes());
+    void* db = scratch(c, "lm_io", st.bytes());
+    if (!hb || !db) return set_err(c, GVX_ERR_OOM, "schur solve staging");
+    st.bind(db, hb);
+    if (n_data) std::memcpy(h_in, data, sizeof(double) * (size_t)n_data);
+    if (D) std::memcpy(h_D, D, sizeof(double) * (size_t)L);
+    e = hipMemcpyAsync(d_in, h_in, (size_t)((char*)d_delta - (char*)d_in), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "schur solve upload");
+    s = run_lm(c, ls, d_in, D ? d_D : nullptr, m, L, d_delta, d_S, d_info);
+    if (s) return s;
+    e = hipMemcpyAsync(h_delta, d_delta, (size_t)((char*)(d_info + 2) - (char*)d_delta), hipMemcpyDeviceToHost,
+                       c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "schur solve download");
+    std::memcpy(delta, h_delta, sizeof(double) * (size_t)L);
+    if (S) std::memcpy(S, h_S, sizeof(double) * (size_t)r * r);
     if (info) std::memcpy(info, h_info, sizeof(int32_t) * 2);
     return GVX_OK;
 }

@@ -226,3 +226,91 @@ hipError_t launch_lin_chol(gvx_ctx* c, int r, const double* Lp, double* J0, doub
 }
 
 }  // namespace gvx
+
+// ------------------------------------------------ LM step (DENSE_SCHUR)
+namespace gvx {
+namespace {
+
+// H(i, i) += D_i^2 (H column-major, ld L)
+__global__ void __launch_bounds__(256) add_diag_kernel(int L, double* __restrict__ H, const double* __restrict__ D) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < L) H[(long)i * L + i] += D[i] * D[i];
+}
+
+// x = L^-T b (one wave, back substitution over the rows of L, column-major ld n)
+__global__ void __launch_bounds__(64) trsv_t_kernel(int n, const double* __restrict__ L, const double* __restrict__ b,
+                                                    double* __restrict__ x_out, const int* __restrict__ gate) {
+    if (gate && *gate != 0) return;
+    const int lane = threadIdx.x;
+    double x[TRSV_ROWS];
+#pragma unroll
+    for (int s = 0; s < TRSV_ROWS; ++s) {
+        const int i = lane + 64 * s;
+        x[s] = i < n ? b[i] : 0.0;
+    }
+#pragma unroll
+    for (int s = TRSV_ROWS - 1; s >= 0; --s) {
+        if (64 * s >= n) continue;
+        for (int kk = min(63, n - 1 - 64 * s); kk >= 0; --kk) {
+            const int k = 64 * s + kk;
+            // x_k = x_k / L_kk, then x_i -= L(k, i) x_k for i < k (row k of L)
+            const long long bits = __double_as_longlong(x[s] / L[(long)k * n + k]);
+            const int lo = __builtin_amdgcn_readlane((int)bits, kk), hi = __builtin_amdgcn_readlane((int)(bits >> 32), kk);
+            const double xk = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+            if (lane == kk) x[s] = xk;
+#pragma unroll
+            for (int t = 0; t <= s; ++t) {
+                const int i = lane + 64 * t;
+                if (i < k) x[t] -= L[(long)i * n + k] * xk;
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < TRSV_ROWS; ++s) {
+        const int i = lane + 64 * s;
+        if (i < n) x_out[i] = x[s];
+    }
+}
+
+// t = be - Hef delta_f  (Hef = H0(0..m, m..L), column-major ld L)
+__global__ void __launch_bounds__(256) gemv_kernel(int L, int m, const double* __restrict__ H0,
+                                                   const double* __restrict__ b0, const double* __restrict__ df,
+                                                   double* __restrict__ t) {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= m) return;
+    double acc = 0.0;
+    for (int j = 0; j < L - m; ++j) acc += H0[(long)(m + j) * L + a] * df[j];
+    t[a] = b0[a] - acc;
+}
+
+}  // namespace
+
+hipError_t launch_lm_step(gvx_ctx* c, const MargLaunch& p, const double* D, double* delta, double* S, double* bs,
+                          double* tmp) {
+    const int m = p.m, r = p.L - m;
+    hipError_t e = launch_h0(c, p);
+    if (e != hipSuccess) return e;
+    if (D) {
+        add_diag_kernel<<<(p.L + 255) / 256, 256, 0, c->stream>>>(p.L, p.H0, D);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // Hee + D = Lm Lm^T; X = Lm^-1 [Hef | be]; S = Hff - X^T X, bs = bf - X^T y
+    if ((e = launch_potrf(c, m, p.H0, p.L, 0.0, p.Lm, p.chol, nullptr)) != hipSuccess) return e;
+    if ((e = launch_trsv(c, m, p.Lm, r, p.H0 + (size_t)m * p.L, p.L, p.X, r + 1, false, p.chol)) != hipSuccess)
+        return e;
+    if ((e = launch_trsv(c, m, p.Lm, 1, p.b0, m, p.X + r, r + 1, false, p.chol)) != hipSuccess) return e;
+    if ((e = launch_schur_chol(c, p.L, m, p.H0, p.b0, p.X, S, bs, p.chol)) != hipSuccess) return e;
+    // S = Lp Lp^T; delta_f = Lp^-T Lp^-1 bs
+    if ((e = launch_potrf(c, r, S, r, 0.0, p.Lp, p.chol + 1, p.chol)) != hipSuccess) return e;
+    if ((e = launch_trsv(c, r, p.Lp, 1, bs, r, tmp, 1, false, p.chol + 1)) != hipSuccess) return e;
+    trsv_t_kernel<<<1, 64, 0, c->stream>>>(r, p.Lp, tmp, delta + m, p.chol + 1);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // delta_e = Lm^-T Lm^-1 (be - Hef delta_f)
+    gemv_kernel<<<(m + 255) / 256, 256, 0, c->stream>>>(p.L, m, p.H0, p.b0, delta + m, tmp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_trsv(c, m, p.Lm, 1, tmp, m, tmp + m, 1, false, p.chol)) != hipSuccess) return e;
+    trsv_t_kernel<<<1, 64, 0, c->stream>>>(m, p.Lm, tmp + m, delta, p.chol);
+    return hipGetLastError();
+}
+
+}  // namespace gvx

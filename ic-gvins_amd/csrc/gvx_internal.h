@@ -231,8 +231,16 @@ struct MargLaunch {
     int solver;
     double *Lm, *Lp, *X;
     int* chol;
+    // FAST: H0 / b0 from contribution chunks (chunk = {record, c0, c1, partial
+    // offset}; recpart[k] = {first partial, chunks} of record k), partial sums in part
+    int n_chunks;
+    const int4* chunks;
+    const int2* recpart;
+    double* part;
 };
 hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p);
+// constructEquation alone (H0 = sum J^T J, b0 = -sum J^T e; chunked when p.chunks)
+hipError_t launch_h0(gvx_ctx* c, const MargLaunch& p);
 // ---- dense.hip (fp64 Cholesky kernels; gate: skipped unless *gate == 0) ----
 hipError_t launch_potrf(gvx_ctx* c, int n, const double* A, int lda, double shift, double* L, int* fail,
                         const int* gate);
@@ -241,6 +249,11 @@ hipError_t launch_trsv(gvx_ctx* c, int n, const double* L, int nrhs, const doubl
 hipError_t launch_schur_chol(gvx_ctx* c, int L, int m, const double* H0, const double* b0, const double* X,
                              double* Hp, double* bp, const int* gate);
 hipError_t launch_lin_chol(gvx_ctx* c, int r, const double* Lp, double* J0, double* eval, const int* gate);
+// (J^T J + diag(D^2)) delta = -J^T r with the first m local parameters eliminated
+// (DENSE_SCHUR): p's lists / H0 / b0 / Lm / Lp / X / chol (2 flags, zeroed by the
+// caller: potrf failures of Hee + D and of S); S r x r, bs r, tmp >= 2 m + r
+hipError_t launch_lm_step(gvx_ctx* c, const MargLaunch& p, const double* D, double* delta, double* S, double* bs,
+                          double* tmp);
 // SelfAdjointEigenSolver of the lower triangle of src (ld lds): V n x n, w n, hc n scratch, info 1 int;
 // ts (nullable, diagnostics): 7 u64, wall-clock stamps (100 MHz) of the solver's phases + QR iterations
 hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, double* V, double* w, double* hc,

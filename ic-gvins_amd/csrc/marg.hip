@@ -102,6 +102,61 @@ __global__ void __launch_bounds__(H0_THREADS) h0_kernel(int n_pairs, const MargP
     }
 }
 
+// The same sums split into chunks of a record's contribution list (the FAST
+// path: the extrinsic and td pairs of a window carry every reprojection factor,
+// 1,800 contributions that h0_kernel walks in one thread each): one workgroup
+// per chunk writes its partial sums, then h0_sum_kernel adds a record's partials
+// in chunk order.
+__global__ void __launch_bounds__(H0_THREADS) h0_part_kernel(int n_pairs, const MargPairRec* __restrict__ pairs,
+                                                             const int4* __restrict__ chunks,
+                                                             const int4* __restrict__ contrib,
+                                                             const double* __restrict__ data,
+                                                             const double* __restrict__ sr,
+                                                             double* __restrict__ part) {
+    const int4 ch = chunks[blockIdx.x];
+    const MargPairRec pr = pairs[ch.x];
+    const bool hrec = ch.x < n_pairs;
+    const int n_ent = pr.lp * pr.lq;
+    for (int e = threadIdx.x; e < n_ent; e += H0_THREADS) {
+        const int a = e % pr.lp, b = e / pr.lp;
+        double h = 0.0;
+        for (int ci = ch.y; ci < ch.z; ++ci) {
+            const int4 c = contrib[ci];
+            const int gp = c.z & 255, gq = (c.z >> 8) & 255, nres = c.z >> 16;
+            const double s = sr ? sr[c.w] : 1.0;
+            const double* jp = data + c.x + a;
+            const double* jq = data + c.y + (hrec ? b : 0);
+            double acc = 0.0;
+            for (int r = 0; r < nres; ++r) acc += (s * jp[(long)r * gp]) * (s * jq[(long)r * gq]);
+            if (hrec)
+                h += acc;
+            else
+                h -= acc;
+        }
+        part[ch.w + e] = h;
+    }
+}
+
+__global__ void __launch_bounds__(H0_THREADS) h0_sum_kernel(int n_pairs, const MargPairRec* __restrict__ pairs,
+                                                            const int2* __restrict__ recpart,
+                                                            const double* __restrict__ part, int L,
+                                                            double* __restrict__ H0, double* __restrict__ b0) {
+    const MargPairRec pr = pairs[blockIdx.x];
+    const int2 rp = recpart[blockIdx.x];
+    const int n_ent = pr.lp * pr.lq;
+    for (int e = threadIdx.x; e < n_ent; e += H0_THREADS) {
+        const int a = e % pr.lp, b = e / pr.lp;
+        double h = part[rp.x + e];
+        for (int k = 1; k < rp.y; ++k) h += part[rp.x + k * n_ent + e];
+        if ((int)blockIdx.x < n_pairs) {
+            H0[(long)(pr.col0 + b) * L + pr.row0 + a] = h;
+            H0[(long)(pr.row0 + a) * L + pr.col0 + b] = h;
+        } else {
+            b0[pr.row0 + a] = h;
+        }
+    }
+}
+
 // per-factor sqrt(rho') of a HuberLoss (ResidualBlockInfo::Evaluate, residual_block_info.h:59-87)
 __global__ void __launch_bounds__(64) loss_kernel(int n_fac, const int32_t* __restrict__ nres,
                                                   const int64_t* __restrict__ res_off,
@@ -710,20 +765,32 @@ hipError_t launch_sym_eigen(gvx_ctx* c, int n, const double* src, int lds, doubl
     return launch_eigen(c, n, src, lds, V, w, hc, info, ts);
 }
 
-hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p) {
-    const int r = p.L - p.m;
-    const bool fast = p.solver == GVX_MARG_SOLVER_FAST;
+hipError_t launch_h0(gvx_ctx* c, const MargLaunch& p) {
     hipError_t e = hipMemsetAsync(p.H0, 0, sizeof(double) * (size_t)p.L * p.L, c->stream);
     if (e != hipSuccess) return e;
     if (p.loss) {
         loss_kernel<<<(p.n_fac + 63) / 64, 64, 0, c->stream>>>(p.n_fac, p.nres, p.res_off, p.loss, p.data, p.sr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (p.n_pairs + p.n_bvec > 0) {
-        h0_kernel<<<p.n_pairs + p.n_bvec, H0_THREADS, 0, c->stream>>>(p.n_pairs, p.pairs, p.contrib, p.data,
-                                                                       p.loss ? p.sr : nullptr, p.L, p.H0, p.b0);
+    if (p.n_pairs + p.n_bvec <= 0) return hipSuccess;
+    if (p.chunks && p.n_chunks > 0) {
+        h0_part_kernel<<<p.n_chunks, H0_THREADS, 0, c->stream>>>(p.n_pairs, p.pairs, p.chunks, p.contrib, p.data,
+                                                                 p.loss ? p.sr : nullptr, p.part);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        h0_sum_kernel<<<p.n_pairs + p.n_bvec, H0_THREADS, 0, c->stream>>>(p.n_pairs, p.pairs, p.recpart, p.part,
+                                                                           p.L, p.H0, p.b0);
+        return hipGetLastError();
     }
+    h0_kernel<<<p.n_pairs + p.n_bvec, H0_THREADS, 0, c->stream>>>(p.n_pairs, p.pairs, p.contrib, p.data,
+                                                                   p.loss ? p.sr : nullptr, p.L, p.H0, p.b0);
+    return hipGetLastError();
+}
+
+hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p) {
+    const int r = p.L - p.m;
+    const bool fast = p.solver == GVX_MARG_SOLVER_FAST;
+    hipError_t e = launch_h0(c, p);
+    if (e != hipSuccess) return e;
     // FAST: Cholesky path where Hmm - EPS*I (then Hp - EPS*I) is positive definite
     // (dense.hip), the eigen-solver path below only where that check failed;
     // chol[k] != 0 marks the failure, read by the kernels on the device

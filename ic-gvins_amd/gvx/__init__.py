@@ -226,6 +226,8 @@ def _declare(L):
         "gvx_marg_factor_eval": (i32, [P, i32, i32, P, P, P, i32, P, P, P, P, P, P]),
         "gvx_marginalize": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
         "gvx_marginalize_dev": (i32, [P, i32, P, P, P, P, P, P, i64, P, i32, P, P, i32, i32, P, P, P, P, P, P]),
+        "gvx_schur_solve": (i32, [P, i32, P, P, P, P, P, P, i64, i32, P, P, i32, i32, P, P, P, P]),
+        "gvx_schur_solve_dev": (i32, [P, i32, P, P, P, P, P, P, i64, i32, P, P, i32, i32, P, P, P, P]),
         "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
         "gvx_set_marg_solver": (i32, [P, i32]),
         "gvx_find_fundamental_ransac": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
@@ -764,6 +766,28 @@ class Context:
                 np.ascontiguousarray(p["blk"], np.int32), np.ascontiguousarray(p["res_off"], np.int64),
                 np.ascontiguousarray(p["jac_off"], np.int64), np.ascontiguousarray(p["size"], np.int32),
                 np.ascontiguousarray(p["index"], np.int32), int(p["m"]), int(p["L"]))
+
+    def schur_solve(self, p, D=None):
+        """One LM step of the window the way Ceres' DENSE_SCHUR takes it
+        (gvx_schur_solve): p as marginalize's problem dict with the e-blocks
+        (inverse depths) at local indices [0, m) -> dict(delta [L], S [r, r], info [2])."""
+        nres, boff, blk, roff, joff, size, index, m, L = self._marg_struct(p)
+        data = np.ascontiguousarray(p["data"], np.float64)
+        Dv = None if D is None else np.ascontiguousarray(D, np.float64).reshape(L)
+        r = L - m
+        delta, S, info = np.zeros(L), np.zeros(max(r * r, 1)), np.zeros(2, np.int32)
+        self._check(self._L.gvx_schur_solve(self._h, nres.size, _ptr(nres), _ptr(boff), _ptr(blk), _ptr(roff),
+                                            _ptr(joff), _ptr(data), data.size, size.size, _ptr(size), _ptr(index), m,
+                                            L, _ptr(Dv), _ptr(delta), _ptr(S), _ptr(info)), "gvx_schur_solve")
+        return dict(delta=delta, S=S[:r * r].reshape(r, r).T.copy(), info=info)
+
+    def schur_solve_dev(self, p, d_data, d_delta, d_D=None, d_S=None, d_info=None):
+        """Device-pointer LM step (gvx_schur_solve_dev), async on the context stream."""
+        nres, boff, blk, roff, joff, size, index, m, L = self._marg_struct(p)
+        n_data = int(p["n_data"]) if "n_data" in p else int(np.asarray(p["data"]).size)
+        self._check(self._L.gvx_schur_solve_dev(self._h, nres.size, _ptr(nres), _ptr(boff), _ptr(blk), _ptr(roff),
+                                                _ptr(joff), d_data, n_data, size.size, _ptr(size), _ptr(index), m, L,
+                                                d_D, d_delta, d_S, d_info), "gvx_schur_solve_dev")
 
     def marginalize(self, p):
         """MarginalizationInfo::marginalization() after preMarginalization on a

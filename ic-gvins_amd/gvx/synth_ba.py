@@ -276,3 +276,44 @@ class DeviceFactorEvaluator:
 
     def marg(self, size, index, xoff, x0, x, J0, e0):
         return self.ctx.marg_factor_eval(size, index, xoff, x0, x, J0, e0)
+
+
+def lm_problem(p):
+    """A make_marg_problem problem re-laid-out for the LM step (gvx_schur_solve,
+    Ceres' DENSE_SCHUR): the e-blocks (inverse depths) at local indices [0, m), the
+    other blocks after them in block order."""
+    names = p["names"]
+    size = p["size"]
+    e = [b for b, n in enumerate(names) if n.startswith("invdepth")]
+    f = [b for b, n in enumerate(names) if not n.startswith("invdepth")]
+    index = np.zeros(len(names), np.int32)
+    o = 0
+    for b in e + f:
+        index[b] = o
+        o += 6 if size[b] == 7 else size[b]
+    m = sum(int(size[b]) for b in e)
+    return dict(p, index=index, m=int(m), L=int(o))
+
+
+def dense_normal_equations(p):
+    """(J^T J, -J^T r) of a problem dict in its local indices, from the dense
+    stacked Jacobian (pose blocks: the first 6 of their 7 columns) -- the numpy
+    check of gvx_schur_solve / marginalize's constructEquation."""
+    L = int(p["L"])
+    rows = int(np.sum(p["nres"]))
+    J = np.zeros((rows, L))
+    r = np.zeros(rows)
+    row = 0
+    data = p["data"]
+    for f in range(len(p["nres"])):
+        R = int(p["nres"][f])
+        r[row:row + R] = data[p["res_off"][f]:p["res_off"][f] + R]
+        off = int(p["jac_off"][f])
+        for b in p["blk"][p["blk_off"][f]:p["blk_off"][f + 1]]:
+            s = int(p["size"][b])
+            Jb = data[off:off + R * s].reshape(R, s)
+            loc = 6 if s == 7 else s
+            J[row:row + R, p["index"][b]:p["index"][b] + loc] = Jb[:, :loc]
+            off += R * s
+        row += R
+    return J.T @ J, -J.T @ r

@@ -546,6 +546,34 @@ gvx_status gvx_marginalize_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres,
                                const double* d_data, int64_t n_data, const double* d_loss, int32_t nb,
                                const int32_t* size, const int32_t* index, int32_t m, int32_t L, double* d_J0,
                                double* d_e0, double* d_Hp, double* d_bp, double* d_eval, int32_t* d_info);
+/* ------------------------------------------- LM step: DENSE_SCHUR reduced system */
+/* One Levenberg-Marquardt linear step of the sliding-window BA as Ceres takes
+   it with linear_solver_type = DENSE_SCHUR (ic_gvins.cc:1170-1180; Solve at
+   :1217 and :1251): the normal equations of the evaluated residual blocks,
+   (J^T J + diag(D^2)) delta = -J^T r, with the e-blocks (the landmarks' inverse
+   depths: local indices [0, m)) eliminated --
+     S = Hff - Hfe Hee^-1 Hef       (the reduced camera system, dense),
+     S delta_f = bf - Hfe Hee^-1 be  by Cholesky,
+     delta_e = Hee^-1 (be - Hef delta_f),     with b = -J^T r.
+   Residual blocks and block table as gvx_marginalize (pose blocks of global size
+   7 contribute their local 6 columns, PoseParameterization's [I6; 0]); m and
+   L - m at most 512; J and r are what Ceres' linear solver sees (robust-loss
+   corrections applied).  D (nullable, L local parameters): the LM
+   regularisation.  Outputs: delta [L] in local index order; S (nullable, r x r
+   column-major, r = L - m) and info (nullable, 2 ints: 1 where the Cholesky
+   factorisation of Hee + D, resp. S, met a non-positive pivot, else 0). */
+gvx_status gvx_schur_solve(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
+                           const int32_t* blk, const int64_t* res_off, const int64_t* jac_off, const double* data,
+                           int64_t n_data, int32_t nb, const int32_t* size, const int32_t* index, int32_t m,
+                           int32_t L, const double* D, double* delta, double* S, int32_t* info);
+/* The same with data, D and the outputs as device pointers, enqueued on the
+   context stream (the structure arrays stay host arrays). */
+gvx_status gvx_schur_solve_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
+                               const int32_t* blk, const int64_t* res_off, const int64_t* jac_off,
+                               const double* d_data, int64_t n_data, int32_t nb, const int32_t* size,
+                               const int32_t* index, int32_t m, int32_t L, const double* d_D, double* d_delta,
+                               double* d_S, int32_t* d_info);
+
 /* Eigen::SelfAdjointEigenSolver<MatrixXd>(A) with eigenvectors, the solver both
    steps above use: A n x n column-major (ld lda), lower triangle read, n <= 512.
    w [n] ascending, V n x n column-major, info 0 / 1 (NoConvergence). */

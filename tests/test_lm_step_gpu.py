@@ -1,0 +1,92 @@
+"""The LM step's DENSE_SCHUR reduced system on the device (gvx_schur_solve,
+csrc/dense.hip): Ceres with linear_solver_type = DENSE_SCHUR
+(ic_gvins/ic_gvins/ic_gvins.cc:1170-1180, Solve at :1217 and :1251) solves
+(J^T J + diag(D^2)) delta = -J^T r by eliminating the landmarks' inverse depths
+(the e-blocks) and factoring the dense reduced camera system S by Cholesky.
+
+Ceres is not available here, so the check is the linear algebra
+itself, from an independent dense assembly in numpy (synth_ba.dense_normal_
+equations: the stacked Jacobian of every residual block): S against the Schur
+complement of the dense normal matrix, delta against numpy.linalg.solve of the
+full damped system.  The window's normal matrix has a condition number of 2e17
+(inverse depths against the prior's strongest directions), so the forward error is
+held to 1e-9 with LM damping and to 1e-4 without (numpy's own Cholesky-Schur
+solve lands 6e-13 / 1.8e-6 from numpy.linalg.solve); the backward error -- the
+relative residual of the full system -- to 1e-14 either way."""
+import numpy as np
+import pytest
+
+from gvx import synth_ba
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def window(orc):
+    ev = orc.FactorEvaluator()
+    return {"configs[3] window (10 keyframes, 200 landmarks)": synth_ba.lm_problem(synth_ba.make_marg_problem(ev)),
+            "prior over keyframes 0-8": synth_ba.lm_problem(synth_ba.make_marg_problem(ev, n_prior_kf=9)),
+            "two keyframes": synth_ba.lm_problem(synth_ba.make_marg_problem(ev, seed=5, n_kf=2, n_lm=17))}
+
+
+def _check(g, p, D, fwd):
+    H, b = synth_ba.dense_normal_equations(p)
+    if D is not None:
+        H = H + np.diag(D * D)
+    m = p["m"]
+    Hee, Hef, Hff = H[:m, :m], H[:m, m:], H[m:, m:]
+    S = Hff - Hef.T @ np.linalg.solve(Hee, Hef)
+    assert list(g["info"]) == [0, 0]
+    Sg = g["S"]
+    assert np.abs(Sg - S).max() <= 1e-9 * np.abs(S).max(), np.abs(Sg - S).max() / np.abs(S).max()
+    x = np.linalg.solve(H, b)
+    d = g["delta"]
+    # the full damped system's relative residual
+    res = np.abs(H @ d - b).max() / (np.abs(H).max() * np.abs(d).max())
+    assert res <= 1e-14, res
+    assert np.abs(d - x).max() <= fwd * np.abs(x).max(), np.abs(d - x).max() / np.abs(x).max()
+
+
+@pytest.mark.parametrize("name", ["configs[3] window (10 keyframes, 200 landmarks)", "prior over keyframes 0-8",
+                                  "two keyframes"])
+def test_schur_solve_matches_dense(ctx, window, name):
+    p = window[name]
+    H, _ = synth_ba.dense_normal_equations(p)
+    # LM damping of the size Ceres applies: mu * diag(J^T J), mu = 1e-4
+    D = np.sqrt(1e-4 * np.maximum(np.diag(H), 1e-6))
+    _check(ctx.schur_solve(p, D), p, D, 1e-9)
+    _check(ctx.schur_solve(p), p, None, 1e-4)  # undamped (Gauss-Newton)
+
+
+def test_schur_solve_dev_matches_host(ctx, window):
+    import torch
+    p = window["prior over keyframes 0-8"]
+    L = p["L"]
+    D = np.full(L, 1e-2)
+    g = ctx.schur_solve(p, D)
+    dev = torch.device("cuda")
+    d_data = torch.from_numpy(p["data"]).to(dev)
+    d_D = torch.from_numpy(D).to(dev)
+    d_delta = torch.zeros(L, dtype=torch.float64, device=dev)
+    d_info = torch.full((2,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.schur_solve_dev(p, d_data.data_ptr(), d_delta.data_ptr(), d_D=d_D.data_ptr(), d_info=d_info.data_ptr())
+    ctx.sync()
+    assert np.array_equal(d_delta.cpu().numpy(), g["delta"])
+    assert d_info.cpu().tolist() == [0, 0]
+
+
+def test_schur_solve_reports_indefinite(ctx, window):
+    """An unobserved landmark without damping: Hee is singular, info[0] = 1."""
+    p = window["two keyframes"]
+    data = p["data"].copy()
+    lm = [b for b, n in enumerate(p["names"]) if n.startswith("invdepth")][0]
+    for f in range(len(p["nres"])):
+        off = int(p["jac_off"][f])
+        for b in p["blk"][p["blk_off"][f]:p["blk_off"][f + 1]]:
+            n = int(p["nres"][f]) * int(p["size"][b])
+            if b == lm:
+                data[off:off + n] = 0.0
+            off += n
+    g = ctx.schur_solve(dict(p, data=data))
+    assert g["info"][0] == 1
