@@ -744,7 +744,62 @@ def window_factor_leg(ctx, dev, reps=20, cpu=True):
             "gnss_roofline": {"bound": "hbm", "achieved": round(n * bytes_per / (per * 1e-3) / 1e9, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "algorithmic_bytes_per_factor": bytes_per},
             "marg_factor_r": r, "marg_factor_host_call_us": round(marg_us, 1),
-            "marginalization": marg_leg(ctx, dev, cpu=cpu)}
+            "marginalization": marg_leg(ctx, dev, cpu=cpu),
+            "lm_step": lm_step_leg(ctx, dev, cpu=cpu)}
+
+
+def lm_step_leg(ctx, dev, reps=20, cpu=True):
+    """One LM linear step of the configs[3] window as Ceres' DENSE_SCHUR takes it
+    (ic_gvins.cc:1170-1180): the normal equations of the window's evaluated
+    residual blocks (the marginalisation problem's blocks: prior, GNSS,
+    preintegration, 1,800 reprojection factors), the 200 inverse depths
+    eliminated, the 157 x 157 reduced camera system factored by Cholesky, the
+    step back-substituted (gvx_schur_solve_dev).  The CPU baseline is numpy's
+    dense solve of the same damped system (LAPACK, all host threads)."""
+    import torch
+    from gvx import synth_ba
+    p = synth_ba.lm_problem(synth_ba.make_marg_problem(synth_ba.DeviceFactorEvaluator(ctx)))
+    L = p["L"]
+    d_data = torch.from_numpy(p["data"]).to(dev)
+    H, b = synth_ba.dense_normal_equations(p)
+    D = np.sqrt(1e-4 * np.maximum(np.diag(H), 1e-6))
+    d_D = torch.from_numpy(D).to(dev)
+    d_delta = torch.empty(L, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def run():
+        ctx.schur_solve_dev(p, d_data.data_ptr(), d_delta.data_ptr(), d_D=d_D.data_ptr())
+
+    for _ in range(3):
+        run()
+    ctx.sync()
+    ctx.profile_reset()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+        ctx.sync()
+    wall = (time.perf_counter() - t0) / reps
+    ms, k = ctx.profile_read("lm_step")
+    ctx.profile(False)
+    out = {"what": "LM linear step (DENSE_SCHUR) of the configs[3] window: J^T J + D, 200 inverse depths "
+                   "eliminated, reduced camera system by Cholesky (gvx_schur_solve_dev)",
+           "eliminated": p["m"], "reduced": L - p["m"], "residual_blocks": len(p["nres"]),
+           "device_ms_per_call": round(ms / max(k, 1), 3), "call_ms": round(wall * 1e3, 3), "cpu_baseline": None}
+    if cpu:
+        Hd = H + np.diag(D * D)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 1.0 or n < 3:
+            Hs, bs = synth_ba.dense_normal_equations(p)
+            np.linalg.solve(Hs + np.diag(D * D), bs)
+            n += 1
+        el = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": round(el * 1e3, 2), "unit": "ms per LM step", "cores": host_threads(),
+                               "kind": "port", "sample": f"{n} steps: dense assembly of J^T J from the blocks + "
+                                                         "numpy.linalg.solve of the 357 x 357 damped system"}
+        del Hd
+    return out
 
 
 def marg_leg(ctx, dev, reps=10, cpu=True):
@@ -783,7 +838,24 @@ def marg_leg(ctx, dev, reps=10, cpu=True):
                    "linearization, marginalization_info.h:153-230)",
            "marginalized": p["m"], "remained": r, "residual_blocks": len(p["nres"]),
            "device_ms_per_call": round(ms / max(k, 1), 3), "call_ms": round(wall * 1e3, 3),
-           "bound": "latency (dependent fp64 Givens chain, one workgroup per eigen-solver)", "cpu_baseline": None}
+           "solver": "FAST (Cholesky where no eigenvalue is dropped; gvx_set_marg_solver)",
+           "bound": "latency (one-workgroup fp64 Cholesky factorisations and triangular solves)", "cpu_baseline": None}
+    # the EXACT solver (Eigen's SelfAdjointEigenSolver, bit-exact vs the restatement) beside it
+    import gvx
+    ctx.set_marg_solver(gvx.MARG_SOLVER_EXACT)
+    try:
+        run()
+        ctx.sync()
+        ctx.profile_reset()
+        ctx.profile(True)
+        for _ in range(3):
+            run()
+        ctx.sync()
+        ms_x, k_x = ctx.profile_read("marg")
+        ctx.profile(False)
+        out["exact_solver_device_ms_per_call"] = round(ms_x / max(k_x, 1), 3)
+    finally:
+        ctx.set_marg_solver(gvx.MARG_SOLVER_FAST)
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc  # test-infrastructure import: cpu_baseline leg only
