@@ -1,7 +1,7 @@
 // dense.hip -- fp64 dense Cholesky kernels for gfx950: the fast path of the
 // device marginalisation (MarginalizationInfo::schurElimination / linearization,
 // /root/reference/ic_gvins/ic_gvins/factors/marginalization_info.h:153-192) and
-// the building blocks of a reduced (Schur) system solve.
+// the LM step's DENSE_SCHUR reduced system (ic_gvins.cc:1170-1180).
 //
 // The reference inverts Hmm and factors Hp through Eigen's SelfAdjointEigenSolver,
 // dropping eigenvalues <= EPS = 1e-8.  When the smallest eigenvalue is above EPS
@@ -17,12 +17,17 @@
 // only where it failed, so no host round trip decides the path.
 //
 // potrf_kernel   one 1024-thread workgroup: right-looking blocked Cholesky of the
-//                lower triangle, 32-column panels factored in LDS, the trailing
-//                matrix updated in 4 x 4 register tiles from the panel in LDS.
-// trsv_kernel    one wave per right-hand side: forward substitution L x = b in
-//                axpy form (lane i owns rows i, i + 64, ...; the pivot of step k
-//                comes through v_readlane), the solution stored row-major.
-// schur_chol_kernel  Hp = Hrr - X^T X and bp = brr - X^T y, one thread per entry.
+//                lower triangle.  32-column panels in LDS (column-major, so a
+//                thread's rows are consecutive addresses), factored in the
+//                unscaled outer-product form a_ic -= a_ij a_cj / a_jj (column j is
+//                only read in step j: one barrier per step), scaled at the end;
+//                the trailing matrix updated in 4 x 4 register tiles.
+// trsv_kernel / trsv_t_kernel  one wave per right-hand side, L x = b / L^T x = b
+//                by 64-row blocks: the diagonal block in registers (64 steps of a
+//                v_readlane broadcast and one fma), the rows after (before) it
+//                updated with independent loads.
+// schur_chol_kernel  Hp = Hrr - X^T X, bp = brr - X^T y: 32 x 32 output tiles
+//                over 32-deep LDS slabs of X.
 // lin_chol_kernel    J0 = Lp^T.
 #include <hip/hip_runtime.h>
 
@@ -32,9 +37,15 @@ namespace gvx {
 
 namespace {
 
-constexpr int PT = 1024;  // potrf threads
-constexpr int NB = 32;    // panel width
-constexpr int PLD = NB + 1;
+constexpr int PT = 1024;                // potrf threads
+constexpr int NB = 32;                  // panel width
+constexpr int PR = GVX_EIG_MAX_N + 1;   // panel column stride in LDS (doubles)
+
+__device__ __forceinline__ double bcast(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane), hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 // L (n x n column-major, ld n) <- Cholesky factor of the lower triangle of
 // A - shift*I (A column-major, ld lda); the strict upper triangle of L is zeroed.
@@ -43,7 +54,7 @@ constexpr int PLD = NB + 1;
 __global__ void __launch_bounds__(PT) potrf_kernel(int n, const double* __restrict__ A, int lda, double shift,
                                                    double* __restrict__ L, int* __restrict__ fail,
                                                    const int* __restrict__ gate) {
-    __shared__ double P[GVX_EIG_MAX_N * PLD];  // panel rows k0 .. n-1, NB columns
+    __shared__ double P[NB * PR];  // panel rows k0 .. n-1 (i = row - k0), NB columns, P[c * PR + i]
     __shared__ int bad;
     if (gate && *gate != 0) return;
     const int tid = threadIdx.x;
@@ -53,56 +64,55 @@ __global__ void __launch_bounds__(PT) potrf_kernel(int n, const double* __restri
         L[idx] = i >= j ? A[(long)j * lda + i] - (i == j ? shift : 0.0) : 0.0;
     }
     __syncthreads();
+    // thread t: column tc (+ 32 k) of the panel, rows ti + 32 k
+    const int tc = tid >> 5, ti = tid & 31;
     for (int k0 = 0; k0 < n; k0 += NB) {
         const int nb = min(NB, n - k0), rows = n - k0;
-        for (int idx = tid; idx < rows * nb; idx += PT) {
-            const int i = idx % rows, c = idx / rows;
-            P[i * PLD + c] = L[(long)(k0 + c) * n + k0 + i];
-        }
+        for (int c = tc; c < nb; c += PT / 32)
+            for (int i = c + ti; i < rows; i += 32) P[c * PR + i] = L[(long)(k0 + c) * n + k0 + i];
         __syncthreads();
         for (int j = 0; j < nb; ++j) {
-            const double d = P[j * PLD + j];
+            const double d = P[j * PR + j];
             if (!(d > 0.0)) {  // every thread reads the same pivot
                 if (tid == 0) bad = 1;
                 break;
             }
-            const double piv = sqrt(d), inv = 1.0 / piv;
-            // scale column j below the pivot, then the rank-1 update of the panel's
-            // later columns (reading the unscaled column: (a/piv)(b/piv) = ab/d)
-            for (int idx = tid; idx < (rows - j - 1) * (nb - j - 1); idx += PT) {
-                const int c = j + 1 + idx / (rows - j - 1), i = j + 1 + idx % (rows - j - 1);
-                if (i >= c) P[i * PLD + c] -= (P[i * PLD + j] * inv) * (P[c * PLD + j] * inv);
+            const int c = j + 1 + tc;
+            if (c < nb) {
+                const double f = P[j * PR + c] / d;
+                for (int i = c + ti; i < rows; i += 32) P[c * PR + i] -= P[j * PR + i] * f;
             }
-            __syncthreads();
-            for (int i = j + 1 + tid; i < rows; i += PT) P[i * PLD + j] *= inv;
-            if (tid == 0) P[j * PLD + j] = piv;
             __syncthreads();
         }
         __syncthreads();
-        if (bad) break;
-        for (int idx = tid; idx < rows * nb; idx += PT) {
-            const int i = idx % rows, c = idx / rows;
-            if (i >= c) L[(long)(k0 + c) * n + k0 + i] = P[i * PLD + c];
+        if (bad) break;  // read after a barrier: uniform
+        // scale: l_ij = a_ij / sqrt(a_jj)
+        for (int j = tc; j < nb; j += PT / 32) {
+            const double s = sqrt(P[j * PR + j]), inv = 1.0 / s;
+            for (int i = j + 1 + ti; i < rows; i += 32) P[j * PR + i] *= inv;
+            if (ti == 0) P[j * PR + j] = s;
         }
-        // trailing update of the lower triangle, 4 x 4 tiles: T(i, c) -= sum_t P(i, t) P(c, t)
+        __syncthreads();
+        for (int c = tc; c < nb; c += PT / 32)
+            for (int i = c + ti; i < rows; i += 32) L[(long)(k0 + c) * n + k0 + i] = P[c * PR + i];
+        // trailing update of the lower triangle, 4 x 4 tiles: T(i, c) -= sum_q P(i, q) P(c, q)
         const int s = rows - nb;
         if (s > 0) {
             const int nt = (s + 3) / 4;
             const int tiles = nt * (nt + 1) / 2;
             for (int t = tid; t < tiles; t += PT) {
-                // t -> (ti, tc) with tc <= ti (row-major over the lower tile triangle)
-                int ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-                while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-                while (ti * (ti + 1) / 2 > t) --ti;
-                const int tc = t - ti * (ti + 1) / 2;
-                const int i0 = nb + 4 * ti, c0 = nb + 4 * tc;
+                int r4 = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+                while ((r4 + 1) * (r4 + 2) / 2 <= t) ++r4;
+                while (r4 * (r4 + 1) / 2 > t) --r4;
+                const int c4 = t - r4 * (r4 + 1) / 2;
+                const int i0 = nb + 4 * r4, c0 = nb + 4 * c4;
                 double acc[4][4] = {};
                 for (int q = 0; q < nb; ++q) {
                     double a[4], b[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        a[u] = i0 + u < rows ? P[(i0 + u) * PLD + q] : 0.0;
-                        b[u] = c0 + u < rows ? P[(c0 + u) * PLD + q] : 0.0;
+                        a[u] = i0 + u < rows ? P[q * PR + i0 + u] : 0.0;
+                        b[u] = c0 + u < rows ? P[q * PR + c0 + u] : 0.0;
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
@@ -123,10 +133,11 @@ __global__ void __launch_bounds__(PT) potrf_kernel(int n, const double* __restri
     if (tid == 0 && fail) *fail = bad;
 }
 
+constexpr int TRSV_ROWS = GVX_EIG_MAX_N / 64;
+
 // x = L^-1 b for nrhs right-hand sides, one wave each: b column j at B + j*ldb
 // (rows 0..n-1); x stored row-major: X[k * ldx + j].  neg: x = -L^-1 b.
 // Skipped when gate != nullptr and *gate != 0.
-constexpr int TRSV_ROWS = GVX_EIG_MAX_N / 64;
 __global__ void __launch_bounds__(64) trsv_kernel(int n, const double* __restrict__ L, int nrhs,
                                                   const double* __restrict__ B, long ldb, double* __restrict__ X,
                                                   int ldx, int neg, const int* __restrict__ gate) {
@@ -141,20 +152,33 @@ __global__ void __launch_bounds__(64) trsv_kernel(int n, const double* __restric
     }
 #pragma unroll
     for (int s = 0; s < TRSV_ROWS; ++s) {
-        if (64 * s >= n) break;
-        for (int kk = 0; kk < 64 && 64 * s + kk < n; ++kk) {
-            const int k = 64 * s + kk;
-            const double* col = L + (long)k * n;
-            // x_k = x_k / L_kk on its lane, then broadcast
-            const long long bits = __double_as_longlong(x[s] / col[k]);
-            const int lo = __builtin_amdgcn_readlane((int)bits, kk), hi = __builtin_amdgcn_readlane((int)(bits >> 32), kk);
-            const double xk = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-            if (lane == kk) x[s] = xk;
+        const int blk = 64 * s;
+        if (blk >= n) break;
+        const int nk = min(64, n - blk);
+        const int row = blk + lane;
+        // the diagonal block's entries of this lane's row, and 1 / L_ii
+        double d[64];
 #pragma unroll
-            for (int t = s; t < TRSV_ROWS; ++t) {
-                const int i = lane + 64 * t;
-                if (i > k && i < n) x[t] -= col[i] * xk;
+        for (int kk = 0; kk < 64; ++kk) d[kk] = (kk < nk && row < n) ? L[(long)(blk + kk) * n + row] : 0.0;
+        const double inv = row < n ? 1.0 / L[(long)row * n + row] : 0.0;
+        double xs = x[s];
+#pragma unroll
+        for (int kk = 0; kk < 64; ++kk) {
+            if (kk < nk) {
+                const double xk = bcast(xs * inv, kk);
+                if (lane == kk) xs = xk;
+                if (lane > kk) xs -= d[kk] * xk;
             }
+        }
+        x[s] = xs;
+        // rows of the later blocks: x_i -= sum_k L(i, k) x_k over this block's k
+#pragma unroll
+        for (int t = s + 1; t < TRSV_ROWS; ++t) {
+            if (64 * t >= n) break;
+            const int i = 64 * t + lane;
+            double acc = 0.0;
+            for (int kk = 0; kk < nk; ++kk) acc += (i < n ? L[(long)(blk + kk) * n + i] : 0.0) * bcast(xs, kk);
+            x[t] -= acc;
         }
     }
 #pragma unroll
@@ -164,22 +188,50 @@ __global__ void __launch_bounds__(64) trsv_kernel(int n, const double* __restric
     }
 }
 
-// Hp(a, b) = Hrr(a, b) - sum_k X(k, a) X(k, b), bp(a) = brr(a) - sum_k X(k, a) X(k, r)
-// (X row-major m x (r + 1), the last column y = L^-1 bm).  Skipped when *gate != 0.
+// Hp(a, b) = Hrr(a, b) - sum_k X(k, a) X(k, b) for b < r, bp(a) = brr(a) - sum_k
+// X(k, a) X(k, r) (X row-major m x (r + 1), its last column y = L^-1 bm): one
+// 256-thread workgroup per 32 x 32 output tile, 2 x 2 outputs per thread.
+// Skipped when *gate != 0.
+constexpr int ST = 32;
 __global__ void __launch_bounds__(256) schur_chol_kernel(int L, int m, const double* __restrict__ H0,
                                                          const double* __restrict__ b0, const double* __restrict__ X,
                                                          double* __restrict__ Hp, double* __restrict__ bp,
                                                          const int* __restrict__ gate) {
+    __shared__ double Xa[ST][ST + 1], Xb[ST][ST + 1];
     if (*gate != 0) return;
     const int r = L - m, w = r + 1;
-    const int a = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
-    if (a >= r) return;
-    double acc = 0.0;
-    for (int k = 0; k < m; ++k) acc += X[(long)k * w + a] * X[(long)k * w + b];
-    if (b < r)
-        Hp[(long)b * r + a] = H0[(long)(m + b) * L + m + a] - acc;
-    else
-        bp[a] = b0[m + a] - acc;
+    const int a0 = blockIdx.x * ST, b0t = blockIdx.y * ST;
+    const int tid = threadIdx.x, ta = (tid & 15) * 2, tb = (tid >> 4) * 2;
+    double acc[2][2] = {};
+    for (int k0 = 0; k0 < m; k0 += ST) {
+        for (int e = tid; e < ST * ST; e += 256) {
+            const int kk = e / ST, q = e % ST;
+            const int k = k0 + kk;
+            Xa[kk][q] = (k < m && a0 + q < r) ? X[(long)k * w + a0 + q] : 0.0;
+            Xb[kk][q] = (k < m && b0t + q < w) ? X[(long)k * w + b0t + q] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int kk = 0; kk < ST; ++kk) {
+            const double x0 = Xa[kk][ta], x1 = Xa[kk][ta + 1], y0 = Xb[kk][tb], y1 = Xb[kk][tb + 1];
+            acc[0][0] += x0 * y0;
+            acc[0][1] += x0 * y1;
+            acc[1][0] += x1 * y0;
+            acc[1][1] += x1 * y1;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const int a = a0 + ta + u, b = b0t + tb + v;
+            if (a >= r || b > r) continue;
+            if (b < r)
+                Hp[(long)b * r + a] = H0[(long)(m + b) * L + m + a] - acc[u][v];
+            else
+                bp[a] = b0[m + a] - acc[u][v];
+        }
 }
 
 // J0 = Lp^T (column-major r x r: J0(i, j) = Lp(j, i)); eval: NaN (not formed).
@@ -191,6 +243,80 @@ __global__ void __launch_bounds__(256) lin_chol_kernel(int r, const double* __re
     if (i >= r) return;
     J0[(long)j * r + i] = Lp[(long)i * r + j];
     if (j == 0 && eval) eval[i] = __builtin_nan("");
+}
+
+// H(i, i) += D_i^2 (H column-major, ld L)
+__global__ void __launch_bounds__(256) add_diag_kernel(int L, double* __restrict__ H, const double* __restrict__ D) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < L) H[(long)i * L + i] += D[i] * D[i];
+}
+
+// x = L^-T b (one wave, back substitution by 64-row blocks from the last: lane
+// l holds column blk + l of L, rows blk .. blk + 63 -- its diagonal-block row
+// entries, a contiguous run -- then the rows of the earlier blocks)
+__global__ void __launch_bounds__(64) trsv_t_kernel(int n, const double* __restrict__ L, const double* __restrict__ b,
+                                                    double* __restrict__ x_out, const int* __restrict__ gate) {
+    if (gate && *gate != 0) return;
+    const int lane = threadIdx.x;
+    double x[TRSV_ROWS];
+#pragma unroll
+    for (int s = 0; s < TRSV_ROWS; ++s) {
+        const int i = lane + 64 * s;
+        x[s] = i < n ? b[i] : 0.0;
+    }
+#pragma unroll
+    for (int s = TRSV_ROWS - 1; s >= 0; --s) {
+        const int blk = 64 * s;
+        if (blk >= n) continue;
+        const int nk = min(64, n - blk);
+        const int col = blk + lane;
+        // d[kk] = L(blk + kk, col): row blk + kk of L, this lane's column
+        double d[64];
+#pragma unroll
+        for (int kk = 0; kk < 64; ++kk) d[kk] = (kk < nk && col < n) ? L[(long)col * n + blk + kk] : 0.0;
+        const double inv = col < n ? 1.0 / L[(long)col * n + col] : 0.0;
+        double xs = x[s];
+#pragma unroll
+        for (int kk = 63; kk >= 0; --kk) {
+            if (kk >= nk) continue;
+            const double xk = bcast(xs * inv, kk);
+            if (lane == kk) xs = xk;
+            if (lane < kk) xs -= d[kk] * xk;
+        }
+        x[s] = xs;
+        // earlier rows: x_i -= sum_k L(k, i) x_k over this block's k (lane i reads
+        // its own contiguous run of column i)
+#pragma unroll
+        for (int t = 0; t < s; ++t) {
+            const int i = 64 * t + lane;
+            double acc = 0.0;
+            for (int kk = 0; kk < nk; ++kk) acc += L[(long)i * n + blk + kk] * bcast(xs, kk);
+            x[t] -= acc;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < TRSV_ROWS; ++s) {
+        const int i = lane + 64 * s;
+        if (i < n) x_out[i] = x[s];
+    }
+}
+
+// t = be - Hef delta_f  (Hef = H0(0..m, m..L), column-major ld L): a thread per
+// row, four independent partial sums
+__global__ void __launch_bounds__(256) gemv_kernel(int L, int m, const double* __restrict__ H0,
+                                                   const double* __restrict__ b0, const double* __restrict__ df,
+                                                   double* __restrict__ t) {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= m) return;
+    const int r = L - m;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int j = 0;
+    for (; j + 4 <= r; j += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += H0[(long)(m + j + u) * L + a] * df[j + u];
+    }
+    for (; j < r; ++j) acc[0] += H0[(long)(m + j) * L + a] * df[j];
+    t[a] = b0[a] - ((acc[0] + acc[1]) + (acc[2] + acc[3]));
 }
 
 }  // namespace
@@ -215,7 +341,8 @@ hipError_t launch_schur_chol(gvx_ctx* c, int L, int m, const double* H0, const d
                              double* Hp, double* bp, const int* gate) {
     const int r = L - m;
     if (r <= 0) return hipSuccess;
-    schur_chol_kernel<<<dim3((r + 255) / 256, r + 1), 256, 0, c->stream>>>(L, m, H0, b0, X, Hp, bp, gate);
+    schur_chol_kernel<<<dim3((r + ST - 1) / ST, (r + 1 + ST - 1) / ST), 256, 0, c->stream>>>(L, m, H0, b0, X, Hp, bp,
+                                                                                              gate);
     return hipGetLastError();
 }
 
@@ -224,66 +351,6 @@ hipError_t launch_lin_chol(gvx_ctx* c, int r, const double* Lp, double* J0, doub
     lin_chol_kernel<<<dim3((r + 255) / 256, r), 256, 0, c->stream>>>(r, Lp, J0, eval, gate);
     return hipGetLastError();
 }
-
-}  // namespace gvx
-
-// ------------------------------------------------ LM step (DENSE_SCHUR)
-namespace gvx {
-namespace {
-
-// H(i, i) += D_i^2 (H column-major, ld L)
-__global__ void __launch_bounds__(256) add_diag_kernel(int L, double* __restrict__ H, const double* __restrict__ D) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < L) H[(long)i * L + i] += D[i] * D[i];
-}
-
-// x = L^-T b (one wave, back substitution over the rows of L, column-major ld n)
-__global__ void __launch_bounds__(64) trsv_t_kernel(int n, const double* __restrict__ L, const double* __restrict__ b,
-                                                    double* __restrict__ x_out, const int* __restrict__ gate) {
-    if (gate && *gate != 0) return;
-    const int lane = threadIdx.x;
-    double x[TRSV_ROWS];
-#pragma unroll
-    for (int s = 0; s < TRSV_ROWS; ++s) {
-        const int i = lane + 64 * s;
-        x[s] = i < n ? b[i] : 0.0;
-    }
-#pragma unroll
-    for (int s = TRSV_ROWS - 1; s >= 0; --s) {
-        if (64 * s >= n) continue;
-        for (int kk = min(63, n - 1 - 64 * s); kk >= 0; --kk) {
-            const int k = 64 * s + kk;
-            // x_k = x_k / L_kk, then x_i -= L(k, i) x_k for i < k (row k of L)
-            const long long bits = __double_as_longlong(x[s] / L[(long)k * n + k]);
-            const int lo = __builtin_amdgcn_readlane((int)bits, kk), hi = __builtin_amdgcn_readlane((int)(bits >> 32), kk);
-            const double xk = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-            if (lane == kk) x[s] = xk;
-#pragma unroll
-            for (int t = 0; t <= s; ++t) {
-                const int i = lane + 64 * t;
-                if (i < k) x[t] -= L[(long)i * n + k] * xk;
-            }
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < TRSV_ROWS; ++s) {
-        const int i = lane + 64 * s;
-        if (i < n) x_out[i] = x[s];
-    }
-}
-
-// t = be - Hef delta_f  (Hef = H0(0..m, m..L), column-major ld L)
-__global__ void __launch_bounds__(256) gemv_kernel(int L, int m, const double* __restrict__ H0,
-                                                   const double* __restrict__ b0, const double* __restrict__ df,
-                                                   double* __restrict__ t) {
-    const int a = blockIdx.x * 256 + threadIdx.x;
-    if (a >= m) return;
-    double acc = 0.0;
-    for (int j = 0; j < L - m; ++j) acc += H0[(long)(m + j) * L + a] * df[j];
-    t[a] = b0[a] - acc;
-}
-
-}  // namespace
 
 hipError_t launch_lm_step(gvx_ctx* c, const MargLaunch& p, const double* D, double* delta, double* S, double* bs,
                           double* tmp) {
