@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "gvx_internal.h"
 
@@ -61,6 +62,20 @@ constexpr int LUT_THREADS = 256;
 constexpr int HROW = 257;  // histogram stride: one value in neighbouring tiles -> different banks
 constexpr int LUT_UNROLL = 8;
 
+// Inclusive prefix sum of v over the wave's 64 lanes: row_shr DPP steps within
+// each 16-lane row (no LDS round trip, unlike a shuffle), then the totals of
+// the lower rows by readlane.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
+                   r2 = __builtin_amdgcn_readlane(v, 47);
+    const int row = lane >> 4;
+    return v + (row > 0 ? r0 : 0u) + (row > 1 ? r1 : 0u) + (row > 2 ? r2 : 0u);
+}
+
 // CLAHE_CalcLut_Body for one tile, by one wavefront: h = the tile's 256 bins.
 __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, int lane, uint8_t* out) {
     uint32_t h4[4];
@@ -75,27 +90,26 @@ __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, 
                 cl += h4[i] - clip;
                 h4[i] = clip;
             }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) cl += __shfl_xor(cl, o, 64);
+        cl = __builtin_amdgcn_readlane(wave_incl_scan(cl, lane), 63);  // the tile's clipped total
         const uint32_t batch = cl / 256, residual = cl - batch * 256;
         const uint32_t step = residual ? max(256u / residual, 1u) : 1u;
+        // bin b gets one more where b % step == 0 and b / step < residual: one
+        // division for the lane's first bin, then carried over its four bins
+        uint32_t q = (4u * lane) / step, r = 4u * lane - q * step;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint32_t b = 4 * lane + i;
-            h4[i] += batch + ((residual && b % step == 0 && b / step < residual) ? 1u : 0u);
+            h4[i] += batch + ((residual && r == 0 && q < residual) ? 1u : 0u);
+            if (++r == step) {
+                r = 0;
+                ++q;
+            }
         }
     }
     uint32_t c4[4];
     c4[0] = h4[0];
 #pragma unroll
     for (int i = 1; i < 4; ++i) c4[i] = c4[i - 1] + h4[i];
-    uint32_t incl = c4[3];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-    }
-    const uint32_t base = incl - c4[3];
+    const uint32_t base = wave_incl_scan(c4[3], lane) - c4[3];
     uint32_t packed = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) packed |= sat_round_u8((float)(base + c4[i]) * g.lut_scale) << (8 * i);
@@ -412,6 +426,249 @@ __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t
     }
 }
 
+// ---------------------------------------------------------------------------
+// fused_kernel: both passes in one workgroup per (image, segment of bands), for
+// batches.  The workgroup walks its bands top to bottom; each thread owns one
+// 8-pixel column chunk and the rows ph, ph + nph, ... of every tile row, and
+// holds the pixels of the three tile rows in use in registers: while band b is
+// blended from tile rows b-1 and b, tile row b+1 is loaded, its histograms are
+// built and turned into LUT row b+1 (two LUT-row buffers, by parity), and the
+// band's table is rebuilt from LUT rows b and b+1.  Every source pixel is read
+// from HBM once and every output pixel written once (2 B/px against 3 B/px for
+// lut_kernel + apply_kernel), and BGR8 frames are converted in registers (no
+// gray scratch).  The table holds the four LUT values of an entry as fp32
+// (16 B, one ds_read_b128 per pixel), so the blend needs no byte conversions,
+// and the result is rounded and packed by v_cvt_pk_u8_f32 (round half to even,
+// saturating: cvRound + saturate_cast, tools/cvt_pk_u8_probe.hip).  The
+// arithmetic is that of lut_kernel / apply_kernel (same tile_lut, same fp32
+// blend order), so the two paths are bit-identical.  Segments > 1 recompute the
+// LUT row at each seam, so src must not overlap dst (the host keeps in-place
+// calls on the two-kernel path).
+template <int RMAX, int CHAN, bool VEC8>
+__global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__ src, int64_t img_stride,
+                                                     int stride, uint8_t* __restrict__ dst, int64_t dst_img_stride,
+                                                     int dst_stride, ClaheGeom g, int nseg, int cpr, int nph,
+                                                     uint32_t* __restrict__ hist_img) {
+    extern __shared__ float4 smf[];
+    float4* tab = smf;                                                     // (tiles_x + 1) * TROW entries
+    uint32_t* hs = reinterpret_cast<uint32_t*>(tab + (g.tiles_x + 1) * TROW);  // tiles_x histograms, HROW apart
+    uint32_t* lrb = hs + g.tiles_x * HROW;         // 2 x tiles_x * 64 dwords: LUT rows by parity
+    uint32_t* ih = lrb + 2 * g.tiles_x * 64;       // 256: in-image counts (histogram check)
+    const int nb = g.tiles_y + 1;
+    const int img = blockIdx.x / nseg, seg = blockIdx.x - img * nseg;
+    const int b0 = seg * nb / nseg, b1 = (seg + 1) * nb / nseg;
+    const int t = threadIdx.x, nthr = blockDim.x, wave = t >> 6, lane = t & 63, nwave = nthr >> 6;
+    const int c8 = t % cpr, ph = t / cpr;
+    const bool act = ph < nph;
+    const int x0 = 8 * c8, nv = min(8, g.w - x0);
+    const bool fast = VEC8;  // 8-byte aligned rows, w % 8 == 0: every chunk is whole
+    const uint8_t* s = src + (int64_t)img * img_stride;
+    uint8_t* dd = dst + (int64_t)img * dst_img_stride;
+    const float inv_th = 1.0f / g.th, inv_tw = 1.0f / g.tw;
+    const int ew = g.tiles_x * g.tw;
+    for (int i = t; i < g.tiles_x * HROW; i += nthr) hs[i] = 0;
+    if (hist_img)
+        for (int i = t; i < 256; i += nthr) ih[i] = 0;
+    // column terms: the histogram bin offset (-1 past the image) and the blend terms
+    int hoff[8], ko[8];
+    float xa[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int x = x0 + j;
+        hoff[j] = x < g.w ? div_small(x, g.tw, inv_tw) * HROW : -1;
+        const float txf = (float)x * inv_tw - 0.5f;
+        const int tx1 = (int)floorf(txf);
+        xa[j] = txf - (float)tx1;
+        ko[j] = (min(tx1, g.tiles_x - 1) + 1) * TROW;  // table entry of (tx1 + 1, value 0)
+    }
+    auto pixel = [&](int y, int x) -> uint32_t {
+        const uint8_t* p = s + (int64_t)y * stride;
+        return CHAN == 3 ? bgr_gray(p[3 * x], p[3 * x + 1], p[3 * x + 2]) : p[x];
+    };
+    // row slot i of tile row k: y = k*th + ph + nph*i (valid when inside the tile row and the image)
+    auto slot_row = [&](int k, int i) -> int {
+        const int yr = ph + nph * i;
+        return (act && yr < g.th) ? k * g.th + yr : -1;
+    };
+    // raw loads of tile row k (CHAN 3: 24 bytes per chunk, converted in gray_of)
+    auto load = [&](int k, uint2 (&raw)[RMAX][CHAN]) {
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) {
+            const int y = slot_row(k, i);
+            if (y >= 0 && y < g.h) {
+                const uint8_t* p = s + (int64_t)y * stride + CHAN * x0;
+                if (fast) {
+#pragma unroll
+                    for (int q = 0; q < CHAN; ++q) raw[i][q] = reinterpret_cast<const uint2*>(p)[q];
+                } else {
+                    uint32_t lo = 0, hi = 0;
+                    for (int j = 0; j < nv; ++j) {
+                        const uint32_t v = pixel(y, x0 + j);
+                        if (j < 4)
+                            lo |= v << (8 * j);
+                        else
+                            hi |= v << (8 * (j - 4));
+                    }
+                    raw[i][0] = uint2{lo, hi};  // already gray (gray_of passes it through)
+                }
+            }
+        }
+    };
+    auto gray_of = [&](const uint2 (&r)[CHAN]) -> uint2 {
+        if (CHAN == 1 || !fast) return r[0];
+        uint32_t gw[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            gw[j >> 2] |= bgr_gray(byte24(r[0], r[CHAN / 2], r[CHAN - 1], 3 * j),
+                                   byte24(r[0], r[CHAN / 2], r[CHAN - 1], 3 * j + 1),
+                                   byte24(r[0], r[CHAN / 2], r[CHAN - 1], 3 * j + 2))
+                          << (8 * (j & 3));
+        return uint2{gw[0], gw[1]};
+    };
+    // histograms of tile row k: in-image pixels (from registers), the image
+    // histogram, then the REFLECT_101 pad pixels of copyMakeBorder; LUT row -> lr
+    auto build_lut_row = [&](int k, const uint2 (&px)[RMAX], bool count_img) {
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) {
+            const int y = slot_row(k, i);
+            if (y < 0 || y >= g.h) continue;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t v = ((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u;
+                if (hoff[j] >= 0) atomicAdd(&hs[hoff[j] + v], 1u);
+            }
+        }
+        if (hist_img && count_img) {
+            __syncthreads();
+            for (int b = t; b < 256; b += nthr) {
+                uint32_t sum = 0;
+                for (int tx = 0; tx < g.tiles_x; ++tx) sum += hs[tx * HROW + b];
+                ih[b] += sum;
+            }
+            __syncthreads();
+        }
+        const int y0 = k * g.th, rows_in = max(0, min(y0 + g.th, g.h) - y0);
+        if (ew > g.w) {
+            const int pc = ew - g.w;
+            for (int i = t; i < rows_in * pc; i += nthr) {
+                const int r = i / pc, x = g.w + (i - r * pc);
+                atomicAdd(&hs[div_small(x, g.tw, inv_tw) * HROW + pixel(y0 + r, refl101(x, g.w))], 1u);
+            }
+        }
+        const int pr = g.th - rows_in;
+        for (int i = t; i < pr * ew; i += nthr) {
+            const int r = i / ew, x = i - r * ew;
+            const int sy = refl101(y0 + rows_in + r, g.h);
+            atomicAdd(&hs[div_small(x, g.tw, inv_tw) * HROW + pixel(sy, refl101(x, g.w))], 1u);
+        }
+        __syncthreads();
+        uint32_t* lr = lrb + (k & 1) * g.tiles_x * 64;
+        for (int tx = wave; tx < g.tiles_x; tx += nwave) {
+            tile_lut(hs + tx * HROW, g, lane, reinterpret_cast<uint8_t*>(lr + tx * 64));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) hs[tx * HROW + 4 * lane + q] = 0;
+        }
+        __syncthreads();
+    };
+    // the band's table from LUT rows p (ty1) and q (ty2): entry (k, v) =
+    // {L[p][tx1c][v], L[p][tx2c][v], L[q][tx1c][v], L[q][tx2c][v]} as fp32,
+    // tx1c = max(k - 1, 0), tx2c = min(k, tiles_x - 1) (the reference's clamps)
+    auto table = [&](int p, int q) {
+        const uint32_t* P = lrb + (p & 1) * g.tiles_x * 64;
+        const uint32_t* Q = lrb + (q & 1) * g.tiles_x * 64;
+        const int items = (g.tiles_x + 1) * 64;
+        for (int i = t; i < items; i += nthr) {
+            const int k = i >> 6, qd = i & 63;
+            const int ta = max(k - 1, 0) * 64 + qd, tb = min(k, g.tiles_x - 1) * 64 + qd;
+            const uint32_t a = P[ta], bb = P[tb], c = Q[ta], d = Q[tb];
+            float4* o = tab + k * TROW + 4 * qd;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                o[j] = float4{(float)((a >> (8 * j)) & 255u), (float)((bb >> (8 * j)) & 255u),
+                              (float)((c >> (8 * j)) & 255u), (float)((d >> (8 * j)) & 255u)};
+        }
+    };
+    // CLAHE_Interpolation_Body for the rows of tile row k in [ys, ye) held in px
+    auto apply = [&](int k, const uint2 (&px)[RMAX], int ys, int ye) {
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) {
+            const int y = slot_row(k, i);
+            if (y < ys || y >= ye) continue;
+            const float tyf = (float)y * inv_th - 0.5f;
+            const float ya = tyf - floorf(tyf), ya1 = 1.0f - ya;
+            uint32_t out[2] = {0, 0};
+            float4 ev[8];  // the 8 gathers first, then the blends
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ev[j] = tab[ko[j] + (((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u)];
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // the scheduler keeps the 8 reads together
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float4 e = ev[j];
+                const float xa1 = 1.0f - xa[j];
+                const float res = (e.x * xa1 + e.y * xa[j]) * ya1 + (e.z * xa1 + e.w * xa[j]) * ya;
+                out[j >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(res, j & 3, out[j >> 2]);
+            }
+            uint8_t* drow = dd + (int64_t)y * dst_stride + x0;
+            if (fast)
+                *reinterpret_cast<uint2*>(drow) = uint2{out[0], out[1]};
+            else
+                for (int j = 0; j < nv; ++j) drow[j] = (uint8_t)(out[j >> 2] >> (8 * (j & 3)));
+        }
+    };
+    uint2 raw[RMAX][CHAN], prv[RMAX], cur[RMAX];
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i) prv[i] = cur[i] = uint2{0, 0};
+    // prologue: the table of band b0 (LUT rows max(b0-1, 0) and min(b0, tiles_y-1));
+    // tile row k enters the image histogram in the segment with b0 <= k < b1
+    {
+        const int r1 = max(b0 - 1, 0);
+        load(r1, raw);
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) cur[i] = gray_of(raw[i]);
+        build_lut_row(r1, cur, r1 >= b0);
+        if (b0 >= 1 && b0 < g.tiles_y) {
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) prv[i] = cur[i];
+            load(b0, raw);
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) cur[i] = gray_of(raw[i]);
+            build_lut_row(b0, cur, true);
+        } else if (b0 >= 1) {
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) prv[i] = cur[i];
+        }
+        table(r1, min(b0, g.tiles_y - 1));
+        __syncthreads();
+    }
+    for (int b = b0; b < b1; ++b) {
+        const bool more = b + 1 < b1;                // band b+1 is this segment's too
+        const bool nrow = more && b + 1 < g.tiles_y;  // ... and brings tile row b+1
+        if (nrow) load(b + 1, raw);                  // in flight while band b is blended
+        const int ys = b == 0 ? 0 : first_row(b - 1, g, inv_th);
+        const int ye = b == g.tiles_y ? g.h : first_row(b, g, inv_th);
+        if (b >= 1) apply(b - 1, prv, ys, ye);
+        if (b < g.tiles_y) apply(b, cur, ys, ye);
+        if (!more) break;
+#pragma unroll
+        for (int i = 0; i < RMAX; ++i) prv[i] = cur[i];
+        if (nrow) {
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) cur[i] = gray_of(raw[i]);
+            build_lut_row(b + 1, cur, true);  // its first barrier also ends band b's table reads
+            table(b, b + 1);
+        } else {
+            __syncthreads();
+            table(b, b);  // the last band: ty1 = ty2 = tiles_y - 1
+        }
+        __syncthreads();
+    }
+    if (hist_img) {
+        __syncthreads();
+        for (int b = t; b < 256; b += nthr)
+            if (ih[b]) atomicAdd(&hist_img[img * 256 + b], ih[b]);
+    }
+}
+
 __global__ void __launch_bounds__(64) mean_kernel(const uint32_t* __restrict__ hist_img, int n, int w, int h,
                                                   double* __restrict__ mean) {
     const int img = blockIdx.x * 64 + threadIdx.x;
@@ -444,6 +701,48 @@ ClaheGeom clahe_geometry(int w, int h, double clip_limit, int tiles_x, int tiles
     return g;
 }
 
+namespace {
+
+// Batches of at least this many images take fused_kernel; smaller calls (the
+// live path's single frame, picked on the device by src_index) keep the
+// two-kernel form, whose LUT pass spreads one frame over hundreds of workgroups.
+constexpr int FUSED_MIN_BATCH = 8;
+
+// fused_kernel's LDS: the fp32 table, the histograms, two LUT rows, the image histogram
+size_t fused_lds(const ClaheGeom& g) {
+    return (size_t)(g.tiles_x + 1) * TROW * 16 + ((size_t)g.tiles_x * HROW + 2 * g.tiles_x * 64 + 256) * 4;
+}
+
+struct FusedPlan {
+    int rmax = 0;  // 0: two-kernel path
+    int nseg = 1, cpr = 0, nph = 0, threads = 0;
+};
+
+FusedPlan clahe_fused_plan(const gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
+                           int stride, int chan, const uint8_t* dst, int64_t dst_img_stride, int dst_stride,
+                           const int32_t* src_index, int ring) {
+    FusedPlan p;
+    if (n < FUSED_MIN_BATCH || src_index || ring) return p;
+    // source and destination must not overlap: segment seams re-read rows
+    const int r = 0;
+    const uintptr_t s0 = (uintptr_t)src, s1 = s0 + (uintptr_t)((n - 1) * img_stride + (int64_t)(g.h - 1) * stride + chan * g.w);
+    const uintptr_t d0 = (uintptr_t)dst - (uintptr_t)((int64_t)r * dst_stride + r);
+    const uintptr_t d1 = (uintptr_t)dst + (uintptr_t)((n - 1) * dst_img_stride + (int64_t)(g.h - 1 + r) * dst_stride + g.w + r);
+    if (s0 < d1 && d0 < s1) return p;
+    p.cpr = (g.w + 7) / 8;
+    if (p.cpr > 1024 || fused_lds(g) > 160 * 1024) return p;
+    p.nph = std::min(1024 / p.cpr, g.th);
+    const int rows = (g.th + p.nph - 1) / p.nph;  // row slots per thread and tile row
+    if (rows > 8) return p;
+    p.rmax = rows <= 2 ? 2 : (rows == 7 ? 8 : rows);  // the instantiated slot counts
+    p.threads = (p.nph * p.cpr + 63) / 64 * 64;
+    const int nb = g.tiles_y + 1;
+    while ((int64_t)n * p.nseg < c->n_cu && p.nseg < nb) ++p.nseg;
+    return p;
+}
+
+}  // namespace
+
 hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* src, int64_t img_stride,
                         int stride, uint8_t* dst, int64_t dst_img_stride, int dst_stride, uint8_t* lut,
                         uint32_t* hist_img, double* hist_mean, const int32_t* src_index, int n_src, int ring,
@@ -457,6 +756,36 @@ hipError_t launch_clahe(gvx_ctx* c, int n, const ClaheGeom& g, const uint8_t* sr
     }
     const bool src8 = (uintptr_t)src % 8 == 0 && stride % 8 == 0 && img_stride % 8 == 0;
     const bool dst8 = (uintptr_t)dst % 8 == 0 && dst_stride % 8 == 0 && dst_img_stride % 8 == 0;
+    const FusedPlan fp = clahe_fused_plan(c, n, g, src, img_stride, stride, chan, dst, dst_img_stride, dst_stride,
+                                          src_index, ring);
+    if (fp.rmax) {
+        const bool vec8 = src8 && dst8 && g.w % 8 == 0;
+        const size_t lds = fused_lds(g);
+        const dim3 grid(n * fp.nseg), block(fp.threads);
+        auto go = [&](auto k8, auto k1) {
+            hipLaunchKernelGGL(vec8 ? k8 : k1, grid, block, lds, c->stream, src, img_stride, stride, dst,
+                               dst_img_stride, dst_stride, g, fp.nseg, fp.cpr, fp.nph, hist_img);
+        };
+        auto pick = [&](auto chan_tag) {
+            constexpr int C = decltype(chan_tag)::value;
+            switch (fp.rmax) {
+                case 2: go(fused_kernel<2, C, true>, fused_kernel<2, C, false>); break;
+                case 3: go(fused_kernel<3, C, true>, fused_kernel<3, C, false>); break;
+                case 4: go(fused_kernel<4, C, true>, fused_kernel<4, C, false>); break;
+                case 5: go(fused_kernel<5, C, true>, fused_kernel<5, C, false>); break;
+                case 6: go(fused_kernel<6, C, true>, fused_kernel<6, C, false>); break;
+                default: go(fused_kernel<8, C, true>, fused_kernel<8, C, false>); break;
+            }
+        };
+        if (chan == 3)
+            pick(std::integral_constant<int, 3>{});
+        else
+            pick(std::integral_constant<int, 1>{});
+        if (hist_img && hist_mean)
+            hipLaunchKernelGGL(mean_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, (const uint32_t*)hist_img, n,
+                               g.w, g.h, hist_mean);
+        return hipGetLastError();
+    }
     const int lut_vec8 = src8 && g.w % 8 == 0;
     // tiles per workgroup: a whole tile row for batches, fewer for single frames
     int ngrp = 1;
