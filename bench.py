@@ -186,6 +186,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="configs[4]: one graph per frame, frame t+1's CLAHE + pyramid after frame t's tracking "
                          "(default: beside it, a preprocessing graph on a side stream)")
+    ap.add_argument("--eig-branch", action="store_true",
+                    help="configs[4] pipelined: the detection's eigenvalue map on the preprocessing branch")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
     ap.add_argument("--accum", default="exact", choices=tuple(ACCUM_MODES),
                     help="LK window-sum order (gvx_klt_params.accum): exact integer sums (default), or "
@@ -936,7 +938,7 @@ def sequence_main(args):
         # side stream beside frame t's tracking graph (the outputs are the same:
         # tests/test_sequence_gpu.py); --no-pipeline: one graph per frame
         tracker = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=True, device=dev, frames=frames,
-                                        pipeline=not args.no_pipeline)
+                                        pipeline=not args.no_pipeline, eig_branch=args.eig_branch)
 
         def frame(t):
             tracker.step()

@@ -32,7 +32,7 @@ gvx_status hip_err(gvx_ctx* c, hipError_t e, const char* what) {
 }
 
 // both streams of the context (the side branch's too) before memory is freed
-static void sync_all(gvx_ctx* c) {
+void sync_all(gvx_ctx* c) {
     hipStreamSynchronize(c->main);
     if (c->side) hipStreamSynchronize(c->side);
 }
@@ -170,7 +170,10 @@ void gvx_destroy(gvx_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->main);
     if (c->side) hipStreamSynchronize(c->side);
-    for (auto& f : c->frames) hipFree(f.second.pyr);
+    for (auto& f : c->frames) {
+        hipFree(f.second.pyr);
+        hipFree(f.second.eig);
+    }
     for (auto& b : c->dev) hipFree(b.second.p);
     for (auto& b : c->pinned) hipHostFree(b.second.p);
     for (auto& p : c->pending) {
@@ -291,6 +294,7 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
     f.lay = lay;
     f.w = w;
     f.h = h;
+    ++f.gen;
     size_t nb = (size_t)h * w;
     uint8_t* hst = (uint8_t*)pinned(c, "frame_in", nb);
     uint8_t* dsrc = (uint8_t*)scratch(c, "frame_in", nb);
@@ -331,6 +335,7 @@ gvx_status gvx_frame_drop(gvx_ctx* c, uint64_t id) {
     ++c->mem_gen;
     sync_all(c);
     hipFree(it->second.pyr);
+    hipFree(it->second.eig);
     c->frames.erase(it);
     return GVX_OK;
 }
@@ -668,6 +673,7 @@ gvx_status frame_slot(gvx_ctx* c, uint64_t id, int32_t w, int32_t h, const gvx_k
     f.lay = lay;
     f.w = w;
     f.h = h;
+    ++f.gen;  // a new image: an eigenvalue map computed before is stale
     *out = &f;
     return GVX_OK;
 }

@@ -391,7 +391,8 @@ __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t
                     const float l11 = (float)(e & 255u), l12 = (float)((e >> 8) & 255u);
                     const float l21 = (float)((e >> 16) & 255u), l22 = (float)(e >> 24);
                     const float res = (l11 * xa1[j] + l12 * xa[j]) * ya1 + (l21 * xa1[j] + l22 * xa[j]) * ya;
-                    out[j >> 2] |= sat_round_u8(res) << (8 * (j & 3));
+                    // cvRound + saturate_cast<uchar> in one instruction (tools/cvt_pk_u8_probe.hip)
+                    out[j >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(res, j & 3, out[j >> 2]);
                 }
                 uint8_t* drow = dd + (int64_t)y * dst_stride + x0;
                 if (fast) {
@@ -452,7 +453,7 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
     extern __shared__ float4 smf[];
     float4* tab = smf;                                                     // (tiles_x + 1) * TROW entries
     uint32_t* hs = reinterpret_cast<uint32_t*>(tab + (g.tiles_x + 1) * TROW);  // tiles_x histograms, HROW apart
-    uint32_t* lrb = hs + g.tiles_x * HROW;         // 2 x tiles_x * 64 dwords: LUT rows by parity
+    uint32_t* lrb = hs + (g.tiles_x + 1) * HROW;   // 2 x tiles_x * 64 dwords: LUT rows by parity
     uint32_t* ih = lrb + 2 * g.tiles_x * 64;       // 256: in-image counts (histogram check)
     const int nb = g.tiles_y + 1;
     const int img = blockIdx.x / nseg, seg = blockIdx.x - img * nseg;
@@ -470,16 +471,19 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
     if (hist_img)
         for (int i = t; i < 256; i += nthr) ih[i] = 0;
     // column terms: the histogram bin offset (-1 past the image) and the blend terms
-    int hoff[8], ko[8];
+    // kh[j]: the table entry of (tx1 + 1, value 0) in the low half, the histogram
+    // offset of column x in the high half (past the image: a scratch histogram
+    // that is never read), one register per column
+    uint32_t kh[8];
     float xa[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int x = x0 + j;
-        hoff[j] = x < g.w ? div_small(x, g.tw, inv_tw) * HROW : -1;
+        const int hoff = (x < g.w ? div_small(x, g.tw, inv_tw) : g.tiles_x) * HROW;
         const float txf = (float)x * inv_tw - 0.5f;
         const int tx1 = (int)floorf(txf);
         xa[j] = txf - (float)tx1;
-        ko[j] = (min(tx1, g.tiles_x - 1) + 1) * TROW;  // table entry of (tx1 + 1, value 0)
+        kh[j] = (uint32_t)((min(tx1, g.tiles_x - 1) + 1) * TROW) | ((uint32_t)hoff << 16);
     }
     auto pixel = [&](int y, int x) -> uint32_t {
         const uint8_t* p = s + (int64_t)y * stride;
@@ -492,6 +496,22 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
     };
     // raw loads of tile row k (CHAN 3: 24 bytes per chunk, converted in gray_of)
     auto load = [&](int k, uint2 (&raw)[RMAX][CHAN]) {
+        if (fast) {
+            // branch-free: a slot outside the tile row or the image reads row 0
+            // (its value is never used), so the loads issue back to back
+#pragma unroll
+            for (int i = 0; i < RMAX; ++i) {
+                const int y0 = slot_row(k, i);
+                const int y = (y0 >= 0 && y0 < g.h) ? y0 : 0;
+                const uint64_t* p = reinterpret_cast<const uint64_t*>(s + (int64_t)y * stride + CHAN * x0);
+#pragma unroll
+                for (int q = 0; q < CHAN; ++q) {
+                    const uint64_t v = __builtin_nontemporal_load(p + q);
+                    raw[i][q] = uint2{(uint32_t)v, (uint32_t)(v >> 32)};
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < RMAX; ++i) {
             const int y = slot_row(k, i);
@@ -535,7 +555,7 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t v = ((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u;
-                if (hoff[j] >= 0) atomicAdd(&hs[hoff[j] + v], 1u);
+                atomicAdd(&hs[(kh[j] >> 16) + v], 1u);
             }
         }
         if (hist_img && count_img) {
@@ -599,7 +619,8 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
             uint32_t out[2] = {0, 0};
             float4 ev[8];  // the 8 gathers first, then the blends
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ev[j] = tab[ko[j] + (((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u)];
+            for (int j = 0; j < 8; ++j)
+                ev[j] = tab[(kh[j] & 0xffffu) + (((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u)];
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // the scheduler keeps the 8 reads together
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -710,7 +731,7 @@ constexpr int FUSED_MIN_BATCH = 8;
 
 // fused_kernel's LDS: the fp32 table, the histograms, two LUT rows, the image histogram
 size_t fused_lds(const ClaheGeom& g) {
-    return (size_t)(g.tiles_x + 1) * TROW * 16 + ((size_t)g.tiles_x * HROW + 2 * g.tiles_x * 64 + 256) * 4;
+    return (size_t)(g.tiles_x + 1) * TROW * 16 + ((size_t)(g.tiles_x + 1) * HROW + 2 * g.tiles_x * 64 + 256) * 4;
 }
 
 struct FusedPlan {

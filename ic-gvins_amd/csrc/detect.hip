@@ -85,7 +85,7 @@ __device__ void eig_tile(int bx, int by, int bz, const uint8_t* __restrict__ img
     __shared__ uint8_t px[ET_H + 4][ET_W + 4];
     __shared__ float cov[3][ET_H + 2][ET_W + 2];
     if (n_active_dev && bz >= *n_active_dev) return;
-    const int k = blk_ids[bz];
+    const int k = blk_ids ? blk_ids[bz] : bz;  // nullptr: every block, in order
     const int4 roi = rois[k];  // x0, y0, rw, rh
     const int rw = roi.z, rh = roi.w;
     const int tx0 = bx * ET_W, ty0 = by * ET_H;
@@ -371,6 +371,131 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 
 constexpr int SEL_T = 1024;
 
+// goodFeaturesToTrack + cornerSubPix of block k (ROI roi, eigenvalues E in ROI
+// raster order, maxCorners maxc) by one workgroup; allowed(x, y) is the mask at
+// ROI pixel (x, y).  The caller's LDS: sub (one SubpixLds per wave).
+struct SelectShared {
+    float s_max[SEL_T / 64];
+    int s_found[SEL_T / 64];
+    unsigned long long s_key[SEL_T / 64];
+    int s_ncand;
+    float s_acc[64][2];
+    int s_nacc;
+};
+
+template <class Allowed>
+__device__ __forceinline__ void select_block(int k, int4 roi, const float* __restrict__ E, Allowed allowed, int maxc,
+                                             double quality, float min_dist, unsigned long long* __restrict__ CK,
+                                             int2* __restrict__ corners, int max_per_block, int* __restrict__ ncorner,
+                                             const uint8_t* __restrict__ img0, int pitch,
+                                             const float* __restrict__ gmask, int max_iters, double eps2,
+                                             float2* __restrict__ out, SelectShared& S, SubpixLds* s_sub) {
+    const int rw = roi.z, rh = roi.w;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int npx = rw * rh;
+    // minMaxLoc(eig, 0, &maxVal, 0, 0, mask)
+    float mx = -__FLT_MAX__;
+    int found = 0;
+    for (int i = t; i < npx; i += SEL_T) {
+        const int y = i / rw, x = i - y * rw;
+        if (allowed(x, y)) {
+            mx = fmaxf(mx, E[i]);
+            found = 1;
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        found |= __shfl_xor(found, o, 64);
+    }
+    if (lane == 0) {
+        S.s_max[wv] = mx;
+        S.s_found[wv] = found;
+    }
+    if (t == 0) {
+        S.s_ncand = 0;
+        S.s_nacc = 0;
+    }
+    __syncthreads();
+    float mxa = -__FLT_MAX__;
+    int fa = 0;
+    for (int q = 0; q < SEL_T / 64; ++q) {
+        mxa = fmaxf(mxa, S.s_max[q]);
+        fa |= S.s_found[q];
+    }
+    const double maxv = fa ? (double)mxa : 0.0;
+    const float thr = (float)(maxv * quality);
+    // candidates: thresholded local maxima of the 3x3 dilation, inside the
+    // 1-pixel ROI ring, on the mask
+    for (int i = t; i < npx; i += SEL_T) {
+        const int y = i / rw, x = i - y * rw;
+        if (y < 1 || y > rh - 2 || x < 1 || x > rw - 2) continue;
+        float v = E[i];
+        v = v > thr ? v : 0.f;
+        if (v == 0.f || !allowed(x, y)) continue;
+        float d = -__FLT_MAX__;
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                float u = E[(y + dy) * rw + x + dx];
+                u = u > thr ? u : 0.f;
+                d = fmaxf(d, u);
+            }
+        if (v == d) {
+            const int slot = atomicAdd(&S.s_ncand, 1);
+            CK[slot] = ((unsigned long long)fkey(v) << 32) | (unsigned)i;
+        }
+    }
+    __syncthreads();
+    const int nc = S.s_ncand;
+    const float md2 = min_dist * min_dist;
+    for (int round = 0; round < maxc; ++round) {
+        unsigned long long best = 0;
+        const int na = S.s_nacc;
+        for (int i = t; i < nc; i += SEL_T) {
+            const unsigned long long key = CK[i];
+            if (key <= best) continue;
+            const int idx = (int)(key & 0xffffffffu);
+            const int y = idx / rw, x = idx - y * rw;
+            bool good = true;
+            for (int j = 0; j < na && good; ++j) {
+                const float dx = (float)x - S.s_acc[j][0];
+                const float dy = (float)y - S.s_acc[j][1];
+                if (dx * dx + dy * dy < md2) good = false;
+            }
+            if (good) best = key;
+        }
+        best = wave_max_u64(best);
+        if (lane == 0) S.s_key[wv] = best;
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long b = 0;
+            for (int q = 0; q < SEL_T / 64; ++q) b = S.s_key[q] > b ? S.s_key[q] : b;
+            if (b != 0) {
+                const int idx = (int)(b & 0xffffffffu);
+                const int y = idx / rw, x = idx - y * rw;
+                S.s_acc[S.s_nacc][0] = (float)x;
+                S.s_acc[S.s_nacc][1] = (float)y;
+                corners[k * max_per_block + S.s_nacc] = make_int2(x, y);
+                S.s_nacc = S.s_nacc + 1;
+            } else {
+                S.s_key[0] = 0;  // signal: no more candidates
+            }
+        }
+        __syncthreads();
+        if (S.s_nacc == round) break;  // nothing accepted this round
+    }
+    if (t == 0) ncorner[k] = S.s_nacc;
+    // cornerSubPix of the block's corners (the old separate launch), one wave
+    // per corner: the block's ROI and corner list are already here
+    __syncthreads();
+    const int nacc = S.s_nacc;
+    const uint8_t* src = img0 + (int64_t)roi.y * pitch + roi.x;
+    for (int ci = wv; ci < nacc; ci += SEL_T / 64) {
+        const int2 c0 = make_int2((int)S.s_acc[ci][0], (int)S.s_acc[ci][1]);
+        const float2 r = subpix_corner(src, pitch, roi, c0, gmask, max_iters, eps2, lane, s_sub[wv]);
+        if (lane == 0) out[k * max_per_block + ci] = r;
+    }
+}
+
 __global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__ eig, int64_t eig_stride,
                                                        const uint8_t* __restrict__ mask, int w,
                                                        const int4* __restrict__ rois,
@@ -383,126 +508,143 @@ __global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__
                                                        const float* __restrict__ gmask, int max_iters, double eps2,
                                                        float2* __restrict__ out) {
     __shared__ SubpixLds s_sub[SEL_T / 64];
+    __shared__ SelectShared S;
     if (n_active_dev && (int)blockIdx.x >= *n_active_dev) return;
-    __shared__ float s_max[SEL_T / 64];
-    __shared__ int s_found[SEL_T / 64];
-    __shared__ unsigned long long s_key[SEL_T / 64];
-    __shared__ int s_ncand;
-    __shared__ float s_acc[64][2];
-    __shared__ int s_nacc;
     const int k = blk_ids[blockIdx.x];
     const int4 roi = rois[k];
-    const int rw = roi.z, rh = roi.w;
-    const float* E = eig + k * eig_stride;
     const uint8_t* M = mask + (int64_t)roi.y * w + roi.x;
-    unsigned long long* CK = cand + k * eig_stride;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int npx = rw * rh;
-    // minMaxLoc(eig, 0, &maxVal, 0, 0, mask)
-    float mx = -__FLT_MAX__;
-    int found = 0;
-    for (int i = t; i < npx; i += SEL_T) {
-        const int y = i / rw, x = i - y * rw;
-        if (M[(int64_t)y * w + x]) {
-            mx = fmaxf(mx, E[i]);
-            found = 1;
-        }
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        found |= __shfl_xor(found, o, 64);
-    }
-    if (lane == 0) {
-        s_max[wv] = mx;
-        s_found[wv] = found;
-    }
+    auto allowed = [&](int x, int y) -> bool { return M[(int64_t)y * w + x] != 0; };
+    select_block(k, roi, eig + k * eig_stride, allowed, want[k], quality, min_dist, cand + k * eig_stride, corners,
+                 max_per_block, ncorner, img0, pitch, gmask, max_iters, eps2, out, S, s_sub);
+}
+
+// featuresDetection's early exit and block k's maxCorners from the tracked points
+// (the kept FB flags and positions of the frame's LK, or the point list of a
+// first frame): a block-wide count by every workgroup that needs it, so no
+// preparation launch precedes the tracking path's detection.  Returns maxCorners
+// (<= 0: nothing to detect in block k).  The circle centres near roi (ROI
+// coordinates) go to circ / *nc when circ != nullptr.
+__device__ int block_want(const TrackSelect& a, int k, int4 roi, int* s_nk, int* s_cnt, int2* circ, int* s_nc) {
+    const int t = threadIdx.x, r = a.radius;
     if (t == 0) {
-        s_ncand = 0;
-        s_nacc = 0;
+        *s_nk = 0;
+        *s_cnt = 0;
+        if (circ) *s_nc = 0;
     }
     __syncthreads();
-    float mxa = -__FLT_MAX__;
-    int fa = 0;
-    for (int q = 0; q < SEL_T / 64; ++q) {
-        mxa = fmaxf(mxa, s_max[q]);
-        fa |= s_found[q];
-    }
-    const double maxv = fa ? (double)mxa : 0.0;
-    const float thr = (float)(maxv * quality);
-    // candidates: thresholded local maxima of the 3x3 dilation, inside the
-    // 1-pixel ROI ring, on the mask
-    for (int i = t; i < npx; i += SEL_T) {
-        const int y = i / rw, x = i - y * rw;
-        if (y < 1 || y > rh - 2 || x < 1 || x > rw - 2) continue;
-        float v = E[i];
-        v = v > thr ? v : 0.f;
-        if (v == 0.f || !M[(int64_t)y * w + x]) continue;
-        float d = -__FLT_MAX__;
-        for (int dy = -1; dy <= 1; ++dy)
-            for (int dx = -1; dx <= 1; ++dx) {
-                float u = E[(y + dy) * rw + x + dx];
-                u = u > thr ? u : 0.f;
-                d = fmaxf(d, u);
-            }
-        if (v == d) {
-            const int slot = atomicAdd(&s_ncand, 1);
-            CK[slot] = ((unsigned long long)fkey(v) << 32) | (unsigned)i;
+    const int n_in = min(*a.n, a.cap);
+    for (int i = t; i < n_in; i += blockDim.x) {
+        const bool kept = a.flags ? (a.flags[i] & 4) != 0 : true;
+        if (!kept) continue;
+        const float2 p = a.flags ? reinterpret_cast<const float2*>(a.next_xy)[i]
+                                 : reinterpret_cast<const float2*>(a.pts)[i];
+        atomicAdd(s_nk, 1);
+        const int cc = (int)(p.x / (float)a.col), rr = (int)(p.y / (float)a.row);
+        if (rr * a.bcols + cc == k) atomicAdd(s_cnt, 1);
+        if (circ) {
+            const int cx = (int)rintf(p.x), cy = (int)rintf(p.y);
+            if (cx >= roi.x - r && cx <= roi.x + roi.z - 1 + r && cy >= roi.y - r && cy <= roi.y + roi.w - 1 + r)
+                circ[atomicAdd(s_nc, 1)] = make_int2(cx - roi.x, cy - roi.y);
         }
     }
     __syncthreads();
-    const int nc = s_ncand;
-    const int maxc = want[k];
-    const float md2 = min_dist * min_dist;
-    for (int round = 0; round < maxc; ++round) {
-        unsigned long long best = 0;
-        const int na = s_nacc;
-        for (int i = t; i < nc; i += SEL_T) {
-            const unsigned long long key = CK[i];
-            if (key <= best) continue;
-            const int idx = (int)(key & 0xffffffffu);
-            const int y = idx / rw, x = idx - y * rw;
-            bool good = true;
-            for (int j = 0; j < na && good; ++j) {
-                const float dx = (float)x - s_acc[j][0];
-                const float dy = (float)y - s_acc[j][1];
-                if (dx * dx + dy * dy < md2) good = false;
-            }
-            if (good) best = key;
-        }
-        best = wave_max_u64(best);
-        if (lane == 0) s_key[wv] = best;
-        __syncthreads();
-        if (t == 0) {
-            unsigned long long b = 0;
-            for (int q = 0; q < SEL_T / 64; ++q) b = s_key[q] > b ? s_key[q] : b;
-            if (b != 0) {
-                const int idx = (int)(b & 0xffffffffu);
-                const int y = idx / rw, x = idx - y * rw;
-                s_acc[s_nacc][0] = (float)x;
-                s_acc[s_nacc][1] = (float)y;
-                corners[k * max_per_block + s_nacc] = make_int2(x, y);
-                s_nacc = s_nacc + 1;
-            } else {
-                s_key[0] = 0;  // signal: no more candidates
-            }
-        }
-        __syncthreads();
-        if (s_nacc == round) break;  // nothing accepted this round
+    const int nk = *s_nk;
+    const bool skip = !(nk < a.max_features) || nk > a.max_features - 5 || a.maxpb <= 0;
+    return skip ? 0 : a.maxpb - *s_cnt;
+}
+
+// The eigenvalue tiles of the tracking path, for the blocks that detect this
+// frame only (each workgroup counts the tracked points itself, as the selection
+// does): one launch, no preparation launch before it.
+__global__ void __launch_bounds__(256) eig_track_kernel(TrackSelect a, int ex, int ey, float sc, float sc2) {
+    __shared__ int s_nk, s_cnt;
+    const int per = ex * ey;
+    const int k = blockIdx.x / per, r = blockIdx.x - k * per;
+    const int4 roi = a.rois[k];
+    if (block_want(a, k, roi, &s_nk, &s_cnt, nullptr, nullptr) <= 0) return;  // uniform
+    eig_tile(r % ex, r / ex, k, a.img0, a.pitch, a.rois, nullptr, a.eig_stride, const_cast<float*>(a.eig), sc, sc2,
+             nullptr);
+}
+
+// The tracking path's detection (gvx_track_frame_dev), one workgroup per block
+// and no preparation launch: each workgroup counts the tracked points itself
+// (the kept FB flags and tracked positions of the frame's LK, or the point list
+// of a first frame), takes featuresDetection's early exit and the block's
+// maxCorners from them, and rasterises the circle mask of the points near its
+// ROI into an LDS bitmap (cv::circle FILLED, radius minDistance, at the
+// cvRound centres: the same per-row half-widths as mask_tile) instead of
+// reading a full-frame mask.  The eigenvalue map is the frame's, computed
+// beforehand (gvx_frame_eig_dev on the preprocessing branch, or a launch of
+// eig tiles right before this one).  Inactive blocks write ncorner = 0.
+__global__ void __launch_bounds__(SEL_T) select_track_kernel(TrackSelect a) {
+    __shared__ SubpixLds s_sub[SEL_T / 64];
+    __shared__ SelectShared S;
+    __shared__ int s_nk, s_cnt, s_nc;
+    __shared__ int2 s_circ[TS_MAX_POINTS];
+    extern __shared__ uint32_t bm[];  // ROI bitmap, 1 = allowed, wpr words per row
+    const int k = blockIdx.x, t = threadIdx.x;
+    const int4 roi = a.rois[k];
+    const int rw = roi.z, rh = roi.w, r = a.radius;
+    const int want = block_want(a, k, roi, &s_nk, &s_cnt, s_circ, &s_nc);
+    if (want <= 0) {  // uniform over the workgroup
+        if (t == 0) a.ncorner[k] = 0;
+        return;
     }
-    if (t == 0) ncorner[k] = s_nacc;
-    // cornerSubPix of the block's corners (the old separate launch), one wave
-    // per corner: the block's ROI and corner list are already here
+    const int wpr = (rw + 31) >> 5;
+    for (int i = t; i < wpr * rh; i += SEL_T) bm[i] = ~0u;
     __syncthreads();
-    const int nacc = s_nacc;
-    const uint8_t* src = img0 + (int64_t)roi.y * pitch + roi.x;
-    for (int ci = wv; ci < nacc; ci += SEL_T / 64) {
-        const int2 c0 = make_int2((int)s_acc[ci][0], (int)s_acc[ci][1]);
-        const float2 r = subpix_corner(src, pitch, roi, c0, gmask, max_iters, eps2, lane, s_sub[wv]);
-        if (lane == 0) out[k * max_per_block + ci] = r;
+    const int span = 2 * r + 1, nrow = s_nc * span;
+    for (int it = t; it < nrow; it += SEL_T) {
+        const int ci = it / span, dy = it - ci * span - r;
+        const int2 c = s_circ[ci];
+        const int y = c.y + dy;
+        const int hwv = a.hw[dy < 0 ? -dy : dy];
+        if (y < 0 || y >= rh || hwv < 0) continue;
+        const int x0 = max(c.x - hwv, 0), x1 = min(c.x + hwv, rw - 1);
+        for (int x = x0; x <= x1;) {  // clear bits x0..x1 of row y, a word at a time
+            const int wi = x >> 5, b0 = x & 31, b1 = min(31, b0 + (x1 - x));
+            const uint32_t m = (b1 == 31 ? ~0u : ((1u << (b1 + 1)) - 1u)) & ~((1u << b0) - 1u);
+            atomicAnd(&bm[y * wpr + wi], ~m);
+            x += b1 - b0 + 1;
+        }
     }
+    __syncthreads();
+    auto allowed = [&](int x, int y) -> bool { return (bm[y * wpr + (x >> 5)] >> (x & 31)) & 1u; };
+    select_block(k, roi, a.eig + k * a.eig_stride, allowed, want, a.quality, a.min_dist, a.cand + k * a.eig_stride,
+                 a.corners, a.max_per_block, a.ncorner, a.img0, a.pitch, a.gmask, a.max_iters, a.eps2, a.out, S,
+                 s_sub);
 }
 
 }  // namespace
+
+hipError_t launch_eig_all(gvx_ctx* c, int n_blocks, int max_rw, int max_rh, const uint8_t* img0, int pitch,
+                          const int4* rois, int64_t eig_stride, float* eig, float sc, float sc2) {
+    if (n_blocks <= 0) return hipSuccess;
+    const int ex = (max_rw + ET_W - 1) / ET_W, ey = (max_rh + ET_H - 1) / ET_H;
+    hipLaunchKernelGGL(mask_eig_kernel, dim3(ex * ey * n_blocks), dim3(256), 0, c->stream, 0, 1, 0, 0, nullptr, 0,
+                       nullptr, 0, nullptr, nullptr, nullptr, ex, ey, img0, pitch, rois, nullptr, eig_stride, eig, sc,
+                       sc2, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_eig_track(gvx_ctx* c, int n_blocks, int max_rw, int max_rh, const TrackSelect& a, float sc,
+                            float sc2) {
+    if (n_blocks <= 0) return hipSuccess;
+    if (a.cap > TS_MAX_POINTS) return hipErrorInvalidValue;
+    const int ex = (max_rw + ET_W - 1) / ET_W, ey = (max_rh + ET_H - 1) / ET_H;
+    hipLaunchKernelGGL(eig_track_kernel, dim3(ex * ey * n_blocks), dim3(256), 0, c->stream, a, ex, ey, sc, sc2);
+    return hipGetLastError();
+}
+
+size_t select_track_lds(int max_rw, int max_rh) { return (size_t)((max_rw + 31) / 32) * max_rh * 4; }
+
+hipError_t launch_select_track(gvx_ctx* c, int n_blocks, int max_rw, int max_rh, const TrackSelect& a) {
+    if (n_blocks <= 0) return hipSuccess;
+    if (a.cap > TS_MAX_POINTS || select_track_lds(max_rw, max_rh) > TS_MAX_BITMAP) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(select_track_kernel, dim3(n_blocks), dim3(SEL_T), select_track_lds(max_rw, max_rh), c->stream,
+                       a);
+    return hipGetLastError();
+}
 
 hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d) {
     // device-resident counts (n_active_dev): every launch is sized for all blocks

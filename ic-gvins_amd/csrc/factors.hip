@@ -294,20 +294,25 @@ __global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result*
 }
 
 // One factor per 16-lane group, 4 factors per 64-lane workgroup (one wave).
+// Every input is staged into LDS before any of it is used, in two dependent
+// rounds of loads and no more: round 1 (issued first, needing only the factor
+// index) brings each factor's record -- sqrt_info's upper triangle, the 9 x 6
+// bias block of jacobian_, the delta state, gravity and iewn -- through
+// global_load_lds (4 bytes a lane, any source address, no registers), plus the
+// per-factor offsets and pn_ extents; round 2 brings the four parameter blocks
+// into the record and the first 128 pn_ samples into the 16 KB tile region.
+// (r02's form loaded the same data where it was used: five to six dependent
+// memory round trips per wave, half of its 61 k cycles spent waiting.)
 // The residual and the raw Jacobian blocks are uniform per factor: the group's
 // lanes compute them together (one instruction stream for the wave's four
 // factors) and lane 0 of the group stores them into the group's LDS tile
 // Jr[15][33] (32 Jacobian columns [J0 7 | J1 9 | J2 7 | J3 9] + the residual).
-// Earth: the position-correction sum over pn_ runs on lanes 0..2, one
-// component each, in the reference's order, from pn_ staged into LDS by
-// global_load_lds in chunks of PN_CH samples.  Whitening sqrt_info * [Jr | r]
-// runs on the matrix cores (v_mfma_f64_16x16x4, 12 per factor); the wave then
-// stores its four factors' residuals and Jacobians as contiguous runs.
-// Measured (configs[3], 5,247 factors, M = 100): 47 -> 34 us per launch (r02:
-// select-free VALU whitening 41 us, MFMA whitening 37 us, pn_ through LDS 34 us;
-// 8 lanes per factor: 40 us; one 104-sample pn_ chunk: 49 us -- 32 KB of LDS
-// per wave leaves 1,280 wave slots for 1,312 waves).  Per wave (PMC): 61 k
-// cycles, half of them waiting on memory; the per-factor fp64 chain bounds it.
+// Earth: the position-correction sum over pn_ runs on all 16 lanes of the
+// group (a strided partial sum each, then a DPP butterfly), from the staged
+// samples.
+// Whitening sqrt_info * [Jr | r] runs on the matrix cores (v_mfma_f64_16x16x4,
+// 12 per factor); the wave then stores its four factors' residuals and
+// Jacobians as contiguous runs.
 #ifndef PF_LANES
 #define PF_LANES 16
 #endif
@@ -318,6 +323,32 @@ constexpr int PF_LD = 33;                // tile row: 32 Jacobian columns + the 
 constexpr int PN_CH = 64;                // pn_ samples per factor per LDS chunk
 constexpr int PN_PER = PF_L / 2;         // samples per factor per global_load_lds (16 B per lane)
 constexpr int PN_INS = PN_CH / PN_PER;   // instructions per chunk (1 KB each)
+// the factor record in LDS (doubles): sqrt_info upper triangle (row-major,
+// packed), jacobian_ rows 0..8 x columns 9..14, misc, the four parameter blocks
+constexpr int RC_SQ = 0, RC_J6 = 120, RC_MISC = 174, RC_PAR = 197, RC_N = 229, RC_STRIDE = 256;
+// misc: delta_time, then delta.p, .q, .v, .bg, .ba, gravity, iewn (contiguous in the struct)
+constexpr int RC_DT = RC_MISC, RC_DP = RC_MISC + 1, RC_DQ = RC_MISC + 4, RC_DV = RC_MISC + 8,
+              RC_DBG = RC_MISC + 11, RC_DBA = RC_MISC + 14, RC_G = RC_MISC + 17, RC_IEWN = RC_MISC + 20;
+static_assert(offsetof(gvx_preint_result, gravity) == offsetof(gvx_preint_result, delta) + sizeof(gvx_state) &&
+                  offsetof(gvx_preint_result, iewn) == offsetof(gvx_preint_result, gravity) + 24 &&
+                  offsetof(gvx_state, p) == 8 && offsetof(gvx_state, q) == 32 && offsetof(gvx_state, v) == 64 &&
+                  offsetof(gvx_state, bg) == 88 && offsetof(gvx_state, ba) == 112,
+              "the misc block is one contiguous run of the struct");
+static_assert(RC_PAR == RC_MISC + 23 && RC_N == RC_PAR + 32 && RC_N <= RC_STRIDE, "record layout");
+static_assert(RC_DQ - RC_DP == 3 && RC_DV - RC_DQ == 4 && RC_DBG - RC_DV == 3 && RC_DBA - RC_DBG == 3 &&
+                  RC_G - RC_DBA == 3 && RC_IEWN - RC_G == 3,
+              "misc mirrors delta.{p, q, v, bg, ba}, gravity, iewn");
+
+// v of the lane n places down its 16-lane row, cyclically (DPP row_ror:n), fp64
+template <int N>
+__device__ __forceinline__ double dpp_row_ror(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, 0x120 + N, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(0, lo, 0x120 + N, 0xf, 0xf, false));
+}
+
+// packed upper-triangular index of (r, c), c >= r, n = 15
+__device__ __forceinline__ int triu15(int r, int c) { return r * 15 - (r * (r - 1)) / 2 + (c - r); }
 
 __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
                                                            const double* __restrict__ pn,
@@ -326,107 +357,172 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
                                                            const int32_t* __restrict__ offs,
                                                            double* __restrict__ res,
                                                            double* __restrict__ jac) {
-    __shared__ double tile[PF_SLOTS * NS * PF_LD];
-    __shared__ double pnb[PN_INS * 128];  // pn_ chunk: PN_PER samples x PF_GROUPS groups per KB
-    const int grp = threadIdx.x / PF_L, lane = threadIdx.x % PF_L;
+    __shared__ double tile[2 * PN_INS * 128];  // pn_ chunks 0 / 1, then the Jr tiles
+    __shared__ double rec[PF_GROUPS * RC_STRIDE];
+    static_assert(PF_SLOTS * NS * PF_LD <= 2 * PN_INS * 128, "the tiles fit the pn_ staging");
+    const int grp = threadIdx.x / PF_L, lane = threadIdx.x % PF_L, tl = threadIdx.x;
     const int f0 = blockIdx.x * PF_GROUPS;
     // dead groups (past n, or the partial group) recompute a valid factor and store nothing
     const int fi = min(f0 + min(grp, PF_GROUPS - 1), n - 1);
-    double* Jr = tile + grp * NS * PF_LD;
     const gvx_preint_result* s = pre + fi;
-    const bool earth = s->variant == GVX_PREINT_EARTH;
-    for (int e = lane; e < NS * PF_LD; e += PF_L) Jr[e] = 0.0;
-    __syncthreads();
-    // pn_ chunk c0 of this group's factor into LDS (instruction j: lane pair
+    typedef const __attribute__((address_space(1))) void* gptr;
+    typedef __attribute__((address_space(3))) void* lptr;
+    // ---- round 1: the records (dwords 0..393: sqrt_info, jacobian block, misc) ----
+    // record dword d of factor f comes from struct dword src(d); lane l carries
+    // d = 64 j + l of instruction j
+    auto src_dword = [&](int d) -> int {
+        const int h = d & 1, q = d >> 1;  // double q of the record, half h
+        int sd;
+        if (q < RC_J6) {  // sqrt_info (r, c), c >= r
+            int r = 0;
+            while (r < 14 && triu15(r + 1, r + 1) <= q) ++r;
+            sd = (int)(offsetof(gvx_preint_result, sqrt_info) / 8) + r * 15 + (r + q - triu15(r, r));
+        } else if (q < RC_MISC) {
+            const int e = q - RC_J6;
+            sd = (int)(offsetof(gvx_preint_result, jacobian) / 8) + (e / 6) * 15 + 9 + e % 6;
+        } else if (q == RC_DT) {
+            sd = (int)(offsetof(gvx_preint_result, delta_time) / 8);
+        } else {
+            sd = (int)(offsetof(gvx_preint_result, delta) / 8) + 1 + (q - RC_DP);
+        }
+        return 2 * sd + h;
+    };
+    int srcd[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) srcd[j] = src_dword(min(64 * j + tl, 2 * RC_PAR - 1));
+#pragma unroll
+    for (int f = 0; f < PF_GROUPS; ++f) {
+        const uint32_t* sf = reinterpret_cast<const uint32_t*>(pre + min(f0 + f, n - 1));
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+            if (64 * j + tl < 2 * RC_PAR)
+                __builtin_amdgcn_global_load_lds((gptr)(sf + srcd[j]), (lptr)(rec + f * RC_STRIDE + 32 * j), 4, 0, 0);
+    }
+    const int earth_i = s->variant == GVX_PREINT_EARTH;
+    const int m1n = earth_i ? s->m - 1 : 0;
+    const int32_t pno = pn_off[fi];
+    const int32_t* o = offs + 4 * (int64_t)fi;
+    const int o0 = o[0], o1 = o[1], o2 = o[2], o3 = o[3];
+    const bool earth = earth_i != 0;
+    // ---- round 2: the parameter blocks (record doubles RC_PAR.., 64 dwords) and pn_ ----
+    {
+        // dword k of [pose0 (14) | mix0 (18) | pose1 (14) | mix1 (18)]
+        const int k = tl;
+        const int blk = k < 14 ? 0 : (k < 32 ? 1 : (k < 46 ? 2 : 3));
+        const int kb = k - (blk == 0 ? 0 : (blk == 1 ? 14 : (blk == 2 ? 32 : 46)));
+#pragma unroll
+        for (int f = 0; f < PF_GROUPS; ++f) {
+            // the offsets of factor f live in group f's lanes
+            const int b0 = __shfl(o0, f * PF_L, 64), b1 = __shfl(o1, f * PF_L, 64);
+            const int b2 = __shfl(o2, f * PF_L, 64), b3 = __shfl(o3, f * PF_L, 64);
+            const int base = blk == 0 ? b0 : (blk == 1 ? b1 : (blk == 2 ? b2 : b3));
+            const uint32_t* pp = reinterpret_cast<const uint32_t*>(params + base);
+            __builtin_amdgcn_global_load_lds((gptr)(pp + kb), (lptr)(rec + f * RC_STRIDE + RC_PAR), 4, 0, 0);
+        }
+    }
+    // pn_ chunk c0 of this group's factor into LDS half h (instruction j: lane pair
     // (2q, 2q+1) of a group loads sample c0 + PN_PER*j + q, 16 bytes each, to
-    // pnb + j*1 KB + group*16*PF_L B + q*32 B); chunk 0 is issued here, ahead of
-    // the parameter loads, so its latency overlaps theirs
-    const double* pl = pn + 4 * (int64_t)pn_off[fi];
-    const int m1n = earth ? s->m - 1 : 0;
-    auto pn_chunk = [&](int c0) {
+    // tile + h*1024 + j*128 + group*2*PF_L + q*4 doubles)
+    const double* pl = pn + 4 * (int64_t)pno;
+    auto pn_chunk = [&](int c0, int h) {
 #pragma unroll
         for (int j = 0; j < PN_INS; ++j) {
             const int smp = c0 + PN_PER * j + (lane >> 1);
             if (smp < m1n)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(pl + 4 * smp + 2 * (lane & 1)),
-                    (__attribute__((address_space(3))) void*)(pnb + 128 * j), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gptr)(pl + 4 * smp + 2 * (lane & 1)),
+                                                 (lptr)(tile + h * PN_INS * 128 + 128 * j), 16, 0, 0);
         }
     };
-    pn_chunk(0);
-    const int32_t* o = offs + 4 * (int64_t)fi;
-    const double *ps0 = params + o[0], *m0 = params + o[1], *ps1 = params + o[2], *m1 = params + o[3];
+    pn_chunk(0, 0);
+    pn_chunk(PN_CH, 1);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const double* R = rec + grp * RC_STRIDE;
+    const double *ps0 = R + RC_PAR, *m0 = R + RC_PAR + 7, *ps1 = R + RC_PAR + 16, *m1 = R + RC_PAR + 23;
+    // Earth: p_cor = sum over pn_ of (pn.second - state0.p) * pn.first
+    // (preintegration_earth.cc's loop), lane-parallel: lane l of the group sums
+    // the samples k = l mod 16 in order, then a 16-lane butterfly (DPP row_ror)
+    // adds the partial sums -- a different association than the reference's
+    // sequential loop, within 1e-16 relative (the parity bound is 1e-10)
+    double pcs[3] = {0.0, 0.0, 0.0};
+    {
+        const double p00 = ps0[0], p01 = ps0[1], p02 = ps0[2];
+        for (int c0 = 0; __ballot(c0 < m1n); c0 += 2 * PN_CH) {
+            if (c0 > 0) {
+                pn_chunk(c0, 0);
+                pn_chunk(c0 + PN_CH, 1);
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const int kn = min(2 * PN_CH, m1n - c0);
+            const double* P = tile + 2 * PF_L * grp;
+#pragma unroll 4
+            for (int k = lane; k < kn; k += PF_L) {
+                const int kk = k & (PN_CH - 1);
+                const double* e = P + (k >= PN_CH ? PN_INS * 128 : 0) + 128 * (kk / PN_PER) + 4 * (kk % PN_PER);
+                const double dt = e[0];
+                pcs[0] = pcs[0] + (e[1] - p00) * dt;
+                pcs[1] = pcs[1] + (e[2] - p01) * dt;
+                pcs[2] = pcs[2] + (e[3] - p02) * dt;
+            }
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next chunk lands
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            pcs[c] = pcs[c] + dpp_row_ror<8>(pcs[c]);
+            pcs[c] = pcs[c] + dpp_row_ror<4>(pcs[c]);
+            pcs[c] = pcs[c] + dpp_row_ror<2>(pcs[c]);
+            pcs[c] = pcs[c] + dpp_row_ror<1>(pcs[c]);
+        }
+    }
+    // the tile region now holds the Jr tiles
+    double* Jr = tile + grp * NS * PF_LD;
+    for (int e = lane; e < NS * PF_LD; e += PF_L) Jr[e] = 0.0;
     const dq q0 = dq_make(ps0[6], ps0[3], ps0[4], ps0[5]);
     const dq q1 = dq_make(ps1[6], ps1[3], ps1[4], ps1[5]);
     const double *p0 = ps0, *p1 = ps1, *v0 = m0, *v1 = m1;
     const double *bg0 = m0 + 3, *ba0 = m0 + 6, *bg1 = m1 + 3, *ba1 = m1 + 6;
     // ---- residual and raw Jacobian blocks (uniform over the group) ----
-    const double dtt = s->delta_time;
-    const double* Jc = s->jacobian;
+    const double dtt = R[RC_DT];
+    const double* J6 = R + RC_J6;
     double dp_dbg[9], dp_dba[9], dv_dbg[9], dv_dba[9], dq_dbg[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
-            dp_dbg[3 * i + j] = Jc[i * NS + 9 + j];
-            dp_dba[3 * i + j] = Jc[i * NS + 12 + j];
-            dv_dbg[3 * i + j] = Jc[(3 + i) * NS + 9 + j];
-            dv_dba[3 * i + j] = Jc[(3 + i) * NS + 12 + j];
-            dq_dbg[3 * i + j] = Jc[(6 + i) * NS + 9 + j];
+            dp_dbg[3 * i + j] = J6[i * 6 + j];
+            dp_dba[3 * i + j] = J6[i * 6 + 3 + j];
+            dv_dbg[3 * i + j] = J6[(3 + i) * 6 + j];
+            dv_dba[3 * i + j] = J6[(3 + i) * 6 + 3 + j];
+            dq_dbg[3 * i + j] = J6[(6 + i) * 6 + j];
         }
     double dbg[3], dba[3], t[3], u[3], cp[3], cv[3];
     for (int i = 0; i < 3; ++i) {
-        dbg[i] = bg0[i] - s->delta.bg[i];
-        dba[i] = ba0[i] - s->delta.ba[i];
+        dbg[i] = bg0[i] - R[RC_DBG + i];
+        dba[i] = ba0[i] - R[RC_DBA + i];
     }
     mv3(dp_dba, dba, t);
     mv3(dp_dbg, dbg, u);
-    for (int i = 0; i < 3; ++i) cp[i] = s->delta.p[i] + t[i] + u[i];
+    for (int i = 0; i < 3; ++i) cp[i] = R[RC_DP + i] + t[i] + u[i];
     mv3(dv_dba, dba, t);
     mv3(dv_dbg, dbg, u);
-    for (int i = 0; i < 3; ++i) cv[i] = s->delta.v[i] + t[i] + u[i];
+    for (int i = 0; i < 3; ++i) cv[i] = R[RC_DV + i] + t[i] + u[i];
     mv3(dq_dbg, dbg, t);
-    const dq dqd = dq_load(s->delta.q);
+    const dq dqd = dq_load(R + RC_DQ);
     const dq cq = dq_mul(dqd, dq_from_rotvec(t));
-    const double* g = s->gravity;
+    const double* g = R + RC_G;
+    const double* iewn = R + RC_IEWN;
     const dq q0i = dq_inv(q0);
     double cnb0[9], M[9], N[9];
     dq_rot(q0i, cnb0);
     double r[NS];
     const bool w0 = lane == 0;  // lane 0 of the group writes the uniform blocks
-    // Earth: p_cor += (pn.second - state0.p) * pn.first over pn_, in the
-    // reference's order, component c on lane c of the group (broadcast below).
-    // pn_ is staged into LDS in chunks of PN_CH samples per factor with
-    // global_load_lds (no registers; one memory latency per chunk instead of one
-    // per unrolled group of loads), then summed from LDS.
-    double pcc = 0.0;
-    {
-        const int c = lane < 3 ? lane : 0;
-        const double p0c = p0[c];
-        const int grpw = threadIdx.x / PF_L;  // this lane's group
-        for (int c0 = 0; __ballot(c0 < m1n); c0 += PN_CH) {
-            if (c0 > 0) pn_chunk(c0);
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane < 3) {
-                const int kn = min(PN_CH, m1n - c0);
-                const double* P = pnb + 2 * PF_L * grpw;
-#pragma unroll 8
-                for (int k = 0; k < kn; ++k) {
-                    const double* e = P + 128 * (k / PN_PER) + 4 * (k % PN_PER);
-                    pcc = pcc + (e[1 + c] - p0c) * e[0];
-                }
-            }
-            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next chunk lands
-        }
-    }
     if (earth) {
         double S[9], S2[9];
-        skew(s->iewn, S);
-        const int gl = threadIdx.x - lane;
-        double pc[3] = {__shfl(pcc, gl, 64), __shfl(pcc, gl + 1, 64), __shfl(pcc, gl + 2, 64)};
+        skew(iewn, S);
+        double pc[3] = {pcs[0], pcs[1], pcs[2]};
         for (int i = 0; i < 9; ++i) S2[i] = 2.0 * S[i];
         mv3(S2, pc, pc);
         double dp[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]}, vc[3];
         mv3(S2, dp, vc);
-        const double dnn[3] = {-s->iewn[0] * dtt, -s->iewn[1] * dtt, -s->iewn[2] * dtt};
+        const double dnn[3] = {-iewn[0] * dtt, -iewn[1] * dtt, -iewn[2] * dtt};
         const dq qnn = dq_from_rotvec(dnn);
         double dpn[3], dvn[3];
         for (int i = 0; i < 3; ++i) {
@@ -534,16 +630,16 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     if (w0)
         for (int i = 0; i < NS; ++i) Jr[i * PF_LD + 32] = r[i];
     // the whitening's A operands (sqrt_info rows / K) of the wave's four factors,
-    // loaded before the barrier so their latency overlaps it
+    // from the records' packed upper triangles (sqrt_info is upper triangular)
     const int wl = threadIdx.x, wr = wl & 15, wk = wl >> 4;
     double SA[PF_GROUPS][4];
 #pragma unroll
     for (int f = 0; f < PF_GROUPS; ++f) {
-        const double* sq = pre[min(f0 + f, n - 1)].sqrt_info;
+        const double* sq = rec + f * RC_STRIDE + RC_SQ;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const int k = 4 * kk + wk;
-            SA[f][kk] = (wr < NS && k < NS) ? sq[wr * NS + k] : 0.0;
+            SA[f][kk] = (wr < NS && k < NS && k >= wr) ? sq[triu15(wr, k)] : 0.0;
         }
     }
     __syncthreads();
@@ -552,9 +648,9 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     // (zero-padded to 16 x 48), each 4 v_mfma_f64_16x16x4 steps over K = 16.
     // Operand layout (16x16x4 f64): A lane l = (row l%16, k l/16), B lane l =
     // (k l/16, col l%16), D lane l = rows l/16 + 4i (i = 0..3) of col l%16
-    // (measured: tools/mfma_f64_probe.hip).  The MFMA sums
-    // the 15 products in its own order, not the restatement's sequential one
-    // (the parity bound is 1e-9 of the block's magnitude).
+    // (measured: tools/mfma_f64_probe.hip).  The MFMA sums the 15 products in
+    // its own order, not the restatement's sequential one; the results stay
+    // within 1e-10 of each block's magnitude (tests/test_factor_parity_gpu.py).
     {
         const int lr = wr, lk = wk;
         const int cb0 = jac ? 0 : 2;  // residual only: the block holding column 32

@@ -45,6 +45,12 @@ struct Frame {
     PyrLayout lay;
     uint8_t* pyr = nullptr;  // device
     int w = 0, h = 0;
+    // the detection's eigenvalue map of this frame (gvx_frame_eig_dev), for the
+    // block grid of eig_key (block size, 0 = none)
+    float* eig = nullptr;
+    size_t eig_bytes = 0;
+    long eig_key = 0;
+    uint64_t gen = 0, eig_gen = 0;  // pyramid writes so far; the write the eig map belongs to
 };
 
 struct ProfEntry {
@@ -105,7 +111,9 @@ namespace gvx {
 
 gvx_status set_err(gvx_ctx* c, gvx_status s, const char* fmt, ...);
 gvx_status hip_err(gvx_ctx* c, hipError_t e, const char* what);
-void* scratch(gvx_ctx* c, const std::string& name, size_t bytes);   // device
+void* scratch(gvx_ctx* c, const std::string& name, size_t bytes);
+// both streams of the context (the side branch's too): before memory is freed
+void sync_all(gvx_ctx* c);   // device
 void* pinned(gvx_ctx* c, const std::string& name, size_t bytes);    // pinned host
 // the cached frame `id` sized for (w, h, p) (allocated or grown; refuses to
 // reallocate during a graph capture)
@@ -325,6 +333,42 @@ struct DetectLaunch {
     const int* skip_dev = nullptr;
 };
 hipError_t launch_detect(gvx_ctx* c, const DetectLaunch& d);
+// cornerMinEigenVal tiles of every block (block k at eig + k * eig_stride, ROI
+// raster order): the part of the detection that depends on the frame alone
+hipError_t launch_eig_all(gvx_ctx* c, int n_blocks, int max_rw, int max_rh, const uint8_t* img0, int pitch,
+                          const int4* rois, int64_t eig_stride, float* eig, float sc, float sc2);
+// The tracking path's per-block detection (select_track_kernel): counts, early
+// exit, the LDS circle mask and the selection in one workgroup per block.
+constexpr int TS_MAX_POINTS = 1024;        // tracker capacity the kernel's LDS holds
+constexpr size_t TS_MAX_BITMAP = 32 * 1024;  // ROI mask bitmap bytes
+struct TrackSelect {
+    int bcols, col, row, maxpb, max_features, cap, radius;
+    const int32_t* n;       // tracked points before the FB update
+    const uint8_t* flags;   // LK flags (bit 2 = kept) or nullptr: pts[0, n) as they are
+    const float* next_xy;   // tracked positions (flags != nullptr)
+    const float* pts;       // the point list (flags == nullptr)
+    const int4* rois;
+    const int* hw;          // circle half-width per row offset 0..radius
+    const float* eig;
+    int64_t eig_stride;
+    unsigned long long* cand;
+    int2* corners;
+    int* ncorner;
+    int max_per_block;
+    double quality;
+    float min_dist;
+    const uint8_t* img0;
+    int pitch;
+    const float* gmask;
+    int max_iters;
+    double eps2;
+    float2* out;
+};
+size_t select_track_lds(int max_rw, int max_rh);
+// the eigenvalue tiles of the blocks that detect this frame (a.eig is written)
+hipError_t launch_eig_track(gvx_ctx* c, int n_blocks, int max_rw, int max_rh, const TrackSelect& a, float sc,
+                            float sc2);
+hipError_t launch_select_track(gvx_ctx* c, int n_blocks, int max_rw, int max_rh, const TrackSelect& a);
 
 // ---- track.hip (gvx_track_frame_dev, gvx_copy_dev) ----
 hipError_t launch_copy(gvx_ctx* c, void* dst, const void* src, size_t bytes);
@@ -371,6 +415,24 @@ struct TrackRecord {
     int32_t* frame;
     int max_frames, cap;
 };
+// the tracking path's last launch: update (update_cap > 0), the early exit from
+// the kept count, the corners appended, the record (rec.tracks != nullptr)
+struct TrackMerge {
+    int bcnt, bcols, col, row, maxpb, max_features;
+    int out_stride;  // corner slots per block in out (max(maxpb, 1))
+    int update_cap;
+    const uint8_t* flags;
+    const float* next_xy;
+    float *pts, *vel, *init;
+    int32_t* kept_out;
+    int32_t* n;
+    const int* ncorner;
+    const float2* out;
+    float* corners_out;
+    int32_t* n_corners_out;
+    TrackRecord rec;
+};
+hipError_t launch_track_merge(gvx_ctx* c, const TrackMerge& m);
 hipError_t launch_detect_merge(gvx_ctx* c, int bcnt, int bcols, int col, int row, int maxpb, int max_features,
                                const int* skip, const int* ncorner, const float2* out, float* pts, float* vel,
                                float* init, int32_t* n, float* corners_out, int32_t* n_corners_out,

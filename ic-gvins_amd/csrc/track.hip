@@ -195,6 +195,45 @@ __global__ void __launch_bounds__(256) detect_merge_kernel(int bcnt, int bcols, 
     }
 }
 
+// The tracking path's last launch (after select_track_kernel): the frame's
+// reduceVector of the FB result (track frames), featuresDetection's early exit
+// recomputed from the kept count (the selection workgroups took the same
+// decision), the corners appended, and the per-frame record.
+__global__ void __launch_bounds__(256) track_merge_kernel(TrackMerge m) {
+    __shared__ int wsum[TU_THREADS / 64];
+    __shared__ int base_s;
+    __shared__ int off[1025];
+    const int tid = threadIdx.x;
+    if (m.update_cap > 0) {
+        track_update(m.update_cap, m.n, m.flags, reinterpret_cast<const float2*>(m.next_xy),
+                     reinterpret_cast<float2*>(m.pts), reinterpret_cast<float2*>(m.vel),
+                     reinterpret_cast<float2*>(m.init), m.kept_out, wsum, base_s);
+        __syncthreads();
+    }
+    const int n = *m.n;
+    const bool skip = !(n < m.max_features) || n > m.max_features - 5 || m.maxpb <= 0;
+    if (skip) {
+        if (tid == 0 && m.n_corners_out) *m.n_corners_out = -1;
+    } else {
+        merge_corners(m.bcnt, m.bcols, m.col, m.row, m.out_stride, m.max_features, m.ncorner, m.out,
+                      reinterpret_cast<float2*>(m.pts), reinterpret_cast<float2*>(m.vel),
+                      reinterpret_cast<float2*>(m.init), m.n, reinterpret_cast<float2*>(m.corners_out),
+                      m.n_corners_out, off);
+    }
+    if (m.rec.tracks) {
+        __syncthreads();
+        const int f = *m.rec.frame;
+        const int nn = min(*m.n, m.rec.cap);
+        if (f < m.rec.max_frames) {
+            for (int i = tid; i < nn; i += 256)
+                reinterpret_cast<float2*>(m.rec.tracks)[(int64_t)f * m.rec.cap + i] = reinterpret_cast<const float2*>(m.pts)[i];
+            if (tid == 0) m.rec.counts[f] = nn;
+        }
+        __syncthreads();
+        if (tid == 0) *m.rec.frame = f + 1;
+    }
+}
+
 // gvx_copy_dev as a kernel: a copy node on the compute queue instead of a DMA
 // copy (in a captured graph the memcpy node cost more than the pair's kernels)
 __global__ void __launch_bounds__(256) copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
@@ -292,6 +331,12 @@ hipError_t launch_track_update(gvx_ctx* c, int cap, int32_t* n, const uint8_t* f
 hipError_t launch_detect_prep(gvx_ctx* c, const DetectPrep& p) {
     if (p.bcols * p.brows > 1024) return hipErrorInvalidValue;
     detect_prep_kernel<<<1, 256, 0, c->stream>>>(p);
+    return hipGetLastError();
+}
+
+hipError_t launch_track_merge(gvx_ctx* c, const TrackMerge& m) {
+    if (m.bcnt > 1024) return hipErrorInvalidValue;
+    track_merge_kernel<<<1, 256, 0, c->stream>>>(m);
     return hipGetLastError();
 }
 

@@ -248,6 +248,7 @@ def _declare(L):
         "gvx_branch_end": (i32, [P]),
         "gvx_branch_join": (i32, [P]),
         "gvx_index_advance_dev": (i32, [P, P, i32]),
+        "gvx_frame_eig_dev": (i32, [P, u64, P]),
     }
     for name, (res, args) in sig.items():
         # an older build (a GVX_LIB variant timed against the tree) may lack newer
@@ -434,6 +435,12 @@ class Context:
                                                        d_init, d_n, capacity, cam_w, cam_h, fb_thresh, border,
                                                        C.byref(kp), C.byref(dp), d_tracks, d_counts, d_frame_index,
                                                        max_frames), "gvx_track_frame_record_dev")
+
+    def frame_eig_dev(self, frame_id: int, detect: Optional[DetectParams] = None):
+        """The detection's eigenvalue map of a cached frame, kept with the frame for
+        the next tracking call on it (gvx_frame_eig_dev)."""
+        dp = detect or DetectParams.default()
+        self._check(self._L.gvx_frame_eig_dev(self._h, frame_id, C.byref(dp)), "gvx_frame_eig_dev")
 
     def copy_indexed_dev(self, d_dst: int, d_src_base: int, nbytes: int, d_index: int, n_src: int):
         self._check(self._L.gvx_copy_indexed_dev(self._h, d_dst, d_src_base, nbytes, d_index, n_src),

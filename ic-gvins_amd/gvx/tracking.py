@@ -84,7 +84,8 @@ class DeviceSequenceTracker:
 
     def __init__(self, ctx: Context, w: int, h: int, n_features: int = 150,
                  klt: Optional[KltParams] = None, detect: Optional[DetectParams] = None,
-                 ids=(0, 1), graph: bool = False, device=None, frames=None, pipeline: bool = False):
+                 ids=(0, 1), graph: bool = False, device=None, frames=None, pipeline: bool = False,
+                 eig_branch: bool = False):
         import torch
         self.ctx, self.w, self.h, self.n = ctx, w, h, n_features
         self.kp = klt or KltParams.default()
@@ -107,6 +108,10 @@ class DeviceSequenceTracker:
         # at its own device counter.  At t = F - 1 that counter is past the last
         # frame: the device clamps it (the spare preprocessing is never tracked).
         self.pipeline = bool(pipeline) and frames is not None
+        # eig_branch (pipelined only): the detection's eigenvalue map of every block
+        # on the preprocessing branch (gvx_frame_eig_dev) instead of the tiles of the
+        # detecting blocks in the tracking graph
+        self.eig_branch = bool(eig_branch) and self.pipeline
         if self.pipeline:
             if len(self.ids) < 3:
                 self.ids = tuple(self.ids) + (max(self.ids) + 1,)
@@ -123,6 +128,10 @@ class DeviceSequenceTracker:
         self.ctx.frame_preprocess_indexed_dev(self.ids[(t + 1) % 3], self.frames.data_ptr(), self.w * self.h,
                                               self.pindex.data_ptr(), self.frames.shape[0], self.w, self.h,
                                               params=self.kp)
+        # the detection's eigenvalue map of frame t+1 on this branch too: it depends
+        # on the image alone, so frame t+1's tracking only selects
+        if self.eig_branch:
+            self.ctx.frame_eig_dev(self.ids[(t + 1) % 3], detect=self.dp)
         self.ctx.index_advance_dev(self.pindex.data_ptr(), 1)
 
     def _track_cur(self, t: int):
@@ -150,6 +159,8 @@ class DeviceSequenceTracker:
             ctx.frame_preprocess_indexed_dev(self.ids[0], self.frames.data_ptr(), self.w * self.h,
                                              self.index.data_ptr(), self.frames.shape[0], self.w, self.h,
                                              params=self.kp)
+            if self.eig_branch:
+                ctx.frame_eig_dev(self.ids[0], detect=self.dp)
         ctx.branch_join()
         if graphs:
             ga = self._graph(("pre", t % 3), self._pre_next, t)

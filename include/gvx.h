@@ -375,6 +375,15 @@ gvx_status gvx_track_frame_dev(gvx_ctx* ctx, uint64_t prev_frame, uint64_t next_
                                int32_t cam_h, double fb_thresh, double border, const gvx_klt_params* klt,
                                const gvx_detect_params* detect, int32_t* d_kept, float* d_corners,
                                int32_t* d_n_corners);
+/* The part of featuresDetection that depends on the frame alone -- the
+   cornerMinEigenVal map of every detection block (goodFeaturesToTrack's
+   eigenvalue image, tracking.cc:647) -- computed for frame `frame` now, on the
+   context stream, and kept with the frame until it is written again.  A later
+   gvx_track_frame_[record_]dev on that frame with the same detection grid then
+   reads it instead of launching it, so a pipelined tracker can put it on the
+   branch that prepares the next frame (off the tracking critical path).
+   Replaces: nothing in the reference (an evaluation-order split of :647). */
+gvx_status gvx_frame_eig_dev(gvx_ctx* ctx, uint64_t frame, const gvx_detect_params* detect);
 /* gvx_track_frame_dev followed by gvx_track_record_dev (below) on the same state,
    the record appended by the detection's last kernel (one launch less per frame). */
 gvx_status gvx_track_frame_record_dev(gvx_ctx* ctx, uint64_t prev_frame, uint64_t next_frame, int32_t track,

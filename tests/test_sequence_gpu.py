@@ -165,18 +165,20 @@ def test_long_sequence_bit_exact(ctx, orc, gvx_mod, long_sequence):
     assert n_detect >= 10, n_detect
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline):
+@pytest.mark.parametrize("pipeline,eig_branch", [(False, False), (True, False), (True, True)])
+def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline, eig_branch):
     """The bench's loop over the same 300 frames: the HBM-resident sequence, one
     captured graph per frame-slot rotation replayed per frame (pipelined: frame
     t+1's CLAHE + pyramid graph on the side stream beside frame t's tracking
     graph, three slots rotating 100 times), the per-frame track records written
-    on the device -- every record bit-exact against the oracle loop's track list."""
+    on the device -- every record bit-exact against the oracle loop's track list.
+    eig_branch: the detection's eigenvalue maps computed on the preprocessing
+    branch (gvx_frame_eig_dev) instead of in the tracking graph."""
     from gvx.tracking import DeviceSequenceTracker
     frames, ref = long_sequence
     trk = DeviceSequenceTracker(ctx, W, H, N, klt=gvx_mod.KltParams.default(max_level=L),
                                 detect=gvx_mod.DetectParams.default(max_features=N), ids=(40, 41), graph=True,
-                                frames=frames, pipeline=pipeline)
+                                frames=frames, pipeline=pipeline, eig_branch=eig_branch)
     try:
         for _ in range(LONG):
             trk.step()

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Device time of gvx_clahe_batch_dev over the bench's 256 1280x560 frames
-(context profile events), for A/B runs of libgvx variants (GVX_LIB)."""
+(context profile events), for A/B runs of libgvx variants (GVX_LIB).
+--inplace: source = destination, which takes the two-kernel form."""
 import json
 import os
 import sys
@@ -16,7 +17,8 @@ n, w, h = 256, 1280, 560
 rng = np.random.default_rng(5)
 imgs = np.stack([synth.make_image(w, h, rng) for _ in range(16)])
 src = torch.from_numpy(np.tile(imgs, (n // 16, 1, 1))).cuda()
-dst = torch.empty_like(src)
+inplace = "--inplace" in sys.argv
+dst = src if inplace else torch.empty_like(src)
 ctx = gvx.Context(0)
 for _ in range(5):
     ctx.clahe_batch_dev(n, w, h, src.data_ptr(), dst.data_ptr())
@@ -29,6 +31,6 @@ for _ in range(reps):
 ctx.sync()
 ms, _ = ctx.profile_read("clahe")
 ctx.profile(False)
-print(json.dumps({"lib": os.environ.get("GVX_LIB", "base"), "ms_per_call": ms / reps,
+print(json.dumps({"lib": os.environ.get("GVX_LIB", "base"), "inplace": inplace, "ms_per_call": ms / reps,
                   "frac": 2.0 * w * h * n / (ms / reps * 1e-3) / 8e12}))
 ctx.close()
