@@ -37,6 +37,44 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
+def rank_setup(args):
+    """One process per GPU: (dist | None, device, world, rank, local).
+
+    nccl (RCCL over xGMI, the default) needs one GPU per rank.  gloo is the
+    rehearsal backend: ranks may share a GPU (local rank mod the device count),
+    so the real per-rank path (context, kernels, collectives, max over ranks)
+    runs at world_size 2 on a one-GPU box (tests/test_bench_dist_gpu.py)."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = args.backend or "nccl"
+    ndev = torch.cuda.device_count()  # counting devices does not initialise the GPU
+    if world > 1 and backend == "gloo" and ndev > 0:
+        local = local % ndev
+    elif local >= max(ndev, 1):
+        sys.exit(f"bench.py: local rank {local} but {ndev} GPU(s); {backend} needs one GPU per rank")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return dist, dev, world, rank, local
+
+
+def coll_device(dist, dev):
+    """Where a collective's tensors live: the GPU for RCCL, host memory for gloo."""
+    import torch
+    if dist and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return dev
+
+
 def algorithmic_bytes(w, h, levels, n):
     """B = 2*A0 + 4*Ap + 16*(A0 + Ap) + 58*N per frame pair."""
     a0 = w * h
@@ -212,18 +250,7 @@ def main():
     import torch
     import gvx
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dist, dev, world, rank, local = rank_setup(args)
 
     W, H, N, L, Pn = args.width, args.height, args.features, args.levels, args.pairs
     from gvx import synth
@@ -249,12 +276,13 @@ def main():
                                   dN.data_ptr(), dB.data_ptr(), dF.data_ptr(), dK.data_ptr(), dNK.data_ptr(),
                                   params=p)
 
-    gathered = [torch.empty_like(dNK) for _ in range(world)] if world > 1 else None
+    cdev = coll_device(dist, dev)
+    gathered = [torch.empty(dNK.shape, dtype=dNK.dtype, device=cdev) for _ in range(world)] if world > 1 else None
 
     def collect():
         if world > 1 and args.gather:
             ctx.sync()
-            dist.all_gather(gathered, dNK)  # offline batch replay: results to every rank
+            dist.all_gather(gathered, dNK.to(cdev))  # offline batch replay: results to every rank
 
     for _ in range(args.warmup):
         step()
@@ -296,8 +324,8 @@ def main():
                 "what": "gvx_klt_fb_batch on host buffers (2 x %.0f MB image upload + points per step)"
                         % (I.nbytes / 1e6)}
     if world > 1 and not args.gather:
-        collect_once = [torch.empty_like(dNK) for _ in range(world)]
-        dist.all_gather(collect_once, dNK)  # results check, outside the timed region
+        collect_once = [torch.empty(dNK.shape, dtype=dNK.dtype, device=cdev) for _ in range(world)]
+        dist.all_gather(collect_once, dNK.to(cdev))  # results check, outside the timed region
 
     # the metric's second half (BASELINE.json: factor-Jacobian eval/s), timed in
     # the same run: configs[3]'s factor batch (its own line under "factors")
@@ -492,20 +520,8 @@ def preprocess_leg(ctx, dI, dJ, Pn, W, H, steps):
 
 def factors_main(args):
     """`--config 4`: the factor leg on its own, as the line's headline."""
-    import torch
     import gvx
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dist, dev, world, rank, local = rank_setup(args)
     ctx = gvx.Context(local)
     line = factor_leg(args, ctx, dev, dist, world, rank, args.steps, window_extras=True)
     if rank == 0:
@@ -906,18 +922,7 @@ def sequence_main(args):
     import torch
     import gvx
     from gvx import synth
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dist, dev, world, rank, local = rank_setup(args)
     W, H, N, L = args.width, args.height, args.features, args.levels
     F = max(args.frames, args.warmup + 2)
     frames, _ = synth.make_sequence(W, H, F, dev, seed=synth.SEED + 7919 * rank)
@@ -976,7 +981,7 @@ def sequence_main(args):
         tracks[:] = tracker.rec_tracks.cpu().numpy()
         counts[:] = tracker.rec_counts.cpu().numpy()
     ctx.sync()
-    gathered = gather_tracks(torch.from_numpy(tracks), torch.from_numpy(counts), dist, dev)
+    gathered = gather_tracks(torch.from_numpy(tracks), torch.from_numpy(counts), dist, coll_device(dist, dev))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -1046,6 +1051,9 @@ def sequence_main(args):
             "host_overhead_frac": round(max(0.0, 1.0 - dev_ms / (elapsed / timed * 1e3)), 3) if dev_ms else None,
             "host_enqueue_ms_per_frame": round(t_enq / timed * 1e3, 4),
             "gathered_ranks": len(gathered) if gathered else 0,
+            "gather_check": bool(gathered and np.array_equal(gathered[0][0].numpy(), tracks)
+                                 and np.array_equal(gathered[0][1].numpy(), counts)
+                                 and all(int(c[F - timed:].min()) > 0 for _, c in gathered)),
         }))
     if dist:
         dist.destroy_process_group()
@@ -1072,7 +1080,7 @@ def max_over_ranks(elapsed, dist, dev=None):
     if not dist:
         return elapsed
     import torch
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device(dist, dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

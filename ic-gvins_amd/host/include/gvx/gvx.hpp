@@ -278,6 +278,7 @@ inline bool featuresDetection(const GpuFrame& frame, const std::vector<Point2f>&
 class CLAHE {
 public:
     CLAHE(Context& ctx, double clipLimit = 40.0, Size tileGridSize = Size{8, 8}) : ctx_(&ctx) {
+        gvx_clahe_params_default(&p_);  // MONO8 source (cv::CLAHE::apply takes CV_8UC1)
         p_.clip_limit = clipLimit;
         p_.tiles_x = tileGridSize.width;
         p_.tiles_y = tileGridSize.height;

@@ -4,7 +4,9 @@
 // with their marginalized indices, marginalization(), getParamterBlocks(), then a
 // MarginalizationFactor evaluated at the linearisation point.  The residual blocks
 // replay precomputed residuals / Jacobians (files from tests/test_host_cpp.py).
-// Usage: test_marg_host <dir>; writes <dir>/index.bin, J0.bin, e0.bin, res.bin.
+// Usage: test_marg_host <dir> [exact|nodev]; writes <dir>/index.bin, J0.bin, e0.bin,
+// res.bin.  `exact`: gvx_set_marg_solver(EXACT) (Eigen's eigen-solver order, bit-exact
+// against the restatement); default: the FAST solver (device Cholesky).
 #include <gvx/gvx.hpp>
 
 #include <cstdio>
@@ -40,6 +42,10 @@ int main(int argc, char** argv) {
         const auto fmarg = load<int32_t>(d + "/fmarg.bin");
         const auto fdata = load<double>(d + "/fdata.bin");
         gvx::Context ctx(0);
+        if (argc > 2 && std::string(argv[2]) == "exact") {
+            const gvx_status st = gvx_set_marg_solver(ctx.get(), GVX_MARG_SOLVER_EXACT);
+            if (st != GVX_OK) throw gvx::Error(st, "gvx_set_marg_solver");
+        }
         std::vector<std::vector<double>> blocks;
         size_t o = 0;
         for (int s : bsize) {

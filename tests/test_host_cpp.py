@@ -210,7 +210,7 @@ def test_marg_mirror_matches_oracle(marg_bin, orc, tmp_path):
     the next MarginalizationFactor at the linearisation point returns e0."""
     d = str(tmp_path)
     p, nb = _marg_files(d, orc)
-    r = subprocess.run([marg_bin, d], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([marg_bin, d, "exact"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
     index = np.fromfile(f"{d}/index.bin", np.int32)
     marg = set(np.nonzero(p["index"] < p["m"])[0])
@@ -223,5 +223,30 @@ def test_marg_mirror_matches_oracle(marg_bin, orc, tmp_path):
     r_ = p["L"] - m
     assert np.array_equal(np.fromfile(f"{d}/J0.bin").reshape(r_, r_).T, J0)
     assert np.array_equal(np.fromfile(f"{d}/e0.bin"), e0)
+    res = np.fromfile(f"{d}/res.bin")
+    np.testing.assert_allclose(res, e0, rtol=0, atol=1e-14 * np.abs(J0).sum(1).max())
+
+
+@pytest.mark.gpu
+def test_marg_mirror_fast_solver(marg_bin, orc, tmp_path):
+    """The mirror with the default FAST solver (device Cholesky): J0 / e0 are a
+    different factorisation of the same prior, so they are checked by what the
+    next window uses -- J0^T J0 = Hp and J0^T e0 = -bp (marginalization_info.h:153-167)
+    -- and the next MarginalizationFactor at the linearisation point returns e0."""
+    d = str(tmp_path)
+    p, nb = _marg_files(d, orc)
+    r = subprocess.run([marg_bin, d], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+    index = np.fromfile(f"{d}/index.bin", np.int32)
+    marg = set(np.nonzero(p["index"] < p["m"])[0])
+    m = int(sum(6 if p["size"][b] == 7 else p["size"][b] for b in marg))
+    H0, b0 = orc.marg_construct(dict(p, index=index))
+    Hp, bp, _ = orc.marg_schur(H0, b0, m)
+    r_ = p["L"] - m
+    J0 = np.fromfile(f"{d}/J0.bin").reshape(r_, r_).T
+    e0 = np.fromfile(f"{d}/e0.bin")
+    scale = np.abs(Hp).max()
+    np.testing.assert_allclose(J0.T @ J0, Hp, rtol=0, atol=1e-9 * scale)
+    np.testing.assert_allclose(J0.T @ e0, -bp, rtol=0, atol=1e-9 * max(np.abs(bp).max(), 1.0))
     res = np.fromfile(f"{d}/res.bin")
     np.testing.assert_allclose(res, e0, rtol=0, atol=1e-14 * np.abs(J0).sum(1).max())
