@@ -224,6 +224,9 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="configs[4]: one graph per frame, frame t+1's CLAHE + pyramid after frame t's tracking "
                          "(default: beside it, a preprocessing graph on a side stream)")
+    ap.add_argument("--frame-batch", type=int, default=8,
+                    help="configs[4] pipelined: frames per preprocessing / tracking graph (the stream fork / join "
+                         "and the graph launches once per K frames; 1 = a graph pair per frame)")
     ap.add_argument("--eig-branch", action="store_true",
                     help="configs[4] pipelined: the detection's eigenvalue map on the preprocessing branch")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
@@ -943,7 +946,8 @@ def sequence_main(args):
         # side stream beside frame t's tracking graph (the outputs are the same:
         # tests/test_sequence_gpu.py); --no-pipeline: one graph per frame
         tracker = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=True, device=dev, frames=frames,
-                                        pipeline=not args.no_pipeline, eig_branch=args.eig_branch)
+                                        pipeline=not args.no_pipeline, eig_branch=args.eig_branch,
+                                        batch=args.frame_batch)
 
         def frame(t):
             tracker.step()
@@ -1035,10 +1039,12 @@ def sequence_main(args):
                                    f"RCCL gather of all per-frame tracks to rank 0",
                        "loop": (("device-resident: one captured hipGraph launch per frame (gvx_track_frame_dev)"
                                  if args.no_pipeline else
-                                 "device-resident, pipelined: per frame t a tracking graph (gvx_track_frame_dev) on "
-                                 "the context stream beside a graph preprocessing frame t+1 on its side stream "
-                                 "(gvx_branch_begin/_end/_join), then the track record")
+                                 ("device-resident, pipelined: a graph tracking frames t..t+K-1 "
+                                  "(gvx_track_frame_dev + the track record, per frame) on the context stream beside a "
+                                  "graph preprocessing frames t+K..t+2K-1 on its side stream "
+                                  "(gvx_branch_begin/_end/_join), K = %d" % args.frame_batch))
                                 if device_loop else "host loop: SequenceTracker, host round trips per frame"),
+                       "frame_batch": args.frame_batch if device_loop and not args.no_pipeline else None,
                        "parallelism": f"sequences sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,

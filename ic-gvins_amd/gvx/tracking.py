@@ -85,7 +85,7 @@ class DeviceSequenceTracker:
     def __init__(self, ctx: Context, w: int, h: int, n_features: int = 150,
                  klt: Optional[KltParams] = None, detect: Optional[DetectParams] = None,
                  ids=(0, 1), graph: bool = False, device=None, frames=None, pipeline: bool = False,
-                 eig_branch: bool = False):
+                 eig_branch: bool = False, batch: int = 1):
         import torch
         self.ctx, self.w, self.h, self.n = ctx, w, h, n_features
         self.kp = klt or KltParams.default()
@@ -112,10 +112,17 @@ class DeviceSequenceTracker:
         # on the preprocessing branch (gvx_frame_eig_dev) instead of the tiles of the
         # detecting blocks in the tracking graph
         self.eig_branch = bool(eig_branch) and self.pipeline
+        # batch (pipelined only): frames go to the device K = batch at a time -- a
+        # graph preprocessing K frames on the side branch beside a graph tracking the
+        # previous K (3 sets of K frame slots rotating), so the branch fork / join
+        # and the graph launches are paid once per K frames instead of per frame
+        # (tools/graph_probe.hip: a stream-pair fork/join costs ~13-15 us per frame)
+        self.batch = max(1, int(batch)) if self.pipeline else 1
         if self.pipeline:
-            if len(self.ids) < 3:
-                self.ids = tuple(self.ids) + (max(self.ids) + 1,)
-            self.pindex = torch.ones(1, dtype=torch.int32, device=dev)
+            need = 3 * self.batch
+            base = max(self.ids) + 1
+            self.ids = tuple(self.ids)[:need] + tuple(range(base, base + max(0, need - len(self.ids))))
+            self.pindex = torch.full((1,), 0 if self.batch > 1 else 1, dtype=torch.int32, device=dev)
         if frames is not None:
             F = frames.shape[0]
             self.index = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -170,6 +177,54 @@ class DeviceSequenceTracker:
         ctx.branch_end()
         ctx.graph_launch(gb) if graphs else self._track_cur(t)
 
+    def _set(self, b: int):
+        K = self.batch
+        return self.ids[(b % 3) * K:(b % 3 + 1) * K]
+
+    def _batch_len(self, b: int) -> int:
+        return min(self.batch, self.frames.shape[0] - b * self.batch)
+
+    def _pre_batch(self, b: int):
+        # frames b*K .. b*K + len - 1 (read at the branch's own counter) into set b % 3
+        for fid in self._set(b)[:self._batch_len(b)]:
+            self.ctx.frame_preprocess_indexed_dev(fid, self.frames.data_ptr(), self.w * self.h,
+                                                  self.pindex.data_ptr(), self.frames.shape[0], self.w, self.h,
+                                                  params=self.kp)
+            if self.eig_branch:
+                self.ctx.frame_eig_dev(fid, detect=self.dp)
+            self.ctx.index_advance_dev(self.pindex.data_ptr(), 1)
+
+    def _trk_batch(self, b: int):
+        cur, prv = self._set(b), self._set(b - 1)
+        for i in range(self._batch_len(b)):
+            t = b * self.batch + i
+            self.ctx.track_frame_record_dev(cur[i - 1] if i else prv[-1], cur[i], t > 0, self.pts.data_ptr(),
+                                            self.vel.data_ptr(), self.init.data_ptr(), self.count.data_ptr(), self.n,
+                                            self.w, self.h, self.rec_tracks.data_ptr(), self.rec_counts.data_ptr(),
+                                            self.index.data_ptr(), self.frames.shape[0], klt=self.kp, detect=self.dp)
+
+    def _enqueue_batch(self, b: int):
+        """Batch b: join the branch that preprocessed it, fork the preprocessing of
+        batch b+1 (after batch b-1's tracking, the last reader of its slots), then
+        batch b's tracking.  Whole batches replay captured graphs once every set's
+        slots exist (batch >= 3); a short last batch runs eagerly."""
+        ctx, K = self.ctx, self.batch
+        nb = (self.frames.shape[0] + K - 1) // K
+        if b == 0:
+            self._pre_batch(0)
+        ctx.branch_join()
+        # graphs are captured with no branch open
+        gp = gt = None
+        if self.graph and b + 1 < nb and b + 1 >= 3 and self._batch_len(b + 1) == K:
+            gp = self._graph(("preK", (b + 1) % 3), self._pre_batch, b + 1)
+        if self.graph and b >= 3 and self._batch_len(b) == K:
+            gt = self._graph(("trkK", b % 3), self._trk_batch, b)
+        if b + 1 < nb:
+            ctx.branch_begin()
+            ctx.graph_launch(gp) if gp is not None else self._pre_batch(b + 1)
+            ctx.branch_end()
+        ctx.graph_launch(gt) if gt is not None else self._trk_batch(b)
+
     def _enqueue(self, d_frame: Optional[int], t: int):
         if self.pipeline:
             return self._enqueue_pipelined(t, False)
@@ -201,7 +256,11 @@ class DeviceSequenceTracker:
             raise IndexError(f"step {t}: the resident sequence has {self.frames.shape[0]} frames")
         if self.frames is None and d_frame is None:
             raise ValueError("step() needs the frame's device pointer when no sequence is resident")
-        if not self.graph or t < 3:
+        if self.batch > 1:
+            # frames t .. t + K - 1 are enqueued together at the first of them
+            if t % self.batch == 0:
+                self._enqueue_batch(t // self.batch)
+        elif not self.graph or t < 3:
             self._enqueue(d_frame, t)  # the first frames also size every buffer
         elif self.pipeline:
             self._enqueue_pipelined(t, True)

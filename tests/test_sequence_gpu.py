@@ -81,16 +81,19 @@ def test_sequence_replay_bit_exact(ctx, orc, gvx_mod, n_frames):
     assert n_tracked > 100 * (n_frames - 1) and n_detect >= 2
 
 
-@pytest.mark.parametrize("graph,resident,pipeline", [(False, False, False), (True, False, False), (True, True, False),
-                                                     (False, True, True), (True, True, True)])
-def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident, pipeline):
+@pytest.mark.parametrize("graph,resident,pipeline,batch", [(False, False, False, 1), (True, False, False, 1),
+                                                           (True, True, False, 1), (False, True, True, 1),
+                                                           (True, True, True, 1), (False, True, True, 4),
+                                                           (True, True, True, 4)])
+def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident, pipeline, batch):
     """gvx_track_frame_dev (the tracker state on the device, no host round trip;
     with graph=True one captured graph per frame parity replayed per frame)
     gives the same per-frame track list as SequenceTracker, whose every step the
     test above holds bit-exact against the oracle.  pipeline: frame t+1's
     preprocessing runs as a side branch beside frame t's tracking (three frame
     slots; with graphs, a preprocessing graph and a tracking graph per slot
-    rotation on two streams)."""
+    rotation on two streams).  batch: K frames per preprocessing / tracking
+    graph (3 sets of K slots)."""
     import torch
     from gvx import synth
     from gvx.tracking import DeviceSequenceTracker, SequenceTracker
@@ -101,7 +104,7 @@ def test_device_resident_sequence_matches(ctx, gvx_mod, graph, resident, pipelin
     dp = gvx_mod.DetectParams.default(max_features=N)
     ref = SequenceTracker(ctx, W, H, N, klt=kp, detect=dp, ids=(10, 11))
     trk = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, ids=(20, 21), graph=graph, device=dev,
-                                frames=frames if resident else None, pipeline=pipeline)
+                                frames=frames if resident else None, pipeline=pipeline, batch=batch)
     try:
         wants = []
         for t in range(n_frames):
@@ -165,20 +168,23 @@ def test_long_sequence_bit_exact(ctx, orc, gvx_mod, long_sequence):
     assert n_detect >= 10, n_detect
 
 
-@pytest.mark.parametrize("pipeline,eig_branch", [(False, False), (True, False), (True, True)])
-def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline, eig_branch):
+@pytest.mark.parametrize("pipeline,eig_branch,batch", [(False, False, 1), (True, False, 1), (True, True, 1),
+                                                       (True, False, 8), (True, True, 7)])
+def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline, eig_branch, batch):
     """The bench's loop over the same 300 frames: the HBM-resident sequence, one
     captured graph per frame-slot rotation replayed per frame (pipelined: frame
     t+1's CLAHE + pyramid graph on the side stream beside frame t's tracking
     graph, three slots rotating 100 times), the per-frame track records written
     on the device -- every record bit-exact against the oracle loop's track list.
     eig_branch: the detection's eigenvalue maps computed on the preprocessing
-    branch (gvx_frame_eig_dev) instead of in the tracking graph."""
+    branch (gvx_frame_eig_dev) instead of in the tracking graph.  batch: K frames
+    per graph (the bench's configs[4] loop); 300 = 42 x 7 + 6 ends on a short
+    eager batch."""
     from gvx.tracking import DeviceSequenceTracker
     frames, ref = long_sequence
     trk = DeviceSequenceTracker(ctx, W, H, N, klt=gvx_mod.KltParams.default(max_level=L),
                                 detect=gvx_mod.DetectParams.default(max_features=N), ids=(40, 41), graph=True,
-                                frames=frames, pipeline=pipeline, eig_branch=eig_branch)
+                                frames=frames, pipeline=pipeline, eig_branch=eig_branch, batch=batch)
     try:
         for _ in range(LONG):
             trk.step()
