@@ -224,7 +224,7 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="configs[4]: one graph per frame, frame t+1's CLAHE + pyramid after frame t's tracking "
                          "(default: beside it, a preprocessing graph on a side stream)")
-    ap.add_argument("--frame-batch", type=int, default=8,
+    ap.add_argument("--frame-batch", type=int, default=16,
                     help="configs[4] pipelined: frames per preprocessing / tracking graph (the stream fork / join "
                          "and the graph launches once per K frames; 1 = a graph pair per frame)")
     ap.add_argument("--eig-branch", action="store_true",

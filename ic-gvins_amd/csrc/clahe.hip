@@ -45,6 +45,21 @@ __device__ __forceinline__ int refl101(int p, int len) {
     return p;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// a * {b.lo, b.lo} and a * {b.hi, b.hi}: one v_pk_mul_f32 each, the half of b
+// broadcast through op_sel (no register pair per multiplier)
+__device__ __forceinline__ f2 pk_mul_lo(f2 a, f2 b) {
+    f2 r;
+    __asm__("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_hi(f2 a, f2 b) {
+    f2 r;
+    __asm__("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t sat_round_u8(float v) {
     const int r = (int)__builtin_rintf(v);  // cvRound: half to even
     return (uint32_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
@@ -92,10 +107,14 @@ __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, 
             }
         cl = __builtin_amdgcn_readlane(wave_incl_scan(cl, lane), 63);  // the tile's clipped total
         const uint32_t batch = cl / 256, residual = cl - batch * 256;
-        const uint32_t step = residual ? max(256u / residual, 1u) : 1u;
+        // integer quotients through the fp32 reciprocal, corrected to exact
+        // (div_small: no integer division sequence)
+        const uint32_t step =
+            residual ? (uint32_t)max(div_small(256, (int)residual, __builtin_amdgcn_rcpf((float)residual)), 1) : 1u;
         // bin b gets one more where b % step == 0 and b / step < residual: one
         // division for the lane's first bin, then carried over its four bins
-        uint32_t q = (4u * lane) / step, r = 4u * lane - q * step;
+        uint32_t q = (uint32_t)div_small(4 * lane, (int)step, __builtin_amdgcn_rcpf((float)step)),
+                 r = 4u * lane - q * step;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             h4[i] += batch + ((residual && r == 0 && q < residual) ? 1u : 0u);
@@ -475,14 +494,15 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
     // offset of column x in the high half (past the image: a scratch histogram
     // that is never read), one register per column
     uint32_t kh[8];
-    float xa[8];
+    f2 xw[8];  // {xa1, xa} of column j
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int x = x0 + j;
         const int hoff = (x < g.w ? div_small(x, g.tw, inv_tw) : g.tiles_x) * HROW;
         const float txf = (float)x * inv_tw - 0.5f;
         const int tx1 = (int)floorf(txf);
-        xa[j] = txf - (float)tx1;
+        const float xa = txf - (float)tx1;
+        xw[j] = f2{1.0f - xa, xa};
         kh[j] = (uint32_t)((min(tx1, g.tiles_x - 1) + 1) * TROW) | ((uint32_t)hoff << 16);
     }
     auto pixel = [&](int y, int x) -> uint32_t {
@@ -591,8 +611,10 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
         __syncthreads();
     };
     // the band's table from LUT rows p (ty1) and q (ty2): entry (k, v) =
-    // {L[p][tx1c][v], L[p][tx2c][v], L[q][tx1c][v], L[q][tx2c][v]} as fp32,
-    // tx1c = max(k - 1, 0), tx2c = min(k, tiles_x - 1) (the reference's clamps)
+    // {L[p][tx1c][v], L[q][tx1c][v], L[p][tx2c][v], L[q][tx2c][v]} as fp32,
+    // tx1c = max(k - 1, 0), tx2c = min(k, tiles_x - 1) (the reference's clamps);
+    // the two rows of one column are adjacent, so the blend's two rows run as
+    // packed pairs (v_pk_mul_f32 / v_pk_add_f32)
     auto table = [&](int p, int q) {
         const uint32_t* P = lrb + (p & 1) * g.tiles_x * 64;
         const uint32_t* Q = lrb + (q & 1) * g.tiles_x * 64;
@@ -604,8 +626,8 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
             float4* o = tab + k * TROW + 4 * qd;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                o[j] = float4{(float)((a >> (8 * j)) & 255u), (float)((bb >> (8 * j)) & 255u),
-                              (float)((c >> (8 * j)) & 255u), (float)((d >> (8 * j)) & 255u)};
+                o[j] = float4{(float)((a >> (8 * j)) & 255u), (float)((c >> (8 * j)) & 255u),
+                              (float)((bb >> (8 * j)) & 255u), (float)((d >> (8 * j)) & 255u)};
         }
     };
     // CLAHE_Interpolation_Body for the rows of tile row k in [ys, ye) held in px
@@ -616,6 +638,7 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
             if (y < ys || y >= ye) continue;
             const float tyf = (float)y * inv_th - 0.5f;
             const float ya = tyf - floorf(tyf), ya1 = 1.0f - ya;
+            const f2 yv = {ya1, ya};
             uint32_t out[2] = {0, 0};
             float4 ev[8];  // the 8 gathers first, then the blends
 #pragma unroll
@@ -625,8 +648,11 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float4 e = ev[j];
-                const float xa1 = 1.0f - xa[j];
-                const float res = (e.x * xa1 + e.y * xa[j]) * ya1 + (e.z * xa1 + e.w * xa[j]) * ya;
+                // {top, bot} = {L[p][tx1], L[q][tx1]} * xa1 + {L[p][tx2], L[q][tx2]} * xa, then
+                // res = top * ya1 + bot * ya: the reference's products and sums, each rounded
+                const f2 tb = pk_mul_lo(f2{e.x, e.y}, xw[j]) + pk_mul_hi(f2{e.z, e.w}, xw[j]);
+                const f2 u = tb * yv;
+                const float res = u.x + u.y;
                 out[j >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(res, j & 3, out[j >> 2]);
             }
             uint8_t* drow = dd + (int64_t)y * dst_stride + x0;

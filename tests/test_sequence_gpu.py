@@ -169,7 +169,7 @@ def test_long_sequence_bit_exact(ctx, orc, gvx_mod, long_sequence):
 
 
 @pytest.mark.parametrize("pipeline,eig_branch,batch", [(False, False, 1), (True, False, 1), (True, True, 1),
-                                                       (True, False, 8), (True, True, 7)])
+                                                       (True, False, 8), (True, True, 7), (True, False, 16)])
 def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline, eig_branch, batch):
     """The bench's loop over the same 300 frames: the HBM-resident sequence, one
     captured graph per frame-slot rotation replayed per frame (pipelined: frame
