@@ -57,6 +57,7 @@ void* scratch(gvx_ctx* c, const std::string& name, size_t bytes) {
         return nullptr;
     }
     b.bytes = want;
+    b.fresh = true;
     return b.p;
 }
 

@@ -280,6 +280,19 @@ static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, in
             const double eps = dp->subpix_eps > 0 ? dp->subpix_eps : 0.0;
             ts.eps2 = eps * eps;
             ts.out = out;
+            ts.sel = nullptr;
+            if (!pre_eig) {
+                // the tiles' max / candidate counters: zero once at allocation, then
+                // cleared by the selection after each frame
+                DevBuf& sb = c->dev["trk_sel"];
+                ts.sel = (unsigned*)scratch(c, "trk_sel", (size_t)2 * bcnt * sizeof(unsigned));
+                if (!ts.sel) return set_err(c, GVX_ERR_OOM, "selection counters");
+                if (sb.fresh) {
+                    e = hipMemsetAsync(sb.p, 0, sb.bytes, c->stream);
+                    if (e != hipSuccess) return hip_err(c, e, "selection counters");
+                    sb.fresh = false;
+                }
+            }
             // the eigenvalue tiles of the blocks that detect (unless the frame has its map)
             if (!pre_eig) e = launch_eig_track(c, bcnt, col, row, ts, G.sc, G.sc2);
             if (e == hipSuccess) e = launch_select_track(c, bcnt, col, row, ts);

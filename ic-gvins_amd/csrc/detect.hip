@@ -311,8 +311,35 @@ __device__ float2 subpix_corner(const uint8_t* __restrict__ src, int pitch, int4
     int iter = 0;
     double err = 0;
     do {
-        for (int e = lane; e < SP_B * SP_B; e += 64)
-            patch[e] = rect_subpix_px(src, pitch, roi.z, roi.w, cIx, cIy, e / SP_B, e % SP_B, win);
+        // getRectSubPix's per-call terms (one centre for the whole patch) once, then
+        // the interior formula of rect_subpix_px per pixel (the same arithmetic)
+        const float pcx = cIx - (SP_B - 1) * 0.5f, pcy = cIy - (SP_B - 1) * 0.5f;
+        const int ipx = (int)floorf(pcx), ipy = (int)floorf(pcy);
+        if (0 <= ipx && ipx + SP_B < roi.z && 0 <= ipy && ipy + SP_B < roi.w) {
+            float pa = pcx - ipx;
+            const float pb = pcy - ipy;
+            pa = pa > 0.0001f ? pa : 0.0001f;
+            const float a12 = pa * (1.f - pb), a22 = pa * pb, b1 = 1.f - pb, b2 = pb;
+            const double ps = (1. - pa) / pa;
+            for (int e = lane; e < SP_B * SP_B; e += 64) {
+                const int i = e / SP_B, j = e - i * SP_B;
+                const int y0 = ipy + i, x0 = ipx;
+                const float t = a12 * roi_px(src, pitch, win, x0 + j + 1, y0) +
+                                a22 * roi_px(src, pitch, win, x0 + j + 1, y0 + 1);
+                float prev;
+                if (j == 0) {
+                    prev = (1 - pa) * (b1 * roi_px(src, pitch, win, x0, y0) + b2 * roi_px(src, pitch, win, x0, y0 + 1));
+                } else {
+                    const float tp = a12 * roi_px(src, pitch, win, x0 + j, y0) +
+                                     a22 * roi_px(src, pitch, win, x0 + j, y0 + 1);
+                    prev = (float)(tp * ps);
+                }
+                patch[e] = prev + t;
+            }
+        } else {
+            for (int e = lane; e < SP_B * SP_B; e += 64)
+                patch[e] = rect_subpix_px(src, pitch, roi.z, roi.w, cIx, cIy, e / SP_B, e % SP_B, win);
+        }
         wave_lds_sync();
         for (int e = lane; e < SP_W * SP_W; e += 64) {
             const int i = e / SP_W, j = e - i * SP_W;
@@ -332,8 +359,22 @@ __device__ float2 subpix_corner(const uint8_t* __restrict__ src, int pitch, int4
         }
         wave_lds_sync();
         if (lane < 5) {
-            double acc = 0;
-            for (int e = 0; e < SP_W * SP_W; ++e) acc += L.terms[lane][e];
+            // the sequential sum (OpenCV's order), its LDS reads a batch ahead of the adds
+            const double* T = L.terms[lane];
+            double acc = 0, cur[SP_W], nxt[SP_W];
+#pragma unroll
+            for (int q = 0; q < SP_W; ++q) cur[q] = T[q];
+#pragma unroll
+            for (int bt = 0; bt < SP_W; ++bt) {
+                if (bt + 1 < SP_W) {
+#pragma unroll
+                    for (int q = 0; q < SP_W; ++q) nxt[q] = T[(bt + 1) * SP_W + q];
+                }
+#pragma unroll
+                for (int q = 0; q < SP_W; ++q) acc += cur[q];
+#pragma unroll
+                for (int q = 0; q < SP_W; ++q) cur[q] = nxt[q];
+            }
             L.sums[lane] = acc;
         }
         wave_lds_sync();
@@ -361,6 +402,11 @@ __device__ __forceinline__ uint32_t fkey(float v) {
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
+// the inverse of fkey
+__device__ __forceinline__ float funkey(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
     for (int o = 32; o >= 1; o >>= 1) {
         const unsigned long long t = __shfl_xor(v, o, 64);
@@ -383,13 +429,11 @@ struct SelectShared {
     int s_nacc;
 };
 
+// minMaxLoc over the mask, TOZERO threshold, 3x3 dilate and the local-max
+// candidates of block k by one workgroup scanning its whole ROI
 template <class Allowed>
-__device__ __forceinline__ void select_block(int k, int4 roi, const float* __restrict__ E, Allowed allowed, int maxc,
-                                             double quality, float min_dist, unsigned long long* __restrict__ CK,
-                                             int2* __restrict__ corners, int max_per_block, int* __restrict__ ncorner,
-                                             const uint8_t* __restrict__ img0, int pitch,
-                                             const float* __restrict__ gmask, int max_iters, double eps2,
-                                             float2* __restrict__ out, SelectShared& S, SubpixLds* s_sub) {
+__device__ __forceinline__ void scan_block(int4 roi, const float* __restrict__ E, Allowed allowed, double quality,
+                                           unsigned long long* __restrict__ CK, SelectShared& S) {
     const int rw = roi.z, rh = roi.w;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int npx = rw * rh;
@@ -444,6 +488,20 @@ __device__ __forceinline__ void select_block(int k, int4 roi, const float* __res
             CK[slot] = ((unsigned long long)fkey(v) << 32) | (unsigned)i;
         }
     }
+    __syncthreads();
+}
+
+// goodFeaturesToTrack's greedy minDistance suppression over the S.s_ncand
+// candidates in CK, then cornerSubPix of the accepted corners
+__device__ __forceinline__ void select_corners(int k, int4 roi, int maxc, float min_dist,
+                                               const unsigned long long* __restrict__ CK, int2* __restrict__ corners,
+                                               int max_per_block, int* __restrict__ ncorner,
+                                               const uint8_t* __restrict__ img0, int pitch,
+                                               const float* __restrict__ gmask, int max_iters, double eps2,
+                                               float2* __restrict__ out, SelectShared& S, SubpixLds* s_sub) {
+    const int rw = roi.z;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) S.s_nacc = 0;
     __syncthreads();
     const int nc = S.s_ncand;
     const float md2 = min_dist * min_dist;
@@ -514,8 +572,9 @@ __global__ void __launch_bounds__(SEL_T) select_kernel(const float* __restrict__
     const int4 roi = rois[k];
     const uint8_t* M = mask + (int64_t)roi.y * w + roi.x;
     auto allowed = [&](int x, int y) -> bool { return M[(int64_t)y * w + x] != 0; };
-    select_block(k, roi, eig + k * eig_stride, allowed, want[k], quality, min_dist, cand + k * eig_stride, corners,
-                 max_per_block, ncorner, img0, pitch, gmask, max_iters, eps2, out, S, s_sub);
+    scan_block(roi, eig + k * eig_stride, allowed, quality, cand + k * eig_stride, S);
+    select_corners(k, roi, want[k], min_dist, cand + k * eig_stride, corners, max_per_block, ncorner, img0, pitch,
+                   gmask, max_iters, eps2, out, S, s_sub);
 }
 
 // featuresDetection's early exit and block k's maxCorners from the tracked points
@@ -555,15 +614,151 @@ __device__ int block_want(const TrackSelect& a, int k, int4 roi, int* s_nk, int*
 
 // The eigenvalue tiles of the tracking path, for the blocks that detect this
 // frame only (each workgroup counts the tracked points itself, as the selection
-// does): one launch, no preparation launch before it.
+// does): one launch, no preparation launch before it.  Each tile is computed
+// with a one-pixel halo of eigenvalues (the same arithmetic at every pixel, so
+// the halo equals the neighbouring tiles' values), which lets the tile do the
+// selection's two whole-ROI scans for its own pixels, spread over the grid
+// instead of one workgroup per block:
+//  * minMaxLoc over the mask: the tile's maximum over its allowed pixels (the
+//    circle mask of the tracked points, cv::circle FILLED as in the selection's
+//    bitmap) -> atomicMax of fkey(v) into sel[2k] (0: no allowed pixel yet);
+//  * the candidates: for a threshold thr > 0, "v > thr and v equals the 3x3
+//    dilation of the TOZERO-thresholded map" holds exactly when v > thr and v
+//    is >= its 8 raw neighbours (a neighbour above v is above thr; one at or
+//    below thr becomes 0 < v), so the tile appends its allowed raw local maxima
+//    with v > 0 (ROI ring excluded) to the block's list, count sel[2k + 1]; the
+//    selection keeps those above thr.  A block whose maximum is <= 0 (thr <= 0,
+//    where that equivalence fails) falls back to the full scan.
+// sel is zero at entry (the selection clears it after reading it).
+constexpr int EH_W = ET_W + 2, EH_H = ET_H + 2;  // eigenvalues with the halo
 __global__ void __launch_bounds__(256) eig_track_kernel(TrackSelect a, int ex, int ey, float sc, float sc2) {
-    __shared__ int s_nk, s_cnt;
+    __shared__ int s_nk, s_cnt, s_nc, s_nt;
+    __shared__ int2 s_circ[TS_MAX_POINTS], s_tc[TS_MAX_POINTS];
+    __shared__ uint8_t px[EH_H + 4][EH_W + 4];
+    __shared__ float cov[3][EH_H + 2][EH_W + 2];
+    __shared__ float ev[EH_H][EH_W];
+    __shared__ unsigned s_max;
     const int per = ex * ey;
     const int k = blockIdx.x / per, r = blockIdx.x - k * per;
     const int4 roi = a.rois[k];
-    if (block_want(a, k, roi, &s_nk, &s_cnt, nullptr, nullptr) <= 0) return;  // uniform
-    eig_tile(r % ex, r / ex, k, a.img0, a.pitch, a.rois, nullptr, a.eig_stride, const_cast<float*>(a.eig), sc, sc2,
-             nullptr);
+    // the circles near the ROI (ROI coordinates), only when the candidates are wanted
+    if (block_want(a, k, roi, &s_nk, &s_cnt, a.sel ? s_circ : nullptr, &s_nc) <= 0) return;  // uniform
+    if (!a.sel) {
+        eig_tile(r % ex, r / ex, k, a.img0, a.pitch, a.rois, nullptr, a.eig_stride, const_cast<float*>(a.eig), sc,
+                 sc2, nullptr);
+        return;
+    }
+    const int rw = roi.z, rh = roi.w;
+    const int tx0 = (r % ex) * ET_W, ty0 = (r / ex) * ET_H;
+    if (tx0 >= rw || ty0 >= rh) return;
+    const int t = threadIdx.x;
+    // the circles that reach the tile (a pixel then tests only those)
+    if (t == 0) {
+        s_nt = 0;
+        s_max = 0u;
+    }
+    __syncthreads();
+    const int rad = a.radius;
+    for (int i = t; i < s_nc; i += 256) {
+        const int2 c = s_circ[i];
+        if (c.x + rad >= tx0 && c.x - rad <= tx0 + ET_W - 1 && c.y + rad >= ty0 && c.y - rad <= ty0 + ET_H - 1)
+            s_tc[atomicAdd(&s_nt, 1)] = c;
+    }
+    // parent pixels for ROI coords [tx0-3, tx0+ET_W+2] x [ty0-3, ty0+ET_H+2]
+    // (clamped past rw+1 / rh+1 as in eig_tile; the reads stay in the padded ring)
+    for (int i = t; i < (EH_H + 4) * (EH_W + 4); i += 256) {
+        const int rr = i / (EH_W + 4), c = i - rr * (EH_W + 4);
+        const int yy = max(min(ty0 - 3 + rr, rh + 1), -2), xx = max(min(tx0 - 3 + c, rw + 1), -2);
+        px[rr][c] = a.img0[(int64_t)(roi.y + yy) * a.pitch + roi.x + xx];
+    }
+    __syncthreads();
+    // covariance at ROI coords [tx0-2, tx0+ET_W+1] x [ty0-2, ty0+ET_H+1]: the Sobel
+    // at the REFLECT_101 position inside the ROI (staged row / col = roi - (t0 - 3))
+    for (int i = t; i < (EH_H + 2) * (EH_W + 2); i += 256) {
+        const int rr = i / (EH_W + 2), c = i - rr * (EH_W + 2);
+        const int ry = refl(ty0 + rr - 2, rh) - ty0 + 3;
+        const int rx = refl(tx0 + c - 2, rw) - tx0 + 3;
+        float dx = 0.f, dy = 0.f;
+        if (ry >= 1 && ry <= EH_H + 2 && rx >= 1 && rx <= EH_W + 2) {
+            float rdx[3], rdy[3];
+            for (int q = 0; q < 3; ++q) {
+                const float s0 = (float)px[ry - 1 + q][rx - 1];
+                const float s1 = (float)px[ry - 1 + q][rx];
+                const float s2 = (float)px[ry - 1 + q][rx + 1];
+                float aa = -1.f * s0;
+                aa = aa + 0.f * s1;
+                aa = aa + 1.f * s2;
+                rdx[q] = aa;
+                float b = sc * s0;
+                b = b + sc2 * s1;
+                b = b + sc * s2;
+                rdy[q] = b;
+            }
+            dx = (rdx[0] + rdx[2]) * sc + rdx[1] * sc2;
+            dx = dx + 0.f;
+            dy = rdy[2] - rdy[0];
+            dy = dy + 0.f;
+        }
+        cov[0][rr][c] = dx * dx;
+        cov[1][rr][c] = dx * dy;
+        cov[2][rr][c] = dy * dy;
+    }
+    __syncthreads();
+    // eigenvalues at ROI coords [tx0-1, tx0+ET_W] x [ty0-1, ty0+ET_H]; the tile's own
+    // pixels also go to the block's map (the fallback scan reads it)
+    float* E = const_cast<float*>(a.eig) + k * a.eig_stride;
+    for (int i = t; i < EH_H * EH_W; i += 256) {
+        const int rr = i / EH_W, c = i - rr * EH_W;
+        const int x = tx0 + c - 1, y = ty0 + rr - 1;
+        if (x < 0 || y < 0 || x >= rw || y >= rh) continue;
+        double sacc[3];
+        for (int q = 0; q < 3; ++q) {
+            double acc = 0;
+            for (int d = 0; d < 3; ++d) {
+                double rs = (double)cov[q][rr + d][c];
+                rs = rs + (double)cov[q][rr + d][c + 1];
+                rs = rs + (double)cov[q][rr + d][c + 2];
+                acc = acc + rs;
+            }
+            sacc[q] = acc;
+        }
+        const float aa = (float)sacc[0] * 0.5f;
+        const float b = (float)sacc[1];
+        const float cc = (float)sacc[2] * 0.5f;
+        const float v = (aa + cc) - __fsqrt_rn((aa - cc) * (aa - cc) + b * b);
+        ev[rr][c] = v;
+        if (rr >= 1 && rr <= ET_H && c >= 1 && c <= ET_W) E[(int64_t)y * rw + x] = v;
+    }
+    __syncthreads();
+    const int nt = s_nt;
+    unsigned kmax = 0u;
+    unsigned* sel = a.sel + 2 * k;
+    unsigned long long* CK = a.cand + k * a.eig_stride;
+    for (int i = t; i < ET_H * ET_W; i += 256) {
+        const int rr = i / ET_W + 1, c = i % ET_W + 1;
+        const int x = tx0 + c - 1, y = ty0 + rr - 1;
+        if (x >= rw || y >= rh) continue;
+        bool allowed = true;
+        for (int q = 0; q < nt && allowed; ++q) {
+            const int2 cc = s_tc[q];
+            const int dyy = abs(y - cc.y);
+            if (dyy > rad) continue;
+            const int hwv = a.hw[dyy];
+            allowed = !(hwv >= 0 && abs(x - cc.x) <= hwv);
+        }
+        if (!allowed) continue;
+        const float v = ev[rr][c];
+        kmax = max(kmax, fkey(v));
+        if (v > 0.f && y >= 1 && y <= rh - 2 && x >= 1 && x <= rw - 2) {
+            bool lm = true;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) lm = lm && !(ev[rr + q / 3 - 1][c + q % 3 - 1] > v);
+            if (lm) CK[atomicAdd(&sel[1], 1u)] = ((unsigned long long)fkey(v) << 32) | (unsigned)(y * rw + x);
+        }
+    }
+    if (kmax) atomicMax(&s_max, kmax);
+    __syncthreads();
+    if (t == 0 && s_max) atomicMax(&sel[0], s_max);
 }
 
 // The tracking path's detection (gvx_track_frame_dev), one workgroup per block
@@ -586,8 +781,39 @@ __global__ void __launch_bounds__(SEL_T) select_track_kernel(TrackSelect a) {
     const int4 roi = a.rois[k];
     const int rw = roi.z, rh = roi.w, r = a.radius;
     const int want = block_want(a, k, roi, &s_nk, &s_cnt, s_circ, &s_nc);
+    // the tile scan's results (eig_track_kernel): read, then cleared for the next frame
+    unsigned smax = 0u, sncand = 0u;
+    if (a.sel) {
+        smax = a.sel[2 * k];
+        sncand = a.sel[2 * k + 1];
+        __syncthreads();  // every thread has read them
+        if (t == 0) {
+            a.sel[2 * k] = 0u;
+            a.sel[2 * k + 1] = 0u;
+        }
+    }
     if (want <= 0) {  // uniform over the workgroup
         if (t == 0) a.ncorner[k] = 0;
+        return;
+    }
+    unsigned long long* CK = a.cand + k * a.eig_stride;
+    // the tile scan applies when the block's maximum over the mask is > 0
+    const float tmax = smax ? funkey(smax) : 0.f;
+    if (a.sel && tmax > 0.f) {
+        const float thr = (float)((double)tmax * a.quality);
+        if (t == 0) S.s_ncand = 0;
+        __syncthreads();
+        // keep the local maxima above thr, compacted in place a chunk at a time
+        // (every key of a chunk is read before any slot of it is written)
+        for (int c0 = 0; c0 < (int)sncand; c0 += SEL_T) {
+            const int i = c0 + t;
+            const unsigned long long key = i < (int)sncand ? CK[i] : 0ull;
+            __syncthreads();
+            if (i < (int)sncand && funkey((unsigned)(key >> 32)) > thr) CK[atomicAdd(&S.s_ncand, 1)] = key;
+            __syncthreads();
+        }
+        select_corners(k, roi, want, a.min_dist, CK, a.corners, a.max_per_block, a.ncorner, a.img0, a.pitch, a.gmask,
+                       a.max_iters, a.eps2, a.out, S, s_sub);
         return;
     }
     const int wpr = (rw + 31) >> 5;
@@ -610,9 +836,9 @@ __global__ void __launch_bounds__(SEL_T) select_track_kernel(TrackSelect a) {
     }
     __syncthreads();
     auto allowed = [&](int x, int y) -> bool { return (bm[y * wpr + (x >> 5)] >> (x & 31)) & 1u; };
-    select_block(k, roi, a.eig + k * a.eig_stride, allowed, want, a.quality, a.min_dist, a.cand + k * a.eig_stride,
-                 a.corners, a.max_per_block, a.ncorner, a.img0, a.pitch, a.gmask, a.max_iters, a.eps2, a.out, S,
-                 s_sub);
+    scan_block(roi, a.eig + k * a.eig_stride, allowed, a.quality, CK, S);
+    select_corners(k, roi, want, a.min_dist, CK, a.corners, a.max_per_block, a.ncorner, a.img0, a.pitch, a.gmask,
+                   a.max_iters, a.eps2, a.out, S, s_sub);
 }
 
 }  // namespace

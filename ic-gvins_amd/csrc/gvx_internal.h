@@ -39,6 +39,7 @@ PyrLayout make_layout(int w, int h, int max_level, int win);
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool fresh = false;  // (re)allocated since a caller last cleared it (zero-initialised state)
 };
 
 struct Frame {
@@ -363,6 +364,10 @@ struct TrackSelect {
     int max_iters;
     double eps2;
     float2* out;
+    // per block {fkey of the max over the mask, candidate count} from the tiles'
+    // scan (eig_track_kernel), zero between frames; nullptr: the selection scans
+    // the whole ROI itself (an eigenvalue map computed elsewhere)
+    unsigned* sel;
 };
 size_t select_track_lds(int max_rw, int max_rh);
 // the eigenvalue tiles of the blocks that detect this frame (a.eig is written)
