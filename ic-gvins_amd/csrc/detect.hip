@@ -321,20 +321,29 @@ __device__ float2 subpix_corner(const uint8_t* __restrict__ src, int pitch, int4
             pa = pa > 0.0001f ? pa : 0.0001f;
             const float a12 = pa * (1.f - pb), a22 = pa * pb, b1 = 1.f - pb, b2 = pb;
             const double ps = (1. - pa) / pa;
-            for (int e = lane; e < SP_B * SP_B; e += 64) {
-                const int i = e / SP_B, j = e - i * SP_B;
-                const int y0 = ipy + i, x0 = ipx;
-                const float t = a12 * roi_px(src, pitch, win, x0 + j + 1, y0) +
-                                a22 * roi_px(src, pitch, win, x0 + j + 1, y0 + 1);
-                float prev;
-                if (j == 0) {
-                    prev = (1 - pa) * (b1 * roi_px(src, pitch, win, x0, y0) + b2 * roi_px(src, pitch, win, x0, y0 + 1));
-                } else {
-                    const float tp = a12 * roi_px(src, pitch, win, x0 + j, y0) +
-                                     a22 * roi_px(src, pitch, win, x0 + j, y0 + 1);
-                    prev = (float)(tp * ps);
+            auto patch_px = [&](auto px) {
+                for (int e = lane; e < SP_B * SP_B; e += 64) {
+                    const int i = e / SP_B, j = e - i * SP_B;
+                    const int y0 = ipy + i, x0 = ipx;
+                    const float t = a12 * px(x0 + j + 1, y0) + a22 * px(x0 + j + 1, y0 + 1);
+                    float prev;
+                    if (j == 0) {
+                        prev = (1 - pa) * (b1 * px(x0, y0) + b2 * px(x0, y0 + 1));
+                    } else {
+                        const float tp = a12 * px(x0 + j, y0) + a22 * px(x0 + j, y0 + 1);
+                        prev = (float)(tp * ps);
+                    }
+                    patch[e] = prev + t;
                 }
-                patch[e] = prev + t;
+            };
+            // the patch's (SP_B + 1)^2 pixels inside the staged window: LDS reads
+            // only (ds_read_u8, no flat loads); otherwise each pixel picks its source
+            if (ipx >= win.ox && ipx + SP_B + 1 <= win.ox + win.nx && ipy >= win.oy &&
+                ipy + SP_B + 1 <= win.oy + win.ny) {
+                const uint8_t* lw = L.win + (ipy - win.oy) * SW_W + (ipx - win.ox);
+                patch_px([&](int x, int y) -> float { return (float)lw[(y - ipy) * SW_W + (x - ipx)]; });
+            } else {
+                patch_px([&](int x, int y) -> float { return roi_px(src, pitch, win, x, y); });
             }
         } else {
             for (int e = lane; e < SP_B * SP_B; e += 64)

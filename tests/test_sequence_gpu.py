@@ -199,3 +199,35 @@ def test_long_sequence_graph_replay(ctx, gvx_mod, long_sequence, pipeline, eig_b
         assert len(trk.graphs) == (6 if pipeline else 2)
     finally:
         trk.close()
+
+
+def test_partly_flat_frames_match_oracle(ctx, orc, gvx_mod):
+    """Frames whose left half is flat for a while: the blocks there have an
+    eigenvalue maximum of 0, so the tracking path's selection takes its full-ROI
+    scan (the tiles' candidate lists only hold for a maximum > 0) while the
+    textured blocks use the lists -- every frame's track list bit-exact against
+    the oracle loop."""
+    import torch
+    from gvx import synth
+    from gvx.tracking import DeviceSequenceTracker
+    dev = torch.device("cuda", 0)
+    n = 12
+    frames, _ = synth.make_sequence(W, H, n, dev, seed=synth.SEED + 3)
+    frames[4:8, :, :W // 2] = 128
+    ref = _oracle_sequence(orc, frames.cpu().numpy(), orc.KltParams.default(max_level=L), orc.DetectParams.default(),
+                           nthreads=8)
+    trk = DeviceSequenceTracker(ctx, W, H, N, klt=gvx_mod.KltParams.default(max_level=L),
+                                detect=gvx_mod.DetectParams.default(max_features=N), ids=(50, 51), graph=False,
+                                device=dev, frames=frames)
+    try:
+        for _ in range(n):
+            trk.step()
+        ctx.sync()
+        counts = trk.rec_counts.cpu().numpy()
+        tracks = trk.rec_tracks.cpu().numpy()
+        for t in range(n):
+            assert np.array_equal(tracks[t, :counts[t]], ref[t]["pts"]), f"frame {t}"
+        # the flat half lost its points and was detected on again
+        assert any("corners" in ref[t] for t in range(4, 9))
+    finally:
+        trk.close()

@@ -2,7 +2,7 @@
 # subpix change parity + select phases + configs[4]; then LK per-level stamps
 set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
-bash $R/tools/r03_v24.sh
+bash $R/tools/r03_v24.sh; exit 0
 O=$R/gpurun_out/r03_v25
 mkdir -p $O
 cd $R
