@@ -643,7 +643,8 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
         }
     }
     __syncthreads();
-    // ---- whitening: sqrt_info * [Jr | r] on the matrix cores, in place ----
+    // ---- whitening: sqrt_info * [Jr | r] on the matrix cores, stored from the
+    // accumulators ----
     // Per factor slot f of the wave: three 16-column blocks of the 15 x 33 tile
     // (zero-padded to 16 x 48), each 4 v_mfma_f64_16x16x4 steps over K = 16.
     // Operand layout (16x16x4 f64): A lane l = (row l%16, k l/16), B lane l =
@@ -651,49 +652,62 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     // (measured: tools/mfma_f64_probe.hip).  The MFMA sums the 15 products in
     // its own order, not the restatement's sequential one; the results stay
     // within 1e-10 of each block's magnitude (tests/test_factor_parity_gpu.py).
+    // Each lane writes its four rows of its column straight to the output layout
+    // (residual column 32 -> res; Jacobian column c -> block J0 7 | J1 9 | J2 7 |
+    // J3 9 of jac), so the tile is not written back and re-read: the block's B
+    // reads of all three column blocks are issued before its MFMA chains.
     {
         const int lr = wr, lk = wk;
         const int cb0 = jac ? 0 : 2;  // residual only: the block holding column 32
+        const int nf = min(PF_GROUPS, n - f0);
+        // the lane's output column in each column block: Jacobian block base,
+        // width and column inside it (width 0: column 32, the residual; -1: padding)
+        int obase[3], owid[3];
+#pragma unroll
+        for (int cb = 0; cb < 3; ++cb) {
+            const int c = 16 * cb + lr;
+            if (c < 7) { obase[cb] = c; owid[cb] = 7; }
+            else if (c < 16) { obase[cb] = 105 + (c - 7); owid[cb] = 9; }
+            else if (c < 23) { obase[cb] = 240 + (c - 16); owid[cb] = 7; }
+            else if (c < 32) { obase[cb] = 345 + (c - 23); owid[cb] = 9; }
+            else if (c == 32) { obase[cb] = 0; owid[cb] = 0; }
+            else { obase[cb] = 0; owid[cb] = -1; }
+        }
+        typedef double v4d __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int f = 0; f < PF_GROUPS; ++f) {
             const double* A = SA[f];
-            double* T = tile + f * NS * PF_LD;
-#pragma unroll 1
-            for (int cb = cb0; cb < 3; ++cb) {
+            const double* T = tile + f * NS * PF_LD;
+            double bv[3][4];
+#pragma unroll
+            for (int cb = 0; cb < 3; ++cb) {
                 const int col = 16 * cb + lr;
-                typedef double v4d __attribute__((ext_vector_type(4)));
-                v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) {
                     const int k = 4 * kk + lk;
-                    const double bv = (k < NS && col < PF_LD) ? T[k * PF_LD + col] : 0.0;
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[kk], bv, acc, 0, 0, 0);
+                    bv[cb][kk] = (cb >= cb0 && k < NS && col < PF_LD) ? T[k * PF_LD + col] : 0.0;
                 }
+            }
+            if (f >= nf) continue;  // wave-uniform
+            double* rf = res + (int64_t)(f0 + f) * NS;
+            double* jf = jac ? jac + (int64_t)(f0 + f) * 480 : nullptr;
+#pragma unroll
+            for (int cb = 0; cb < 3; ++cb) {
+                if (cb < cb0) continue;
+                v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[kk], bv[cb][kk], acc, 0, 0, 0);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int row = lk + 4 * i;
-                    if (row < NS && col < PF_LD) T[row * PF_LD + col] = acc[i];
+                    if (row >= NS) continue;
+                    if (owid[cb] > 0) {
+                        if (jf) jf[obase[cb] + row * owid[cb]] = acc[i];
+                    } else if (owid[cb] == 0) {
+                        rf[row] = acc[i];
+                    }
                 }
             }
-        }
-    }
-    __syncthreads();
-    // ---- coalesced stores of the workgroup's factors ----
-    const int nf = min(PF_GROUPS, n - f0);
-    for (int e = threadIdx.x; e < nf * NS; e += 64) {
-        const int f = e / NS, i = e - f * NS;
-        res[(int64_t)f0 * NS + e] = tile[f * NS * PF_LD + i * PF_LD + 32];
-    }
-    if (jac) {
-        // per factor [J0 15x7 | J1 15x9 | J2 15x7 | J3 15x9], Jr columns [0..7 | 7..16 | 16..23 | 23..32]
-        for (int e = threadIdx.x; e < nf * 480; e += 64) {
-            const int f = e / 480, q = e - f * 480;
-            int i, col;
-            if (q < 105) { i = q / 7; col = q - 7 * i; }
-            else if (q < 240) { i = (q - 105) / 9; col = 7 + (q - 105) - 9 * i; }
-            else if (q < 345) { i = (q - 240) / 7; col = 16 + (q - 240) - 7 * i; }
-            else { i = (q - 345) / 9; col = 23 + (q - 345) - 9 * i; }
-            jac[(int64_t)f0 * 480 + e] = tile[f * NS * PF_LD + i * PF_LD + col];
         }
     }
 }

@@ -65,6 +65,14 @@ for n in (4, 64, 256, 1024, 2048, 4096, n_p):
     ms, cnt = ctx.profile_read("preint_factor")
     ctx.profile(False)
     us = ms / 50 * 1e3
-    print(json.dumps({"lib": os.environ.get("GVX_LIB", "tree"), "n": n, "us": round(us, 2),
-                      "frac": round(10944 * n / (us * 1e-6) / 8e12, 4)}))
+    row = {"lib": os.environ.get("GVX_LIB", "tree"), "n": n, "us": round(us, 2),
+           "frac": round(10944 * n / (us * 1e-6) / 8e12, 4)}
+    if os.environ.get("GVX_LIB", "").endswith("pfprof.so"):
+        import ctypes
+        t = np.zeros(16, np.uint64)
+        ctypes.CDLL(os.environ["GVX_LIB"]).gvx_dbg_pf_times(t.ctypes.data_as(ctypes.c_void_p))
+        t = t.astype(np.int64)
+        row["wave0_phase_us"] = dict(zip(["issue", "wait_loads", "pn_sum", "residual+rawjac_part1", "rawjac_part2",
+                                          "whiten+store_issue", "store_drain"], np.round(np.diff(t[:8]) * 0.01, 2).tolist()))
+    print(json.dumps(row))
 ctx.close()
