@@ -75,4 +75,29 @@ for n in (4, 64, 256, 1024, 2048, 4096, n_p):
         row["wave0_phase_us"] = dict(zip(["issue", "wait_loads", "pn_sum", "residual+rawjac_part1", "rawjac_part2",
                                           "whiten+store_issue", "store_drain"], np.round(np.diff(t[:8]) * 0.01, 2).tolist()))
     print(json.dumps(row))
+# the bench's order: the 1,049,400-factor reprojection launch before each
+# preintegration-factor launch (its 550 MB evicts the factor records from the
+# L2 / MALL), timed on the same HIP events as the bench line
+n_rp = len(prob["consts"])
+n_r = n_rp * reps
+d_consts = dev_t(np.tile(prob["consts"], reps).view(np.uint8))
+d_offs = dev_t(np.tile(prob["offs"], (reps, 1)))
+d_res = torch.empty((n_r, 2), dtype=torch.float64, device=dev)
+d_jac = torch.empty((n_r, 46), dtype=torch.float64, device=dev)
+f = lambda: ctx.factor_batch_eval_dev(n_r, d_consts.data_ptr(), d_offs.data_ptr(), d_res.data_ptr(), d_jac.data_ptr(),
+                                      n_p, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(), d_poffs.data_ptr(),
+                                      d_pres.data_ptr(), d_pjac.data_ptr(), d_params.data_ptr())
+for _ in range(10):
+    f()
+ctx.sync()
+ctx.profile_reset()
+ctx.profile(True)
+for _ in range(50):
+    f()
+ctx.sync()
+us = ctx.profile_read("preint_factor")[0] / 50 * 1e3
+rus = ctx.profile_read("reproj")[0] / 50 * 1e3
+ctx.profile(False)
+print(json.dumps({"lib": os.environ.get("GVX_LIB", "tree"), "n": n_p, "after_reproj": True, "us": round(us, 2),
+                  "frac": round(10944 * n_p / (us * 1e-6) / 8e12, 4), "reproj_us": round(rus, 2)}))
 ctx.close()
