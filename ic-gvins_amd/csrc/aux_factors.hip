@@ -122,10 +122,10 @@ __global__ void __launch_bounds__(64) small_kernel(int n, const double* __restri
     }
     __syncthreads();
     double* ro = residuals + (int64_t)i0 * R;
-    for (int k = lane; k < cnt * R; k += 64) ro[k] = sres[k];
+    for (int k = lane; k < cnt * R; k += 64) __builtin_nontemporal_store(sres[k], ro + k);
     if (jacobians) {
         double* jo = jacobians + (int64_t)i0 * R * P;
-        for (int k = lane; k < cnt * R * P; k += 64) jo[k] = sjac[k];
+        for (int k = lane; k < cnt * R * P; k += 64) __builtin_nontemporal_store(sjac[k], jo + k);
     }
 }
 

@@ -171,12 +171,12 @@ __global__ void __launch_bounds__(RP_THREADS) reproj_kernel(int n, const gvx_rep
     const int cnt = min(RP_THREADS, n - base);
     for (int k = t; k < cnt * 2; k += RP_THREADS) {
         const int f = k >> 1, q = k & 1;
-        res[(int64_t)base * 2 + k] = stage[f * (RP_OUT + 1) + q];
+        __builtin_nontemporal_store(stage[f * (RP_OUT + 1) + q], res + (int64_t)base * 2 + k);
     }
     if (jac)
         for (int k = t; k < cnt * 46; k += RP_THREADS) {
             const int f = k / 46, q = k - f * 46;
-            jac[(int64_t)base * 46 + k] = stage[f * (RP_OUT + 1) + 2 + q];
+            __builtin_nontemporal_store(stage[f * (RP_OUT + 1) + 2 + q], jac + (int64_t)base * 46 + k);
         }
 }
 
@@ -702,9 +702,9 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
                     const int row = lk + 4 * i;
                     if (row >= NS) continue;
                     if (owid[cb] > 0) {
-                        if (jf) jf[obase[cb] + row * owid[cb]] = acc[i];
+                        if (jf) __builtin_nontemporal_store(acc[i], jf + obase[cb] + row * owid[cb]);
                     } else if (owid[cb] == 0) {
-                        rf[row] = acc[i];
+                        __builtin_nontemporal_store(acc[i], rf + row);
                     }
                 }
             }
