@@ -106,6 +106,12 @@ void prof_end(gvx_ctx* c, const char* fam, hipEvent_t a) {
     if (!c->prof) return;
     hipEvent_t b = get_event(c);
     hipEventRecord(b, c->stream);
+    prof_push(c, fam, a, b);
+}
+
+hipEvent_t prof_event(gvx_ctx* c) { return get_event(c); }
+
+void prof_push(gvx_ctx* c, const char* fam, hipEvent_t a, hipEvent_t b) {
     c->pending.push_back({fam, a, b});
     if (c->pending.size() > 4096) prof_drain(c);
 }

@@ -26,10 +26,7 @@ gvx_status gvx_small_factor_eval_dev(gvx_ctx* c, int32_t kind, int32_t n, const 
     if ((NC && !d_consts) || !d_params || !d_offs || !d_residuals)
         return set_err(c, GVX_ERR_INVALID, "null device pointer");
     hipSetDevice(c->device);
-    hipEvent_t ev{};
-    prof_begin(c, "aux_factor", &ev);
-    hipError_t e = launch_small_factor(c, kind, n, d_consts, d_params, d_offs, d_residuals, d_jacobians);
-    prof_end(c, "aux_factor", ev);
+    hipError_t e = launch_small_factor(c, kind, n, d_consts, d_params, d_offs, d_residuals, d_jacobians);  // timed
     return hip_err(c, e, "small factor kernel");
 }
 

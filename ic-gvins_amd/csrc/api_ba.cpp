@@ -164,10 +164,7 @@ gvx_status gvx_reproj_eval_dev(gvx_ctx* c, int32_t n, const gvx_reproj_const* d_
     if (n == 0) return GVX_OK;
     if (!d_c || !d_params || !d_offs || !d_res) return set_err(c, GVX_ERR_INVALID, "null device pointer");
     hipSetDevice(c->device);
-    hipEvent_t ev{};
-    prof_begin(c, "reproj", &ev);
-    hipError_t e = launch_reproj(c, n, d_c, d_params, d_offs, d_res, d_jac);
-    prof_end(c, "reproj", ev);
+    hipError_t e = launch_reproj(c, n, d_c, d_params, d_offs, d_res, d_jac);  // timed as "reproj"
     return hip_err(c, e, "reproj kernel");
 }
 
@@ -223,18 +220,13 @@ gvx_status gvx_factor_batch_eval_dev(gvx_ctx* c, int32_t n_reproj, const gvx_rep
     // one after the other on the context stream: the preintegration launch on a
     // second stream beside the reprojection one measured slower (both kernels
     // stretch: 0.162 -> 0.168 ms per configs[3] batch, r02 v17)
-    hipEvent_t ev{};
     hipError_t e = hipSuccess;
     if (n_reproj > 0) {
-        prof_begin(c, "reproj", &ev);
         e = launch_reproj(c, n_reproj, d_rc, d_params, d_roffs, d_rres, d_rjac);
-        prof_end(c, "reproj", ev);
         if (e != hipSuccess) return hip_err(c, e, "reproj kernel");
     }
     if (n_preint > 0) {
-        prof_begin(c, "preint_factor", &ev);
         e = launch_preint_factor(c, n_preint, d_pre, d_pn, d_pn_off, d_params, d_poffs, d_pres, d_pjac);
-        prof_end(c, "preint_factor", ev);
     }
     return hip_err(c, e, "preint factor kernel");
 }
@@ -247,10 +239,7 @@ gvx_status gvx_preint_factor_eval_dev(gvx_ctx* c, int32_t n, const gvx_preint_re
     if (n == 0) return GVX_OK;
     if (!d_pre || !d_params || !d_offs || !d_res) return set_err(c, GVX_ERR_INVALID, "null device pointer");
     hipSetDevice(c->device);
-    hipEvent_t ev{};
-    prof_begin(c, "preint_factor", &ev);
-    hipError_t e = launch_preint_factor(c, n, d_pre, d_pn, d_pn_off, d_params, d_offs, d_res, d_jac);
-    prof_end(c, "preint_factor", ev);
+    hipError_t e = launch_preint_factor(c, n, d_pre, d_pn, d_pn_off, d_params, d_offs, d_res, d_jac);  // timed
     return hip_err(c, e, "preint factor kernel");
 }
 

@@ -191,23 +191,18 @@ hipError_t launch_small_factor(gvx_ctx* c, int kind, int n, const double* consts
     const dim3 grid((n + 63) / 64), block(64);
     switch (kind) {
         case GVX_FACTOR_GNSS:
-            hipLaunchKernelGGL(small_kernel<GVX_FACTOR_GNSS>, grid, block, 0, c->stream, n, consts, params, offs,
-                               residuals, jacobians);
-            break;
+            return launch_timed(c, "aux_factor", small_kernel<GVX_FACTOR_GNSS>, grid, block, 0, n, consts, params, offs,
+                                residuals, jacobians);
         case GVX_FACTOR_IMU_ERROR:
-            hipLaunchKernelGGL(small_kernel<GVX_FACTOR_IMU_ERROR>, grid, block, 0, c->stream, n, consts, params,
-                               offs, residuals, jacobians);
-            break;
+            return launch_timed(c, "aux_factor", small_kernel<GVX_FACTOR_IMU_ERROR>, grid, block, 0, n, consts, params, offs,
+                                residuals, jacobians);
         case GVX_FACTOR_POSE_PRIOR:
-            hipLaunchKernelGGL(small_kernel<GVX_FACTOR_POSE_PRIOR>, grid, block, 0, c->stream, n, consts, params,
-                               offs, residuals, jacobians);
-            break;
+            return launch_timed(c, "aux_factor", small_kernel<GVX_FACTOR_POSE_PRIOR>, grid, block, 0, n, consts, params, offs,
+                                residuals, jacobians);
         default:
-            hipLaunchKernelGGL(small_kernel<GVX_FACTOR_MIX_PRIOR>, grid, block, 0, c->stream, n, consts, params,
-                               offs, residuals, jacobians);
-            break;
+            return launch_timed(c, "aux_factor", small_kernel<GVX_FACTOR_MIX_PRIOR>, grid, block, 0, n, consts, params, offs,
+                                residuals, jacobians);
     }
-    return hipGetLastError();
 }
 
 hipError_t launch_marg_factor(gvx_ctx* c, int r, int nb, const int32_t* blk, const double* x0, const double* x,

@@ -717,18 +717,16 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
 hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
                          const int32_t* offs, double* res, double* jac) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(reproj_kernel, dim3((n + RP_THREADS - 1) / RP_THREADS), dim3(RP_THREADS), 0,
-                       c->stream, n, cs, params, offs, res, jac);
-    return hipGetLastError();
+    return launch_timed(c, "reproj", reproj_kernel, dim3((n + RP_THREADS - 1) / RP_THREADS), dim3(RP_THREADS), 0, n,
+                        cs, params, offs, res, jac);
 }
 
 hipError_t launch_preint_factor(gvx_ctx* c, int n, const gvx_preint_result* pre, const double* pn,
                                 const int32_t* pn_off, const double* params, const int32_t* offs,
                                 double* res, double* jac) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(preint_factor_kernel, dim3((n + PF_GROUPS - 1) / PF_GROUPS), dim3(64), 0, c->stream, n, pre,
-                       pn, pn_off, params, offs, res, jac);
-    return hipGetLastError();
+    return launch_timed(c, "preint_factor", preint_factor_kernel, dim3((n + PF_GROUPS - 1) / PF_GROUPS), dim3(64), 0,
+                        n, pre, pn, pn_off, params, offs, res, jac);
 }
 
 hipError_t launch_sqrt_info(gvx_ctx* c, int n, gvx_preint_result* pre) {
