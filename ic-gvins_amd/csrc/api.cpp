@@ -310,10 +310,7 @@ gvx_status gvx_frame_put(gvx_ctx* c, uint64_t id, const uint8_t* gray, int32_t w
     for (int y = 0; y < h; ++y) std::memcpy(hst + (size_t)y * w, gray + (size_t)y * stride, w);
     hipError_t e = hipMemcpyAsync(dsrc, hst, nb, hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "hipMemcpyAsync(frame)");
-    hipEvent_t ev{};
-    prof_begin(c, "pyramid", &ev);
     e = launch_build_pyramids(c, dsrc, (int64_t)nb, w, 1, lay, f.pyr, true);
-    prof_end(c, "pyramid", ev);
     if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
     return hip_err(c, hipStreamSynchronize(c->stream), "frame_put sync");
 }
@@ -326,11 +323,8 @@ gvx_status gvx_frame_put_dev(gvx_ctx* c, uint64_t id, const uint8_t* d_gray, int
     if (s) return s;
     Frame& f = *fp;
     const PyrLayout& lay = f.lay;
-    hipEvent_t ev{};
-    prof_begin(c, "pyramid", &ev);
     // the padded level-0 copy reads the caller's device image in place (any stride)
     hipError_t e = launch_build_pyramids(c, d_gray, (int64_t)h * stride, stride, 1, lay, f.pyr, true);
-    prof_end(c, "pyramid", ev);
     return hip_err(c, e, "pyramid kernels");
 }
 
@@ -403,10 +397,7 @@ gvx_status gvx_build_pyramids_dev(gvx_ctx* c, int32_t n_img, int32_t w, int32_t 
     if (!d_imgs || !d_out) return set_err(c, GVX_ERR_INVALID, "bad pyramid batch pointers");
     hipSetDevice(c->device);
     const PyrLayout lay = make_layout(w, h, max_level, WIN);
-    hipEvent_t ev{};
-    prof_begin(c, "pyramid", &ev);
     hipError_t e = launch_build_pyramids(c, d_imgs, img_stride, stride, n_img, lay, d_out, false);
-    prof_end(c, "pyramid", ev);
     return hip_err(c, e, "pyramid kernels");
 }
 
@@ -466,17 +457,12 @@ static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, con
     a.border = border;
     a.cam_w = cam_w;
     a.cam_h = cam_h;
-    hipEvent_t ev{};
-    prof_begin(c, "klt", &ev);
     const Level0 l0{fp.pyr + lay.off[0], fn.pyr + lay.off[0], 0, 0, PAD * lay.pitch[0] + PAD, lay.pitch[0], 0};
     e = launch_klt(c, a, lay, fp.pyr, fn.pyr, 0, 0, l0, d_prev, d_next, mode ? d_back : nullptr, d_flags,
                    d_err);
-    prof_end(c, "klt", ev);
     if (e != hipSuccess) return hip_err(c, e, "klt kernel");
     if (mode == 1) {
-        prof_begin(c, "compact", &ev);
         e = launch_compact(c, 1, n, d_flags, d_kept, d_nkept);
-        prof_end(c, "compact", ev);
         if (e != hipSuccess) return hip_err(c, e, "compact kernel");
     }
     // one D2H of next | back | err | kept | n_kept | flags
@@ -556,13 +542,10 @@ gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int
     if (!pyr) return set_err(c, GVX_ERR_OOM, "batch pyramids (%lld bytes)", (long long)lay.bytes * 2 * n_pairs);
     uint8_t* pyr_prev = pyr;
     uint8_t* pyr_next = pyr + (size_t)lay.bytes * n_pairs;
-    hipEvent_t ev{};
-    prof_begin(c, "pyramid", &ev);
     // level 0 stays in the caller's images; levels >= 1 go to the pyramid slots
     // one launch for both frames of every pair (pyr_next follows pyr_prev)
     hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, 2 * n_pairs, lay, pyr_prev, false, d_next,
                                          n_pairs);
-    prof_end(c, "pyramid", ev);
     if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
     if (n_pts == 0) {
         e = hipMemsetAsync(d_n_kept, 0, sizeof(int32_t) * n_pairs, c->stream);
@@ -579,15 +562,11 @@ gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int
     // without OPTFLOW_USE_INITIAL_FLOW the kernel starts from prevPts and never
     // reads the initial flow
     a.init_xy = d_init_xy;
-    prof_begin(c, "klt", &ev);
     const Level0 l0{d_prev, d_next, (int64_t)w * h, (int64_t)w * h, 0, w, 1};
     e = launch_klt(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, l0, d_prev_xy, d_next_xy, d_back_xy,
                    d_flags, nullptr);
-    prof_end(c, "klt", ev);
     if (e != hipSuccess) return hip_err(c, e, "klt kernel");
-    prof_begin(c, "compact", &ev);
     e = launch_compact(c, n_pairs, n_pts, d_flags, d_kept_idx, d_n_kept);
-    prof_end(c, "compact", ev);
     return hip_err(c, e, "compact kernel");
 }
 

@@ -111,10 +111,7 @@ static gvx_status preprocess_into_slot(gvx_ctx* c, uint64_t id, const uint8_t* d
     s = clahe_enqueue(c, 1, w, h, d_gray, img_stride, stride, slot0, lay.bytes, lay.pitch[0], cp, d_hist_mean,
                       src_index, n_src, 1);
     if (s) return s;
-    hipEvent_t ev{};
-    prof_begin(c, "pyramid", &ev);
     hipError_t e = launch_build_pyramids(c, slot0, lay.bytes, lay.pitch[0], 1, lay, f->pyr, false, nullptr, 0, true);
-    prof_end(c, "pyramid", ev);
     return hip_err(c, e, "pyramid kernels");
 }
 static bool ring_in_apply(int w, int h) { return w >= 2 * PAD + 2 && h >= 2 * PAD + 2; }

@@ -240,10 +240,8 @@ static gvx_status track_frame(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, in
         a.cam_w = cam_w;
         a.cam_h = cam_h;
         const Level0 l0{fp->pyr + lay.off[0], fn.pyr + lay.off[0], 0, 0, PAD * lay.pitch[0] + PAD, lay.pitch[0], 0};
-        prof_begin(c, "klt", &ev);
         // d_init is the initial flow in and the tracked positions out
         e = launch_klt(c, a, lay, fp->pyr, fn.pyr, 0, 0, l0, d_pts, d_init, nullptr, flags, nullptr);
-        prof_end(c, "klt", ev);
         if (e != hipSuccess) return hip_err(c, e, "klt kernel");
     }
     if (fused) {

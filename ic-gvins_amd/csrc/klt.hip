@@ -946,8 +946,8 @@ static void launch_klt_ppw(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, c
                            float* err) {
     const int n_waves = a.n_pairs * ((a.n_pts + PPW - 1) / PPW);
     dim3 grid((unsigned)(N_XCD * xcd_per((n_waves + KLT_WPB - 1) / KLT_WPB)));
-    hipLaunchKernelGGL((klt_kernel<PPW, ACC>), grid, dim3(64 * KLT_WPB), 0, c->stream, a, lay, pyr_prev, pyr_next,
-                       prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
+    launch_timed(c, "klt", klt_kernel<PPW, ACC>, grid, dim3(64 * KLT_WPB), 0, a, lay, pyr_prev, pyr_next,
+                 prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
 }
 
 template <int ACC>
@@ -992,8 +992,7 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
 hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
                           int32_t* n_kept) {
     if (n_pairs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(compact_kernel, dim3(n_pairs), dim3(256), 0, c->stream, n_pts, flags, kept_idx, n_kept);
-    return hipGetLastError();
+    return launch_timed(c, "compact", compact_kernel, dim3(n_pairs), dim3(256), 0, n_pts, flags, kept_idx, n_kept);
 }
 
 }  // namespace gvx

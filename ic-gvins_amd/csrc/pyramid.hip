@@ -598,9 +598,8 @@ hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrL
     // must not run without it (a scratch buffer cannot grow inside a capture)
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
     if (!trash) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, c->stream, src, dst, lay.bytes,
-                       D, n_strips, n_bands, n_units, band, trash);
-    return hipSuccess;
+    return launch_timed(c, "pyramid", stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, src, dst,
+                        lay.bytes, D, n_strips, n_bands, n_units, band, trash);
 }
 
 
@@ -683,7 +682,7 @@ void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, u
     }
     if (R.n == 0) return;
     dim3 grid((most + 255) / 256, n_img, R.n);
-    hipLaunchKernelGGL(ring_kernel, grid, dim3(256), 0, c->stream, dst, lay.bytes, R);
+    launch_timed(c, "pyramid", ring_kernel, grid, dim3(256), 0, dst, lay.bytes, R);
 }
 
 }  // namespace
@@ -744,8 +743,8 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
         const int items = groups * (lay.h[0] + 2 * PAD);
         dim3 grid((items + 255) / 256, n_img);
-        hipLaunchKernelGGL(level0_kernel, grid, dim3(256), 0, c->stream, src, img_stride, stride, lay.w[0],
-                           lay.h[0], lay.pitch[0], lay.bytes, dst);
+        launch_timed(c, "pyramid", level0_kernel, grid, dim3(256), 0, src, img_stride, stride, lay.w[0], lay.h[0],
+                     lay.pitch[0], lay.bytes, dst);
         s0 = slot0;
         s0_img = lay.bytes;
         s0_pitch = lay.pitch[0];
