@@ -40,6 +40,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 def rank_setup(args):
     """One process per GPU: (dist | None, device, world, rank, local).
 
+    A process group is opened at world > 1, and at world 1 with --dist (under
+    torch.distributed.run), so the RCCL code path -- device-tensor all_gather,
+    gather and all_reduce -- runs on a one-GPU box (tests/test_bench_rccl_gpu.py).
+
     nccl (RCCL over xGMI, the default) needs one GPU per rank.  gloo is the
     rehearsal backend: ranks may share a GPU (local rank mod the device count),
     so the real per-rank path (context, kernels, collectives, max over ranks)
@@ -57,7 +61,7 @@ def rank_setup(args):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -194,6 +198,34 @@ def host_threads():
 ACCUM_MODES = {"exact": 0, "f32_scalar": 1, "f32_simd4": 2}  # include/gvx.h GVX_LK_ACCUM_*
 
 
+class KltWorkload:
+    """The timed KLT step's inputs and launch, shared with the parity test of
+    this exact launch (tests/test_bench_batch_gpu.py): `n_pairs` synthetic pairs
+    (`distinct` of them rendered, then tiled; seed synth.SEED + 100000 * rank)
+    resident in HBM, and one gvx_klt_fb_batch_init_dev over them -- the pyramid
+    pass, forward LK from the predictions in their own buffer, backward LK, FB
+    and compaction (tracking.cc:385-408)."""
+
+    def __init__(self, n_pairs, w, h, n, dev, rank=0, distinct=16):
+        import torch
+        from gvx import synth
+        self.n_pairs, self.w, self.h, self.n = n_pairs, w, h, n
+        self.host = synth.make_batch(n_pairs, w, h, n, seed=synth.SEED + 100000 * rank, distinct=distinct)
+        self.I, self.J, self.P, self.Q = (torch.from_numpy(a).to(dev) for a in self.host)
+        self.N = torch.empty_like(self.Q)  # tracked points (next)
+        self.B = torch.empty_like(self.Q)  # backward points
+        self.F = torch.empty((n_pairs, n), dtype=torch.uint8, device=dev)
+        self.K = torch.empty((n_pairs, n), dtype=torch.int32, device=dev)
+        self.NK = torch.empty((n_pairs,), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+
+    def step(self, ctx, params):
+        # initial flow (the predictions) read from Q, tracked points out to N
+        ctx.klt_fb_batch_init_dev(self.n_pairs, self.w, self.h, self.I.data_ptr(), self.J.data_ptr(), self.n,
+                                  self.P.data_ptr(), self.Q.data_ptr(), self.N.data_ptr(), self.B.data_ptr(),
+                                  self.F.data_ptr(), self.K.data_ptr(), self.NK.data_ptr(), params=params)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +262,9 @@ def main():
     ap.add_argument("--eig-branch", action="store_true",
                     help="configs[4] pipelined: the detection's eigenvalue map on the preprocessing branch")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl, mock: gloo)")
+    ap.add_argument("--dist", action="store_true",
+                    help="open the process group even at world size 1 (run under torch.distributed.run): the "
+                         "collectives of --gather / configs[4] / max-over-ranks then go through RCCL")
     ap.add_argument("--accum", default="exact", choices=tuple(ACCUM_MODES),
                     help="LK window-sum order (gvx_klt_params.accum): exact integer sums (default), or "
                          "OpenCV 4.x's fp32 scalar-loop / CV_SIMD128 orders")
@@ -256,34 +291,21 @@ def main():
     dist, dev, world, rank, local = rank_setup(args)
 
     W, H, N, L, Pn = args.width, args.height, args.features, args.levels, args.pairs
-    from gvx import synth
-    I, J, P, Q = synth.make_batch(Pn, W, H, N, seed=synth.SEED + 100000 * rank, distinct=args.distinct)
-    dI = torch.from_numpy(I).to(dev)
-    dJ = torch.from_numpy(J).to(dev)
-    dP = torch.from_numpy(P).to(dev)
-    dQ = torch.from_numpy(Q).to(dev)
-    dN = torch.empty_like(dQ)
-    dB = torch.empty_like(dQ)
-    dF = torch.empty((Pn, N), dtype=torch.uint8, device=dev)
-    dK = torch.empty((Pn, N), dtype=torch.int32, device=dev)
-    dNK = torch.empty((Pn,), dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
+    wl = KltWorkload(Pn, W, H, N, dev, rank=rank, distinct=args.distinct)
+    I, J, P, Q = wl.host
+    dI, dJ, dP, dQ, dNK = wl.I, wl.J, wl.P, wl.Q, wl.NK
 
     ctx = gvx.Context(local)
-    stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
     params = gvx.KltParams.default(max_level=L, accum=ACCUM_MODES[args.accum])
 
     def step(p=params):
-        # initial flow (the predictions) read from dQ, tracked points out to dN
-        ctx.klt_fb_batch_init_dev(Pn, W, H, dI.data_ptr(), dJ.data_ptr(), N, dP.data_ptr(), dQ.data_ptr(),
-                                  dN.data_ptr(), dB.data_ptr(), dF.data_ptr(), dK.data_ptr(), dNK.data_ptr(),
-                                  params=p)
+        wl.step(ctx, p)
 
     cdev = coll_device(dist, dev)
-    gathered = [torch.empty(dNK.shape, dtype=dNK.dtype, device=cdev) for _ in range(world)] if world > 1 else None
+    gathered = [torch.empty(dNK.shape, dtype=dNK.dtype, device=cdev) for _ in range(world)] if dist else None
 
     def collect():
-        if world > 1 and args.gather:
+        if dist and args.gather:
             ctx.sync()
             dist.all_gather(gathered, dNK.to(cdev))  # offline batch replay: results to every rank
 
@@ -326,9 +348,14 @@ def main():
         pcie = {"pairs_per_s": round(Pn * hs / (time.perf_counter() - t1), 1), "steps": hs,
                 "what": "gvx_klt_fb_batch on host buffers (2 x %.0f MB image upload + points per step)"
                         % (I.nbytes / 1e6)}
-    if world > 1 and not args.gather:
-        collect_once = [torch.empty(dNK.shape, dtype=dNK.dtype, device=cdev) for _ in range(world)]
-        dist.all_gather(collect_once, dNK.to(cdev))  # results check, outside the timed region
+    gather_ok = None
+    if dist:
+        if not args.gather:
+            gathered = [torch.empty(dNK.shape, dtype=dNK.dtype, device=cdev) for _ in range(world)]
+            dist.all_gather(gathered, dNK.to(cdev))  # results exchange, outside the timed region
+        # the exchange delivered this rank's own results, and every rank's are sane
+        gather_ok = bool(torch.equal(gathered[rank].cpu(), dNK.cpu())
+                         and all(int(g.min()) > 0 for g in gathered))
 
     # the metric's second half (BASELINE.json: factor-Jacobian eval/s), timed in
     # the same run: configs[3]'s factor batch (its own line under "factors")
@@ -396,6 +423,8 @@ def main():
             "single_pair": single,
             "host_buffers": pcie,
             "factors": factors,
+            "dist_backend": dist.get_backend() if dist else None,
+            "gather_check": gather_ok,
         }
         print(json.dumps(line))
     if dist:
@@ -693,6 +722,7 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
                              "factor_set_prepare_ms": round(el_p / k_w * 1e3, 4)},
             "window_factors": wf,
             "cpu_baseline": None,
+            "dist_backend": dist.get_backend() if dist else None,
         }
         if world == 1 and not args.no_cpu:
             ref = cpu_factor_baseline(prob, segs, states, iewn, params, poffs, threads=4)
@@ -898,18 +928,42 @@ def gather_tracks(tracks, counts, dist, dev):
     """configs[4]'s exchange: every rank's per-frame tracks ([F, N, 2] f32 and
     [F] counts) to rank 0 in one collective (RCCL gather over xGMI on the GPU
     box, gloo in the CPU test).  Returns the list of (tracks, counts) per rank
-    on rank 0, None elsewhere."""
+    on rank 0 (tensors where the collective left them: the caller copies them
+    to the host after its timed region), None elsewhere."""
     import torch
-    packed = torch.cat([tracks.reshape(-1).to(torch.float32), counts.to(torch.float32)]).to(dev)
     if not dist:
         return [(tracks, counts)]
+    packed = torch.cat([tracks.reshape(-1).to(torch.float32), counts.to(torch.float32)]).to(dev)
     world, rank = dist.get_world_size(), dist.get_rank()
     bufs = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
     dist.gather(packed, bufs, dst=0)
     if rank != 0:
         return None
     n = tracks.numel()
-    return [(b[:n].reshape(tracks.shape).cpu(), b[n:].to(torch.int32).cpu()) for b in bufs]
+    return [(b[:n].reshape(tracks.shape), b[n:].to(torch.int32)) for b in bufs]
+
+
+def records_digest(tracks, counts):
+    """Order-sensitive digest of one rank's per-frame records (tracks [F, N, 2]
+    f32 -- only the first counts[f] rows of frame f are defined -- and counts
+    [F]): two float64 sums, exact for these magnitudes, weighted by position."""
+    F, N = tracks.shape[:2]
+    valid = np.arange(N)[None, :] < counts[:, None]
+    t = np.where(valid[..., None], tracks.astype(np.float64), 0.0)
+    wts = 1.0 + (np.arange(F * N * 2, dtype=np.float64) % 7919).reshape(F, N, 2)
+    return (float((t * wts).sum()), int(counts.astype(np.int64) @ (1 + np.arange(F, dtype=np.int64))))
+
+
+def all_digests(tracks, counts, dist, cdev):
+    """records_digest of every rank, all-gathered (one small collective)."""
+    import torch
+    d = records_digest(tracks, counts)
+    if not dist:
+        return [d]
+    mine = torch.tensor([d[0], float(d[1])], dtype=torch.float64, device=cdev)
+    out = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, mine)
+    return [(float(o[0]), int(o[1])) for o in (x.cpu() for x in out)]
 
 
 def sequence_main(args):
@@ -961,8 +1015,15 @@ def sequence_main(args):
             tracks[t, :pts.shape[0]] = pts
             counts[t] = pts.shape[0]
 
+    # K-frame batches are enqueued whole at their first frame: round the warm-up
+    # up to a batch boundary, so the timed frames are exactly the batches enqueued
+    # inside the timed region
+    K = tracker.batch if device_loop else 1
+    warm = -(-args.warmup // K) * K
+    if warm >= F:
+        sys.exit(f"bench.py: --warmup {args.warmup} rounds to {warm} >= {F} frames (batch {K})")
     t = 0
-    for _ in range(args.warmup):
+    for _ in range(warm):
         frame(t)
         t += 1
     ctx.sync()
@@ -980,22 +1041,31 @@ def sequence_main(args):
         t += 1
         timed += 1
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed frames
-    if device_loop:
-        ctx.sync()
-        tracks[:] = tracker.rec_tracks.cpu().numpy()
-        counts[:] = tracker.rec_counts.cpu().numpy()
     ctx.sync()
-    gathered = gather_tracks(torch.from_numpy(tracks), torch.from_numpy(counts), dist, coll_device(dist, dev))
+    if device_loop:
+        # the records stay in HBM: RCCL gathers them device to device
+        d_tracks, d_counts = tracker.rec_tracks, tracker.rec_counts
+    else:
+        d_tracks, d_counts = torch.from_numpy(tracks), torch.from_numpy(counts)
+    gathered = gather_tracks(d_tracks, d_counts, dist, coll_device(dist, dev))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if device_loop:
+        tracks[:] = tracker.rec_tracks.cpu().numpy()  # for the line's statistics, after the timed region
+        counts[:] = tracker.rec_counts.cpu().numpy()
+    # every rank's digest of its own records (outside the timed region): rank 0
+    # checks each gathered record set against its owner's digest
+    digests = all_digests(tracks, counts, dist, coll_device(dist, dev))
+    if gathered:
+        gathered = [(t.cpu(), c.cpu()) for t, c in gathered]
+    if device_loop:
         # device time per kernel family of the same per-frame work, eager with event
         # brackets (outside the timed region: a captured graph cannot hold them)
         prof = DeviceSequenceTracker(ctx, W, H, N, klt=kp, detect=dp, graph=False, device=dev, frames=frames,
                                      ids=(2, 3))
-        for _ in range(min(F, args.warmup + 2)):
+        for _ in range(min(F, warm + 2)):
             prof.step()
         ctx.sync()
         ctx.profile_reset()
@@ -1030,7 +1100,7 @@ def sequence_main(args):
         tr = counts[F - timed:]
         print(json.dumps({
             "metric": f"KLT sequence frames/sec @{W}x{H},{N} feat (configs[4])", "value": round(value, 2),
-            "unit": "frames/s", "n_gpus": world, "steps": timed, "warmup": args.warmup,
+            "unit": "frames/s", "n_gpus": world, "steps": timed, "warmup": warm,
             "ms_per_step": round(elapsed / timed * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8/i32 windows, f32 solve",
             "data": "synthetic sequences (moving camera over a band-limited texture, seed 20261015 + 7919*rank)",
@@ -1059,7 +1129,10 @@ def sequence_main(args):
             "gathered_ranks": len(gathered) if gathered else 0,
             "gather_check": bool(gathered and np.array_equal(gathered[0][0].numpy(), tracks)
                                  and np.array_equal(gathered[0][1].numpy(), counts)
-                                 and all(int(c[F - timed:].min()) > 0 for _, c in gathered)),
+                                 and all(int(c[F - timed:].min()) > 0 for _, c in gathered)
+                                 and all(records_digest(t.numpy(), c.numpy()) == d
+                                         for (t, c), d in zip(gathered, digests))),
+            "dist_backend": dist.get_backend() if dist else None,
         }))
     if dist:
         dist.destroy_process_group()

@@ -146,6 +146,7 @@ const char* gvx_status_string(gvx_status s) {
         case GVX_ERR_OOM: return "out of memory";
         case GVX_ERR_NOT_FOUND: return "not found";
         case GVX_ERR_UNSUPPORTED: return "unsupported";
+        case GVX_ERR_NUMERIC: return "not positive definite";
         default: return "unknown";
     }
 }

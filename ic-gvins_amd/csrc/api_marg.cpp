@@ -470,6 +470,9 @@ gvx_status gvx_schur_solve(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const
     std::memcpy(delta, h_delta, sizeof(double) * (size_t)L);
     if (S) std::memcpy(S, h_S, sizeof(double) * (size_t)r * r);
     if (info) std::memcpy(info, h_info, sizeof(int32_t) * 2);
+    if (h_info[0] || h_info[1])
+        return set_err(c, GVX_ERR_NUMERIC, "schur solve: %s not positive definite (delta is NaN)",
+                       h_info[0] ? "Hee + D" : "the reduced system S");
     return GVX_OK;
 }
 

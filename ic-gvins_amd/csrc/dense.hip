@@ -319,6 +319,20 @@ __global__ void __launch_bounds__(256) gemv_kernel(int L, int m, const double* _
     t[a] = b0[a] - ((acc[0] + acc[1]) + (acc[2] + acc[3]));
 }
 
+// The LM step's failure epilogue: a non-positive pivot in Hee + D (chol[0]) or
+// in S (chol[1]) leaves delta undefined -- the S stage is skipped after a failed
+// Hee, and the stages after a failed factorisation read factors that were never
+// written.  Every delta entry becomes NaN and chol[1] also records a failed
+// Hee + D (S was never formed).  All threads read both flags before thread 0
+// may set chol[1]; the answer is the same either way.
+__global__ void __launch_bounds__(256) lm_fail_kernel(int L, int* __restrict__ chol, double* __restrict__ delta) {
+    const int f0 = chol[0], f1 = chol[1];
+    if (!(f0 | f1)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < L) delta[i] = __builtin_nan("");
+    if (i == 0 && f0 && !f1) chol[1] = 1;
+}
+
 }  // namespace
 
 hipError_t launch_potrf(gvx_ctx* c, int n, const double* A, int lda, double shift, double* L, int* fail,
@@ -377,6 +391,8 @@ hipError_t launch_lm_step(gvx_ctx* c, const MargLaunch& p, const double* D, doub
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_trsv(c, m, p.Lm, 1, tmp, m, tmp + m, 1, false, p.chol)) != hipSuccess) return e;
     trsv_t_kernel<<<1, 64, 0, c->stream>>>(m, p.Lm, tmp + m, delta, p.chol);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    lm_fail_kernel<<<(p.L + 255) / 256, 256, 0, c->stream>>>(p.L, p.chol, delta);
     return hipGetLastError();
 }
 

@@ -663,7 +663,7 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
 
 // Rings of the levels lo..hi whose side bands the streaming pass did not write
 // (no launch when it wrote them all).
-void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst) {
+hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst) {
     RingLevels R{};
     int most = 0;
     for (int lv = lo; lv <= hi; ++lv) {
@@ -680,9 +680,9 @@ void launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, u
         R.items[k] = 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
         most = R.items[k] > most ? R.items[k] : most;
     }
-    if (R.n == 0) return;
+    if (R.n == 0) return hipSuccess;
     dim3 grid((most + 255) / 256, n_img, R.n);
-    launch_timed(c, "pyramid", ring_kernel, grid, dim3(256), 0, dst, lay.bytes, R);
+    return launch_timed(c, "pyramid", ring_kernel, grid, dim3(256), 0, dst, lay.bytes, R);
 }
 
 }  // namespace
@@ -743,8 +743,9 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         const int groups = (lay.w[0] + 2 * PAD + 15) / 16;
         const int items = groups * (lay.h[0] + 2 * PAD);
         dim3 grid((items + 255) / 256, n_img);
-        launch_timed(c, "pyramid", level0_kernel, grid, dim3(256), 0, src, img_stride, stride, lay.w[0], lay.h[0],
-                     lay.pitch[0], lay.bytes, dst);
+        const hipError_t e = launch_timed(c, "pyramid", level0_kernel, grid, dim3(256), 0, src, img_stride, stride,
+                                          lay.w[0], lay.h[0], lay.pitch[0], lay.bytes, dst);
+        if (e != hipSuccess) return e;
         s0 = slot0;
         s0_img = lay.bytes;
         s0_pitch = lay.pitch[0];
@@ -767,7 +768,8 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
                              : nl == 2 ? launch_stream<2>(c, s, n_img, lay, l, dst)
                                        : launch_stream<1>(c, s, n_img, lay, l, dst);
         if (e != hipSuccess) return e;
-        launch_rings(c, n_img, lay, l + 1, l + nl, dst);
+        const hipError_t er = launch_rings(c, n_img, lay, l + 1, l + nl, dst);
+        if (er != hipSuccess) return er;
         l += nl;
     }
     return hipGetLastError();

@@ -23,6 +23,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GVX_LIB") or os.path.join(_HERE, "libgvx.so")  # GVX_LIB: A/B builds (tools/variant.sh)
 
 GVX_OK = 0
+GVX_ERR_NUMERIC = -7  # include/gvx.h: a factorisation met a non-positive pivot
 GVX_PREINT_NORMAL = 0
 GVX_PREINT_EARTH = 2
 
@@ -783,10 +784,12 @@ class Context:
         Dv = None if D is None else np.ascontiguousarray(D, np.float64).reshape(L)
         r = L - m
         delta, S, info = np.zeros(L), np.zeros(max(r * r, 1)), np.zeros(2, np.int32)
-        self._check(self._L.gvx_schur_solve(self._h, nres.size, _ptr(nres), _ptr(boff), _ptr(blk), _ptr(roff),
-                                            _ptr(joff), _ptr(data), data.size, size.size, _ptr(size), _ptr(index), m,
-                                            L, _ptr(Dv), _ptr(delta), _ptr(S), _ptr(info)), "gvx_schur_solve")
-        return dict(delta=delta, S=S[:r * r].reshape(r, r).T.copy(), info=info)
+        s = self._L.gvx_schur_solve(self._h, nres.size, _ptr(nres), _ptr(boff), _ptr(blk), _ptr(roff),
+                                    _ptr(joff), _ptr(data), data.size, size.size, _ptr(size), _ptr(index), m,
+                                    L, _ptr(Dv), _ptr(delta), _ptr(S), _ptr(info))
+        if s != GVX_ERR_NUMERIC:  # a failed factorisation is a result (ok = False), not an error
+            self._check(s, "gvx_schur_solve")
+        return dict(delta=delta, S=S[:r * r].reshape(r, r).T.copy(), info=info, ok=s == GVX_OK)
 
     def schur_solve_dev(self, p, d_data, d_delta, d_D=None, d_S=None, d_info=None):
         """Device-pointer LM step (gvx_schur_solve_dev), async on the context stream."""

@@ -28,7 +28,8 @@ enum {
     GVX_ERR_HIP = -3,       /* a HIP runtime call failed */
     GVX_ERR_OOM = -4,       /* device or host allocation failed */
     GVX_ERR_NOT_FOUND = -5, /* unknown frame id */
-    GVX_ERR_UNSUPPORTED = -6
+    GVX_ERR_UNSUPPORTED = -6,
+    GVX_ERR_NUMERIC = -7    /* a factorisation met a non-positive pivot (gvx_schur_solve: outputs NaN) */
 };
 
 typedef struct gvx_ctx gvx_ctx;
@@ -570,13 +571,18 @@ gvx_status gvx_marginalize_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres,
    corrections applied).  D (nullable, L local parameters): the LM
    regularisation.  Outputs: delta [L] in local index order; S (nullable, r x r
    column-major, r = L - m) and info (nullable, 2 ints: 1 where the Cholesky
-   factorisation of Hee + D, resp. S, met a non-positive pivot, else 0). */
+   factorisation of Hee + D, resp. S, met a non-positive pivot, else 0; a
+   failed Hee + D also sets info[1], since S is then never formed).  When either
+   factorisation fails every entry of delta is NaN and gvx_schur_solve returns
+   GVX_ERR_NUMERIC after writing delta, S and info (Ceres' linear solver
+   reports FAILURE and LM rejects the step). */
 gvx_status gvx_schur_solve(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
                            const int32_t* blk, const int64_t* res_off, const int64_t* jac_off, const double* data,
                            int64_t n_data, int32_t nb, const int32_t* size, const int32_t* index, int32_t m,
                            int32_t L, const double* D, double* delta, double* S, int32_t* info);
 /* The same with data, D and the outputs as device pointers, enqueued on the
-   context stream (the structure arrays stay host arrays). */
+   context stream (the structure arrays stay host arrays).  Asynchronous: a
+   failed factorisation shows as NaN in d_delta and in d_info only. */
 gvx_status gvx_schur_solve_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
                                const int32_t* blk, const int64_t* res_off, const int64_t* jac_off,
                                const double* d_data, int64_t n_data, int32_t nb, const int32_t* size,

@@ -50,7 +50,7 @@ def test_sequence_two_ranks_track_gather():
     """configs[4] at world 2: each rank replays its own sequence; rank 0 gets
     both ranks' per-frame tracks, its own intact."""
     d = _run_two_ranks(["--config", "5", "--frames", "40", "--warmup", "4"])
-    assert d["n_gpus"] == 2 and d["steps"] == 36
+    assert d["n_gpus"] == 2 and d["warmup"] == 16 and d["steps"] == 24  # warm-up rounded to the K = 16 batch
     assert d["gathered_ranks"] == 2 and d["gather_check"] is True
 
 

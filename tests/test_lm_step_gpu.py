@@ -89,4 +89,15 @@ def test_schur_solve_reports_indefinite(ctx, window):
                 data[off:off + n] = 0.0
             off += n
     g = ctx.schur_solve(dict(p, data=data))
-    assert g["info"][0] == 1
+    assert g["info"][0] == 1 and g["info"][1] == 1  # S is never formed after a failed Hee
+    assert g["ok"] is False
+    assert np.isnan(g["delta"]).all()  # no stale step survives
+    # the device entry reports the same through d_info and a NaN d_delta
+    import torch
+    L = int(p["L"]) if "L" in p else g["delta"].size
+    d_data = torch.from_numpy(data).cuda()
+    d_delta = torch.zeros(g["delta"].size, dtype=torch.float64, device="cuda")
+    d_info = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ctx.schur_solve_dev(dict(p, data=data), d_data.data_ptr(), d_delta.data_ptr(), d_info=d_info.data_ptr())
+    ctx.sync()
+    assert d_info.cpu().tolist() == [1, 1] and torch.isnan(d_delta).all().item() and L == d_delta.numel()

@@ -163,6 +163,33 @@ def test_marginalize_fast_falls_back_on_singular_hmm(ctx, gvx_mod, problems):
     assert np.abs(J0.T @ e0 + g["bp"]).max() <= 1e-10 * np.abs(g["bp"]).max()
 
 
+@pytest.mark.parametrize("name", ["two keyframes", "prior over keyframes 0-8 (r = 133)"])
+def test_marginalize_fast_falls_back_on_singular_hp(ctx, orc, problems, name):
+    """A remaining block with every Jacobian column zeroed: Hmm stays positive
+    definite (Cholesky Schur complement), but Hp has a zero eigenvalue, so
+    Hp - EPS*I is not positive definite and the FAST solver linearises with
+    Eigen's eigen-solver on the device (marg.hip: the gated sym_eigen +
+    linearize_kernel instead of lin_chol / trsv).  The eigenvalues
+    are then real numbers (NaN marks the Cholesky path), and J0 / e0 are
+    bit-identical to the restatement's linearization of the same Hp / bp
+    (marginalization_info.h:153-166)."""
+    p = problems[name]
+    m = p["m"]
+    rem = [b for b in range(len(p["size"])) if p["index"][b] >= m]
+    q = _unobserved(p, rem[-1])
+    g = ctx.marginalize(q)
+    assert list(g["info"]) == [0, 0]  # eigen-solver converged
+    assert not np.isnan(g["eval"]).any()  # the eigen path produced the linearisation
+    assert g["eval"].min() <= 1e-8 * max(1.0, g["eval"].max())  # the dropped direction
+    J0, e0, ev, info2 = orc.marg_linearize(g["Hp"], g["bp"])
+    assert info2 == 0
+    _same(g["eval"], ev, "eigenvalues of Hp")
+    _same(g["J0"], J0, "J0")
+    _same(g["e0"], e0, "e0")
+    # the healthy problem still takes the Cholesky path
+    assert np.isnan(ctx.marginalize(p)["eval"]).all()
+
+
 def test_marginalize_dev_matches_host(ctx, problems):
     import torch
     p = problems["prior over keyframes 0-8 (r = 133)"]

@@ -18,12 +18,14 @@ pytestmark = pytest.mark.gpu
 W, H, N, L = 1280, 560, 150, 3
 
 
-def _oracle_sequence(orc, frames, kp, dp, nthreads=1):
+def _oracle_sequence(orc, frames, kp, dp, nthreads=1, equalised=None):
+    """The oracle's Tracking::track loop; `equalised` (optional): the frames'
+    CLAHE outputs computed beforehand (they depend on the frame alone)."""
     pts, vel = np.zeros((0, 2), np.float32), np.zeros((0, 2), np.float32)
     prev_eq = None
     out = []
     for t, f in enumerate(frames):
-        eq = orc.clahe(f)
+        eq = orc.clahe(f) if equalised is None else equalised[t]
         rec = {}
         if t > 0 and pts.shape[0]:
             # each pyramid built once (bit-identical to OpenCV's per-call rebuild)
