@@ -45,6 +45,16 @@ __device__ __forceinline__ int dot2k(uint32_t a, uint32_t b, int k) {
     __asm__("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
     return r;
 }
+typedef unsigned short v2us __attribute__((ext_vector_type(2)));
+// a.lo*b.lo + a.hi*b.hi + c on unsigned int16 halves (v_dot2_u32_u16)
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(v2us, a), __builtin_bit_cast(v2us, b), c, false);
+}
+__device__ __forceinline__ uint32_t udot2k(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    __asm__("v_dot2_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
 // (lo & 0xffff) | (hi << 16)
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) {
     return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
@@ -312,9 +322,23 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
 // Mismatch of one unit against J at integer offset (jx, jy) with weights
 // (W0, W1): accumulates b1 += diff*Ix, b2 += diff*Iy (or es += |diff| for ERR).
 // r0 / r1: bytes jx+7*seg .. +7 of rows jy+row and jy+row+1.
-template <bool ERR>
-__device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
-                                           uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
+// Bytes (b[T], b[T+1]) of the 8-byte value {d1:d0} as the HIGH bytes of two
+// uint16 halves (b*256), for the unsigned dot2 below.
+template <int T>
+__device__ __forceinline__ uint32_t byte_pair_hi(uint32_t d0, uint32_t d1) {
+    return __builtin_amdgcn_perm(d1, d0, 0x000c000cu | ((uint32_t)T << 8) | ((uint32_t)(T + 1) << 24));
+}
+// The J window values of a unit as packed int16 pairs (pixel 2k, 2k+1; pair 3
+// high = 0): CV_DESCALE(w00 J00 + w01 J01 + w10 J10 + w11 J11, W_BITS - 5).
+// The sum runs on v_dot2_u32_u16 with the bytes scaled by 256 (b*256 <= 65280
+// and w <= 2^14 are uint16; X = 256 (sum + 2^8) < 2^30), so the value is X >> 17:
+// one v_perm takes the high halves of two pixels' X and one packed shift by 1
+// finishes both (2 operations per pixel pair instead of 2 shifts and a pack).
+// Only for w11 >= 0: w11 = 2^14 - w00 - w01 - w10 of three separately rounded
+// weights is -1 or -2 when a*b*2^14 is below ~1.5, and such iterations take
+// j_pairs_signed (the signed v_dot2_i32_i16 on plain bytes).
+__device__ __forceinline__ void j_pairs_signed(const uint32_t (&r0)[2], const uint32_t (&r1)[2], uint32_t W0,
+                                               uint32_t W1, uint32_t (&jp)[4]) {
     constexpr int RND = 1 << (W_BITS - 6);
     int jv[8];
     jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2k(byte_pair<0>(r0[0], r0[1]), W0, RND));
@@ -327,21 +351,51 @@ __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2
 #pragma unroll
     for (int t = 0; t < 7; ++t) jv[t] >>= (W_BITS - 5);
     jv[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
+}
+__device__ __forceinline__ void j_pairs(const uint32_t (&r0)[2], const uint32_t (&r1)[2], uint32_t W0, uint32_t W1,
+                                        uint32_t (&jp)[4]) {
+    constexpr uint32_t RND = 1u << (W_BITS - 6 + 8);
+    uint32_t X[8];
+    X[0] = udot2(byte_pair_hi<0>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<0>(r0[0], r0[1]), W0, RND));
+    X[1] = udot2(byte_pair_hi<1>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<1>(r0[0], r0[1]), W0, RND));
+    X[2] = udot2(byte_pair_hi<2>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<2>(r0[0], r0[1]), W0, RND));
+    X[3] = udot2(byte_pair_hi<3>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<3>(r0[0], r0[1]), W0, RND));
+    X[4] = udot2(byte_pair_hi<4>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<4>(r0[0], r0[1]), W0, RND));
+    X[5] = udot2(byte_pair_hi<5>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<5>(r0[0], r0[1]), W0, RND));
+    X[6] = udot2(byte_pair_hi<6>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<6>(r0[0], r0[1]), W0, RND));
+    X[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t hi = __builtin_amdgcn_perm(X[2 * k + 1], X[2 * k], 0x07060302u);  // (X0 >> 16, X1 >> 16)
+        jp[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2us, hi) >> (unsigned short)1);
+    }
+}
+
+template <bool ERR, bool SIGNED = false>
+__device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
+                                           uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
+    uint32_t jp[4];
+    if constexpr (SIGNED)
+        j_pairs_signed(r0, r1, W0, W1, jp);
+    else
+        j_pairs(r0, r1, W0, W1, jp);
     if (ERR) {
         int e = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);  // diff pair
+            const uint32_t d = psub16(jp[k], u.iv[k]);  // diff pair
             const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
             e += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
         }
         es += valid ? e : 0;
     } else {
-        const uint32_t d0 = psub16(pack16(jv[0], jv[1]), u.iv[0]);
+        const uint32_t d0 = psub16(jp[0], u.iv[0]);
         int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
 #pragma unroll
         for (int k = 1; k < 4; ++k) {
-            const uint32_t d = psub16(pack16(jv[2 * k], jv[2 * k + 1]), u.iv[k]);
+            const uint32_t d = psub16(jp[k], u.iv[k]);
             s1 = dot2(d, u.ix[k], s1);
             s2 = dot2(d, u.iy[k], s2);
         }
@@ -702,18 +756,31 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
         // weights change, so the rows are reused instead of loaded again
         int cinx = INT_MIN, ciny = INT_MIN;
         uint32_t jr0[U][2], jr1[U][2];
-        for (int j = 0; j < cfg.max_iter; ++j) {
+        // one exit, at the bottom: every loop-carried value is updated in place
+        // (with the early exits the register allocator copied all of them -- the
+        // cached J rows, the position, the previous step -- on every iteration)
+        bool more = cfg.max_iter > 0;
+        int j = 0;
+        while (more) {
             const float fnx = floorf(nextx), fny = floorf(nexty);
-            const int inx = (int)fnx, iny = (int)fny;
-            if (inx < -WIN || inx >= W || iny < -WIN || iny >= H) {
-                if (l == 0) status = 0;
-                break;
-            }
+            // a window off the level ends the point's iterations (status 0 at level
+            // 0) with its position as it was.  The body still runs (no divergent
+            // branch around it: see the reloads below) at a position clamped into
+            // the padded level, and its result is discarded by the selects.
+            const bool oob = (int)fnx < -WIN || (int)fnx >= W || (int)fny < -WIN || (int)fny >= H;
+            const int inx = min(max((int)fnx, -WIN), W - 1), iny = min(max((int)fny, -WIN), H - 1);
             uint32_t J0, J1;
             weights(nextx - fnx, nexty - fny, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
-            if (inx != cinx || iny != ciny) {
-                const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+            // reload decisions are wave-uniform (ballots): a group whose position did
+            // not move reloads the same rows, and a border window of either group
+            // sends both groups through their LDS tiles (the tile path is correct for
+            // any window).  Branches on a group's own conditions made the compiler
+            // copy every cached row in and out of a second register set each
+            // iteration, to keep the other group's values.
+            if (__builtin_amdgcn_ballot_w64(inx != cinx || iny != ciny)) {
+                const bool fast =
+                    !__builtin_amdgcn_ballot_w64(raw && !(inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H));
                 if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
                 if (U > 1 && fast) {
                     // every unit's two rows in flight before the first is realigned
@@ -749,10 +816,19 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             }
             float fb1, fb2;
             if constexpr (ACC == 0) {
+                // a negative w11 anywhere in the wave (rare): the signed form (uniform branch)
+                if (__builtin_amdgcn_ballot_w64((int)J1 < 0)) {
 #pragma unroll
-                for (int s = 0; s < U; ++s) {
-                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                    match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    for (int s = 0; s < U; ++s) {
+                        if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                        match_unit<false, true>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < U; ++s) {
+                        if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                        match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    }
                 }
                 group_sums_f32<G>(b1, b2, fb1, fb2);
             } else {
@@ -775,19 +851,21 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             fb2 *= FLT_SCALE;
             const float dx = (A12 * fb2 - A22 * fb1) * D;
             const float dy = (A12 * fb1 - A11 * fb2) * D;
-            nextx += dx;
-            nexty += dy;
-            nx = nextx + halfw;
-            ny = nexty + halfw;
+            const float tx = nextx + dx, ty = nexty + dy;
             // delta.ddot(delta) <= eps^2 in double: dx*dx is exact in fp64, so the fma rounds once like the sum
-            if (__builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps) break;
-            if (j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f) {
-                nx -= dx * 0.5f;
-                ny -= dy * 0.5f;
-                break;
-            }
+            const bool conv = __builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps;
+            const bool osc = !conv && j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f;
+            // (tx + halfw) - dx*0.5 in that order: next_pts = nextPt + halfWin, then -= delta*0.5
+            const float ux = osc ? (tx + halfw) - dx * 0.5f : tx + halfw;
+            const float uy = osc ? (ty + halfw) - dy * 0.5f : ty + halfw;
+            nx = oob ? nx : ux;
+            ny = oob ? ny : uy;
+            nextx = oob ? nextx : tx;
+            nexty = oob ? nexty : ty;
+            status = (oob && l == 0) ? 0 : status;
             pdx = dx;
             pdy = dy;
+            more = !oob && !conv && !osc && ++j < cfg.max_iter;
         }
         if (status && l == 0) {
             // final error (OPTFLOW_LK_GET_MIN_EIGENVALS not set)
@@ -810,7 +888,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                     uint32_t r0[2], r1[2];
                     load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
                     if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                    match_unit<true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    match_unit<true, true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
                 }
             }
             err = __fdiv_rn((float)group_sum<G>(es) * 1.f, (float)(32 * WIN * WIN));

@@ -22,6 +22,12 @@
 /* LK iterations per (level, point) -- diagnostic builds (-DORC_ITER_STATS, one thread) */
 long orc_iter_hist[8][64];
 #endif
+#ifdef ORC_ACC_STATS
+/* window sums whose absolute sum stays <= 2^24 (every fp32 partial sum exact) --
+   diagnostic builds (-DORC_ACC_STATS, one thread): [0] A sets, [1] A sets with
+   all three small, [2] b pairs, [3] b pairs with both small */
+long orc_acc_stats[16];
+#endif
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
@@ -301,6 +307,10 @@ static void lk_level(const lk_job* jb) {
         int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
 
         int64_t iA11 = 0, iA12 = 0, iA22 = 0;
+#ifdef ORC_ACC_STATS
+        int64_t aA12 = 0, cA[3][5] = {{0}};
+        double gx2[3] = {0, 0, 0}, gy2[3] = {0, 0, 0}, gax[3] = {0, 0, 0}, gay[3] = {0, 0, 0};
+#endif
         float fA11 = 0.f, fA12 = 0.f, fA22 = 0.f;
         f4 qA11 = {{0}}, qA12 = {{0}}, qA22 = {{0}};
         const int simd_w = lk_accum == ORC_ACC_F32X4 ? win / 8 * 8 : 0;
@@ -324,6 +334,16 @@ static void lk_level(const lk_job* jb) {
                 iA11 += (int64_t)ixval * ixval;
                 iA12 += (int64_t)ixval * iyval;
                 iA22 += (int64_t)iyval * iyval;
+#ifdef ORC_ACC_STATS
+                aA12 += llabs((int64_t)ixval * iyval);
+                cA[0][x < 16 ? (x & 3) : 4] += (int64_t)ixval * ixval;
+                cA[1][x < 16 ? (x & 3) : 4] += llabs((int64_t)ixval * iyval);
+                cA[2][x < 16 ? (x & 3) : 4] += (int64_t)iyval * iyval;
+                gx2[x >= 16 ? 2 : (x & 1)] += (double)ixval * ixval;
+                gy2[x >= 16 ? 2 : (x & 1)] += (double)iyval * iyval;
+                gax[x >= 16 ? 2 : (x & 1)] += abs(ixval);
+                gay[x >= 16 ? 2 : (x & 1)] += abs(iyval);
+#endif
                 if (x < simd_w) {
                     const float fx = (float)ixval, fy = (float)iyval;
                     volatile float t11 = fx * fx, t12 = fx * fy, t22 = fy * fy;  /* no contraction */
@@ -337,6 +357,16 @@ static void lk_level(const lk_job* jb) {
                 }
             }
         }
+#ifdef ORC_ACC_STATS
+        orc_acc_stats[0]++;
+        orc_acc_stats[1] += iA11 <= (1 << 24) && iA22 <= (1 << 24) && aA12 <= (1 << 24);
+        {
+            int ok = 1;
+            for (int k = 0; k < 3; k++)
+                for (int c = 0; c < 5; c++) ok &= cA[k][c] <= (1 << 24);
+            orc_acc_stats[5] += ok;
+        }
+#endif
         float A11, A12, A22;
         if (lk_accum == ORC_ACC_EXACT) {
             A11 = (float)iA11 * FLT_SCALE;
@@ -386,6 +416,16 @@ static void lk_level(const lk_job* jb) {
             iw10 = cv_round((1.f - a) * b * (1 << W_BITS));
             iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
             int64_t ib1 = 0, ib2 = 0;
+#ifdef ORC_ACC_STATS
+            int64_t ab1 = 0, ab2 = 0, cb[2][5] = {{0}};
+            int64_t cls[2][3] = {{0}};           /* |p| by class: even x<16, odd x<16, x>=16 */
+            int64_t lane[32][2][3];              /* per lane (unit k -> lane k % 32) */
+            int maxd[32];
+            double d2c[3] = {0, 0, 0};
+            int mdc[3] = {0, 0, 0};
+            memset(lane, 0, sizeof lane);
+            memset(maxd, 0, sizeof maxd);
+#endif
             float fb1 = 0.f, fb2 = 0.f;
             f4 qb0 = {{0}}, qb1 = {{0}};
             for (int y = 0; y < win; y++) {
@@ -399,6 +439,23 @@ static void lk_level(const lk_job* jb) {
                     const int p1 = diff * dIwin[(y * win + x) * 2], p2 = diff * dIwin[(y * win + x) * 2 + 1];
                     ib1 += p1;
                     ib2 += p2;
+#ifdef ORC_ACC_STATS
+                    ab1 += p1 < 0 ? -p1 : p1;
+                    ab2 += p2 < 0 ? -p2 : p2;
+                    cb[0][x < 16 ? (x & 3) : 4] += p1 < 0 ? -p1 : p1;
+                    cb[1][x < 16 ? (x & 3) : 4] += p2 < 0 ? -p2 : p2;
+                    {
+                        const int c = x >= 16 ? 2 : (x & 1), ln = (3 * y + x / 7) % 32;
+                        cls[0][c] += p1 < 0 ? -p1 : p1;
+                        cls[1][c] += p2 < 0 ? -p2 : p2;
+                        lane[ln][0][c] += p1 < 0 ? -p1 : p1;
+                        lane[ln][1][c] += p2 < 0 ? -p2 : p2;
+                        d2c[c] += (double)diff * diff;
+                        if ((diff < 0 ? -diff : diff) > mdc[c]) mdc[c] = diff < 0 ? -diff : diff;
+                        const int ad = diff < 0 ? -diff : diff;
+                        if (ad > maxd[ln]) maxd[ln] = ad;
+                    }
+#endif
                     if (x < simd_w) {
                         /* v_mul_expand of (dx,dy) pairs by (diff,diff): pixels x%4 in {0,1}
                            feed qb0 lanes (2(x%2), 2(x%2)+1), pixels x%4 in {2,3} feed qb1 */
@@ -411,6 +468,43 @@ static void lk_level(const lk_job* jb) {
                     }
                 }
             }
+#ifdef ORC_ACC_STATS
+            orc_acc_stats[2]++;
+            orc_acc_stats[3] += ab1 <= (1 << 24) && ab2 <= (1 << 24);
+            {
+                int ok = 1;
+                for (int k = 0; k < 2; k++)
+                    for (int c = 0; c < 5; c++) ok &= cb[k][c] <= (1 << 24);
+                orc_acc_stats[4] += ok;
+                int ok1 = 1, ok2 = 1;
+                for (int k = 0; k < 2; k++)
+                    for (int c = 0; c < 3; c++) ok1 &= cls[k][c] <= (1 << 24);
+                for (int ln = 0; ln < 32; ln++)
+                    for (int k = 0; k < 2; k++)
+                        for (int c = 0; c < 3; c++) ok2 &= lane[ln][k][c] <= (1 << 19);
+                orc_acc_stats[6] += ok1;
+                orc_acc_stats[7] += ok2;
+                {
+                    /* Cauchy-Schwarz bounds: per class D2_c, and D2 total */
+                    int ok3 = 1, ok4 = 1;
+                    const double d2t = d2c[0] + d2c[1] + d2c[2];
+                    for (int c = 0; c < 3; c++) {
+                        ok3 &= d2c[c] * gx2[c] <= 281474976710656.0 && d2c[c] * gy2[c] <= 281474976710656.0;
+                        ok4 &= d2t * gx2[c] <= 281474976710656.0 && d2t * gy2[c] <= 281474976710656.0;
+                    }
+                    orc_acc_stats[8] += ok3;
+                    int ok5 = 1, ok6 = 1;
+                    const int mdt = mdc[0] > mdc[1] ? (mdc[0] > mdc[2] ? mdc[0] : mdc[2]) : (mdc[1] > mdc[2] ? mdc[1] : mdc[2]);
+                    for (int c = 0; c < 3; c++) {
+                        ok5 &= (double)mdc[c] * gax[c] <= 16777216.0 && (double)mdc[c] * gay[c] <= 16777216.0;
+                        ok6 &= (double)mdt * gax[c] <= 16777216.0 && (double)mdt * gay[c] <= 16777216.0;
+                    }
+                    orc_acc_stats[10] += ok5;
+                    orc_acc_stats[11] += ok6;
+                    orc_acc_stats[9] += ok4;
+                }
+            }
+#endif
             float b1, b2;
             if (lk_accum == ORC_ACC_EXACT) {
                 b1 = (float)ib1 * FLT_SCALE;
