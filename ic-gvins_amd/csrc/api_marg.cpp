@@ -56,14 +56,17 @@ void make_chunks(Lists& ls) {
 
 // Validates the problem and builds the contribution lists.  Returns GVX_OK or
 // an error with the message set.
+// m_max: the largest eliminated set the caller's solver takes (the dense
+// eigen / Cholesky kernels: GVX_EIG_MAX_N; the LM step with a diagonal Hee: any)
 gvx_status build_lists(gvx_ctx* c, int n_fac, const int32_t* nres, const int32_t* blk_off, const int32_t* blk,
                        const int64_t* res_off, const int64_t* jac_off, int64_t n_data, int nb, const int32_t* size,
-                       const int32_t* index, int m, int L, Lists& out) {
+                       const int32_t* index, int m, int L, Lists& out, int m_max = GVX_EIG_MAX_N) {
     if (n_fac < 0 || nb < 0 || n_data < 0) return set_err(c, GVX_ERR_INVALID, "negative size");
     if (m <= 0) return set_err(c, GVX_ERR_INVALID, "nothing to marginalize (m = %d)", m);
     if (L < m) return set_err(c, GVX_ERR_INVALID, "local size %d < marginalized size %d", L, m);
-    if (m > GVX_EIG_MAX_N || L - m > GVX_EIG_MAX_N)
-        return set_err(c, GVX_ERR_UNSUPPORTED, "marginalized %d / remained %d above %d", m, L - m, GVX_EIG_MAX_N);
+    if (m > m_max || L - m > GVX_EIG_MAX_N)
+        return set_err(c, GVX_ERR_UNSUPPORTED, "marginalized %d / remained %d above %d / %d", m, L - m, m_max,
+                       GVX_EIG_MAX_N);
     if (n_fac && (!nres || !blk_off || !blk || !res_off || !jac_off)) return set_err(c, GVX_ERR_INVALID, "null pointer");
     if (nb && (!size || !index)) return set_err(c, GVX_ERR_INVALID, "null block table");
     for (int b = 0; b < nb; ++b)
@@ -157,6 +160,19 @@ gvx_status build_lists(gvx_ctx* c, int n_fac, const int32_t* nres, const int32_t
     }
     out.recs = std::move(recs);
     return GVX_OK;
+}
+
+// Hee (the first m local parameters) is diagonal: every block below m has one
+// local parameter and no H0 record couples two different such blocks -- the
+// reference's DENSE_SCHUR window, one inverse depth per landmark, each
+// reprojection factor touching one landmark (ic_gvins.cc:1170-1180).
+bool diagonal_e(const Lists& ls, int m) {
+    for (int k = 0; k < ls.n_pairs; ++k) {
+        const MargPairRec& r = ls.recs[k];  // row0 >= col0
+        if (r.row0 >= m) continue;          // not an (eliminated, eliminated) pair
+        if (r.row0 != r.col0 || r.lp != 1) return false;
+    }
+    return true;
 }
 
 struct DevOut {
@@ -353,6 +369,10 @@ namespace {
 gvx_status run_lm(gvx_ctx* c, Lists& ls, const double* d_data, const double* d_D, int m, int L, double* d_delta,
                   double* d_S, int32_t* d_info) {
     const int r = L - m;
+    const bool diag = diagonal_e(ls, m);
+    if (!diag && m > GVX_EIG_MAX_N)
+        return set_err(c, GVX_ERR_UNSUPPORTED, "schur solve: %d eliminated parameters with a non-diagonal Hee (max %d)",
+                       m, GVX_EIG_MAX_N);
     make_chunks(ls);
     MargPairRec *d_rec, *h_rec;
     int4 *d_con, *h_con, *d_chk, *h_chk;
@@ -367,7 +387,7 @@ gvx_status run_lm(gvx_ctx* c, Lists& ls, const double* d_data, const double* d_D
     Staging work;
     work.add((size_t)L * L, &H0);
     work.add((size_t)L, &b0);
-    work.add((size_t)m * m, &Lm);
+    work.add(diag ? (size_t)m : (size_t)m * m, &Lm);
     work.add((size_t)r * r, &Lp);
     work.add((size_t)m * (r + 1), &X);
     work.add((size_t)ls.n_part, &part);
@@ -408,6 +428,7 @@ gvx_status run_lm(gvx_ctx* c, Lists& ls, const double* d_data, const double* d_D
     p.chunks = d_chk;
     p.recpart = d_rpart;
     p.part = part;
+    p.diag_e = diag ? 1 : 0;
     hipEvent_t ev{};
     prof_begin(c, "lm_step", &ev);
     e = launch_lm_step(c, p, d_D, d_delta, d_S ? d_S : S, bs, tmp);
@@ -427,7 +448,8 @@ gvx_status gvx_schur_solve_dev(gvx_ctx* c, int32_t n_fac, const int32_t* nres, c
     if (!d_delta || (n_fac && !d_data)) return set_err(c, GVX_ERR_INVALID, "null device pointer");
     hipSetDevice(c->device);
     Lists ls;
-    gvx_status s = build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls);
+    gvx_status s =
+        build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls, INT32_MAX);
     if (s) return s;
     return run_lm(c, ls, d_data, d_D, m, L, d_delta, d_S, d_info);
 }
@@ -440,7 +462,8 @@ gvx_status gvx_schur_solve(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const
     if (!delta || (n_fac && !data)) return set_err(c, GVX_ERR_INVALID, "null pointer");
     hipSetDevice(c->device);
     Lists ls;
-    gvx_status s = build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls);
+    gvx_status s =
+        build_lists(c, n_fac, nres, blk_off, blk, res_off, jac_off, n_data, nb, size, index, m, L, ls, INT32_MAX);
     if (s) return s;
     const int r = L - m;
     double *d_in, *h_in, *d_D, *h_D, *d_delta, *h_delta, *d_S, *h_S;

@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(LUT_THREADS) lut_kernel(const uint8_t* __restr
                  lut + ((int64_t)img * g.tiles_x * g.tiles_y + ty * g.tiles_x + tx) * 256);
 }
 
-constexpr int TROW = 257;  // LDS dwords per table row (bank skew between tiles)
+constexpr int TROW = 260;  // LDS dwords per table row (16-B aligned, bank skew between tiles)
 constexpr int PPT = 8;     // pixels (columns) per thread
 constexpr int ROWS_UNROLL = 8;
 constexpr int TAB_UNROLL = 8;
@@ -456,10 +456,14 @@ __global__ void __launch_bounds__(1024) apply_kernel(const uint8_t* src, int64_t
 // band's table is rebuilt from LUT rows b and b+1.  Every source pixel is read
 // from HBM once and every output pixel written once (2 B/px against 3 B/px for
 // lut_kernel + apply_kernel), and BGR8 frames are converted in registers (no
-// gray scratch).  The table holds the four LUT values of an entry as fp32
-// (16 B, one ds_read_b128 per pixel), so the blend needs no byte conversions,
-// and the result is rounded and packed by v_cvt_pk_u8_f32 (round half to even,
-// saturating: cvRound + saturate_cast, tools/cvt_pk_u8_probe.hip).  The
+// gray scratch).  The table holds the four LUT values of an entry as bytes (one
+// ds_read_b32 per pixel, converted by v_cvt_f32_ubyte0..3): the LDS, not the
+// VALU, bounds this kernel (r04: LDS-array cycles ~60 % of the launch, two thirds
+// of them bank conflicts), and the fp32 table's ds_read_b128 took four LDS
+// cycles per pixel group and four times the table stores -- 0.236 -> 0.223 ms per
+// 256 frames (r04 v9).  The result is rounded and packed by v_cvt_pk_u8_f32
+// (round half to even, saturating: cvRound + saturate_cast,
+// tools/cvt_pk_u8_probe.hip).  The
 // arithmetic is that of lut_kernel / apply_kernel (same tile_lut, same fp32
 // blend order), so the two paths are bit-identical.  Segments > 1 recompute the
 // LUT row at each seam, so src must not overlap dst (the host keeps in-place
@@ -470,8 +474,8 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
                                                      int dst_stride, ClaheGeom g, int nseg, int cpr, int nph,
                                                      uint32_t* __restrict__ hist_img) {
     extern __shared__ float4 smf[];
-    float4* tab = smf;                                                     // (tiles_x + 1) * TROW entries
-    uint32_t* hs = reinterpret_cast<uint32_t*>(tab + (g.tiles_x + 1) * TROW);  // tiles_x histograms, HROW apart
+    uint32_t* tab = reinterpret_cast<uint32_t*>(smf);                      // (tiles_x + 1) * TROW entries
+    uint32_t* hs = tab + (g.tiles_x + 1) * TROW;  // tiles_x histograms, HROW apart
     uint32_t* lrb = hs + (g.tiles_x + 1) * HROW;   // 2 x tiles_x * 64 dwords: LUT rows by parity
     uint32_t* ih = lrb + 2 * g.tiles_x * 64;       // 256: in-image counts (histogram check)
     const int nb = g.tiles_y + 1;
@@ -623,11 +627,14 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
             const int k = i >> 6, qd = i & 63;
             const int ta = max(k - 1, 0) * 64 + qd, tb = min(k, g.tiles_x - 1) * 64 + qd;
             const uint32_t a = P[ta], bb = P[tb], c = Q[ta], d = Q[tb];
-            float4* o = tab + k * TROW + 4 * qd;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                o[j] = float4{(float)((a >> (8 * j)) & 255u), (float)((c >> (8 * j)) & 255u),
-                              (float)((bb >> (8 * j)) & 255u), (float)((d >> (8 * j)) & 255u)};
+            // byte j of (a, c, bb, d) -> dword for value 4qd + j: {a_j, c_j, bb_j, d_j}
+            const uint32_t ac_lo = __builtin_amdgcn_perm(c, a, 0x05010400u);   // a0 c0 a1 c1
+            const uint32_t ac_hi = __builtin_amdgcn_perm(c, a, 0x07030602u);   // a2 c2 a3 c3
+            const uint32_t bd_lo = __builtin_amdgcn_perm(d, bb, 0x05010400u);
+            const uint32_t bd_hi = __builtin_amdgcn_perm(d, bb, 0x07030602u);
+            uint4* o = reinterpret_cast<uint4*>(tab + k * TROW + 4 * qd);
+            *o = uint4{__builtin_amdgcn_perm(bd_lo, ac_lo, 0x05040100u), __builtin_amdgcn_perm(bd_lo, ac_lo, 0x07060302u),
+                       __builtin_amdgcn_perm(bd_hi, ac_hi, 0x05040100u), __builtin_amdgcn_perm(bd_hi, ac_hi, 0x07060302u)};
         }
     };
     // CLAHE_Interpolation_Body for the rows of tile row k in [ys, ye) held in px
@@ -640,14 +647,15 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
             const float ya = tyf - floorf(tyf), ya1 = 1.0f - ya;
             const f2 yv = {ya1, ya};
             uint32_t out[2] = {0, 0};
-            float4 ev[8];  // the 8 gathers first, then the blends
+            uint32_t ev[8];  // the 8 gathers first, then the blends
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 ev[j] = tab[(kh[j] & 0xffffu) + (((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u)];
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // the scheduler keeps the 8 reads together
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float4 e = ev[j];
+                const float4 e = float4{(float)(ev[j] & 255u), (float)((ev[j] >> 8) & 255u),
+                                        (float)((ev[j] >> 16) & 255u), (float)(ev[j] >> 24)};
                 // {top, bot} = {L[p][tx1], L[q][tx1]} * xa1 + {L[p][tx2], L[q][tx2]} * xa, then
                 // res = top * ya1 + bot * ya: the reference's products and sums, each rounded
                 const f2 tb = pk_mul_lo(f2{e.x, e.y}, xw[j]) + pk_mul_hi(f2{e.z, e.w}, xw[j]);
@@ -757,7 +765,7 @@ constexpr int FUSED_MIN_BATCH = 8;
 
 // fused_kernel's LDS: the fp32 table, the histograms, two LUT rows, the image histogram
 size_t fused_lds(const ClaheGeom& g) {
-    return (size_t)(g.tiles_x + 1) * TROW * 16 + ((size_t)(g.tiles_x + 1) * HROW + 2 * g.tiles_x * 64 + 256) * 4;
+    return (size_t)(g.tiles_x + 1) * TROW * 4 + ((size_t)(g.tiles_x + 1) * HROW + 2 * g.tiles_x * 64 + 256) * 4;
 }
 
 struct FusedPlan {

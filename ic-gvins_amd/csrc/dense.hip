@@ -333,6 +333,45 @@ __global__ void __launch_bounds__(256) lm_fail_kernel(int L, int* __restrict__ c
     if (i == 0 && f0 && !f1) chol[1] = 1;
 }
 
+// ---- the LM step with a diagonal Hee (MargLaunch::diag_e): one inverse depth per
+// landmark, each reprojection factor touching one, as in the reference's window.
+// The Cholesky factor of a diagonal matrix is its square root, and the general
+// potrf / trsv kernels reduce to exactly these operations on it (sqrt(a_ii), then
+// b_i * (1 / l_ii)), without their one-workgroup m <= 512 limit.
+// Ld[i] = sqrt(Hee(i, i) + D_i^2); chol[0] = 1 where a pivot is not positive.
+__global__ void __launch_bounds__(256) diag_chol_kernel(int m, int L, const double* __restrict__ H0,
+                                                        double* __restrict__ Ld, int* __restrict__ chol) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const double a = H0[(long)i * L + i];
+    if (!(a > 0.0)) chol[0] = 1;
+    Ld[i] = sqrt(a);
+}
+// X = Ld^-1 [Hef | be] (row-major m x (r + 1)), as trsv_kernel: x = b * (1 / l).
+// Skipped when *gate != 0.
+__global__ void __launch_bounds__(256) diag_x_kernel(int m, int L, const double* __restrict__ H0,
+                                                     const double* __restrict__ b0, const double* __restrict__ Ld,
+                                                     double* __restrict__ X, const int* __restrict__ gate) {
+    if (*gate != 0) return;
+    const int r = L - m;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long)m * (r + 1)) return;
+    const int k = (int)(idx / (r + 1)), j = (int)(idx - (long)k * (r + 1));
+    const double inv = 1.0 / Ld[k];
+    X[idx] = (j < r ? H0[(long)(m + j) * L + k] : b0[k]) * inv;
+}
+// delta_e = Ld^-T Ld^-1 t (trsv_kernel then trsv_t_kernel: (t * inv) * inv).
+// Skipped when *gate != 0.
+__global__ void __launch_bounds__(256) diag_back_kernel(int m, const double* __restrict__ Ld,
+                                                        const double* __restrict__ t, double* __restrict__ delta,
+                                                        const int* __restrict__ gate) {
+    if (*gate != 0) return;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= m) return;
+    const double inv = 1.0 / Ld[k];
+    delta[k] = (t[k] * inv) * inv;
+}
+
 }  // namespace
 
 hipError_t launch_potrf(gvx_ctx* c, int n, const double* A, int lda, double shift, double* L, int* fail,
@@ -376,10 +415,17 @@ hipError_t launch_lm_step(gvx_ctx* c, const MargLaunch& p, const double* D, doub
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // Hee + D = Lm Lm^T; X = Lm^-1 [Hef | be]; S = Hff - X^T X, bs = bf - X^T y
-    if ((e = launch_potrf(c, m, p.H0, p.L, 0.0, p.Lm, p.chol, nullptr)) != hipSuccess) return e;
-    if ((e = launch_trsv(c, m, p.Lm, r, p.H0 + (size_t)m * p.L, p.L, p.X, r + 1, false, p.chol)) != hipSuccess)
-        return e;
-    if ((e = launch_trsv(c, m, p.Lm, 1, p.b0, m, p.X + r, r + 1, false, p.chol)) != hipSuccess) return e;
+    if (p.diag_e) {
+        diag_chol_kernel<<<(m + 255) / 256, 256, 0, c->stream>>>(m, p.L, p.H0, p.Lm, p.chol);
+        const long nx = (long)m * (r + 1);
+        diag_x_kernel<<<(unsigned)((nx + 255) / 256), 256, 0, c->stream>>>(m, p.L, p.H0, p.b0, p.Lm, p.X, p.chol);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else {
+        if ((e = launch_potrf(c, m, p.H0, p.L, 0.0, p.Lm, p.chol, nullptr)) != hipSuccess) return e;
+        if ((e = launch_trsv(c, m, p.Lm, r, p.H0 + (size_t)m * p.L, p.L, p.X, r + 1, false, p.chol)) != hipSuccess)
+            return e;
+        if ((e = launch_trsv(c, m, p.Lm, 1, p.b0, m, p.X + r, r + 1, false, p.chol)) != hipSuccess) return e;
+    }
     if ((e = launch_schur_chol(c, p.L, m, p.H0, p.b0, p.X, S, bs, p.chol)) != hipSuccess) return e;
     // S = Lp Lp^T; delta_f = Lp^-T Lp^-1 bs
     if ((e = launch_potrf(c, r, S, r, 0.0, p.Lp, p.chol + 1, p.chol)) != hipSuccess) return e;
@@ -389,8 +435,12 @@ hipError_t launch_lm_step(gvx_ctx* c, const MargLaunch& p, const double* D, doub
     // delta_e = Lm^-T Lm^-1 (be - Hef delta_f)
     gemv_kernel<<<(m + 255) / 256, 256, 0, c->stream>>>(p.L, m, p.H0, p.b0, delta + m, tmp);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_trsv(c, m, p.Lm, 1, tmp, m, tmp + m, 1, false, p.chol)) != hipSuccess) return e;
-    trsv_t_kernel<<<1, 64, 0, c->stream>>>(m, p.Lm, tmp + m, delta, p.chol);
+    if (p.diag_e) {
+        diag_back_kernel<<<(m + 255) / 256, 256, 0, c->stream>>>(m, p.Lm, tmp, delta, p.chol);
+    } else {
+        if ((e = launch_trsv(c, m, p.Lm, 1, tmp, m, tmp + m, 1, false, p.chol)) != hipSuccess) return e;
+        trsv_t_kernel<<<1, 64, 0, c->stream>>>(m, p.Lm, tmp + m, delta, p.chol);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     lm_fail_kernel<<<(p.L + 255) / 256, 256, 0, c->stream>>>(p.L, p.chol, delta);
     return hipGetLastError();

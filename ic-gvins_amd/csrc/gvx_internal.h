@@ -266,6 +266,9 @@ struct MargLaunch {
     const int4* chunks;
     const int2* recpart;
     double* part;
+    // LM step: Hee is diagonal (every eliminated block has one local parameter and
+    // no factor couples two of them): Lm holds only its diagonal, no m limit
+    int diag_e;
 };
 hipError_t launch_marginalize(gvx_ctx* c, const MargLaunch& p);
 // constructEquation alone (H0 = sum J^T J, b0 = -sum J^T e; chunked when p.chunks)

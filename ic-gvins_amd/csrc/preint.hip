@@ -832,6 +832,219 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
         }
 }
 
+// preint_cov_kernel with the step's Phi / W blocks off the sequential path:
+// 16 lanes per segment (lane c owns column c of J and row c of P), and every 16
+// steps each lane of a segment's group forms ONE step's blocks -- the bias-
+// compensated sample, C = cbb0 skew(dv), D = cbb0 dt, W = gR N_v gR^T, the
+// RRec's rotated increments -- into LDS (StepRec), so the per-step chain keeps
+// only the velocity / position sums and the three column mat-vecs.  The blocks
+// are formed by the same operations as in preint_cov_kernel / preint_kernel, and
+// the column updates are the same code, so the outputs are the same bits
+// (tests/test_ba_gpu.py::test_preint_two_phase_bits_equal_one_phase).  The
+// 8-lane kernel above spent ~6.5 k cycles per step on one wave per SIMD (656
+// waves for 5,247 segments), most of them the per-lane scalar chain.
+struct StepRec {
+    double dt, f;             // Phi's scalars (the layout of Phi, so phi_mv reads it in place)
+    double C[9], D[9], M[9];  // Phi(3:6, 6:9), Phi(3:6, 12:15), Phi(6:9, 6:9) = I - skew(dtheta)
+    double W[9];              // W(3:6, 3:6)
+    double a[3], b[3];        // RRec's velocity / delta-velocity increments
+};
+static_assert(sizeof(Phi) == 29 * 8, "Phi is StepRec's prefix");
+constexpr int SREC_DW = sizeof(StepRec) / 8;  // 44
+constexpr int C16_CK = 8;  // steps per record chunk (one per lane of half a group): 18.5 KB of LDS per
+                           // wave, so every wave of a 5,247-segment batch is resident at once
+
+__global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_params prm, int n_seg,
+                                                          const gvx_imu* __restrict__ imu,
+                                                          const int32_t* __restrict__ seg_off,
+                                                          const gvx_state* __restrict__ state0,
+                                                          const double* __restrict__ iewn_in,
+                                                          const RRec* __restrict__ rrec,
+                                                          gvx_preint_result* __restrict__ out, double* __restrict__ pn) {
+    constexpr int LANES = 16, SPWL = 64 / LANES;
+    __shared__ StepRec sR[SPWL][C16_CK];
+    __shared__ double sG[SPWL][MS];
+    const int lane = threadIdx.x;
+    const int grp = lane / LANES, c = lane % LANES;
+    const int seg = blockIdx.x * SPWL + grp;
+    const bool live = seg < n_seg;
+    const int b0 = live ? seg_off[seg] : 0;
+    const int m = live ? seg_off[seg + 1] - b0 : 0;
+    int mmax = m;
+#pragma unroll
+    for (int o = LANES; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+    const bool earth = variant == GVX_PREINT_EARTH;
+    double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    gvx_state s0{};
+    double iewn[3] = {0, 0, 0};
+    if (live) {
+        s0 = state0[seg];
+        if (earth)
+            for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    }
+    double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        p[i] = s0.p[i];
+        v[i] = s0.v[i];
+    }
+    const double g3[3] = {0, 0, prm.gravity};
+    const double nacc = prm.acc_vrw * prm.acc_vrw;
+    const double ngyr = prm.gyr_arw * prm.gyr_arw;
+    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
+    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
+    const double g60 = earth ? -1.0 : 1.0;
+    const double wg = (g60 * ngyr) * g60;
+    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    double Jc[NS], Pc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        Jc[i] = i == c ? 1.0 : 0.0;
+        Pc[i] = 0.0;
+    }
+    const RRec* rr0 = rrec + (live ? b0 - seg : 0);
+    const gvx_imu* im = imu + b0;
+    for (int kc = 1; kc < mmax; kc += C16_CK) {
+        // ---- this chunk's step records, one step per lane ----
+        {
+            const int k = kc + c;
+            if (c < C16_CK && k < m) {
+                const RRec& rr = rr0[k - 1];
+                const gvx_imu& sm = im[k];
+                StepRec r;
+                const double dt = sm.dt;
+                double cbb0[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) cbb0[i] = rr.cbb0[i];
+                double sdv[3], sdth[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    sdth[i] = sm.dtheta[i] - dt * s0.bg[i];
+                    sdv[i] = sm.dvel[i] - dt * s0.ba[i];
+                    r.a[i] = rr.a[i];
+                    r.b[i] = rr.b[i];
+                }
+                const double sg = earth ? 1.0 : -1.0;
+                double gR[9];
+                for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) {
+                        double g = (gR[3 * a] * nacc) * gR[3 * b];
+                        g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+                        g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+                        r.W[3 * a + b] = g;
+                    }
+                double S[9];
+                skew(sdv, S);
+                mm3(cbb0, S, r.C);
+                for (int i = 0; i < 9; ++i) r.D[i] = cbb0[i] * dt;
+                skew(sdth, S);
+                for (int i = 0; i < 9; ++i) r.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+                r.dt = dt;
+                r.f = 1 - dt / prm.corr_time;
+                double* dst = reinterpret_cast<double*>(&sR[grp][c]);
+                const double* w = reinterpret_cast<const double*>(&r);
+#pragma unroll
+                for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+            }
+        }
+        __syncthreads();
+        const int kend = min(kc + C16_CK, mmax);
+        for (int k = kc; k < kend; ++k) {
+            const bool act = k < m;
+            const StepRec& r = sR[grp][k - kc];
+            // Phi read in place from the record (LDS, broadcast within the group): it
+            // is re-read after the barrier instead of held in registers across it
+            const Phi& f = *reinterpret_cast<const Phi*>(&r);
+            if (act) {
+                const double dt = r.dt;
+                // the velocity / position sums (integrationProcess, the order of preint_kernel)
+                double dvel[3];
+                if (!earth) {
+                    for (int i = 0; i < 3; ++i) dvel[i] = r.a[i] + g3[i] * dt;
+                } else {
+                    double cc3[3], dvcg[3];
+                    cross3(iewn, v, cc3);
+                    for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
+                    for (int i = 0; i < 3; ++i) dvel[i] = r.a[i] + dvcg[i];
+                }
+                for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
+                for (int i = 0; i < 3; ++i) v[i] += dvel[i];
+                if (pns && c == 0)
+                    *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
+                for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * r.b[i];
+                for (int i = 0; i < 3; ++i) dv[i] += r.b[i];
+                double y[NS];
+                phi_mv(f, Pc, y);
+                if (c < NS) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
+                }
+                phi_mv(f, Jc, y);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            }
+            __syncthreads();
+            if (act) {
+                const double a = 0.5 * f.dt;
+                const int cl = c < NS ? c : 0;
+                double K[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
+                if (c >= 3 && c < 6) {
+                    K[3] = K[3] + a * r.W[c - 3];
+                    K[4] = K[4] + a * r.W[3 + c - 3];
+                    K[5] = K[5] + a * r.W[6 + c - 3];
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i)
+                    if (i == c) K[i] = K[i] + a * wd(i);
+                const int r3 = c - 3, r6 = c - 6;
+                double ph[NS];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    ph[3 + b] = (c == b) ? f.dt : (c == 3 + b ? 1.0 : 0.0);
+                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
+                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
+                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
+                    ph[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
+                    ph[9 + b] = (c == 6 + b) ? -f.dt : (c == 9 + b ? f.f : 0.0);
+                    ph[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (c == 12 + b ? f.f : 0.0);
+                }
+                double y[NS];
+                phi_mv(f, K, y);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[i] = y[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    double u = r.W[3 * i] * ph[3];
+                    u = u + r.W[3 * i + 1] * ph[4];
+                    u = u + r.W[3 * i + 2] * ph[5];
+                    Pc[3 + i] = y[3 + i] + a * u;
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i) Pc[i] = y[i] + a * (wd(i) * ph[i]);
+            }
+            __syncthreads();
+        }
+    }
+    if (!live) return;
+    gvx_preint_result* o = out + seg;
+    if (c < NS) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            o->jacobian[i * NS + c] = Jc[i];
+            o->covariance[c * NS + i] = Pc[i];
+        }
+    }
+    if (c == 0)
+        for (int i = 0; i < 3; ++i) {
+            o->current.p[i] = p[i];
+            o->current.v[i] = v[i];
+            o->delta.p[i] = dp[i];
+            o->delta.v[i] = dv[i];
+        }
+}
+
 }  // namespace
 
 hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
@@ -863,10 +1076,16 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                                (const PreG*)pre, qr, out);
             hipLaunchKernelGGL(preint_rot_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, seg_off,
                                state0, (const PreG*)pre, (const QRec*)qr, rr);
-            // 8 lanes per segment in the covariance pass (16 measured 0.428 against
-            // 0.400 ms per 5,247 segments, r02 v17)
-            hipLaunchKernelGGL(preint_cov_kernel<8>, dim3((n_seg + 7) / 8), dim3(64), 0, c->stream, variant, prm,
-                               n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
+            // the covariance pass: 16 lanes per segment with the step blocks formed
+            // 16 steps at a time off the sequential chain (GVX_PREINT_COV8=1: the
+            // 8-lane kernel that forms them per step on every lane, for A/B)
+            const char* e8 = getenv("GVX_PREINT_COV8");
+            if (e8 && atoi(e8) != 0)
+                hipLaunchKernelGGL(preint_cov_kernel<8>, dim3((n_seg + 7) / 8), dim3(64), 0, c->stream, variant, prm,
+                                   n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
+            else
+                hipLaunchKernelGGL(preint_cov16_kernel, dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, variant, prm,
+                                   n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
             return hipGetLastError();
         }
     }

@@ -566,8 +566,11 @@ gvx_status gvx_marginalize_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres,
      S delta_f = bf - Hfe Hee^-1 be  by Cholesky,
      delta_e = Hee^-1 (be - Hef delta_f),     with b = -J^T r.
    Residual blocks and block table as gvx_marginalize (pose blocks of global size
-   7 contribute their local 6 columns, PoseParameterization's [I6; 0]); m and
-   L - m at most 512; J and r are what Ceres' linear solver sees (robust-loss
+   7 contribute their local 6 columns, PoseParameterization's [I6; 0]); L - m
+   at most 512, and m at most 512 unless Hee is diagonal -- every eliminated
+   block of local size 1 and no factor coupling two of them, the reference's
+   window of one inverse depth per landmark -- which any m may have (Hee's
+   Cholesky factor is then its square root); J and r are what Ceres' linear solver sees (robust-loss
    corrections applied).  D (nullable, L local parameters): the LM
    regularisation.  Outputs: delta [L] in local index order; S (nullable, r x r
    column-major, r = L - m) and info (nullable, 2 ints: 1 where the Cholesky

@@ -58,6 +58,19 @@ def test_schur_solve_matches_dense(ctx, window, name):
     _check(ctx.schur_solve(p), p, None, 1e-4)  # undamped (Gauss-Newton)
 
 
+def test_schur_solve_many_landmarks(ctx, orc):
+    """A window with 700 landmarks: m = 700 inverse depths, above the dense
+    Cholesky kernels' 512, taken by the diagonal-Hee path (one inverse depth per
+    landmark, each reprojection factor touching one: Hee's factor is its square
+    root) -- checked against the dense numpy solve like the windows above
+    (the LM step refused windows of more than 512 landmarks)."""
+    p = synth_ba.lm_problem(synth_ba.make_marg_problem(orc.FactorEvaluator(), seed=11, n_kf=10, n_lm=700))
+    assert p["m"] == 700
+    H, _ = synth_ba.dense_normal_equations(p)
+    D = np.sqrt(1e-4 * np.maximum(np.diag(H), 1e-6))
+    _check(ctx.schur_solve(p, D), p, D, 1e-9)
+
+
 def test_schur_solve_dev_matches_host(ctx, window):
     import torch
     p = window["prior over keyframes 0-8"]

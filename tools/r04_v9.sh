@@ -1,0 +1,12 @@
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; O=gpurun_out/r04_v9; mkdir -p $O
+# parity of the u8-table variant (the fused tests through GVX_LIB)
+GVX_LIB=$PWD/ic-gvins_amd/gvx/variants/libgvx_u8tab.so timeout -k 10 300 python -u -m pytest tests/test_clahe_fused_gpu.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for r in 1 2 3; do
+  for n in base u8tab; do
+    if [ $n = base ]; then L=""; else L=$PWD/ic-gvins_amd/gvx/variants/libgvx_$n.so; fi
+    GVX_CLAHE_FUSED1=1 GVX_LIB=$L timeout -k 10 120 python tools/clahe_ab.py > $O/${n}_$r.json
+    echo $n $(python3 -c "import json;print(round(json.load(open('$O/${n}_$r.json'))['ms_per_call'],4))")
+  done
+done
