@@ -225,6 +225,56 @@ class KltWorkload:
                                   self.P.data_ptr(), self.Q.data_ptr(), self.N.data_ptr(), self.B.data_ptr(),
                                   self.F.data_ptr(), self.K.data_ptr(), self.NK.data_ptr(), params=params)
 
+    # ---- the same steps software-pipelined: batch t+1's pyramid pass on a side
+    # branch beside batch t's LK (gvx_klt_batch_pyramids_dev / _pyr_dev, two
+    # pyramid slots).  k steps run k pyramid passes and k LK passes, the first
+    # pyramid pass alone and the last LK alone, so a timed run of k steps holds
+    # all of its work and nothing of the steps around it.
+    def _pyr_slots(self, ctx, max_level):
+        import torch
+        import gvx
+        if getattr(self, "_pyr_level", None) != max_level:
+            nb = 2 * self.n_pairs * gvx.pyramid_layout(self.w, self.h, max_level)["bytes"]
+            self._pyr = [torch.empty(nb, dtype=torch.uint8, device=self.I.device) for _ in range(2)]
+            self._pyr_level = max_level
+        return self._pyr
+
+    def build(self, ctx, params, slot):
+        pyr = self._pyr_slots(ctx, params.max_level)
+        ctx.klt_batch_pyramids_dev(self.n_pairs, self.w, self.h, self.I.data_ptr(), self.J.data_ptr(),
+                                   params.max_level, pyr[slot].data_ptr())
+
+    def track(self, ctx, params, slot):
+        pyr = self._pyr_slots(ctx, params.max_level)
+        ctx.klt_fb_batch_pyr_dev(self.n_pairs, self.w, self.h, self.I.data_ptr(), self.J.data_ptr(),
+                                 pyr[slot].data_ptr(), self.n, self.P.data_ptr(), self.Q.data_ptr(),
+                                 self.N.data_ptr(), self.B.data_ptr(), self.F.data_ptr(), self.K.data_ptr(),
+                                 self.NK.data_ptr(), params=params)
+
+    def run(self, ctx, params, k, pipelined, after_step=None):
+        """k steps; after_step() (if any) is called after each step's LK is enqueued."""
+        if not pipelined:
+            for _ in range(k):
+                self.step(ctx, params)
+                if after_step:
+                    after_step()
+            return
+        if k <= 0:
+            return
+        self.build(ctx, params, 0)
+        for t in range(k):
+            if t + 1 < k:
+                # the branch waits for everything before it, batch t-1's LK included,
+                # which read the slot it is about to overwrite
+                ctx.branch_begin()
+                self.build(ctx, params, (t + 1) & 1)
+                ctx.branch_end()
+            self.track(ctx, params, t & 1)
+            if t + 1 < k:
+                ctx.branch_join()
+            if after_step:
+                after_step()
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -265,6 +315,9 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="open the process group even at world size 1 (run under torch.distributed.run): the "
                          "collectives of --gather / configs[4] / max-over-ranks then go through RCCL")
+    ap.add_argument("--overlap", action="store_true",
+                    help="configs[1]/[2]: batch t+1's pyramid pass on a side stream beside batch t's LK (default: "
+                         "back to back; the overlap measured slower, DESIGN.md 8)")
     ap.add_argument("--accum", default="exact", choices=tuple(ACCUM_MODES),
                     help="LK window-sum order (gvx_klt_params.accum): exact integer sums (default), or "
                          "OpenCV 4.x's fp32 scalar-loop / CV_SIMD128 orders")
@@ -319,19 +372,22 @@ def main():
         else None
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if not args.no_pre else None
     t_side = time.perf_counter() - t_side
-    for _ in range(args.warmup):
-        step()
-        collect()
+    pipelined = args.overlap
+    wl.run(ctx, params, args.warmup, pipelined, collect)
     ctx.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     ctx.profile_reset()
     ctx.profile(True)
+    # HIP events on the context stream around the K steps: the device span of the
+    # whole pipeline (the side branch joins back into this stream every step)
+    cstream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        collect()
+    ev0.record(cstream)
+    wl.run(ctx, params, args.steps, pipelined, collect)
+    ev1.record(cstream)
     ctx.sync()
     torch.cuda.synchronize()
     if dist:
@@ -372,8 +428,8 @@ def main():
     value = total_pairs / elapsed
     ms_step = elapsed / args.steps * 1e3
     B = algorithmic_bytes(W, H, L, N)
-    dev_ms = sum(v[0] for v in fam.values()) / args.steps  # device time per step (all kernels)
-    achieved = B * Pn / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
+    span_ms = ev0.elapsed_time(ev1) / args.steps  # device span per step (all kernels, overlap included)
+    achieved = B * Pn / (span_ms * 1e-3) / 1e9 if span_ms > 0 else None
     workload = f"klt_fb_batch {Pn}x{W}x{H} N{N} L{L}"
     tr = traffic_for(workload)
 
@@ -413,14 +469,19 @@ def main():
             "config": {"workload": f"configs[{args.config - 1}]: batch of {Pn} frame pairs/GPU, {W}x{H} mono, {N} feat, "
                                    f"maxLevel {L}, win 21, fwd+bwd LK + FB + compaction",
                        "pairs_per_gpu_per_step": Pn, "parallelism": f"pairs sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "kernel": "klt pipeline (pyramid pass + LK/FB + compaction) per step",
+            "roofline": {"bound": "hbm",
+                         "kernel": ("klt pipeline per step: batch t+1's pyramid pass beside batch t's LK/FB + "
+                                    "compaction" if pipelined else
+                                    "klt pipeline (pyramid pass + LK/FB + compaction) per step"),
+                         "device_span_ms_per_step": round(span_ms, 4),
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": round(tr["bytes_per_step"]) if tr else None,
                          "traffic_unit": "HBM bytes per step (PMC 2*FETCH_SIZE+WRITE_SIZE)",
                          "traffic_source": tr["source"] if tr else None,
                          "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
-                         "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()}},
+                         "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()},
+                         "overlap": pipelined},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
             "lk_accum": args.accum,

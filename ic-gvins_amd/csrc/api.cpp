@@ -118,7 +118,9 @@ void prof_push(gvx_ctx* c, const char* fam, hipEvent_t a, hipEvent_t b) {
 
 void prof_drain(gvx_ctx* c) {
     if (c->pending.empty()) return;
-    hipStreamSynchronize(c->stream);
+    // events may sit on the context stream and on its branch stream
+    hipStreamSynchronize(c->main);
+    if (c->side) hipStreamSynchronize(c->side);
     for (auto& p : c->pending) {
         float ms = 0;
         hipEventElapsedTime(&ms, p.a, p.b);
@@ -523,31 +525,15 @@ gvx_status gvx_klt_fb(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, const floa
     return GVX_OK;
 }
 
-gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h,
-                                     const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
-                                     const float* d_prev_xy, const float* d_init_xy, float* d_next_xy,
-                                     float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
-                                     double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
-                                     const gvx_klt_params* p) {
-    if (!c) return GVX_ERR_INVALID;
-    gvx_status s = check_klt_params(c, p);
-    if (s) return s;
-    if (n_pairs < 0 || n_pts < 0 || w <= WIN || h <= WIN || !d_prev || !d_next)
-        return set_err(c, GVX_ERR_INVALID, "bad batch");
-    if (n_pairs == 0) return GVX_OK;
-    if (n_pts > 0 && (!d_prev_xy || !d_next_xy || !d_flags || !d_kept_idx || !d_n_kept))
-        return set_err(c, GVX_ERR_INVALID, "bad batch pointers");
-    hipSetDevice(c->device);
-    PyrLayout lay = make_layout(w, h, p->max_level, p->win);
-    uint8_t* pyr = (uint8_t*)scratch(c, "batch_pyr", (size_t)lay.bytes * 2 * n_pairs);
-    if (!pyr) return set_err(c, GVX_ERR_OOM, "batch pyramids (%lld bytes)", (long long)lay.bytes * 2 * n_pairs);
-    uint8_t* pyr_prev = pyr;
-    uint8_t* pyr_next = pyr + (size_t)lay.bytes * n_pairs;
-    // level 0 stays in the caller's images; levels >= 1 go to the pyramid slots
-    // one launch for both frames of every pair (pyr_next follows pyr_prev)
-    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, 2 * n_pairs, lay, pyr_prev, false, d_next,
-                                         n_pairs);
-    if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
+// LK / FB + compaction of a batch over built pyramids (levels >= 1 at pyr_prev /
+// pyr_next + i * lay.bytes; level 0 read in place from the caller's images).
+static gvx_status klt_batch_on_pyramids(gvx_ctx* c, const PyrLayout& lay, int32_t n_pairs, int32_t w, int32_t h,
+                                        const uint8_t* d_prev, const uint8_t* d_next, const uint8_t* pyr_prev,
+                                        const uint8_t* pyr_next, int32_t n_pts, const float* d_prev_xy,
+                                        const float* d_init_xy, float* d_next_xy, float* d_back_xy, uint8_t* d_flags,
+                                        int32_t* d_kept_idx, int32_t* d_n_kept, double fb_thresh, double border,
+                                        int32_t cam_w, int32_t cam_h, const gvx_klt_params* p) {
+    hipError_t e;
     if (n_pts == 0) {
         e = hipMemsetAsync(d_n_kept, 0, sizeof(int32_t) * n_pairs, c->stream);
         return hip_err(c, e, "memset n_kept");
@@ -569,6 +555,78 @@ gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int
     if (e != hipSuccess) return hip_err(c, e, "klt kernel");
     e = launch_compact(c, n_pairs, n_pts, d_flags, d_kept_idx, d_n_kept);
     return hip_err(c, e, "compact kernel");
+}
+
+static gvx_status check_batch(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* d_prev,
+                              const uint8_t* d_next, int32_t n_pts, const float* d_prev_xy, float* d_next_xy,
+                              uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept) {
+    if (n_pairs < 0 || n_pts < 0 || w <= WIN || h <= WIN || !d_prev || !d_next)
+        return set_err(c, GVX_ERR_INVALID, "bad batch");
+    if (n_pts > 0 && (!d_prev_xy || !d_next_xy || !d_flags || !d_kept_idx || !d_n_kept))
+        return set_err(c, GVX_ERR_INVALID, "bad batch pointers");
+    return GVX_OK;
+}
+
+gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h,
+                                     const uint8_t* d_prev, const uint8_t* d_next, int32_t n_pts,
+                                     const float* d_prev_xy, const float* d_init_xy, float* d_next_xy,
+                                     float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                     double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                     const gvx_klt_params* p) {
+    if (!c) return GVX_ERR_INVALID;
+    gvx_status s = check_klt_params(c, p);
+    if (s) return s;
+    s = check_batch(c, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_flags, d_kept_idx, d_n_kept);
+    if (s) return s;
+    if (n_pairs == 0) return GVX_OK;
+    hipSetDevice(c->device);
+    PyrLayout lay = make_layout(w, h, p->max_level, p->win);
+    uint8_t* pyr = (uint8_t*)scratch(c, "batch_pyr", (size_t)lay.bytes * 2 * n_pairs);
+    if (!pyr) return set_err(c, GVX_ERR_OOM, "batch pyramids (%lld bytes)", (long long)lay.bytes * 2 * n_pairs);
+    uint8_t* pyr_prev = pyr;
+    uint8_t* pyr_next = pyr + (size_t)lay.bytes * n_pairs;
+    // level 0 stays in the caller's images; levels >= 1 go to the pyramid slots
+    // one launch for both frames of every pair (pyr_next follows pyr_prev)
+    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, 2 * n_pairs, lay, pyr_prev, false, d_next,
+                                         n_pairs);
+    if (e != hipSuccess) return hip_err(c, e, "pyramid kernels");
+    return klt_batch_on_pyramids(c, lay, n_pairs, w, h, d_prev, d_next, pyr_prev, pyr_next, n_pts, d_prev_xy,
+                                 d_init_xy, d_next_xy, d_back_xy, d_flags, d_kept_idx, d_n_kept, fb_thresh, border,
+                                 cam_w, cam_h, p);
+}
+
+gvx_status gvx_klt_batch_pyramids_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* d_prev,
+                                      const uint8_t* d_next, int32_t max_level, uint8_t* d_pyr) {
+    if (!c) return GVX_ERR_INVALID;
+    if (n_pairs < 0 || w <= WIN || h <= WIN || max_level < 0 || max_level >= MAX_LEVELS)
+        return set_err(c, GVX_ERR_INVALID, "bad pyramid batch");
+    if (n_pairs == 0) return GVX_OK;
+    if (!d_prev || !d_next || !d_pyr) return set_err(c, GVX_ERR_INVALID, "bad pyramid batch pointers");
+    hipSetDevice(c->device);
+    const PyrLayout lay = make_layout(w, h, max_level, WIN);
+    hipError_t e = launch_build_pyramids(c, d_prev, (int64_t)w * h, w, 2 * n_pairs, lay, d_pyr, false, d_next,
+                                         n_pairs);
+    return hip_err(c, e, "pyramid kernels");
+}
+
+gvx_status gvx_klt_fb_batch_pyr_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* d_prev,
+                                    const uint8_t* d_next, const uint8_t* d_pyr, int32_t n_pts,
+                                    const float* d_prev_xy, const float* d_init_xy, float* d_next_xy,
+                                    float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                    double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                    const gvx_klt_params* p) {
+    if (!c) return GVX_ERR_INVALID;
+    gvx_status s = check_klt_params(c, p);
+    if (s) return s;
+    s = check_batch(c, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_flags, d_kept_idx, d_n_kept);
+    if (s) return s;
+    if (n_pairs == 0) return GVX_OK;
+    if (!d_pyr) return set_err(c, GVX_ERR_INVALID, "bad batch pyramids");
+    hipSetDevice(c->device);
+    const PyrLayout lay = make_layout(w, h, p->max_level, p->win);
+    return klt_batch_on_pyramids(c, lay, n_pairs, w, h, d_prev, d_next, d_pyr, d_pyr + (size_t)lay.bytes * n_pairs,
+                                 n_pts, d_prev_xy, d_init_xy, d_next_xy, d_back_xy, d_flags, d_kept_idx, d_n_kept,
+                                 fb_thresh, border, cam_w, cam_h, p);
 }
 
 gvx_status gvx_klt_fb_batch_dev(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h,

@@ -124,7 +124,7 @@ gvx_status gvx_copy_dev(gvx_ctx* c, void* d_dst, const void* d_src, size_t bytes
 gvx_status gvx_branch_begin(gvx_ctx* c) {
     if (!c) return GVX_ERR_INVALID;
     if (c->in_branch || c->branch_open) return set_err(c, GVX_ERR_INVALID, "a branch is already open");
-    if (c->prof) return set_err(c, GVX_ERR_INVALID, "disable profiling before branching");
+    if (c->prof && c->capturing) return set_err(c, GVX_ERR_INVALID, "disable profiling before branching");
     hipSetDevice(c->device);
     if (!c->side) {
         if (c->capturing) return set_err(c, GVX_ERR_INVALID, "open a first branch outside a capture");

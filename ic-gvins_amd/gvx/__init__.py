@@ -181,6 +181,9 @@ def _declare(L):
                                             i32, C.POINTER(KltParams)]),
         "gvx_klt_fb_batch": (i32, [P, i32, i32, i32, P, P, i32, P, P, P, P, P, P, f64, f64, i32, i32,
                                    C.POINTER(KltParams)]),
+        "gvx_klt_batch_pyramids_dev": (i32, [P, i32, i32, i32, P, P, i32, P]),
+        "gvx_klt_fb_batch_pyr_dev": (i32, [P, i32, i32, i32, P, P, P, i32, P, P, P, P, P, P, P, f64, f64, i32,
+                                           i32, C.POINTER(KltParams)]),
         "gvx_preint_integrate": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
         "gvx_preint_integrate_dev": (i32, [P, i32, C.POINTER(ImuParams), i32, P, P, P, P, P, P]),
         "gvx_earth_iewn": (None, [P, P, P]),
@@ -695,6 +698,22 @@ class Context:
                                                       d_init_xy, d_next_xy, d_back_xy, d_flags, d_kept, d_nkept,
                                                       fb_thresh, border, cam_w or w, cam_h or h, C.byref(p)),
                     "gvx_klt_fb_batch_init_dev")
+
+    def klt_batch_pyramids_dev(self, n_pairs, w, h, d_prev, d_next, max_level, d_pyr):
+        """gvx_klt_batch_pyramids_dev: levels >= 1 of the prev then next images of a
+        batch into d_pyr (2 * n_pairs * pyramid_layout(w, h, max_level)["bytes"])."""
+        self._check(self._L.gvx_klt_batch_pyramids_dev(self._h, n_pairs, w, h, d_prev, d_next, max_level, d_pyr),
+                    "gvx_klt_batch_pyramids_dev")
+
+    def klt_fb_batch_pyr_dev(self, n_pairs, w, h, d_prev, d_next, d_pyr, n_pts, d_prev_xy, d_init_xy, d_next_xy,
+                             d_back_xy, d_flags, d_kept, d_nkept, cam_w=None, cam_h=None, fb_thresh=0.5,
+                             border=5.0, params: Optional[KltParams] = None):
+        """klt_fb_batch_init_dev over pyramids built by klt_batch_pyramids_dev."""
+        p = params or KltParams.default()
+        self._check(self._L.gvx_klt_fb_batch_pyr_dev(self._h, n_pairs, w, h, d_prev, d_next, d_pyr, n_pts,
+                                                     d_prev_xy, d_init_xy, d_next_xy, d_back_xy, d_flags, d_kept,
+                                                     d_nkept, fb_thresh, border, cam_w or w, cam_h or h,
+                                                     C.byref(p)), "gvx_klt_fb_batch_pyr_dev")
 
     def klt_fb_batch_dev(self, n_pairs, w, h, d_prev, d_next, n_pts, d_prev_xy, d_next_xy, d_back_xy,
                          d_flags, d_kept, d_nkept, cam_w=None, cam_h=None, fb_thresh=0.5, border=5.0,

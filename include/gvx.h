@@ -179,6 +179,24 @@ gvx_status gvx_klt_fb_batch_init_dev(gvx_ctx* ctx, int32_t n_pairs, int32_t w, i
                                      float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
                                      double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
                                      const gvx_klt_params* p);
+/* The batch unit in its two halves, buildOpticalFlowPyramid and
+   calcOpticalFlowPyrLK on the built pyramids (the split OpenCV itself offers), so
+   a caller can build batch t+1's pyramids on a gvx_branch beside batch t's LK:
+   gvx_klt_batch_pyramids_dev builds levels >= 1 of the 2 * n_pairs images (prev
+   images first, then next) into d_pyr (2 * n_pairs * bytes of gvx_pyramid_layout(w,
+   h, max_level), image i at d_pyr + i * bytes); gvx_klt_fb_batch_pyr_dev is
+   gvx_klt_fb_batch_init_dev over them.  Level 0 is read from d_prev / d_next in
+   both, so those images must stay unchanged until the LK has run, and d_pyr must
+   have been built from them with the same n_pairs, w, h and p->max_level.  The
+   results are those of gvx_klt_fb_batch_init_dev (the same kernels). */
+gvx_status gvx_klt_batch_pyramids_dev(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* d_prev,
+                                      const uint8_t* d_next, int32_t max_level, uint8_t* d_pyr);
+gvx_status gvx_klt_fb_batch_pyr_dev(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* d_prev,
+                                    const uint8_t* d_next, const uint8_t* d_pyr, int32_t n_pts,
+                                    const float* d_prev_xy, const float* d_init_xy, float* d_next_xy,
+                                    float* d_back_xy, uint8_t* d_flags, int32_t* d_kept_idx, int32_t* d_n_kept,
+                                    double fb_thresh, double border, int32_t cam_w, int32_t cam_h,
+                                    const gvx_klt_params* p);
 /* Host-pointer convenience wrapper of the above (copies in and out, synchronous). */
 gvx_status gvx_klt_fb_batch(gvx_ctx* ctx, int32_t n_pairs, int32_t w, int32_t h,
                             const uint8_t* prev, const uint8_t* next, int32_t n_pts,

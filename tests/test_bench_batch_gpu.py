@@ -75,3 +75,34 @@ def test_bench_launch_bit_exact(ctx, orc, gvx_mod, w, h, n, L, mode):
             assert nk[i] == len(o["kept_idx"]), f"pair {i} n_kept {nk[i]} vs {len(o['kept_idx'])}"
             _assert_same(kept[i][:nk[i]], o["kept_idx"], f"pair {i} kept_idx")
             assert nk[i] > 0.9 * n  # the synthetic pairs track
+
+
+@pytest.mark.parametrize("w,h,n,L", CONFIGS[:1])
+def test_bench_pipelined_run_equals_step(ctx, gvx_mod, w, h, n, L):
+    """The headline's software-pipelined steps (bench.KltWorkload.run: batch t+1's
+    pyramid pass on a side branch beside batch t's LK, gvx_klt_batch_pyramids_dev +
+    gvx_klt_fb_batch_pyr_dev, two pyramid slots) give the bits of the single
+    launch checked against the oracle above, after every one of k steps."""
+    import torch
+    wl = _workload(w, h, n)
+    p = gvx_mod.KltParams.default(max_level=L)
+    wl.step(ctx, p)
+    ctx.sync()
+    ref = [t.cpu().numpy() for t in (wl.N, wl.B, wl.F, wl.K, wl.NK)]
+    seen = []
+
+    def check():
+        ctx.sync()
+        got = [t.cpu().numpy() for t in (wl.N, wl.B, wl.F, wl.K, wl.NK)]
+        for name, a, b in zip(("next", "back", "flags", "kept_idx", "n_kept"), got, ref):
+            _assert_same(a, b, f"pipelined step {len(seen)} {name}")
+        seen.append(1)
+        for t in (wl.N, wl.B):
+            t.fill_(np.nan)
+        wl.NK.fill_(-1)
+        torch.cuda.synchronize()  # the fills (torch's stream) land before the next LK (the context's)
+
+    wl.run(ctx, p, 5, True, check)
+    assert len(seen) == 5
+    lay = gvx_mod.pyramid_layout(w, h, L)
+    assert wl._pyr[0].numel() == 2 * wl.n_pairs * lay["bytes"]
