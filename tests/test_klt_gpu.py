@@ -215,3 +215,34 @@ def test_batch_two_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
         flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
         _assert_same(g["flags"][i], flags, f"pair {i} flags")
         _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
+
+
+def test_split_batch_entry_points_validate(ctx, gvx_mod):
+    """gvx_klt_batch_pyramids_dev / gvx_klt_fb_batch_pyr_dev refuse what the one-call
+    batch refuses (bad sizes, missing buffers) plus a missing pyramid buffer, and a
+    zero-pair call is a no-op."""
+    import torch
+    dev = torch.device("cuda", 0)
+    W, H = 64, 48
+    img = torch.zeros((1, H, W), dtype=torch.uint8, device=dev)
+    pyr = torch.zeros(2 * gvx_mod.pyramid_layout(W, H, 3)["bytes"], dtype=torch.uint8, device=dev)
+    pts = torch.zeros((1, 4, 2), dtype=torch.float32, device=dev)
+    flags = torch.zeros((1, 4), dtype=torch.uint8, device=dev)
+    kept = torch.zeros((1, 4), dtype=torch.int32, device=dev)
+    nk = torch.zeros((1,), dtype=torch.int32, device=dev)
+    p = gvx_mod.KltParams.default(max_level=3)
+    with pytest.raises(gvx_mod.GvxError):
+        ctx.klt_batch_pyramids_dev(1, 16, H, img.data_ptr(), img.data_ptr(), 3, pyr.data_ptr())  # w <= win
+    with pytest.raises(gvx_mod.GvxError):
+        ctx.klt_batch_pyramids_dev(1, W, H, img.data_ptr(), img.data_ptr(), 3, 0)
+    with pytest.raises(gvx_mod.GvxError):
+        ctx.klt_fb_batch_pyr_dev(1, W, H, img.data_ptr(), img.data_ptr(), 0, 4, pts.data_ptr(), pts.data_ptr(),
+                                 pts.data_ptr(), pts.data_ptr(), flags.data_ptr(), kept.data_ptr(), nk.data_ptr(),
+                                 params=p)
+    with pytest.raises(gvx_mod.GvxError):
+        ctx.klt_fb_batch_pyr_dev(1, W, H, img.data_ptr(), img.data_ptr(), pyr.data_ptr(), 4, pts.data_ptr(),
+                                 pts.data_ptr(), 0, pts.data_ptr(), flags.data_ptr(), kept.data_ptr(), nk.data_ptr(),
+                                 params=p)
+    ctx.klt_batch_pyramids_dev(0, W, H, 0, 0, 3, 0)
+    ctx.klt_fb_batch_pyr_dev(0, W, H, img.data_ptr(), img.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0, 0, params=p)
+    ctx.sync()
