@@ -16,6 +16,8 @@
 // rotation-vector exponentials and the fused multiply-adds of phi_mv.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 
 #include "dmath.h"
@@ -26,6 +28,35 @@ namespace gvx {
 namespace {
 
 constexpr int NS = 15;
+
+// q / |q| through one reciprocal square root (v_rsq_f64 and two fused Newton
+// steps) instead of a square root and four divisions: within an ulp or two of
+// Eigen's normalized(), and a shorter dependent chain for the quaternion
+// recursions (their contract is 1e-10 relative)
+__device__ __forceinline__ dq dq_renorm(dq q) {
+    const double n2 = dq_sqnorm(q);
+    if (n2 > 0) {
+        double y = __builtin_amdgcn_rsq(n2);
+        double e = __builtin_fma(-n2 * y, y, 1.0);
+        y = __builtin_fma(0.5 * y, e, y);
+        e = __builtin_fma(-n2 * y, y, 1.0);
+        y = __builtin_fma(0.5 * y, e, y);
+        q.x *= y;
+        q.y *= y;
+        q.z *= y;
+        q.w *= y;
+    }
+    return q;
+}
+
+// Every kernel below is one wavefront per workgroup: its LDS traffic is in order
+// within the wave, so a step's hand-over through LDS needs a compiler fence, not
+// s_barrier and the lgkmcnt(0) drain in front of it.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 struct Imu {
     double dt, dth[3], dv[3], time;
@@ -93,6 +124,24 @@ __device__ __forceinline__ void phi_mv(const Phi& f, const double* v, double* y)
     }
 #pragma unroll
     for (int i = 9; i < NS; ++i) y[i] = f.f * v[i];
+}
+
+// P'(:,c) = Phi K + a W phi_c for rows 3..14 (rows 0..2 have no Q term): the
+// W(3:6,3:6) block times phi_c(3:6) and the constant diagonal of W from row 6 on
+// (wg, nbg, nba), multiply-adds fused.  Shared by every covariance kernel so
+// their outputs stay the same bits.
+__device__ __forceinline__ void q_terms(double a, const double* W, double wg, double nbg, double nba,
+                                        const double* ph, const double* y, double* P) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double u = W[3 * i] * ph[3];
+        u = __builtin_fma(W[3 * i + 1], ph[4], u);
+        u = __builtin_fma(W[3 * i + 2], ph[5], u);
+        P[3 + i] = __builtin_fma(a, u, y[3 + i]);
+    }
+    const double ag = a * wg, abg = a * nbg, aba = a * nba;
+#pragma unroll
+    for (int i = 6; i < 15; ++i) P[i] = __builtin_fma(i < 9 ? ag : (i < 12 ? abg : aba), ph[i], y[i]);
 }
 
 constexpr int GL = 16;                  // lanes per segment: lane c owns column c of J and row c of P
@@ -204,7 +253,7 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
                 for (int i = 0; i < PRE_DW; ++i) dst[i] = w[i];
             }
         }
-        __syncthreads();
+        wave_lds_sync();
         const int kend = min(kc + CH, mmax);
         for (int k = kc; k < kend; ++k) {
             const bool act = k < m;
@@ -223,12 +272,12 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
                     for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + g3[i] * dt;
                     for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
                     for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
-                    dq_store(dq_normalized(dq_mul(dq_load(cur.q), qd)), cur.q);
+                    dq_store(dq_renorm(dq_mul(dq_load(cur.q), qd)), cur.q);
                     dq_rot(dqt, R);
                     mv3(R, sp.dvfb, dvel);
                     for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
                     for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
-                    dqt = dq_normalized(dq_mul(dqt, qd));
+                    dqt = dq_renorm(dq_mul(dqt, qd));
                     dq_rot(dqt, R);
                     for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
                 } else {
@@ -250,12 +299,12 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
                         pns[4 * (k - 1) + 2] = cur.p[1];
                         pns[4 * (k - 1) + 3] = cur.p[2];
                     }
-                    dq_store(dq_normalized(dq_mul(dq_mul(dq_load(sp.qnn), dq_load(cur.q)), qd)), cur.q);
+                    dq_store(dq_renorm(dq_mul(dq_mul(dq_load(sp.qnn), dq_load(cur.q)), qd)), cur.q);
                     dq_rot(dq_mul(dq_load(sp.qa), dqt), R);
                     mv3(R, sp.dvfb, dvel);
                     for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
                     for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
-                    dqt = dq_normalized(dq_mul(dqt, qd));
+                    dqt = dq_renorm(dq_mul(dqt, qd));
                     dq_rot(dq_mul(dq_load(sp.qb), dqt), R);
                     for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
                 }
@@ -291,7 +340,7 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
 #pragma unroll
                 for (int i = 0; i < NS; ++i) Jc[i] = y[i];
             }
-            __syncthreads();
+            wave_lds_sync();
             if (act) {
                 const double a = 0.5 * f.dt;
                 const int cl = c < NS ? c : 0;
@@ -325,17 +374,9 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
                 phi_mv(f, K, y);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Pc[i] = y[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    double u = Wv[3 * i] * ph[3];
-                    u = u + Wv[3 * i + 1] * ph[4];
-                    u = u + Wv[3 * i + 2] * ph[5];
-                    Pc[3 + i] = y[3 + i] + a * u;
-                }
-#pragma unroll
-                for (int i = 6; i < NS; ++i) Pc[i] = y[i] + a * (wd(i) * ph[i]);
+                q_terms(a, Wv, wg, nbg, nba, ph, y, Pc);
             }
-            __syncthreads();
+            wave_lds_sync();
         }
     }
 
@@ -534,9 +575,9 @@ __global__ void __launch_bounds__(128) preint_chain_kernel(gvx_imu_params prm, i
     auto step = [&](int k, const double (&r)[8]) {
         const dq qd = dq_load(r);
         if (two)
-            q = dq_normalized(dq_mul(dq_mul(dq_load(r + 4), q), qd));
+            q = dq_renorm(dq_mul(dq_mul(dq_load(r + 4), q), qd));
         else  // Normal cur.q, and dqt in both variants
-            q = dq_normalized(dq_mul(q, qd));
+            q = dq_renorm(dq_mul(q, qd));
         *reinterpret_cast<double4*>(qs + (size_t)(k - 1) * 8) = double4{q.x, q.y, q.z, q.w};
     };
     double X[CK][8], Y[CK][8];
@@ -579,10 +620,10 @@ __global__ void __launch_bounds__(64) preint_rot_kernel(int variant, int n_seg, 
                                                         const gvx_state* __restrict__ state0,
                                                         const PreG* __restrict__ pre,
                                                         const QRec* __restrict__ qrec, RRec* __restrict__ rrec) {
-    const int seg = blockIdx.x;
+    const bool earth = variant == GVX_PREINT_EARTH;
+    for (int seg = blockIdx.x; seg < n_seg; seg += gridDim.x) {  // waves loop over segments
     const int b0 = seg_off[seg];
     const int m = seg_off[seg + 1] - b0;
-    const bool earth = variant == GVX_PREINT_EARTH;
     const size_t o0 = (size_t)(b0 - seg);
     for (int k = 1 + threadIdx.x; k < m; k += 64) {
         const PreG& g = pre[o0 + k - 1];
@@ -615,6 +656,7 @@ __global__ void __launch_bounds__(64) preint_rot_kernel(int variant, int n_seg, 
         const double* w = reinterpret_cast<const double*>(&r);
 #pragma unroll
         for (int i = 0; i < RREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+    }
     }
 }
 
@@ -702,7 +744,7 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
 #pragma unroll
         for (int q = 0; q < LPL; ++q) x0[q] = x1[q];
         fetch(k + 2, x1);
-        __syncthreads();
+        wave_lds_sync();
         Phi f;
         double Wv[9];
         if (act) {
@@ -766,7 +808,7 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
                 for (int i = 0; i < NS; ++i) Jc[j][i] = y[i];
             }
         }
-        __syncthreads();
+        wave_lds_sync();
         if (act) {
             const double a = 0.5 * f.dt;
 #pragma unroll
@@ -800,15 +842,7 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
                 phi_mv(f, K, y);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Pc[j][i] = y[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    double u = Wv[3 * i] * phr[3];
-                    u = u + Wv[3 * i + 1] * phr[4];
-                    u = u + Wv[3 * i + 2] * phr[5];
-                    Pc[j][3 + i] = y[3 + i] + a * u;
-                }
-#pragma unroll
-                for (int i = 6; i < NS; ++i) Pc[j][i] = y[i] + a * (wd(i) * phr[i]);
+                q_terms(a, Wv, wg, nbg, nba, phr, y, Pc[j]);
             }
         }
     }
@@ -835,7 +869,7 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
 }
 
 // preint_cov_kernel with the step's Phi / W blocks off the sequential path:
-// 16 lanes per segment (lane c owns column c of J and row c of P), and every 16
+// 16 lanes per segment (lane c owns column c of J and row c of P), and every 8
 // steps each lane of a segment's group forms ONE step's blocks -- the bias-
 // compensated sample, C = cbb0 skew(dv), D = cbb0 dt, W = gR N_v gR^T, the
 // RRec's rotated increments -- into LDS (StepRec), so the per-step chain keeps
@@ -845,15 +879,26 @@ __global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_par
 // (tests/test_ba_gpu.py::test_preint_two_phase_bits_equal_one_phase).  The
 // 8-lane kernel above spent ~6.5 k cycles per step on one wave per SIMD (656
 // waves for 5,247 segments), most of them the per-lane scalar chain.
+// r04: row c of Phi is read from the record at a lane-dependent offset (no
+// selects), K's Q terms are LDS adds into the transpose (q_terms fuses the
+// rest) and the steps hand over through LDS with a wave fence, not s_barrier:
+// 321 -> 221 VALU instructions per step, but only 3-5 % of the launch -- the step
+// is bound by its dependent latency (PMC r04 v14: VALU active 30 % of a wave's
+// cycles at 1.3 waves per SIMD; timing probes: the record phases' loads 16 us,
+// the record phases altogether 24 us of ~240, profiles/r04_v17/).
 struct StepRec {
     double dt, f;             // Phi's scalars (the layout of Phi, so phi_mv reads it in place)
     double C[9], D[9], M[9];  // Phi(3:6, 6:9), Phi(3:6, 12:15), Phi(6:9, 6:9) = I - skew(dtheta)
     double W[9];              // W(3:6, 3:6)
     double a[3], b[3];        // RRec's velocity / delta-velocity increments
+    // row c of Phi, read by lane c at a lane-dependent offset instead of selected:
+    // S = {0,0,dt,0,0,f,0,0,-dt,0,0} (rows of dt I, f I, -dt I at 2-j, 5-j, 8-j),
+    // S1 = {0,0,1,0,0} (rows of I), Z = zeros
+    double S[11], S1[5], Z[3], pad;
 };
 static_assert(sizeof(Phi) == 29 * 8, "Phi is StepRec's prefix");
-constexpr int SREC_DW = sizeof(StepRec) / 8;  // 44
-constexpr int C16_CK = 8;  // steps per record chunk (one per lane of half a group): 18.5 KB of LDS per
+constexpr int SREC_DW = sizeof(StepRec) / 8;  // 64
+constexpr int C16_CK = 8;  // steps per record chunk (one per lane of half a group): 23.6 KB of LDS per
                            // wave, so every wave of a 5,247-segment batch is resident at once
 
 __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_params prm, int n_seg,
@@ -897,6 +942,13 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
     const double g60 = earth ? -1.0 : 1.0;
     const double wg = (g60 * ngyr) * g60;
     auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    const double wdc = wd(c);
+    constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
+    constexpr int oS = offsetof(StepRec, S) / 8, oS1 = offsetof(StepRec, S1) / 8, oZ = offsetof(StepRec, Z) / 8;
+    const int ph3 = c < 3 ? oS + 2 - c : (c < 6 ? oS1 + 2 - (c - 3) : oZ);
+    const int ph6 = (c >= 3 && c < 6) ? oC + 3 * (c - 3) : ((c >= 6 && c < 9) ? oM + 3 * (c - 6) : oZ);
+    const int ph9 = (c >= 6 && c < 9) ? oS + 8 - (c - 6) : ((c >= 9 && c < 12) ? oS + 5 - (c - 9) : oZ);
+    const int ph12 = (c >= 3 && c < 6) ? oD + 3 * (c - 3) : ((c >= 12 && c < NS) ? oS + 5 - (c - 12) : oZ);
     double Jc[NS], Pc[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -943,13 +995,23 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
                 for (int i = 0; i < 9; ++i) r.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
                 r.dt = dt;
                 r.f = 1 - dt / prm.corr_time;
+#pragma unroll
+                for (int i = 0; i < 11; ++i) r.S[i] = 0.0;
+                r.S[2] = dt;
+                r.S[5] = r.f;
+                r.S[8] = -dt;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) r.S1[i] = i == 2 ? 1.0 : 0.0;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) r.Z[i] = 0.0;
+                r.pad = 0.0;
                 double* dst = reinterpret_cast<double*>(&sR[grp][c]);
                 const double* w = reinterpret_cast<const double*>(&r);
 #pragma unroll
                 for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
             }
         }
-        __syncthreads();
+        wave_lds_sync();
         const int kend = min(kc + C16_CK, mmax);
         for (int k = kc; k < kend; ++k) {
             const bool act = k < m;
@@ -981,52 +1043,48 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
 #pragma unroll
                     for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
                 }
+                // K's Q terms added where K is read from (LDS add after this lane's
+                // own column write; the same fp64 add as K[i] + a*w): the W block for
+                // lanes 3..5, the diagonal for lanes 6..14
+                {
+                    const double a = 0.5 * f.dt;
+                    if (c >= 3 && c < 6) {
+#pragma unroll
+                        for (int j = 0; j < 3; ++j)
+                            __hip_atomic_fetch_add(&sG[grp][(3 + j) * NS + c], a * r.W[3 * j + c - 3],
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else if (c >= 6 && c < NS) {
+                        __hip_atomic_fetch_add(&sG[grp][c * NS + c], a * wdc, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
                 phi_mv(f, Jc, y);
 #pragma unroll
                 for (int i = 0; i < NS; ++i) Jc[i] = y[i];
             }
-            __syncthreads();
+            wave_lds_sync();
             if (act) {
                 const double a = 0.5 * f.dt;
                 const int cl = c < NS ? c : 0;
                 double K[NS];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
-                if (c >= 3 && c < 6) {
-                    K[3] = K[3] + a * r.W[c - 3];
-                    K[4] = K[4] + a * r.W[3 + c - 3];
-                    K[5] = K[5] + a * r.W[6 + c - 3];
-                }
-#pragma unroll
-                for (int i = 6; i < NS; ++i)
-                    if (i == c) K[i] = K[i] + a * wd(i);
-                const int r3 = c - 3, r6 = c - 6;
+                const double* rw = reinterpret_cast<const double*>(&r);
                 double ph[NS];
 #pragma unroll
                 for (int b = 0; b < 3; ++b) {
-                    ph[3 + b] = (c == b) ? f.dt : (c == 3 + b ? 1.0 : 0.0);
-                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
-                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
-                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
-                    ph[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
-                    ph[9 + b] = (c == 6 + b) ? -f.dt : (c == 9 + b ? f.f : 0.0);
-                    ph[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (c == 12 + b ? f.f : 0.0);
+                    ph[3 + b] = rw[ph3 + b];
+                    ph[6 + b] = rw[ph6 + b];
+                    ph[9 + b] = rw[ph9 + b];
+                    ph[12 + b] = rw[ph12 + b];
                 }
                 double y[NS];
                 phi_mv(f, K, y);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Pc[i] = y[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    double u = r.W[3 * i] * ph[3];
-                    u = u + r.W[3 * i + 1] * ph[4];
-                    u = u + r.W[3 * i + 2] * ph[5];
-                    Pc[3 + i] = y[3 + i] + a * u;
-                }
-#pragma unroll
-                for (int i = 6; i < NS; ++i) Pc[i] = y[i] + a * (wd(i) * ph[i]);
+                q_terms(a, r.W, wg, nbg, nba, ph, y, Pc);
             }
-            __syncthreads();
+            wave_lds_sync();
         }
     }
     if (!live) return;
@@ -1076,7 +1134,7 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
             hipLaunchKernelGGL(variant == GVX_PREINT_EARTH ? preint_chain_kernel<true> : preint_chain_kernel<false>,
                                dim3((n_seg + 63) / 64), dim3(128), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
                                (const PreG*)pre, qr, out);
-            hipLaunchKernelGGL(preint_rot_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, seg_off,
+            hipLaunchKernelGGL(preint_rot_kernel, dim3(std::min(n_seg, c->n_cu * 8)), dim3(64), 0, c->stream, variant, n_seg, seg_off,
                                state0, (const PreG*)pre, (const QRec*)qr, rr);
             // the covariance pass: 16 lanes per segment with the step blocks formed
             // 16 steps at a time off the sequential chain (GVX_PREINT_COV8=1: the
