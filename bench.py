@@ -217,7 +217,8 @@ class KltWorkload:
         self.F = torch.empty((n_pairs, n), dtype=torch.uint8, device=dev)
         self.K = torch.empty((n_pairs, n), dtype=torch.int32, device=dev)
         self.NK = torch.empty((n_pairs,), dtype=torch.int32, device=dev)
-        torch.cuda.synchronize()
+        if self.I.is_cuda:
+            torch.cuda.synchronize()
 
     def step(self, ctx, params):
         # initial flow (the predictions) read from Q, tracked points out to N
