@@ -298,12 +298,30 @@ struct DownLevels {
 // columns of some level's side bands.  Both are wave-uniform, so the kernel
 // branches once into one of three instances and the loop has no per-row path
 // choice (loads stay in flight across iterations).
+// Buffer stores at 32-bit offsets into one image's pyramid (stream_walk).
+constexpr int GVX_OOB = 0x7fffffff;  // past every pyramid: the store is dropped
+__device__ __forceinline__ void st_b32(__amdgpu_buffer_rsrc_t rs, int off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs, off, 0, 0);
+}
+__device__ __forceinline__ void st_b16(__amdgpu_buffer_rsrc_t rs, int off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, rs, off, 0, 0);
+}
+__device__ __forceinline__ void st_b8(__amdgpu_buffer_rsrc_t rs, int off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, rs, off, 0, 0);
+}
+
 template <int NL, bool GATHER, bool SIDES, int SKIP>
 __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                             const DownLevels& L, int st, int bd, int img, int band, int lane,
                                             uint8_t* __restrict__ tl, bool side1, bool side2, bool side3) {
     const uint8_t* S = img < src.n_a ? src.a + img * src.img_stride : src.b + (img - src.n_a) * src.img_stride;
     uint8_t* P = pyr + img * pyr_bytes;
+    // interior strips store through a buffer view of the image's pyramid: lanes that
+    // own no output pass an offset past its end and the bounds check drops the store
+    // (no 64-bit address or trash select per store: 1,262 -> 655 VALU per 8 level-1
+    // rows); the edge-strip instances keep the flat stores, which fit their registers
+    constexpr bool BUF = !SIDES;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)pyr_bytes, 0x00020000);
     const int w0 = src.w, h0 = src.h, sp = src.pitch;
     const int x0 = ST_COLS * st + 8 * lane - 20;  // this lane's 16 source bytes
     // padded sources: lanes past the ring read inside it (their outputs are unused)
@@ -391,12 +409,13 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
             const int a = c1 + 4 * (lane - 2);
             const bool ok = own_lane && a < w1;
             uint8_t* const rb = P + L.off[0] + PAD;  // column 0 of padded row 0
+            const int rbo = (int)L.off[0] + PAD;
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
             if constexpr ((SKIP & 1) != 0) {
                 nsink ^= l1;
             } else {
-                *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(r1 + PAD) * p1 : tl) = l1;
-                if (mr != r1) *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p1 : tl) = l1;
+                if constexpr (BUF) st_b32(rs, ok ? rbo + a + (r1 + PAD) * p1 : GVX_OOB, l1); else *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(r1 + PAD) * p1 : tl) = l1;
+                if (mr != r1) if constexpr (BUF) st_b32(rs, ok ? rbo + a + (mr + PAD) * p1 : GVX_OOB, l1); else *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p1 : tl) = l1;
                 if constexpr (SIDES) {
                     if (side1) {  // wave-uniform
                         const uint32_t nx = wave_shl1(l1), pv = wave_shr1(l1);
@@ -405,16 +424,16 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                         const uint32_t v = lw ? __builtin_amdgcn_perm(nx, l1, 0x01020304u)
                                               : __builtin_amdgcn_perm(l1, pv, 0x03040506u);
                         const int col = lw ? -a - 4 : 2 * w1 - 4 - a;
-                        *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(r1 + PAD) * p1 : tl) = v;
+                        if constexpr (BUF) st_b32(rs, lw || rw ? rbo + col + (r1 + PAD) * p1 : GVX_OOB, v); else *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(r1 + PAD) * p1 : tl) = v;
                         if (mr != r1)
-                            *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(mr + PAD) * p1 : tl) = v;
+                            if constexpr (BUF) st_b32(rs, lw || rw ? rbo + col + (mr + PAD) * p1 : GVX_OOB, v); else *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(mr + PAD) * p1 : tl) = v;
                         if (!r1dw) {  // odd widths: the right band byte by byte
 #pragma unroll
                             for (int b = 0; b < 4; ++b) {
                                 const int c = a + b, rc = ring_col(c, w1);
                                 const bool wb = own_lane && rc > 0;
-                                *(wb ? rb + rc + (int64_t)(r1 + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
-                                if (mr != r1) *(wb ? rb + rc + (int64_t)(mr + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
+                                if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (r1 + PAD) * p1 : GVX_OOB, (uint8_t)(l1 >> (8 * b))); else *(wb ? rb + rc + (int64_t)(r1 + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
+                                if (mr != r1) if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (mr + PAD) * p1 : GVX_OOB, (uint8_t)(l1 >> (8 * b))); else *(wb ? rb + rc + (int64_t)(mr + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
                             }
                         }
                     }
@@ -453,13 +472,14 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                     const int a = c2 + 2 * (lane - 2);
                     const bool ok = own_lane && a < w2;
                     uint8_t* const rb = P + L.off[1] + PAD;
+                    const int rbo = (int)L.off[1] + PAD;
                     const int mr = mirror_row(r2, h2);
                     if constexpr ((SKIP & 2) != 0) {
                         nsink ^= l2 << 7;
                     } else {
-                        *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
+                        if constexpr (BUF) st_b16(rs, ok ? rbo + a + (r2 + PAD) * p2 : GVX_OOB, (uint16_t)l2); else *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
                         if (mr != r2)
-                            *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
+                            if constexpr (BUF) st_b16(rs, ok ? rbo + a + (mr + PAD) * p2 : GVX_OOB, (uint16_t)l2); else *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
                         if constexpr (SIDES) {
                             if (side2) {  // wave-uniform
 #pragma unroll
@@ -467,8 +487,8 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                                     const int rc = ring_col(a + b, w2);
                                     const bool wb = own_lane && rc != 0;
                                     const uint8_t v8 = (uint8_t)(l2 >> (8 * b));
-                                    *(wb ? rb + rc + (int64_t)(r2 + PAD) * p2 : tl) = v8;
-                                    if (mr != r2) *(wb ? rb + rc + (int64_t)(mr + PAD) * p2 : tl) = v8;
+                                    if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (r2 + PAD) * p2 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(r2 + PAD) * p2 : tl) = v8;
+                                    if (mr != r2) if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (mr + PAD) * p2 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(mr + PAD) * p2 : tl) = v8;
                                 }
                             }
                         }
@@ -496,19 +516,20 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                         const int a = c3 + (lane - 2);
                         const bool ok = own_lane && a < w3;
                         uint8_t* const rb = P + L.off[2] + PAD;
+                        const int rbo = (int)L.off[2] + PAD;
                         const int mr = mirror_row(r3, h3);
                         const uint8_t v8 = (uint8_t)(s3 >> 8);
                         if constexpr ((SKIP & 4) != 0) {
                             nsink ^= s3 << 13;
                         } else if (k >= 12 && r3 >= o3lo && r3 < o3hi) {
-                            *(ok ? rb + a + (int64_t)(r3 + PAD) * p3 : tl) = v8;
-                            if (mr != r3) *(ok ? rb + a + (int64_t)(mr + PAD) * p3 : tl) = v8;
+                            if constexpr (BUF) st_b8(rs, ok ? rbo + a + (r3 + PAD) * p3 : GVX_OOB, v8); else *(ok ? rb + a + (int64_t)(r3 + PAD) * p3 : tl) = v8;
+                            if (mr != r3) if constexpr (BUF) st_b8(rs, ok ? rbo + a + (mr + PAD) * p3 : GVX_OOB, v8); else *(ok ? rb + a + (int64_t)(mr + PAD) * p3 : tl) = v8;
                             if constexpr (SIDES) {
                                 if (side3) {  // wave-uniform
                                     const int rc = ring_col(a, w3);
                                     const bool wb = own_lane && rc != 0;
-                                    *(wb ? rb + rc + (int64_t)(r3 + PAD) * p3 : tl) = v8;
-                                    if (mr != r3) *(wb ? rb + rc + (int64_t)(mr + PAD) * p3 : tl) = v8;
+                                    if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (r3 + PAD) * p3 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(r3 + PAD) * p3 : tl) = v8;
+                                    if (mr != r3) if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (mr + PAD) * p3 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(mr + PAD) * p3 : tl) = v8;
                                 }
                             }
                         }
