@@ -298,16 +298,35 @@ struct DownLevels {
 // columns of some level's side bands.  Both are wave-uniform, so the kernel
 // branches once into one of three instances and the loop has no per-row path
 // choice (loads stay in flight across iterations).
-// Buffer stores at 32-bit offsets into one image's pyramid (stream_walk).
-constexpr int GVX_OOB = 0x7fffffff;  // past every pyramid: the store is dropped
-__device__ __forceinline__ void st_b32(__amdgpu_buffer_rsrc_t rs, int off, uint32_t v) {
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs, off, 0, 0);
-}
-__device__ __forceinline__ void st_b16(__amdgpu_buffer_rsrc_t rs, int off, uint32_t v) {
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, rs, off, 0, 0);
-}
-__device__ __forceinline__ void st_b8(__amdgpu_buffer_rsrc_t rs, int off, uint32_t v) {
-    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, rs, off, 0, 0);
+// One output store of stream_walk: pixel column `col` of padded row `row` of a
+// level whose column 0 of padded row 0 is d.ptr (byte d.off of the image's
+// pyramid).  Lanes that own no output (own == false) must not write the level:
+// BUF (interior strips) stores through a buffer view at an offset past the
+// pyramid, which the bounds check drops -- a 32-bit offset and no select of a
+// 64-bit address per store: 1,262 -> 655 VALU per 8 level-1 rows, pyramid pass
+// -2 % (profiles/r04_v24/); otherwise a flat store, those lanes writing the
+// wave's trash line.  The edge-strip instances keep the flat form: with buffer
+// stores they spill at the kernel's 128 registers and ran 2.3x slower.
+struct PyrDst {
+    __amdgpu_buffer_rsrc_t rs;
+    uint8_t* ptr;
+    int off;
+    uint8_t* tl;
+};
+constexpr int PYR_OOB = 0x7fffffff;
+template <bool BUF, typename T>
+__device__ __forceinline__ void pyr_store(const PyrDst& d, bool own, int col, int row, int pitch, T v) {
+    if constexpr (BUF) {
+        const int o = own ? d.off + col + row * pitch : PYR_OOB;
+        if constexpr (sizeof(T) == 4)
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, d.rs, o, 0, 0);
+        else if constexpr (sizeof(T) == 2)
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, d.rs, o, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, d.rs, o, 0, 0);
+    } else {
+        *reinterpret_cast<T*>(own ? d.ptr + col + (int64_t)row * pitch : d.tl) = v;
+    }
 }
 
 template <int NL, bool GATHER, bool SIDES, int SKIP>
@@ -316,10 +335,7 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                                             uint8_t* __restrict__ tl, bool side1, bool side2, bool side3) {
     const uint8_t* S = img < src.n_a ? src.a + img * src.img_stride : src.b + (img - src.n_a) * src.img_stride;
     uint8_t* P = pyr + img * pyr_bytes;
-    // interior strips store through a buffer view of the image's pyramid: lanes that
-    // own no output pass an offset past its end and the bounds check drops the store
-    // (no 64-bit address or trash select per store: 1,262 -> 655 VALU per 8 level-1
-    // rows); the edge-strip instances keep the flat stores, which fit their registers
+    // interior strips store through a buffer view of the image's pyramid (pyr_store)
     constexpr bool BUF = !SIDES;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)pyr_bytes, 0x00020000);
     const int w0 = src.w, h0 = src.h, sp = src.pitch;
@@ -408,14 +424,13 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
         if (r1 >= o1lo && r1 < o1hi) {  // wave-uniform: rows of the band
             const int a = c1 + 4 * (lane - 2);
             const bool ok = own_lane && a < w1;
-            uint8_t* const rb = P + L.off[0] + PAD;  // column 0 of padded row 0
-            const int rbo = (int)L.off[0] + PAD;
+            const PyrDst rb{rs, P + L.off[0] + PAD, (int)L.off[0] + PAD, tl};  // column 0 of padded row 0
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
             if constexpr ((SKIP & 1) != 0) {
                 nsink ^= l1;
             } else {
-                if constexpr (BUF) st_b32(rs, ok ? rbo + a + (r1 + PAD) * p1 : GVX_OOB, l1); else *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(r1 + PAD) * p1 : tl) = l1;
-                if (mr != r1) if constexpr (BUF) st_b32(rs, ok ? rbo + a + (mr + PAD) * p1 : GVX_OOB, l1); else *reinterpret_cast<uint32_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p1 : tl) = l1;
+                pyr_store<BUF, uint32_t>(rb, ok, a, r1 + PAD, p1, l1);
+                if (mr != r1) pyr_store<BUF, uint32_t>(rb, ok, a, mr + PAD, p1, l1);
                 if constexpr (SIDES) {
                     if (side1) {  // wave-uniform
                         const uint32_t nx = wave_shl1(l1), pv = wave_shr1(l1);
@@ -424,16 +439,16 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                         const uint32_t v = lw ? __builtin_amdgcn_perm(nx, l1, 0x01020304u)
                                               : __builtin_amdgcn_perm(l1, pv, 0x03040506u);
                         const int col = lw ? -a - 4 : 2 * w1 - 4 - a;
-                        if constexpr (BUF) st_b32(rs, lw || rw ? rbo + col + (r1 + PAD) * p1 : GVX_OOB, v); else *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(r1 + PAD) * p1 : tl) = v;
+                        pyr_store<BUF, uint32_t>(rb, lw || rw, col, r1 + PAD, p1, v);
                         if (mr != r1)
-                            if constexpr (BUF) st_b32(rs, lw || rw ? rbo + col + (mr + PAD) * p1 : GVX_OOB, v); else *reinterpret_cast<uint32_t*>(lw || rw ? rb + col + (int64_t)(mr + PAD) * p1 : tl) = v;
+                            pyr_store<BUF, uint32_t>(rb, lw || rw, col, mr + PAD, p1, v);
                         if (!r1dw) {  // odd widths: the right band byte by byte
 #pragma unroll
                             for (int b = 0; b < 4; ++b) {
                                 const int c = a + b, rc = ring_col(c, w1);
                                 const bool wb = own_lane && rc > 0;
-                                if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (r1 + PAD) * p1 : GVX_OOB, (uint8_t)(l1 >> (8 * b))); else *(wb ? rb + rc + (int64_t)(r1 + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
-                                if (mr != r1) if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (mr + PAD) * p1 : GVX_OOB, (uint8_t)(l1 >> (8 * b))); else *(wb ? rb + rc + (int64_t)(mr + PAD) * p1 : tl) = (uint8_t)(l1 >> (8 * b));
+                                pyr_store<BUF, uint8_t>(rb, wb, rc, r1 + PAD, p1, (uint8_t)(l1 >> (8 * b)));
+                                if (mr != r1) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p1, (uint8_t)(l1 >> (8 * b)));
                             }
                         }
                     }
@@ -471,15 +486,14 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                 if (k >= 4 && r2 >= o2lo && r2 < o2hi) {
                     const int a = c2 + 2 * (lane - 2);
                     const bool ok = own_lane && a < w2;
-                    uint8_t* const rb = P + L.off[1] + PAD;
-                    const int rbo = (int)L.off[1] + PAD;
+                    const PyrDst rb{rs, P + L.off[1] + PAD, (int)L.off[1] + PAD, tl};
                     const int mr = mirror_row(r2, h2);
                     if constexpr ((SKIP & 2) != 0) {
                         nsink ^= l2 << 7;
                     } else {
-                        if constexpr (BUF) st_b16(rs, ok ? rbo + a + (r2 + PAD) * p2 : GVX_OOB, (uint16_t)l2); else *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(r2 + PAD) * p2 : tl) = (uint16_t)l2;
+                        pyr_store<BUF, uint16_t>(rb, ok, a, r2 + PAD, p2, (uint16_t)l2);
                         if (mr != r2)
-                            if constexpr (BUF) st_b16(rs, ok ? rbo + a + (mr + PAD) * p2 : GVX_OOB, (uint16_t)l2); else *reinterpret_cast<uint16_t*>(ok ? rb + a + (int64_t)(mr + PAD) * p2 : tl) = (uint16_t)l2;
+                            pyr_store<BUF, uint16_t>(rb, ok, a, mr + PAD, p2, (uint16_t)l2);
                         if constexpr (SIDES) {
                             if (side2) {  // wave-uniform
 #pragma unroll
@@ -487,8 +501,8 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                                     const int rc = ring_col(a + b, w2);
                                     const bool wb = own_lane && rc != 0;
                                     const uint8_t v8 = (uint8_t)(l2 >> (8 * b));
-                                    if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (r2 + PAD) * p2 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(r2 + PAD) * p2 : tl) = v8;
-                                    if (mr != r2) if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (mr + PAD) * p2 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(mr + PAD) * p2 : tl) = v8;
+                                    pyr_store<BUF, uint8_t>(rb, wb, rc, r2 + PAD, p2, v8);
+                                    if (mr != r2) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p2, v8);
                                 }
                             }
                         }
@@ -515,21 +529,20 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
                         const int a = c3 + (lane - 2);
                         const bool ok = own_lane && a < w3;
-                        uint8_t* const rb = P + L.off[2] + PAD;
-                        const int rbo = (int)L.off[2] + PAD;
+                        const PyrDst rb{rs, P + L.off[2] + PAD, (int)L.off[2] + PAD, tl};
                         const int mr = mirror_row(r3, h3);
                         const uint8_t v8 = (uint8_t)(s3 >> 8);
                         if constexpr ((SKIP & 4) != 0) {
                             nsink ^= s3 << 13;
                         } else if (k >= 12 && r3 >= o3lo && r3 < o3hi) {
-                            if constexpr (BUF) st_b8(rs, ok ? rbo + a + (r3 + PAD) * p3 : GVX_OOB, v8); else *(ok ? rb + a + (int64_t)(r3 + PAD) * p3 : tl) = v8;
-                            if (mr != r3) if constexpr (BUF) st_b8(rs, ok ? rbo + a + (mr + PAD) * p3 : GVX_OOB, v8); else *(ok ? rb + a + (int64_t)(mr + PAD) * p3 : tl) = v8;
+                            pyr_store<BUF, uint8_t>(rb, ok, a, r3 + PAD, p3, v8);
+                            if (mr != r3) pyr_store<BUF, uint8_t>(rb, ok, a, mr + PAD, p3, v8);
                             if constexpr (SIDES) {
                                 if (side3) {  // wave-uniform
                                     const int rc = ring_col(a, w3);
                                     const bool wb = own_lane && rc != 0;
-                                    if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (r3 + PAD) * p3 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(r3 + PAD) * p3 : tl) = v8;
-                                    if (mr != r3) if constexpr (BUF) st_b8(rs, wb ? rbo + rc + (mr + PAD) * p3 : GVX_OOB, v8); else *(wb ? rb + rc + (int64_t)(mr + PAD) * p3 : tl) = v8;
+                                    pyr_store<BUF, uint8_t>(rb, wb, rc, r3 + PAD, p3, v8);
+                                    if (mr != r3) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p3, v8);
                                 }
                             }
                         }
