@@ -1,0 +1,1190 @@
+// klt.hip -- pyramidal Lucas-Kanade (fwd / fwd+bwd+FB) and compaction kernels
+// for gfx950.  Replaces the four cv::calcOpticalFlowPyrLK calls per frame at
+// /root/reference/ic_gvins/ic_gvins/tracking/tracking.cc:385,390,487,493 and the
+// status / reduceVector logic at tracking.cc:396-408, :831-849.
+//
+// Design (DESIGN.md "KLT"):
+//  * pyramids are built once per image (pyramid.hip) into a padded layout;
+//  * the Scharr derivative planes are never materialised: each window's
+//    derivative is computed in registers from the padded pyramid (zero outside
+//    the image, as OpenCV's BORDER_CONSTANT derivative padding);
+//  * one point per 64-lane wavefront: lane k < 63 owns the 7-pixel "unit"
+//    (window row k/3, segment k%3) of the 21x21 window; window rows are read
+//    with aligned dword loads and realigned with v_alignbyte;
+//  * window values are kept as packed int16 pairs and the bilinear weights,
+//    gradients and mismatch products run on v_dot2_i32_i16; every per-pixel
+//    quantity is an exact integer, and the window sums are exact 64-bit DPP
+//    wave reductions -- so the fp32 2x2 solve sees bit-identical inputs to
+//    the CPU restatement (oracle/klt.c), whose LK outputs are matched bit-exactly.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "gvx_internal.h"
+
+namespace gvx {
+
+namespace {
+
+constexpr int W_BITS = 14;
+constexpr float FLT_SCALE = 1.f / (1 << 20);
+
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+typedef uint32_t v3u __attribute__((ext_vector_type(3)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+// a.lo*b.lo + a.hi*b.hi + c on signed int16 halves (v_dot2_i32_i16)
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c, false);
+}
+// the same with a wave-uniform addend taken straight from an SGPR (the VOP3P
+// form: no per-accumulator v_mov of the rounding constant)
+__device__ __forceinline__ int dot2k(uint32_t a, uint32_t b, int k) {
+    int r;
+    __asm__("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+typedef unsigned short v2us __attribute__((ext_vector_type(2)));
+// a.lo*b.lo + a.hi*b.hi + c on unsigned int16 halves (v_dot2_u32_u16)
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(v2us, a), __builtin_bit_cast(v2us, b), c, false);
+}
+__device__ __forceinline__ uint32_t udot2k(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    __asm__("v_dot2_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+// (lo & 0xffff) | (hi << 16)
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) {
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+// signed int16 half `hi` of a packed pair
+__device__ __forceinline__ int half16(uint32_t v, int hi) { return hi ? ((int)v >> 16) : (int)(short)(v & 0xffffu); }
+// bytes (b[t], b[t+1]) of the 8-byte value {d1:d0} zero-extended to int16 halves
+template <int T>
+__device__ __forceinline__ uint32_t byte_pair(uint32_t d0, uint32_t d1) {
+    return __builtin_amdgcn_perm(d1, d0, 0x0c000c00u | ((uint32_t)(T + 1) << 16) | (uint32_t)T);
+}
+// the same for byte T of a 12-byte row held in three dwords (T <= 10)
+template <int T>
+__device__ __forceinline__ uint32_t byte_pair3(const uint32_t (&d)[3]) {
+    return byte_pair<(T & 3)>(d[T >> 2], d[(T >> 2) + 1 < 3 ? (T >> 2) + 1 : 2]);
+}
+__device__ __forceinline__ uint32_t psub16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) - __builtin_bit_cast(v2s, b));
+}
+__device__ __forceinline__ uint32_t padd16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) + __builtin_bit_cast(v2s, b));
+}
+// a*k + c on int16 halves (k small)
+__device__ __forceinline__ uint32_t pmad16(uint32_t a, short k, uint32_t c) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) * k + __builtin_bit_cast(v2s, c));
+}
+__device__ __forceinline__ uint32_t pmul16(uint32_t a, short k) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) * k);
+}
+// (hi half of a, lo half of b): the pair starting one column later
+__device__ __forceinline__ uint32_t shift_pair(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_alignbit(b, a, 16);
+}
+
+// A pyramid level (or level-0 image) as a buffer resource: pixel (x, y) is at
+// byte o0 + y*pitch + x (every offset the LK loop produces is non-negative).
+struct Plane {
+    __amdgpu_buffer_rsrc_t rs;
+    int o0, pitch;
+};
+__device__ __forceinline__ Plane make_plane(const uint8_t* base, int o0, int pitch) {
+    Plane p;
+    p.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, 0x7fffffff, 0x00020000);
+    p.o0 = o0;
+    p.pitch = pitch;
+    return p;
+}
+// NDW realigned dwords of a row starting at byte `off` (any alignment), the row
+// `soff` bytes further (soff wave-uniform, in the SGPR soffset).
+template <int NDW>
+__device__ __forceinline__ void brow(const Plane& P, int off_al, uint32_t sh, int soff, uint32_t (&d)[NDW]) {
+    if constexpr (NDW == 3) {
+        const v4u w = __builtin_amdgcn_raw_buffer_load_b128(P.rs, off_al, soff, 0);
+        d[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+        d[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+        d[2] = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
+    } else {
+        const v3u w = __builtin_amdgcn_raw_buffer_load_b96(P.rs, off_al, soff, 0);
+        d[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+        d[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+    }
+}
+
+// BORDER_REFLECT_101 index, branchless: exact for -(2*len-2) <= p <= 3*len-3;
+// LK windows overshoot a level (> 21 px) by at most 26 px.
+__device__ __forceinline__ int refl(int p, int len) {
+    int a = abs(p);
+    a = min(a, 2 * len - 2 - a);
+    a = abs(a);
+    return min(a, len - 1);
+}
+// Border windows of an unpadded plane (level 0 read in place): a point's lane
+// group gathers its window -- rows y0 .. y0+rows-1, bytes x0 .. x0+31,
+// REFLECT_101 outside the image (the values the padded ring of OpenCV's
+// pyramid level holds there) -- into its own LDS tile once (byte buffer loads
+// off the wave-uniform plane base), then every lane reads its rows from LDS
+// like the aligned global path.
+constexpr int WIN_DW = 8;  // dwords per LDS tile row
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int G>
+__device__ __forceinline__ void fill_win(uint32_t* win, const Plane& P, int W, int H, int x0, int y0, int rows,
+                                         int gl) {
+    wave_lds_sync();  // earlier reads of the tile are done
+#pragma unroll 1
+    for (int i = gl; i < rows * WIN_DW; i += G) {
+        const int r = i >> 3, q = i & 7;
+        const int ro = P.o0 + refl(y0 + r, H) * P.pitch;
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(P.rs, ro + refl(x0 + 4 * q + b, W), 0, 0) << (8 * b);
+        win[i] = v;
+    }
+    wave_lds_sync();
+}
+template <int NDW>
+__device__ __forceinline__ void read_win(const uint32_t* win, int row, int byteoff, uint32_t (&d)[NDW]) {
+    const uint32_t* p = win + row * WIN_DW + (byteoff >> 2);
+    const uint32_t sh = (uint32_t)(byteoff & 3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for (int k = 0; k <= NDW; ++k) w[k] = p[k];
+#pragma unroll
+    for (int k = 0; k < NDW; ++k) d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+}
+
+// The lane id, recomputed where it is used (volatile: never hoisted or kept
+// live): everything lane-derived (the lane group, the window units, LDS slots,
+// the point index) is rebuilt from it inside each LK pass, so nothing per-lane
+// stays live across the forward and backward passes (where the register
+// allocator spilled such values to scratch: 45 MB of writes per 256 pairs, r02).
+__device__ __forceinline__ int lane_v() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// cvRound((1-a)(1-b) 2^14) ... in fp32 (LKTrackerInvoker), packed as int16 pairs
+// W0 = (w00, w01), W1 = (w10, w11).  p*2^14 is exact, so fma(p, 2^14, 1.5*2^23)
+// is 1.5*2^23 + cvRound(p*2^14) (round to nearest even, 0 <= p*2^14 <= 2^14)
+// with the integer in the low mantissa bits; the packs read those bits and
+// w11 = 2^14 - w00 - w01 - w10 is taken on the raw bit patterns (mod 2^32).
+__device__ __forceinline__ void weights(float a, float b, uint32_t& W0, uint32_t& W1) {
+    constexpr float M = 12582912.0f;  // 1.5 * 2^23, bit pattern 0x4B400000
+    const float ra = 1.f - a, rb = 1.f - b;
+    const uint32_t f00 = __float_as_uint(__builtin_fmaf(ra * rb, (float)(1 << W_BITS), M));
+    const uint32_t f01 = __float_as_uint(__builtin_fmaf(a * rb, (float)(1 << W_BITS), M));
+    const uint32_t f10 = __float_as_uint(__builtin_fmaf(ra * b, (float)(1 << W_BITS), M));
+    const uint32_t f11 = ((1u << W_BITS) + 3u * 0x4B400000u) - (f00 + f01 + f10);
+    W0 = __builtin_amdgcn_perm(f01, f00, 0x05040100u);
+    W1 = __builtin_amdgcn_perm(f11, f10, 0x05040100u);
+}
+
+
+struct LkCfg {
+    int max_iter;
+    double crit_eps;
+    float min_eig;
+    int use_initial_flow;
+    int want_err;  // compute the level-0 error (the status checks run regardless)
+};
+
+// One window unit: 7 pixels (cols 7*seg .. 7*seg+6 of window row `row`).
+struct Unit {
+    int row, seg;
+    bool valid;
+    uint32_t iv[4], ix[4], iy[4];  // packed int16 pairs (pixel 2k, 2k+1); pair 3 high = 0
+};
+// A lane's extracted window values live in LDS between the extraction and the
+// iterations (registers hold only the unit being matched): slot (s, q) of lane
+// `lane` at ust[(3*s + q)*64], ust = wave base + lane (16-B per lane, linear).
+__device__ __forceinline__ void unit_put(v4u* ust, int s, const Unit& u) {
+    ust[(3 * s + 0) * 64] = v4u{u.iv[0], u.iv[1], u.iv[2], u.iv[3]};
+    ust[(3 * s + 1) * 64] = v4u{u.ix[0], u.ix[1], u.ix[2], u.ix[3]};
+    ust[(3 * s + 2) * 64] = v4u{u.iy[0], u.iy[1], u.iy[2], u.iy[3]};
+}
+__device__ __forceinline__ void unit_get(const v4u* ust, int s, Unit& u) {
+    const v4u a = ust[(3 * s + 0) * 64], b = ust[(3 * s + 1) * 64], c = ust[(3 * s + 2) * 64];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        u.iv[k] = a[k];
+        u.ix[k] = b[k];
+        u.iy[k] = c[k];
+    }
+}
+
+// byte pair (T, T+1) of a 12-byte row in three dwords, as int16 halves (T <= 9;
+// T is a constant after unrolling)
+__device__ __forceinline__ uint32_t bpair(const uint32_t (&d)[3], int T) {
+    const int q = T >> 2, r = T & 3;
+    const uint32_t lo = d[q], hi = d[q + 1 < 3 ? q + 1 : 2];
+    return __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | ((uint32_t)(r + 1) << 16) | (uint32_t)r);
+}
+
+// Extract I (5 fractional bits) and the Scharr gradient at the bilinear
+// window positions of one unit (LKTrackerInvoker window extraction), and
+// accumulate its structure-tensor partial sums.
+// d[r]: bytes X .. X+11 (X = ipx + 7*seg - 1) of rows ipy+row-1+r, r = 0..3.
+// The Scharr taps run on int16 column pairs (v_pk_*): t0 = 3(a+e)+10b and
+// t1 = e-a per column, dx = t0[c+1]-t0[c-1], dy = 3(t1[c+1]+t1[c-1])+10 t1[c],
+// every value an exact integer of at most 13 bits.  `interior`: the whole
+// window of every unit is inside the image (no derivative masking).
+__device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3], int W, int H, int ipx,
+                                             int ipy, bool interior, uint32_t W0, uint32_t W1, int& a11,
+                                             int& a12, int& a22) {
+    const int X = ipx + 7 * u.seg - 1;
+    constexpr int RNDV = 1 << (W_BITS - 6), RNDD = 1 << (W_BITS - 1);
+    // even-aligned column pairs (2k, 2k+1), k = 0..4, of the four rows
+    uint32_t E[4][5];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) E[r][k] = bpair(d[r], 2 * k);
+    int iv[7], ix[7], iy[7];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const uint32_t Wr = rr ? W1 : W0;
+        uint32_t T0[5], T1[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            T0[k] = pmad16(padd16(E[rr][k], E[rr + 2][k]), 3, pmul16(E[rr + 1][k], 10));
+            T1[k] = psub16(E[rr + 2][k], E[rr][k]);
+        }
+        // derivative pairs at columns (2k+1, 2k+2), k = 0..3
+        uint32_t DX[4], DY[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            DX[k] = psub16(T0[k + 1], T0[k]);
+            DY[k] = pmad16(padd16(T1[k + 1], T1[k]), 3, pmul16(shift_pair(T1[k], T1[k + 1]), 10));
+        }
+        if (!interior) {
+            // derivatives are zero outside the image (BORDER_CONSTANT padding of
+            // OpenCV's derivative pyramid)
+            const bool row_in = (unsigned)(ipy + u.row + rr) < (unsigned)H;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool lo = row_in && (unsigned)(X + 2 * k + 1) < (unsigned)W;
+                const bool hi = row_in && (unsigned)(X + 2 * k + 2) < (unsigned)W;
+                const uint32_t m = (lo ? 0xffffu : 0u) | (hi ? 0xffff0000u : 0u);
+                DX[k] &= m;
+                DY[k] &= m;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            // pixel pair (t+1, t+2): CV_DESCALE(sum, 9) for I, (sum, 14) for dI
+            const int k = t >> 1;
+            const uint32_t pv = (t & 1) ? E[rr + 1][k + 1] : bpair(d[rr + 1], t + 1);
+            const uint32_t px = (t & 1) ? shift_pair(DX[k], DX[k + 1]) : DX[k];
+            const uint32_t py = (t & 1) ? shift_pair(DY[k], DY[k + 1]) : DY[k];
+            if (rr == 0) {
+                iv[t] = dot2k(pv, Wr, RNDV);
+                ix[t] = dot2k(px, Wr, RNDD);
+                iy[t] = dot2k(py, Wr, RNDD);
+            } else {
+                iv[t] = dot2(pv, Wr, iv[t]);
+                ix[t] = dot2(px, Wr, ix[t]);
+                iy[t] = dot2(py, Wr, iy[t]);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int h = 2 * k + 1 < 7 ? 2 * k + 1 : 0;
+        u.iv[k] = pack16(iv[2 * k] >> (W_BITS - 5), 2 * k + 1 < 7 ? iv[h] >> (W_BITS - 5) : 0);
+        u.ix[k] = pack16(ix[2 * k] >> W_BITS, 2 * k + 1 < 7 ? ix[h] >> W_BITS : 0);
+        u.iy[k] = pack16(iy[2 * k] >> W_BITS, 2 * k + 1 < 7 ? iy[h] >> W_BITS : 0);
+    }
+    int s11 = dot2k(u.ix[0], u.ix[0], 0), s12 = dot2k(u.ix[0], u.iy[0], 0), s22 = dot2k(u.iy[0], u.iy[0], 0);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        s11 = dot2(u.ix[k], u.ix[k], s11);
+        s12 = dot2(u.ix[k], u.iy[k], s12);
+        s22 = dot2(u.iy[k], u.iy[k], s22);
+    }
+    a11 = u.valid ? s11 : 0;
+    a12 = u.valid ? s12 : 0;
+    a22 = u.valid ? s22 : 0;
+}
+
+// Mismatch of one unit against J at integer offset (jx, jy) with weights
+// (W0, W1): accumulates b1 += diff*Ix, b2 += diff*Iy (or es += |diff| for ERR).
+// r0 / r1: bytes jx+7*seg .. +7 of rows jy+row and jy+row+1.
+// Bytes (b[T], b[T+1]) of the 8-byte value {d1:d0} as the HIGH bytes of two
+// uint16 halves (b*256), for the unsigned dot2 below.
+template <int T>
+__device__ __forceinline__ uint32_t byte_pair_hi(uint32_t d0, uint32_t d1) {
+    return __builtin_amdgcn_perm(d1, d0, 0x000c000cu | ((uint32_t)T << 8) | ((uint32_t)(T + 1) << 24));
+}
+// The J window values of a unit as packed int16 pairs (pixel 2k, 2k+1; pair 3
+// high = 0): CV_DESCALE(w00 J00 + w01 J01 + w10 J10 + w11 J11, W_BITS - 5).
+// The sum runs on v_dot2_u32_u16 with the bytes scaled by 256 (b*256 <= 65280
+// and w <= 2^14 are uint16; X = 256 (sum + 2^8) < 2^30), so the value is X >> 17:
+// one v_perm takes the high halves of two pixels' X and one packed shift by 1
+// finishes both (2 operations per pixel pair instead of 2 shifts and a pack).
+// Only for w11 >= 0: w11 = 2^14 - w00 - w01 - w10 of three separately rounded
+// weights is -1 or -2 when a*b*2^14 is below ~1.5, and such iterations take
+// j_pairs_signed (the signed v_dot2_i32_i16 on plain bytes).
+__device__ __forceinline__ void j_pairs_signed(const uint32_t (&r0)[2], const uint32_t (&r1)[2], uint32_t W0,
+                                               uint32_t W1, uint32_t (&jp)[4]) {
+    constexpr int RND = 1 << (W_BITS - 6);
+    int jv[8];
+    jv[0] = dot2(byte_pair<0>(r1[0], r1[1]), W1, dot2k(byte_pair<0>(r0[0], r0[1]), W0, RND));
+    jv[1] = dot2(byte_pair<1>(r1[0], r1[1]), W1, dot2k(byte_pair<1>(r0[0], r0[1]), W0, RND));
+    jv[2] = dot2(byte_pair<2>(r1[0], r1[1]), W1, dot2k(byte_pair<2>(r0[0], r0[1]), W0, RND));
+    jv[3] = dot2(byte_pair<3>(r1[0], r1[1]), W1, dot2k(byte_pair<3>(r0[0], r0[1]), W0, RND));
+    jv[4] = dot2(byte_pair<4>(r1[0], r1[1]), W1, dot2k(byte_pair<4>(r0[0], r0[1]), W0, RND));
+    jv[5] = dot2(byte_pair<5>(r1[0], r1[1]), W1, dot2k(byte_pair<5>(r0[0], r0[1]), W0, RND));
+    jv[6] = dot2(byte_pair<6>(r1[0], r1[1]), W1, dot2k(byte_pair<6>(r0[0], r0[1]), W0, RND));
+#pragma unroll
+    for (int t = 0; t < 7; ++t) jv[t] >>= (W_BITS - 5);
+    jv[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
+}
+__device__ __forceinline__ void j_pairs(const uint32_t (&r0)[2], const uint32_t (&r1)[2], uint32_t W0, uint32_t W1,
+                                        uint32_t (&jp)[4]) {
+    constexpr uint32_t RND = 1u << (W_BITS - 6 + 8);
+    uint32_t X[8];
+    X[0] = udot2(byte_pair_hi<0>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<0>(r0[0], r0[1]), W0, RND));
+    X[1] = udot2(byte_pair_hi<1>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<1>(r0[0], r0[1]), W0, RND));
+    X[2] = udot2(byte_pair_hi<2>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<2>(r0[0], r0[1]), W0, RND));
+    X[3] = udot2(byte_pair_hi<3>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<3>(r0[0], r0[1]), W0, RND));
+    X[4] = udot2(byte_pair_hi<4>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<4>(r0[0], r0[1]), W0, RND));
+    X[5] = udot2(byte_pair_hi<5>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<5>(r0[0], r0[1]), W0, RND));
+    X[6] = udot2(byte_pair_hi<6>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<6>(r0[0], r0[1]), W0, RND));
+    X[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t hi = __builtin_amdgcn_perm(X[2 * k + 1], X[2 * k], 0x07060302u);  // (X0 >> 16, X1 >> 16)
+        jp[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2us, hi) >> (unsigned short)1);
+    }
+}
+
+template <bool ERR, bool SIGNED = false>
+__device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
+                                           uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
+    uint32_t jp[4];
+    if constexpr (SIGNED)
+        j_pairs_signed(r0, r1, W0, W1, jp);
+    else
+        j_pairs(r0, r1, W0, W1, jp);
+    if (ERR) {
+        int e = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t d = psub16(jp[k], u.iv[k]);  // diff pair
+            const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
+            e += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
+        }
+        es += valid ? e : 0;
+    } else {
+        const uint32_t d0 = psub16(jp[0], u.iv[0]);
+        int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const uint32_t d = psub16(jp[k], u.iv[k]);
+            s1 = dot2(d, u.ix[k], s1);
+            s2 = dot2(d, u.iy[k], s2);
+        }
+        b1 += valid ? s1 : 0;
+        b2 += valid ? s2 : 0;
+    }
+}
+
+// match_unit's products for the fp32 orders: p1[t] = (float)(diff*Ix),
+// p2[t] = (float)(diff*Iy) of the unit's 7 pixels (OpenCV converts the int32
+// products, `ib1 += (itemtype)(diff*dIptr[0])`; |diff*Ix| < 2^25, round to
+// nearest even like the CPU's int -> float conversion).
+__device__ __forceinline__ uint32_t bp2(const uint32_t (&r)[2], int T) {
+    return __builtin_amdgcn_perm(r[1], r[0], 0x0c000c00u | ((uint32_t)(T + 1) << 16) | (uint32_t)T);
+}
+__device__ __forceinline__ void match_unit_f32(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
+                                               uint32_t W0, uint32_t W1, float (&p1)[7], float (&p2)[7]) {
+    constexpr int RND = 1 << (W_BITS - 6);
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        const int jv = dot2(bp2(r1, t), W1, dot2k(bp2(r0, t), W0, RND)) >> (W_BITS - 5);
+        const int d = jv - half16(u.iv[t >> 1], t & 1);
+        p1[t] = (float)__mul24(d, half16(u.ix[t >> 1], t & 1));
+        p2[t] = (float)__mul24(d, half16(u.iy[t >> 1], t & 1));
+    }
+}
+
+// Exact sums over a point's lane group (G = 16, 32 or 64 lanes, aligned):
+// a butterfly, so every lane of the group ends with the group total --
+// DPP quad / row mirrors inside 16-lane rows, then v_permlane16_swap /
+// v_permlane32_swap across rows (CDNA4).
+template <int G>
+__device__ __forceinline__ int group_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm 2,3,0,1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);  // row_mirror
+    if constexpr (G >= 32) {
+        const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+        v = (int)(r[0] + r[1]);
+    }
+    if constexpr (G >= 64) {
+        const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+        v = (int)(r[0] + r[1]);
+    }
+    return v;
+}
+// (float) of the exact group sums of per-lane values |v| < 2^31, round to
+// nearest even: v = hi*2^10 + lo with lo in [0, 1024); the hi sums stay below
+// 2^27 and two lo sums (< 2^16 each) share one packed chain; hi*2^10 + lo is
+// exact in fp64 (|sum| < 2^37) and the fp64 -> fp32 conversion rounds once.
+template <int G>
+__device__ __forceinline__ void group_sums_f32(int v0, int v1, float& f0, float& f1) {
+    const int h0 = group_sum<G>(v0 >> 10), h1 = group_sum<G>(v1 >> 10);
+    const uint32_t l = (uint32_t)group_sum<G>((int)(((uint32_t)v0 & 1023u) | (((uint32_t)v1 & 1023u) << 16)));
+    f0 = (float)__builtin_fma((double)h0, 1024.0, (double)(l & 0xffffu));
+    f1 = (float)__builtin_fma((double)h1, 1024.0, (double)(l >> 16));
+}
+template <int G>
+__device__ __forceinline__ float group_sum_f32(int v) {
+    const int h = group_sum<G>(v >> 10), l = group_sum<G>(v & 1023);
+    return (float)__builtin_fma((double)h, 1024.0, (double)l);
+}
+
+// ---- OpenCV's fp32 window-sum orders (gvx_klt_params.accum, oracle/klt.c
+// ORC_ACC_F32 / ORC_ACC_F32X4) ----
+// The products of one window sum are computed lane-parallel like the exact
+// path, staged in the point group's LDS region, and summed in OpenCV's order
+// by one lane per fp32 accumulator (a dependent chain: 441 adds for the scalar
+// loop, at most 105 for the CV_SIMD128 lanes and the scalar tail); the finished
+// accumulators are combined in OpenCV's reduction order by every lane.
+// Region layout (floats), two arrays k = 0, 1 (two sums at once):
+//  ACC 1 (scalar): array k at 512k; unit q's 7 pixels at 8q .. 8q+6 (window
+//    pixel (y, x) is unit 3y + x/7, slot x%7: row-major order is unit order);
+//    accumulator lane gl = k walks q = 0..62.
+//  ACC 2 (SIMD4): array k at 540k; lane m = 0..3 (pixels x = m, m+4, m+8, m+12
+//    of every row, index 4y + x/4) at 108m, the scalar tail (x = 16..20, index
+//    5y + x - 16) at 432; zero padded to 108 per accumulator (adding +0 is
+//    exact: no partial sum is -0); accumulator lane gl = 5k + m.
+//  Accumulator results at ACC_RES + gl.
+constexpr int ACC_RES = 1080, ACC_FLOATS = 1092;
+template <int ACC>
+constexpr int acc_chains() {
+    return ACC == 1 ? 2 : 10;
+}
+
+// unit q's 7 values into array k
+template <int ACC>
+__device__ __forceinline__ void acc_put(float* scr, int k, int q, const float (&v)[7]) {
+    if constexpr (ACC == 1) {
+        float4* p = reinterpret_cast<float4*>(scr + 512 * k + 8 * q);
+        p[0] = float4{v[0], v[1], v[2], v[3]};
+        p[1] = float4{v[4], v[5], v[6], 0.f};
+    } else {
+        const int y = q / 3, x0 = 7 * (q - 3 * y);
+        float* a = scr + 540 * k;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int x = x0 + t;
+            const int idx = x < 16 ? (x & 3) * 108 + 4 * y + (x >> 2) : 432 + 5 * y + (x - 16);
+            a[idx] = v[t];
+        }
+    }
+}
+// zero the region once per wave (the SIMD4 pads are never written again)
+template <int ACC, int G>
+__device__ __forceinline__ void acc_clear(float* scr, int gl) {
+    if constexpr (ACC != 0) {
+        float4* p = reinterpret_cast<float4*>(scr);
+        for (int i = gl; i < ACC_FLOATS / 4; i += G) p[i] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+// the accumulator lanes' sequential sums; every lane of the group ends with
+// the region's accumulators published at ACC_RES
+template <int ACC>
+__device__ __forceinline__ void acc_chains_run(float* scr, int gl) {
+    wave_lds_sync();  // the products are in place
+    float s = 0.f;
+    if constexpr (ACC == 1) {
+        const float4* p = reinterpret_cast<const float4*>(scr + 512 * (gl & 1));
+#pragma unroll 9
+        for (int q = 0; q < 63; ++q) {
+            const float4 a = p[2 * q], b = p[2 * q + 1];
+            s += a.x;
+            s += a.y;
+            s += a.z;
+            s += a.w;
+            s += b.x;
+            s += b.y;
+            s += b.z;
+        }
+    } else {
+        const int c = gl < 10 ? gl : 9, k = c >= 5 ? 1 : 0, m = c - 5 * k;
+        const float4* p = reinterpret_cast<const float4*>(scr + 540 * k + 108 * m);
+#pragma unroll 9
+        for (int i = 0; i < 27; ++i) {
+            const float4 a = p[i];
+            s += a.x;
+            s += a.y;
+            s += a.z;
+            s += a.w;
+        }
+    }
+    if (gl < acc_chains<ACC>()) scr[ACC_RES + gl] = s;
+    wave_lds_sync();
+}
+// sum k of the region in OpenCV's reduction order (after acc_chains_run).
+// A (qA..: lane x mod 4): tail + ((l0 + l1) + (l2 + l3)) (v_reduce_sum);
+// b (qb0 = (b1, b2) of x%4 = 0, 1; qb1 of x%4 = 2, 3): tail + ((l0 + l2) + (l1 + l3))
+// (v_interleave_pairs(qb0 + qb1), then the two-lane v_reduce_sum).
+template <int ACC, bool B>
+__device__ __forceinline__ float acc_result(const float* scr, int k) {
+    if constexpr (ACC == 1) {
+        return scr[ACC_RES + k];
+    } else {
+        const float* r = scr + ACC_RES + 5 * k;
+        return B ? r[4] + ((r[0] + r[2]) + (r[1] + r[3])) : r[4] + ((r[0] + r[1]) + (r[2] + r[3]));
+    }
+}
+
+// Window rows of a point's units: 4 rows x 12 bytes of I per unit for the
+// extraction, 2 rows x 8 bytes of J for a match.  `raw` planes (level 0 read in
+// place from the caller's image) take the aligned-load path only when every
+// byte the window touches is inside the image, and gather with REFLECT_101
+// otherwise; padded levels always take the aligned path (their PAD ring covers
+// every window the LK loop admits).  lane_off[s] = row*pitch + 7*seg of unit s.
+__device__ __forceinline__ void load_i_unit(const Unit& u, const Plane& P, int lane_off, int ipx, int ipy, bool fast,
+                                            const uint32_t* win, uint32_t (&d)[4][3]) {
+    if (fast) {
+        const int off = lane_off + (P.o0 + (ipy - 1) * P.pitch + ipx - 1);
+        const int al = off & ~3;
+        const uint32_t sh = (uint32_t)off & 3u;
+        brow<3>(P, al, sh, 0, d[0]);
+        brow<3>(P, al, sh, P.pitch, d[1]);
+        brow<3>(P, al, sh, 2 * P.pitch, d[2]);
+        brow<3>(P, al, sh, 3 * P.pitch, d[3]);
+    } else {
+        // tile: rows ipy-1 .., bytes ipx-1 ..; the unit reads 4 rows x 12 bytes
+#pragma unroll
+        for (int r = 0; r < 4; ++r) read_win<3>(win, u.row + r, 7 * u.seg, d[r]);
+    }
+}
+__device__ __forceinline__ void load_j_unit(const Unit& u, const Plane& P, int lane_off, int jx, int jy, bool fast,
+                                            const uint32_t* win, uint32_t (&r0)[2], uint32_t (&r1)[2]) {
+    if (fast) {
+        const int off = lane_off + (P.o0 + jy * P.pitch + jx);
+        const int al = off & ~3;
+        const uint32_t sh = (uint32_t)off & 3u;
+        brow<2>(P, al, sh, 0, r0);
+        brow<2>(P, al, sh, P.pitch, r1);
+    } else {
+        // tile: rows jy .., bytes jx ..; the unit reads 2 rows x 8 bytes
+        read_win<2>(win, u.row, 7 * u.seg, r0);
+        read_win<2>(win, u.row + 1, 7 * u.seg, r1);
+    }
+}
+
+// Level-0 planes of one pair: pointers to pixel (0,0), row pitch, and whether
+// they are the caller's unpadded images.
+struct L0Planes {
+    const uint8_t* i;  // plane bases; pixel (0,0) at byte o0
+    const uint8_t* j;
+    int o0, pitch;
+    bool raw;
+};
+
+// LKTrackerInvoker::operator() for one point across all levels (coarse to
+// fine).  PPW points share a wavefront: each point has a group of G = 64/PPW
+// lanes and lane gl of the group owns the PPW 7-pixel window units
+// gl, gl+G, .. (unit k = window row k/3, segment k%3; unit 63 does not exist).
+// The per-point scalar work (weights, sums, 2x2 solve, convergence) is thus
+// issued once for PPW points.  I/J: padded pyramids of the prev / next image
+// (levels >= 1); level 0 from `p0`.  Every per-point value below is uniform
+// over the point's group; control flow diverges only between groups.
+// ACC: the window-sum order (0 exact, 1 / 2 OpenCV's fp32 scalar / SIMD4
+// orders through the group's LDS region `acc`).
+// wins / units / accs: the wave's LDS bases (wave-uniform); the lane's slots
+// are derived from lane_v() here.
+// two-point waves: a point still iterating after the other stopped takes the whole wave
+#ifndef KLT_SOLO
+#define KLT_SOLO 1
+#endif
+template <int PPW, int ACC>
+__device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
+                                         const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
+                                         float p0y, float& nx, float& ny, int& status, float& err,
+                                         uint32_t (*wins)[(WIN + 3) * WIN_DW], v4u* units, float (*accs)[ACC_FLOATS]) {
+    constexpr int G = 64 / PPW, U = PPW;
+    constexpr bool SOLO = KLT_SOLO && PPW == 2 && ACC == 0;
+    const int lane = lane_v(), grp = lane / G, gl = lane & (G - 1);
+    uint32_t* win = wins[grp];
+    v4u* ust = units + lane;
+    float* acc = ACC ? accs[grp] : nullptr;
+    Unit u[U];
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+        const int k = gl + s * G;
+        u[s].valid = k < 63;
+        const int kc = k < 63 ? k : 62;
+        u[s].row = kc / 3;
+        u[s].seg = kc - 3 * u[s].row;
+    }
+    const float halfw = (float)((WIN - 1) * 0.5f);
+    const int max_level = lay.nlev - 1;
+    status = 1;
+    err = 0.f;
+    for (int l = max_level; l >= 0; --l) {
+        const int W = lay.w[l], H = lay.h[l];
+        const bool raw = l == 0 && p0.raw;
+        const int pitch = l == 0 ? p0.pitch : lay.pitch[l];
+        const int o0 = l == 0 ? p0.o0 : PAD * pitch + PAD;
+        const Plane PI = make_plane(l == 0 ? p0.i : I + lay.off[l], o0, pitch);
+        const Plane PJ = make_plane(l == 0 ? p0.j : J + lay.off[l], o0, pitch);
+        int lane_off[U];
+#pragma unroll
+        for (int s = 0; s < U; ++s) lane_off[s] = __mul24(u[s].row, pitch) + 7 * u[s].seg;
+        const float sc = ldexpf(1.f, -l);  // == (float)(1./(1 << l)), exact
+        float prevx = p0x * sc, prevy = p0y * sc;
+        float nextx, nexty;
+        if (l == max_level) {
+            if (cfg.use_initial_flow) {
+                nextx = nx * sc;
+                nexty = ny * sc;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = nx * 2.f;
+            nexty = ny * 2.f;
+        }
+        nx = nextx;
+        ny = nexty;
+        prevx -= halfw;
+        prevy -= halfw;
+        const float fpx = floorf(prevx), fpy = floorf(prevy);
+        const int ipx = (int)fpx, ipy = (int)fpy;
+        if (ipx < -WIN || ipx >= W || ipy < -WIN || ipy >= H) {
+            if (l == 0) {
+                status = 0;
+                err = 0.f;
+            }
+            continue;
+        }
+        uint32_t W0, W1;
+        weights(prevx - fpx, prevy - fpy, W0, W1);
+        int a11 = 0, a12 = 0, a22 = 0;
+        {
+            const bool fast = !raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H);
+            if (!fast) fill_win<G>(win, PI, W, H, ipx - 1, ipy - 1, WIN + 3, gl);
+            // every unit's derivative columns / rows inside the image
+            const bool interior = ipx >= 0 && ipx + WIN + 1 <= W && ipy >= 0 && ipy + WIN + 1 <= H;
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                uint32_t d[4][3];
+                load_i_unit(u[s], PI, lane_off[s], ipx, ipy, fast, win, d);
+                int t11, t12, t22;
+                extract_unit(u[s], d, W, H, ipx, ipy, interior, W0, W1, t11, t12, t22);
+                a11 += t11;
+                a12 += t12;
+                a22 += t22;
+                if constexpr (PPW > 1) unit_put(ust, s, u[s]);  // one unit per lane: kept in registers
+            }
+        }
+        float A11, A12, A22;
+        if constexpr (ACC == 0) {
+            group_sums_f32<G>(a11, a12, A11, A12);
+            A22 = group_sum_f32<G>(a22);
+        } else {
+            // Ix*Ix and Ix*Iy first, then Iy*Iy (exact int products < 2^24: the
+            // float conversion is exact, as OpenCV's fx*fx of converted values)
+            wave_lds_sync();  // the previous readers of the region are done
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                if (!u[s].valid) continue;
+                float v0[7], v1[7];
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const int x = half16(u[s].ix[t >> 1], t & 1), y = half16(u[s].iy[t >> 1], t & 1);
+                    v0[t] = (float)__mul24(x, x);
+                    v1[t] = (float)__mul24(x, y);
+                }
+                acc_put<ACC>(acc, 0, gl + s * G, v0);
+                acc_put<ACC>(acc, 1, gl + s * G, v1);
+            }
+            acc_chains_run<ACC>(acc, gl);
+            A11 = acc_result<ACC, false>(acc, 0);
+            A12 = acc_result<ACC, false>(acc, 1);
+#pragma unroll
+            for (int s = 0; s < U; ++s) {
+                if (!u[s].valid) continue;
+                float v0[7];
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const int y = half16(u[s].iy[t >> 1], t & 1);
+                    v0[t] = (float)__mul24(y, y);
+                }
+                acc_put<ACC>(acc, 0, gl + s * G, v0);
+            }
+            acc_chains_run<ACC>(acc, gl);
+            A22 = acc_result<ACC, false>(acc, 0);
+        }
+        A11 *= FLT_SCALE;
+        A12 *= FLT_SCALE;
+        A22 *= FLT_SCALE;
+        float D = A11 * A22 - A12 * A12;
+        const float minEig =
+            __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12), (float)(2 * WIN * WIN));
+        if (minEig < cfg.min_eig || D < __FLT_EPSILON__) {
+            if (l == 0) {
+                status = 0;
+                err = 0.f;
+            }
+            continue;
+        }
+        D = __fdiv_rn(1.f, D);
+
+        nextx -= halfw;
+        nexty -= halfw;
+        float pdx = 0.f, pdy = 0.f;
+        // the J rows of the last integer position: once the steps fall below a
+        // pixel the window stays on the same pixel grid and only the bilinear
+        // weights change, so the rows are reused instead of loaded again
+        int cinx = INT_MIN, ciny = INT_MIN;
+        uint32_t jr0[U][2], jr1[U][2];
+        // one exit, at the bottom: every loop-carried value is updated in place
+        // (with the early exits the register allocator copied all of them -- the
+        // cached J rows, the position, the previous step -- on every iteration)
+        bool more = cfg.max_iter > 0;
+        int j = 0;
+        while (more) {
+            const float fnx = floorf(nextx), fny = floorf(nexty);
+            // a window off the level ends the point's iterations (status 0 at level
+            // 0) with its position as it was.  The body still runs (no divergent
+            // branch around it: see the reloads below) at a position clamped into
+            // the padded level, and its result is discarded by the selects.
+            const bool oob = (int)fnx < -WIN || (int)fnx >= W || (int)fny < -WIN || (int)fny >= H;
+            const int inx = min(max((int)fnx, -WIN), W - 1), iny = min(max((int)fny, -WIN), H - 1);
+            uint32_t J0, J1;
+            weights(nextx - fnx, nexty - fny, J0, J1);
+            int b1 = 0, b2 = 0, es = 0;
+            // reload decisions are wave-uniform (ballots): a group whose position did
+            // not move reloads the same rows, and a border window of either group
+            // sends both groups through their LDS tiles (the tile path is correct for
+            // any window).  Branches on a group's own conditions made the compiler
+            // copy every cached row in and out of a second register set each
+            // iteration, to keep the other group's values.
+            if (__builtin_amdgcn_ballot_w64(inx != cinx || iny != ciny)) {
+                const bool fast =
+                    !__builtin_amdgcn_ballot_w64(raw && !(inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H));
+                if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
+                if (U > 1 && fast) {
+                    // every unit's two rows in flight before the first is realigned
+                    // (one memory round trip per reload, not one per unit; the
+                    // compiler otherwise reuses one unit's load registers and waits
+                    // in between: batch LK 0.449 -> 0.443 ms, r03 v39)
+                    const int base = PJ.o0 + iny * PJ.pitch + inx;
+                    v3u w0[U], w1[U];
+                    uint32_t sh[U];
+                    int al[U];
+#pragma unroll
+                    for (int s = 0; s < U; ++s) {
+                        const int off = lane_off[s] + base;
+                        al[s] = off & ~3;
+                        sh[s] = (uint32_t)off & 3u;
+                        w0[s] = __builtin_amdgcn_raw_buffer_load_b96(PJ.rs, al[s], 0, 0);
+                        w1[s] = __builtin_amdgcn_raw_buffer_load_b96(PJ.rs, al[s], PJ.pitch, 0);
+                    }
+#pragma unroll
+                    for (int s = 0; s < U; ++s) {
+                        jr0[s][0] = __builtin_amdgcn_alignbyte(w0[s].y, w0[s].x, sh[s]);
+                        jr0[s][1] = __builtin_amdgcn_alignbyte(w0[s].z, w0[s].y, sh[s]);
+                        jr1[s][0] = __builtin_amdgcn_alignbyte(w1[s].y, w1[s].x, sh[s]);
+                        jr1[s][1] = __builtin_amdgcn_alignbyte(w1[s].z, w1[s].y, sh[s]);
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < U; ++s)
+                        load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, jr0[s], jr1[s]);
+                }
+                cinx = inx;
+                ciny = iny;
+            }
+            float fb1, fb2;
+            if constexpr (ACC == 0) {
+                // a negative w11 anywhere in the wave (rare): the signed form (uniform branch)
+                if (__builtin_amdgcn_ballot_w64((int)J1 < 0)) {
+#pragma unroll
+                    for (int s = 0; s < U; ++s) {
+                        if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                        match_unit<false, true>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < U; ++s) {
+                        if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                        match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    }
+                }
+                group_sums_f32<G>(b1, b2, fb1, fb2);
+            } else {
+                wave_lds_sync();  // the previous readers of the region are done
+#pragma unroll
+                for (int s = 0; s < U; ++s) {
+                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                    float p1[7], p2[7];
+                    match_unit_f32(u[s], jr0[s], jr1[s], J0, J1, p1, p2);
+                    if (u[s].valid) {
+                        acc_put<ACC>(acc, 0, gl + s * G, p1);
+                        acc_put<ACC>(acc, 1, gl + s * G, p2);
+                    }
+                }
+                acc_chains_run<ACC>(acc, gl);
+                fb1 = acc_result<ACC, true>(acc, 0);
+                fb2 = acc_result<ACC, true>(acc, 1);
+            }
+            fb1 *= FLT_SCALE;
+            fb2 *= FLT_SCALE;
+            const float dx = (A12 * fb2 - A22 * fb1) * D;
+            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            const float tx = nextx + dx, ty = nexty + dy;
+            // delta.ddot(delta) <= eps^2 in double: dx*dx is exact in fp64, so the fma rounds once like the sum
+            const bool conv = __builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps;
+            const bool osc = !conv && j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f;
+            // (tx + halfw) - dx*0.5 in that order: next_pts = nextPt + halfWin, then -= delta*0.5
+            const float ux = osc ? (tx + halfw) - dx * 0.5f : tx + halfw;
+            const float uy = osc ? (ty + halfw) - dy * 0.5f : ty + halfw;
+            nx = oob ? nx : ux;
+            ny = oob ? ny : uy;
+            nextx = oob ? nextx : tx;
+            nexty = oob ? nexty : ty;
+            status = (oob && l == 0) ? 0 : status;
+            pdx = dx;
+            pdy = dy;
+            more = !oob && !conv && !osc && ++j < cfg.max_iter;
+            // two points: the first to stop hands the wave to the other (below)
+            if constexpr (SOLO) {
+                if (__builtin_amdgcn_ballot_w64(!more)) break;
+            }
+        }
+        if constexpr (SOLO) {
+            // One point of the wave still iterating (the loop was entered by both
+            // groups: a group that skipped the level never enters it, and then the
+            // other's exit leaves no lane with `more`).  Its iterations run on all
+            // 64 lanes, one window unit each (unit q on lane q, read from the LDS
+            // slot its group's lane q % 32 stored at slot q / 32): half the per-lane
+            // work of the two-unit body instead of a half-idle wave.  The sums are
+            // exact integers, so the lane partition does not change them.
+            const uint64_t m = __builtin_amdgcn_ballot_w64(more);
+            if (m) {
+                const int a = (uint32_t)m ? 0 : 1, src = a * G;
+                const auto rlf = [&](float v) {
+                    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+                };
+                float snx = rlf(nx), sny = rlf(ny), sxx = rlf(nextx), syy = rlf(nexty);
+                float spdx = rlf(pdx), spdy = rlf(pdy);
+                const float sA11 = rlf(A11), sA12 = rlf(A12), sA22 = rlf(A22), sD = rlf(D);
+                int sj = __builtin_amdgcn_readlane(j, src), sst = __builtin_amdgcn_readlane(status, src);
+                Unit v;
+                v.valid = lane < 63;
+                {
+                    const int kc = lane < 63 ? lane : 62;
+                    v.row = kc / 3;
+                    v.seg = kc - 3 * v.row;
+                }
+                const int voff = __mul24(v.row, pitch) + 7 * v.seg;
+                const v4u* vst = units + (src + (lane & (G - 1)));
+                const int vslot = lane / G;
+                uint32_t* swin = wins[a];
+                int cx = INT_MIN, cy = INT_MIN;
+                uint32_t vr0[2], vr1[2];
+                bool smore = true;
+                while (smore) {
+                    const float fnx = floorf(sxx), fny = floorf(syy);
+                    const bool oob = (int)fnx < -WIN || (int)fnx >= W || (int)fny < -WIN || (int)fny >= H;
+                    const int inx = min(max((int)fnx, -WIN), W - 1), iny = min(max((int)fny, -WIN), H - 1);
+                    uint32_t J0, J1;
+                    weights(sxx - fnx, syy - fny, J0, J1);
+                    int b1 = 0, b2 = 0, es = 0;
+                    if (inx != cx || iny != cy) {
+                        const bool fast = !(raw && !(inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H));
+                        if (!fast) fill_win<64>(swin, PJ, W, H, inx, iny, WIN + 1, lane);
+                        load_j_unit(v, PJ, voff, inx, iny, fast, swin, vr0, vr1);
+                        cx = inx;
+                        cy = iny;
+                    }
+                    unit_get(vst, vslot, v);
+                    if ((int)J1 < 0)
+                        match_unit<false, true>(v, vr0, vr1, J0, J1, v.valid, b1, b2, es);
+                    else
+                        match_unit<false>(v, vr0, vr1, J0, J1, v.valid, b1, b2, es);
+                    float fb1, fb2;
+                    group_sums_f32<64>(b1, b2, fb1, fb2);
+                    fb1 *= FLT_SCALE;
+                    fb2 *= FLT_SCALE;
+                    const float dx = (sA12 * fb2 - sA22 * fb1) * sD;
+                    const float dy = (sA12 * fb1 - sA11 * fb2) * sD;
+                    const float tx = sxx + dx, ty = syy + dy;
+                    const bool conv = __builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps;
+                    const bool osc = !conv && sj > 0 && fabsf(dx + spdx) < 0.01f && fabsf(dy + spdy) < 0.01f;
+                    const float ux = osc ? (tx + halfw) - dx * 0.5f : tx + halfw;
+                    const float uy = osc ? (ty + halfw) - dy * 0.5f : ty + halfw;
+                    snx = oob ? snx : ux;
+                    sny = oob ? sny : uy;
+                    sxx = oob ? sxx : tx;
+                    syy = oob ? syy : ty;
+                    sst = (oob && l == 0) ? 0 : sst;
+                    spdx = dx;
+                    spdy = dy;
+                    smore = !oob && !conv && !osc && ++sj < cfg.max_iter;
+                }
+                if (grp == a) {
+                    nx = snx;
+                    ny = sny;
+                    status = sst;
+                }
+            }
+        }
+        if (status && l == 0) {
+            // final error (OPTFLOW_LK_GET_MIN_EIGENVALS not set)
+            const float exf = nx - halfw, eyf = ny - halfw;
+            const float fex = floorf(exf), fey = floorf(eyf);
+            const int inx = (int)fex, iny = (int)fey;
+            if (inx < -WIN || inx >= W || iny < -WIN || iny >= H) {
+                status = 0;
+                continue;
+            }
+            if (!cfg.want_err) continue;
+            uint32_t J0, J1;
+            weights(exf - fex, eyf - fey, J0, J1);
+            int b1 = 0, b2 = 0, es = 0;
+            {
+                const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+                if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
+#pragma unroll
+                for (int s = 0; s < U; ++s) {
+                    uint32_t r0[2], r1[2];
+                    load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
+                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                    match_unit<true, true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                }
+            }
+            err = __fdiv_rn((float)group_sum<G>(es) * 1.f, (float)(32 * WIN * WIN));
+        }
+    }
+}
+
+// One launch for a batch of pairs: PPW points per wavefront, the points of a
+// wave always from one pair (wave-uniform plane bases); ceil(n_pts / PPW)
+// waves per pair, the spare groups of a pair's last wave recompute its last
+// point and store nothing.
+// Waves per workgroup.  One: a finished wave's slot (and its LDS) is refilled
+// at once instead of idling until the slowest wave of its workgroup is done
+// (per-point iteration counts differ).
+#ifndef KLT_WPB
+#define KLT_WPB 1
+#endif
+// minimum waves per SIMD the register allocation must allow
+// (the fp32-order instances are LDS-limited: 16 KB per two-point wave)
+template <int PPW, int ACC>
+constexpr int klt_occupancy() {
+    return PPW == 1 ? 4 : ACC ? 2 : 5;
+}
+template <int PPW, int ACC>
+__global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
+                                                  const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
+                                                  int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
+                                                  float* __restrict__ next_xy, float* __restrict__ back_xy,
+                                                  uint8_t* __restrict__ flags, float* __restrict__ err_out) {
+    constexpr int G = 64 / PPW;
+    __shared__ uint32_t wins[KLT_WPB * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
+    __shared__ v4u units[KLT_WPB][3 * PPW * 64];                  // per-lane window values
+    // fp32-order window sums: one region per point group
+    __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC_FLOATS];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair (launch capacity)
+    const int n_waves = a.n_pairs * wpp;
+    const int nb = (n_waves + KLT_WPB - 1) / KLT_WPB;
+    const int wg = xcd_swizzle(blockIdx.x, nb) * KLT_WPB + wv;
+    if (wg >= n_waves) return;
+    const int pair = wg / wpp;
+    // device-resident count (the per-frame loop without host round trips)
+    const int npt = a.n_dev ? min(a.n_pts, *a.n_dev) : a.n_pts;
+    if ((wg - pair * wpp) * PPW >= npt) return;  // the whole wave is past the count
+    // the group's point (a spare group of a pair's last wave recomputes the last
+    // point); rebuilt from the lane id where needed
+    auto point = [&](bool& writer) -> int64_t {
+        const int lane = lane_v(), pt_raw = (wg - pair * wpp) * PPW + lane / G;
+        writer = pt_raw < npt && (lane & (G - 1)) == 0;
+        return (int64_t)pair * a.n_pts + (pt_raw < npt ? pt_raw : npt - 1);
+    };
+    uint32_t(*wv_wins)[(WIN + 3) * WIN_DW] = wins + wv * PPW;
+    v4u* wv_units = units[wv];
+    float(*wv_accs)[ACC_FLOATS] = accs + (ACC ? wv * PPW : 0);
+    const uint8_t* I = pyr_prev + pair * prev_stride;
+    const uint8_t* J = pyr_next + pair * next_stride;
+    const L0Planes pf{l0.prev + pair * l0.prev_stride, l0.next + pair * l0.next_stride, l0.o0, l0.pitch,
+                      l0.raw != 0};
+    const L0Planes pb{pf.j, pf.i, pf.o0, pf.pitch, pf.raw};
+    LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, a.use_initial_flow, err_out != nullptr};
+    bool writer;
+    int64_t gp = point(writer);
+    float nx = 0.f, ny = 0.f;
+    int st = 1;
+    float e = 0.f;
+    {
+        const float p0x = prev_xy[2 * gp], p0y = prev_xy[2 * gp + 1];
+        const float* init_xy = a.init_xy ? a.init_xy : next_xy;
+        nx = init_xy[2 * gp];
+        ny = init_xy[2 * gp + 1];
+        if constexpr (ACC != 0) {
+            const int lane = lane_v();
+            acc_clear<ACC, G>(wv_accs[lane / G], lane & (G - 1));
+        }
+        lk_group<PPW, ACC>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, wv_wins, wv_units, wv_accs);
+    }
+    if (a.mode == 0) {
+        gp = point(writer);
+        if (writer) {
+            next_xy[2 * gp] = nx;
+            next_xy[2 * gp + 1] = ny;
+            flags[gp] = (uint8_t)st;
+            if (err_out) err_out[gp] = e;
+        }
+        return;
+    }
+    // backward: prevPts = forward result, initial flow = original prev points
+    // (re-read: an opaque copy of the pointer keeps the compiler from holding
+    // the first load's values live across the forward pass)
+    const float* pxy = prev_xy;
+    asm volatile("" : "+s"(pxy));
+    gp = point(writer);
+    float bx = pxy[2 * gp], by = pxy[2 * gp + 1];
+    int st2 = 1;
+    float e2 = 0.f;
+    cfg.use_initial_flow = 1;
+    cfg.want_err = 0;  // the backward error is not reported
+    lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, wv_wins, wv_units, wv_accs);
+    gp = point(writer);
+    if (writer) {
+        const float p0x = pxy[2 * gp], p0y = pxy[2 * gp + 1];
+        const double B = a.border;
+        const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
+        const double ddx = (double)(bx - p0x), ddy = (double)(by - p0y);
+        const double dist = __dsqrt_rn(ddx * ddx + ddy * ddy);
+        const bool keep = st && st2 && !on_border && dist < a.fb_thresh;
+        next_xy[2 * gp] = nx;
+        next_xy[2 * gp + 1] = ny;
+        if (back_xy) {
+            back_xy[2 * gp] = bx;
+            back_xy[2 * gp + 1] = by;
+        }
+        flags[gp] = (uint8_t)((st ? 1 : 0) | (st2 ? 2 : 0) | (keep ? 4 : 0));
+        if (err_out) err_out[gp] = e;
+    }
+}
+
+
+// reduceVector (tracking.cc:831-839): order-preserving index compaction of the
+// keep bit, one workgroup per pair.
+__global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* __restrict__ flags,
+                                                      int32_t* __restrict__ kept_idx, int32_t* __restrict__ n_kept) {
+    __shared__ int wsum[4];
+    const int pair = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint8_t* f = flags + (int64_t)pair * n_pts;
+    int32_t* out = kept_idx + (int64_t)pair * n_pts;
+    int base = 0;
+    for (int start = 0; start < n_pts; start += 256) {
+        const int i = start + tid;
+        const bool k = i < n_pts && (f[i] & 4);
+        const unsigned long long m = __ballot(k);
+        const int before = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wv] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int q = 0; q < wv; ++q) off += wsum[q];
+        if (k) out[off + before] = i;
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+        base += tot;
+    }
+    if (tid == 0) n_kept[pair] = base;
+}
+
+}  // namespace
+
+// Points per wavefront of the LK launch.  Batches that fill the chip take 2
+// (the per-point scalar work is shared; 0.47 vs 0.61 ms per 256 pairs); small
+// ones (one frame of a sequence: 150 points) take 1, which halves the work of
+// the slowest wave (41 vs 54 us per frame), built for 4 waves per SIMD (no
+// spills; at most 4 waves per SIMD below the threshold: 36.8 -> 35.8 us per
+// sequence frame, 50.3 -> 49.0 us per pair, r02 v18).
+static int klt_ppw(int64_t total_points) { return total_points <= 4096 ? 1 : 2; }
+
+template <int PPW, int ACC>
+static void launch_klt_ppw(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                           const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                           const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                           float* err) {
+    const int n_waves = a.n_pairs * ((a.n_pts + PPW - 1) / PPW);
+    dim3 grid((unsigned)(N_XCD * xcd_per((n_waves + KLT_WPB - 1) / KLT_WPB)));
+    launch_timed(c, "klt", klt_kernel<PPW, ACC>, grid, dim3(64 * KLT_WPB), 0, a, lay, pyr_prev, pyr_next,
+                 prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
+}
+
+template <int ACC>
+static void launch_klt_acc(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                           const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                           const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                           float* err) {
+    if (klt_ppw((int64_t)a.n_pairs * a.n_pts) == 1)
+        launch_klt_ppw<1, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                               next_xy, back_xy, flags, err);
+    else
+        launch_klt_ppw<2, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                               next_xy, back_xy, flags, err);
+}
+
+hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                      const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                      const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy, uint8_t* flags,
+                      float* err) {
+    const int64_t total = (int64_t)a.n_pairs * a.n_pts;
+    if (total <= 0) return hipSuccess;
+    if (total > (int64_t)1 << 30) return hipErrorInvalidValue;  // wave indices are int32
+    switch (a.accum) {
+        case GVX_LK_ACCUM_EXACT:
+            launch_klt_acc<0>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+            break;
+        case GVX_LK_ACCUM_F32_SCALAR:
+            launch_klt_acc<1>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+            break;
+        case GVX_LK_ACCUM_F32_SIMD4:
+            launch_klt_acc<2>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy,
+                              back_xy, flags, err);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
+                          int32_t* n_kept) {
+    if (n_pairs <= 0) return hipSuccess;
+    return launch_timed(c, "compact", compact_kernel, dim3(n_pairs), dim3(256), 0, n_pts, flags, kept_idx, n_kept);
+}
+
+}  // namespace gvx
