@@ -1,0 +1,1163 @@
+// preint.hip -- batched IMU preintegration for gfx950 (fp64).
+//
+// Replaces Preintegration::createPreintegration + addNewImu for k = 1..m-1
+// (/root/reference/ic_gvins/ic_gvins/ic_gvins.cc:946-953) for both reachable
+// variants: PreintegrationNormal (preintegration_normal.cc:183-232 with
+// preintegration_base.cc:39-70) and PreintegrationEarth
+// (preintegration_earth.cc:205-303).
+//
+// One 64-lane wavefront per segment; the scan over IMU samples is sequential.
+// Per step every lane evaluates the (uniform) state update, then the 15x15
+// products J <- Phi J and P <- Phi P Phi^T + Qk are spread over the lanes
+// (entries e = lane + 64 r).  Phi, G and the noise are structurally sparse; the
+// sparse sums visit the non-zero terms in ascending k like the dense products
+// of the reference (adding an exact 0*x never changes a non-zero sum), so the
+// GPU J/P match the sequential CPU restatement up to the fp64 sin/cos of the
+// rotation-vector exponentials and the fused multiply-adds of phi_mv.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdlib>
+
+#include "dmath.h"
+#include "gvx_internal.h"
+
+namespace gvx {
+
+namespace {
+
+constexpr int NS = 15;
+
+// q / |q| through one reciprocal square root (v_rsq_f64 and two fused Newton
+// steps) instead of a square root and four divisions: within an ulp or two of
+// Eigen's normalized(), and a shorter dependent chain for the quaternion
+// recursions (their contract is 1e-10 relative)
+__device__ __forceinline__ dq dq_renorm(dq q) {
+    const double n2 = dq_sqnorm(q);
+    if (n2 > 0) {
+        double y = __builtin_amdgcn_rsq(n2);
+        double e = __builtin_fma(-n2 * y, y, 1.0);
+        y = __builtin_fma(0.5 * y, e, y);
+        e = __builtin_fma(-n2 * y, y, 1.0);
+        y = __builtin_fma(0.5 * y, e, y);
+        q.x *= y;
+        q.y *= y;
+        q.z *= y;
+        q.w *= y;
+    }
+    return q;
+}
+
+// Every kernel below is one wavefront per workgroup: its LDS traffic is in order
+// within the wave, so a step's hand-over through LDS needs a compiler fence, not
+// s_barrier and the lgkmcnt(0) drain in front of it.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct Imu {
+    double dt, dth[3], dv[3], time;
+};
+
+__device__ __forceinline__ Imu load_imu(const gvx_imu* p, const double* bg, const double* ba) {
+    // PreintegrationBase::compensationBias (preintegration_base.cc:86-92)
+    Imu r;
+    r.time = p->time;
+    r.dt = p->dt;
+    for (int i = 0; i < 3; ++i) {
+        r.dth[i] = p->dtheta[i] - p->dt * bg[i];
+        r.dv[i] = p->dvel[i] - p->dt * ba[i];
+    }
+    return r;
+}
+
+// Quantities of step k that depend only on the IMU samples, the (constant)
+// biases, iewn and the running delta_time -- not on the recursion.  They
+// carry all the transcendental work (rotvec2quaternion) and are computed for
+// CH steps at once, one step per lane, before the sequential part.
+struct StepPre {
+    double dt, time, dtime;    // dt, sample time, delta_time after this step
+    double dvfb[3];            // two-sample sculling (preintegration_base.cc:47-48)
+    double dv[3], dth[3];      // bias-compensated dvel / dtheta (Phi's C and M blocks)
+    double qd[4];              // rotvec2quaternion(dtheta + coning)
+    double qnn[4];             // Earth: rotvec2quaternion(-iewn dt)
+    double qa[4], qb[4];       // Earth: q0^-1 q(-(dtime - dt/2) iewn) q0, q0^-1 q(-dtime iewn) q0
+};
+constexpr int PRE_DW = sizeof(StepPre) / 8;
+
+// Sparse Phi (updateJacobianAndCovariance: preintegration_base.cc:94-125,
+// preintegration_earth.cc:266-303) applied to one column vector; terms in
+// ascending k like the dense product, each multiply-add fused (one rounding
+// instead of Eigen's two: 1e-16 relative per step, inside the 1e-10 contract;
+// 0.418 -> 0.390 ms per configs[3] launch, profiles/r04_v12/cov).
+struct Phi {
+    double dt, f;        // Phi(0:3, 3:6) = dt I ; Phi(9:15, 9:15) = (1 - dt/T) I
+    double C[9];         // Phi(3:6, 6:9) = cbb0 * skew(dvel)
+    double D[9];         // Phi(3:6, 12:15) = cbb0 * dt
+    double M[9];         // Phi(6:9, 6:9) = I - skew(dtheta); Phi(6:9, 9:12) = -dt I
+};
+
+__device__ __forceinline__ void phi_mv(const Phi& f, const double* v, double* y) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = __builtin_fma(f.dt, v[3 + i], v[i]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double s = v[3 + a];
+        s = __builtin_fma(f.C[3 * a], v[6], s);
+        s = __builtin_fma(f.C[3 * a + 1], v[7], s);
+        s = __builtin_fma(f.C[3 * a + 2], v[8], s);
+        s = __builtin_fma(f.D[3 * a], v[12], s);
+        s = __builtin_fma(f.D[3 * a + 1], v[13], s);
+        s = __builtin_fma(f.D[3 * a + 2], v[14], s);
+        y[3 + a] = s;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double s = f.M[3 * a] * v[6];
+        s = __builtin_fma(f.M[3 * a + 1], v[7], s);
+        s = __builtin_fma(f.M[3 * a + 2], v[8], s);
+        s = __builtin_fma(-f.dt, v[9 + a], s);
+        y[6 + a] = s;
+    }
+#pragma unroll
+    for (int i = 9; i < NS; ++i) y[i] = f.f * v[i];
+}
+
+// P'(:,c) = Phi K + a W phi_c for rows 3..14 (rows 0..2 have no Q term): the
+// W(3:6,3:6) block times phi_c(3:6) and the constant diagonal of W from row 6 on
+// (wg, nbg, nba), multiply-adds fused.  Shared by every covariance kernel so
+// their outputs stay the same bits.
+__device__ __forceinline__ void q_terms(double a, const double* W, double wg, double nbg, double nba,
+                                        const double* ph, const double* y, double* P) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double u = W[3 * i] * ph[3];
+        u = __builtin_fma(W[3 * i + 1], ph[4], u);
+        u = __builtin_fma(W[3 * i + 2], ph[5], u);
+        P[3 + i] = __builtin_fma(a, u, y[3 + i]);
+    }
+    const double ag = a * wg, abg = a * nbg, aba = a * nba;
+#pragma unroll
+    for (int i = 6; i < 15; ++i) P[i] = __builtin_fma(i < 9 ? ag : (i < 12 ? abg : aba), ph[i], y[i]);
+}
+
+constexpr int GL = 16;                  // lanes per segment: lane c owns column c of J and row c of P
+constexpr int SPW = 64 / GL;            // segments per (one-wave) workgroup
+constexpr int CH = GL;                  // steps per precompute chunk (one per lane)
+constexpr int MS = NS * NS;
+
+// One wavefront = 4 segments x 16 lanes.  Per IMU step:
+//   * the state recursion (cheap once the StepPre terms exist) runs redundantly
+//     on the 16 lanes of a segment, so Phi's blocks are in every lane's registers;
+//   * J <- Phi J: lane c updates column c (sparse mat-vec, 45 MAC);
+//   * P <- Phi P Phi^T + Qk, Qk = a (Phi W + W Phi^T), a = dt/2, W = gt N gt^T
+//     (block diagonal): lane c writes G(:,c) = Phi P(:,c) to LDS and reads row
+//     c back; with P symmetric, P Phi^T = G^T, so
+//     P'(:,c) = Phi (G(c,:)^T + a W(:,c)) + a W Phi(c,:)^T.
+// Sums are reassociated against the dense Eigen products (relative 1e-16 per
+// step); the parity bound is 1e-10 of each block's magnitude (tests/test_ba_gpu.py).
+__global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params prm, int n_seg,
+                                                    const gvx_imu* __restrict__ imu,
+                                                    const int32_t* __restrict__ seg_off,
+                                                    const gvx_state* __restrict__ state0,
+                                                    const double* __restrict__ iewn_in,
+                                                    gvx_preint_result* __restrict__ out,
+                                                    double* __restrict__ pn) {
+    __shared__ double sPre[SPW][CH][PRE_DW];
+    __shared__ double sG[SPW][MS];
+    const int lane = threadIdx.x;
+    const int grp = lane / GL, c = lane % GL;
+    const int seg = blockIdx.x * SPW + grp;
+    const bool live = seg < n_seg;
+    const int b0 = live ? seg_off[seg] : 0;
+    const int m = live ? seg_off[seg + 1] - b0 : 0;
+    // wave-uniform trip count over the 4 segments (ragged m)
+    int mmax = m;
+#pragma unroll
+    for (int o = GL; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+    const gvx_imu* im = imu + b0;
+    double* pns = (pn && live) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    const bool earth = variant == GVX_PREINT_EARTH;
+
+    // ---- constructor: resetState(state, NUM_STATE) + setNoiseMatrix ----
+    gvx_state cur = live ? state0[seg] : gvx_state{};
+    double dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+    dq dqt = dq_make(1, 0, 0, 0);
+    double bg[3], ba[3];
+    for (int i = 0; i < 3; ++i) {
+        bg[i] = cur.bg[i];
+        ba[i] = cur.ba[i];
+    }
+    const dq q0 = dq_load(cur.q);
+    const dq q0i = dq_inv(q0);
+    double iewn[3] = {0, 0, 0};
+    if (earth && live)
+        for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    const double g3[3] = {0, 0, prm.gravity};
+    const double ngyr = prm.gyr_arw * prm.gyr_arw, nacc = prm.acc_vrw * prm.acc_vrw;
+    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
+    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
+    const double g60 = earth ? -1.0 : 1.0;
+    const double wg = (g60 * ngyr) * g60;
+    // W's constant diagonal from row 6 on: (g60 N_g g60, N_bg, N_ba)
+    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    double Jc[NS], Pc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        Jc[i] = i == c ? 1.0 : 0.0;
+        Pc[i] = 0.0;
+    }
+    double delta_time = 0.0;
+    double* pre_base = &sPre[grp][0][0];
+
+    for (int kc = 1; kc < mmax; kc += CH) {
+        // ---- precompute StepPre for steps kc .. kc+CH-1, one per lane ----
+        {
+            const int k = kc + c;
+            StepPre sp;
+            if (k < m) {
+                const Imu pr = load_imu(im + k - 1, bg, ba);
+                const Imu ic = load_imu(im + k, bg, ba);
+                double dtime = delta_time;
+                for (int i = kc; i <= k; ++i) dtime += im[i].dt;  // sequential, as delta_time_ += dt
+                sp.dt = ic.dt;
+                sp.time = ic.time;
+                sp.dtime = dtime;
+                double c1[3], c2[3], c3[3], dth[3];
+                cross3(ic.dth, ic.dv, c1);
+                cross3(pr.dth, ic.dv, c2);
+                cross3(pr.dv, ic.dth, c3);
+                for (int i = 0; i < 3; ++i) sp.dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
+                cross3(pr.dth, ic.dth, c1);
+                for (int i = 0; i < 3; ++i) {
+                    dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
+                    sp.dv[i] = ic.dv[i];
+                    sp.dth[i] = ic.dth[i];
+                }
+                dq_store(dq_from_rotvec(dth), sp.qd);
+                if (earth) {
+                    const double dt = ic.dt;
+                    const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
+                    dq_store(dq_from_rotvec(dnn), sp.qnn);
+                    const double sc = -(dtime - 0.5 * dt);
+                    const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
+                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), sp.qa);
+                    const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
+                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), sp.qb);
+                }
+                const double* w = reinterpret_cast<const double*>(&sp);
+                double* dst = pre_base + c * PRE_DW;
+                for (int i = 0; i < PRE_DW; ++i) dst[i] = w[i];
+            }
+        }
+        wave_lds_sync();
+        const int kend = min(kc + CH, mmax);
+        for (int k = kc; k < kend; ++k) {
+            const bool act = k < m;
+            Phi f;
+            double Wv[9];
+            if (act) {
+                const StepPre& sp = *reinterpret_cast<const StepPre*>(pre_base + (k - kc) * PRE_DW);
+                const double dt = sp.dt;
+                delta_time = sp.dtime;
+                const dq qd = dq_load(sp.qd);
+                double R[9], dvel[3], cbb0[9];
+                if (!earth) {
+                    // PreintegrationNormal::integrationProcess (preintegration_normal.cc:183-214)
+                    dq_rot(dq_load(cur.q), R);
+                    mv3(R, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + g3[i] * dt;
+                    for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
+                    dq_store(dq_renorm(dq_mul(dq_load(cur.q), qd)), cur.q);
+                    dq_rot(dqt, R);
+                    mv3(R, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
+                    dqt = dq_renorm(dq_mul(dqt, qd));
+                    dq_rot(dqt, R);
+                    for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
+                } else {
+                    // PreintegrationEarth::integrationProcess (preintegration_earth.cc:205-260)
+                    double cc[3], dvcg[3], T[9], M1[9];
+                    cross3(iewn, cur.v, cc);
+                    for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc[i]) * dt;
+                    dq_rot(dq_load(sp.qnn), T);
+                    for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
+                    dq_rot(dq_load(cur.q), R);
+                    mm3(M1, R, T);
+                    mv3(T, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dvel[i] = dvel[i] + dvcg[i];
+                    for (int i = 0; i < 3; ++i) cur.p[i] += dt * cur.v[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) cur.v[i] += dvel[i];
+                    if (pns && c == 0) {
+                        pns[4 * (k - 1)] = dt;
+                        pns[4 * (k - 1) + 1] = cur.p[0];
+                        pns[4 * (k - 1) + 2] = cur.p[1];
+                        pns[4 * (k - 1) + 3] = cur.p[2];
+                    }
+                    dq_store(dq_renorm(dq_mul(dq_mul(dq_load(sp.qnn), dq_load(cur.q)), qd)), cur.q);
+                    dq_rot(dq_mul(dq_load(sp.qa), dqt), R);
+                    mv3(R, sp.dvfb, dvel);
+                    for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * dvel[i];
+                    for (int i = 0; i < 3; ++i) dv[i] += dvel[i];
+                    dqt = dq_renorm(dq_mul(dqt, qd));
+                    dq_rot(dq_mul(dq_load(sp.qb), dqt), R);
+                    for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
+                }
+                cur.time = sp.time;
+                // gt(3:6, 3:6) = R (Normal) or cbb0 (Earth); W(3:6, 3:6) = gR N_v gR^T
+                const double sg = earth ? 1.0 : -1.0;  // gR = sg * cbb0
+                double gR[9];
+                for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) {
+                        double g = (gR[3 * a] * nacc) * gR[3 * b];
+                        g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+                        g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+                        Wv[3 * a + b] = g;
+                    }
+                double S[9];
+                skew(sp.dv, S);
+                mm3(cbb0, S, f.C);
+                for (int i = 0; i < 9; ++i) f.D[i] = cbb0[i] * dt;
+                skew(sp.dth, S);
+                for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+                f.dt = dt;
+                f.f = 1 - dt / prm.corr_time;
+
+                // G(:,c) = Phi P(:,c) to LDS; J <- Phi J
+                double y[NS];
+                phi_mv(f, Pc, y);
+                if (c < NS) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
+                }
+                phi_mv(f, Jc, y);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            }
+            wave_lds_sync();
+            if (act) {
+                const double a = 0.5 * f.dt;
+                const int cl = c < NS ? c : 0;
+                // K(:,c) = G(c,:)^T + a W(:,c)   (P symmetric: P Phi^T = (Phi P)^T)
+                double K[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
+                if (c >= 3 && c < 6) {
+                    K[3] = K[3] + a * Wv[c - 3];
+                    K[4] = K[4] + a * Wv[3 + c - 3];
+                    K[5] = K[5] + a * Wv[6 + c - 3];
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i)
+                    if (i == c) K[i] = K[i] + a * wd(i);
+                // phi_c = row c of Phi (lane-dependent selects)
+                const int r3 = c - 3, r6 = c - 6;
+                double ph[NS];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    ph[3 + b] = (c == b) ? f.dt : (c == 3 + b ? 1.0 : 0.0);
+                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
+                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
+                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
+                    ph[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
+                    ph[9 + b] = (c == 6 + b) ? -f.dt : (c == 9 + b ? f.f : 0.0);
+                    ph[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (c == 12 + b ? f.f : 0.0);
+                }
+                // P'(:,c) = Phi K(:,c) + a W phi_c
+                double y[NS];
+                phi_mv(f, K, y);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[i] = y[i];
+                q_terms(a, Wv, wg, nbg, nba, ph, y, Pc);
+            }
+            wave_lds_sync();
+        }
+    }
+
+    // ---- outputs ----
+    if (!live) return;
+    gvx_preint_result* o = out + seg;
+    if (c < NS) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            o->jacobian[i * NS + c] = Jc[i];
+            o->covariance[c * NS + i] = Pc[i];
+        }
+    }
+    if (c == 0) {
+        o->variant = variant;
+        o->m = m;
+        o->delta_time = delta_time;
+        o->start_time = im[0].time;
+        o->end_time = m > 1 ? im[m - 1].time : im[0].time;
+        o->current = cur;
+        gvx_state d;
+        d.time = 0;
+        for (int i = 0; i < 3; ++i) {
+            d.p[i] = dp[i];
+            d.v[i] = dv[i];
+            d.bg[i] = bg[i];
+            d.ba[i] = ba[i];
+            o->gravity[i] = g3[i];
+            o->iewn[i] = iewn[i];
+        }
+        dq_store(dqt, d.q);
+        o->delta = d;
+        dq_store(q0, o->q0);
+    }
+}
+
+// ------------------------------------------------ four-launch preintegration
+// preint_kernel's sequential part runs on every lane of a wave that serves 4
+// segments: the wave's issue time per step is the same whether it advances 4
+// segments or 64, and 5,247 segments give 1.3 k such waves for 1,024 SIMDs.
+// Of that part only the two quaternion chains (cur.q and the delta rotation
+// dqt) and the velocity / position sums are truly sequential; the rotation
+// matrices and rotated increments of a step follow from the chain values.  So:
+//   preint_pre_kernel    one lane per STEP (a workgroup per segment): the
+//                        StepPre terms -- every transcendental of the step;
+//   preint_chain_kernel  one lane per SEGMENT (64 per wave): the two quaternion
+//                        chains alone, StepPre prefetched three steps ahead;
+//   preint_rot_kernel    one lane per STEP: the rotated increments of the
+//                        velocity updates and cbb0 from the chain values;
+//   preint_cov_kernel    16 lanes per segment: the velocity / position sums
+//                        (a few adds per step, on every lane of the group), J <-
+//                        Phi J and P <- Phi P Phi^T + Qk with Phi and W rebuilt
+//                        from cbb0 and the IMU sample.
+// Every value is formed by the same operations in the same order as in
+// preint_kernel, so the results are the same bits (tests/test_ba_gpu.py).
+struct PreG {                // StepPre terms of one step (scratch, per IMU step)
+    double dtime;            // delta_time after the step
+    double dvfb[3];
+    double qd[4];
+    double qnn[4], qa[4], qb[4];  // Earth only
+};
+constexpr int PREG_DW = sizeof(PreG) / 8;  // 20
+constexpr int PREG_NORMAL_DW = 8;          // dtime, dvfb, qd
+struct QRec {                // the chains after step k
+    double q[4], dqt[4];
+};
+struct RRec {                // rotated terms of step k
+    double cbb0[9];          // -R(dqt) (Normal) or -R(qb dqt) (Earth)
+    double a[3];             // velocity increment before gravity / Coriolis
+    double b[3];             // delta-velocity increment
+    double pad;
+};
+constexpr int RREC_DW = sizeof(RRec) / 8;  // 16
+constexpr size_t STEP_SCRATCH = sizeof(PreG) + sizeof(QRec) + sizeof(RRec);
+
+__global__ void __launch_bounds__(64) preint_pre_kernel(int variant, int n_seg, const gvx_imu* __restrict__ imu,
+                                                        const int32_t* __restrict__ seg_off,
+                                                        const gvx_state* __restrict__ state0,
+                                                        const double* __restrict__ iewn_in, PreG* __restrict__ pre) {
+    const int seg = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int b0 = seg_off[seg];
+    const int m = seg_off[seg + 1] - b0;
+    const gvx_imu* im = imu + b0;
+    PreG* pg = pre + (b0 - seg);
+    const bool earth = variant == GVX_PREINT_EARTH;
+    const gvx_state& s0 = state0[seg];
+    double bg[3], ba[3], iewn[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        bg[i] = s0.bg[i];
+        ba[i] = s0.ba[i];
+    }
+    const dq q0 = dq_load(s0.q);
+    const dq q0i = dq_inv(q0);
+    if (earth)
+        for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    double base = 0.0;  // delta_time before the chunk
+    for (int kc = 1; kc < m; kc += 64) {
+        const int k = kc + lane;
+        const int cnt = min(64, m - kc);
+        // delta_time_ += dt in sample order: a running sum over the chunk's
+        // samples (read lane by lane), lane k keeps its prefix
+        const double mydt = k < m ? im[k].dt : 0.0;
+        double acc = base, dtime = 0.0;
+        for (int i = 0; i < cnt; ++i) {
+            acc += __shfl(mydt, i);
+            if (lane == i) dtime = acc;
+        }
+        base = acc;
+        if (k >= m) continue;
+        const Imu pr = load_imu(im + k - 1, bg, ba);
+        const Imu ic = load_imu(im + k, bg, ba);
+        PreG g;
+        g.dtime = dtime;
+        double c1[3], c2[3], c3[3], dth[3];
+        cross3(ic.dth, ic.dv, c1);
+        cross3(pr.dth, ic.dv, c2);
+        cross3(pr.dv, ic.dth, c3);
+        for (int i = 0; i < 3; ++i) g.dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
+        cross3(pr.dth, ic.dth, c1);
+        for (int i = 0; i < 3; ++i) dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
+        dq_store(dq_from_rotvec(dth), g.qd);
+        double* dst = reinterpret_cast<double*>(pg + (k - 1));
+        const double* w = reinterpret_cast<const double*>(&g);
+        if (earth) {
+            const double dt = ic.dt;
+            const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
+            dq_store(dq_from_rotvec(dnn), g.qnn);
+            const double sc = -(dtime - 0.5 * dt);
+            const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
+            dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), g.qa);
+            const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
+            dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), g.qb);
+#pragma unroll
+            for (int i = 0; i < PREG_DW; i += 2)
+                *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+        } else {
+#pragma unroll
+            for (int i = 0; i < PREG_NORMAL_DW; i += 2)
+                *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+        }
+    }
+}
+
+// The quaternion chains, and every output field that does not depend on the
+// velocity / position sums or on J / P.
+#ifndef PREINT_CHAIN_CK
+#define PREINT_CHAIN_CK 8
+#endif
+template <bool EARTH>
+__global__ void __launch_bounds__(128) preint_chain_kernel(gvx_imu_params prm, int n_seg,
+                                                           const gvx_imu* __restrict__ imu,
+                                                           const int32_t* __restrict__ seg_off,
+                                                           const gvx_state* __restrict__ state0,
+                                                           const double* __restrict__ iewn_in,
+                                                           const PreG* __restrict__ pre, QRec* __restrict__ qrec,
+                                                           gvx_preint_result* __restrict__ out) {
+    // wave 0 runs the cur.q chain, wave 1 the dqt chain of the same 64 segments:
+    // the two chains are independent, and each wave issues half the work
+    const bool dwave = threadIdx.x >= 64;
+    const int seg = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (seg >= n_seg) return;  // no barriers below
+    const int b0 = seg_off[seg];
+    const int m = seg_off[seg + 1] - b0;
+    const gvx_imu* im = imu + b0;
+    const double* pg = reinterpret_cast<const double*>(pre + (b0 - seg));
+    double* qs = reinterpret_cast<double*>(qrec + (b0 - seg)) + (dwave ? 4 : 0);
+    constexpr bool earth = EARTH;
+    constexpr int variant = EARTH ? GVX_PREINT_EARTH : GVX_PREINT_NORMAL;
+    const gvx_state s0 = state0[seg];
+    // the q chain reads qd and qnn (PreG doubles 4..11), the dqt chain qd
+    const bool two = earth && !dwave;
+    dq q = dwave ? dq_make(1, 0, 0, 0) : dq_load(s0.q);
+    // StepPre inputs in chunks of CK steps: chunk i+1 is loaded while chunk i
+    // runs and copied over at the chunk's end, so each load has CK steps of the
+    // chain to land (loads never predicated: a clamped index)
+    constexpr int CK = PREINT_CHAIN_CK;
+    const int last = m >= 2 ? m - 2 : 0;
+    auto ldc = [&](int kc, double (&X)[CK][8]) {
+#pragma unroll
+        for (int j = 0; j < CK; ++j) {
+            const double* src = pg + (size_t)min(kc + j - 1, last) * PREG_DW + 4;
+            const double2 v0 = *reinterpret_cast<const double2*>(src);
+            const double2 v1 = *reinterpret_cast<const double2*>(src + 2);
+            X[j][0] = v0.x;
+            X[j][1] = v0.y;
+            X[j][2] = v1.x;
+            X[j][3] = v1.y;
+            if (two) {
+                const double2 v2 = *reinterpret_cast<const double2*>(src + 4);
+                const double2 v3 = *reinterpret_cast<const double2*>(src + 6);
+                X[j][4] = v2.x;
+                X[j][5] = v2.y;
+                X[j][6] = v3.x;
+                X[j][7] = v3.y;
+            }
+        }
+    };
+    auto step = [&](int k, const double (&r)[8]) {
+        const dq qd = dq_load(r);
+        if (two)
+            q = dq_renorm(dq_mul(dq_mul(dq_load(r + 4), q), qd));
+        else  // Normal cur.q, and dqt in both variants
+            q = dq_renorm(dq_mul(q, qd));
+        *reinterpret_cast<double4*>(qs + (size_t)(k - 1) * 8) = double4{q.x, q.y, q.z, q.w};
+    };
+    double X[CK][8], Y[CK][8];
+    if (m > 1) ldc(1, X);
+    for (int kc = 1; kc < m; kc += 2 * CK) {
+        // two chunks per trip, X and Y in turn: each chunk's loads are issued a
+        // whole chunk of steps before its first step, with no register copies
+        ldc(kc + CK, Y);
+#pragma unroll
+        for (int j = 0; j < CK; ++j)
+            if (kc + j < m) step(kc + j, X[j]);
+        ldc(kc + 2 * CK, X);
+#pragma unroll
+        for (int j = 0; j < CK; ++j)
+            if (kc + CK + j < m) step(kc + CK + j, Y[j]);
+    }
+    gvx_preint_result* o = out + seg;
+    if (dwave) {
+        o->delta.time = 0;
+        dq_store(q, o->delta.q);
+        return;
+    }
+    dq_store(q, o->current.q);
+    o->variant = variant;
+    o->m = m;
+    o->delta_time = m > 1 ? pg[(size_t)(m - 2) * PREG_DW] : 0.0;
+    o->start_time = im[0].time;
+    o->end_time = m > 1 ? im[m - 1].time : im[0].time;
+    o->current.time = m > 1 ? im[m - 1].time : s0.time;
+    for (int i = 0; i < 3; ++i) {
+        o->current.bg[i] = s0.bg[i];
+        o->current.ba[i] = s0.ba[i];
+        o->delta.bg[i] = s0.bg[i];
+        o->delta.ba[i] = s0.ba[i];
+        o->gravity[i] = i == 2 ? prm.gravity : 0.0;
+        o->iewn[i] = earth ? iewn_in[3 * seg + i] : 0.0;
+    }
+    dq_store(dq_load(s0.q), o->q0);
+}
+
+__global__ void __launch_bounds__(64) preint_rot_kernel(int variant, int n_seg, const int32_t* __restrict__ seg_off,
+                                                        const gvx_state* __restrict__ state0,
+                                                        const PreG* __restrict__ pre,
+                                                        const QRec* __restrict__ qrec, RRec* __restrict__ rrec) {
+    const bool earth = variant == GVX_PREINT_EARTH;
+    for (int seg = blockIdx.x; seg < n_seg; seg += gridDim.x) {  // waves loop over segments
+    const int b0 = seg_off[seg];
+    const int m = seg_off[seg + 1] - b0;
+    const size_t o0 = (size_t)(b0 - seg);
+    for (int k = 1 + threadIdx.x; k < m; k += 64) {
+        const PreG& g = pre[o0 + k - 1];
+        const dq qprev = k > 1 ? dq_load(qrec[o0 + k - 2].q) : dq_load(state0[seg].q);
+        const dq dprev = k > 1 ? dq_load(qrec[o0 + k - 2].dqt) : dq_make(1, 0, 0, 0);
+        const dq dcur = dq_load(qrec[o0 + k - 1].dqt);
+        double dvfb[3] = {g.dvfb[0], g.dvfb[1], g.dvfb[2]};
+        RRec r;
+        double R[9];
+        if (!earth) {
+            dq_rot(qprev, R);
+            mv3(R, dvfb, r.a);
+            dq_rot(dprev, R);
+            mv3(R, dvfb, r.b);
+            dq_rot(dcur, R);
+        } else {
+            double T[9], M1[9];
+            dq_rot(dq_load(g.qnn), T);
+            for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
+            dq_rot(qprev, R);
+            mm3(M1, R, T);
+            mv3(T, dvfb, r.a);
+            dq_rot(dq_mul(dq_load(g.qa), dprev), R);
+            mv3(R, dvfb, r.b);
+            dq_rot(dq_mul(dq_load(g.qb), dcur), R);
+        }
+        for (int i = 0; i < 9; ++i) r.cbb0[i] = -R[i];
+        r.pad = 0.0;
+        double* dst = reinterpret_cast<double*>(rrec + o0 + k - 1);
+        const double* w = reinterpret_cast<const double*>(&r);
+#pragma unroll
+        for (int i = 0; i < RREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+    }
+    }
+}
+
+template <int LANES>
+__global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_params prm, int n_seg,
+                                                        const gvx_imu* __restrict__ imu,
+                                                        const int32_t* __restrict__ seg_off,
+                                                        const gvx_state* __restrict__ state0,
+                                                        const double* __restrict__ iewn_in,
+                                                        const RRec* __restrict__ rrec,
+                                                        gvx_preint_result* __restrict__ out,
+                                                        double* __restrict__ pn) {
+    // LANES lanes per segment; lane c owns columns c, c + LANES, .. (< 15) of J
+    // and rows of P.  The per-step scalar work (the velocity / position sums, Phi
+    // and W) is issued once per wave for 64 / LANES segments.
+    constexpr int SPWL = 64 / LANES;
+    constexpr int CPL = (NS + LANES - 1) / LANES;  // columns per lane
+    constexpr int NIN = RREC_DW + 7;               // + the sample's dt, dtheta, dvel
+    constexpr int LPL = (NIN + LANES - 1) / LANES; // inputs loaded per lane per step
+    __shared__ double sIn[SPWL][2][LPL * LANES];
+    __shared__ double sG[SPWL][MS];
+    const int lane = threadIdx.x;
+    const int grp = lane / LANES, c = lane % LANES;
+    const int seg = blockIdx.x * SPWL + grp;
+    const bool live = seg < n_seg;
+    const int b0 = live ? seg_off[seg] : 0;
+    const int m = live ? seg_off[seg + 1] - b0 : 0;
+    int mmax = m;
+#pragma unroll
+    for (int o = LANES; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+    const bool earth = variant == GVX_PREINT_EARTH;
+    double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    gvx_state s0{};
+    double iewn[3] = {0, 0, 0};
+    if (live) {
+        s0 = state0[seg];
+        if (earth)
+            for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    }
+    double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        p[i] = s0.p[i];
+        v[i] = s0.v[i];
+    }
+    const double g3[3] = {0, 0, prm.gravity};
+    const double nacc = prm.acc_vrw * prm.acc_vrw;
+    const double ngyr = prm.gyr_arw * prm.gyr_arw;
+    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
+    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
+    const double g60 = earth ? -1.0 : 1.0;
+    const double wg = (g60 * ngyr) * g60;
+    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    double Jc[CPL][NS], Pc[CPL][NS];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j)
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            Jc[j][i] = i == c + j * LANES ? 1.0 : 0.0;
+            Pc[j][i] = 0.0;
+        }
+    // input e of a step (e < 16: RRec double e; 16..22: the sample's double
+    // e - 15, i.e. dt, dtheta, dvel); lane c loads inputs c, c + LANES, ..
+    // never predicated (a clamped step; spare slots re-read an input), so the
+    // compiler's counters keep the prefetches in flight across the step
+    const double* src_r = reinterpret_cast<const double*>(rrec + (live ? b0 - seg : 0));
+    const double* src_im = reinterpret_cast<const double*>(imu + b0);
+    const int klast = m >= 2 ? m - 1 : 1;
+    auto fetch = [&](int k, double (&x)[LPL]) {
+        const int kk = min(k, klast);
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) {
+            const int e = c + q * LANES;
+            x[q] = e < RREC_DW ? src_r[(size_t)(kk - 1) * RREC_DW + e]
+                               : src_im[(size_t)kk * (sizeof(gvx_imu) / 8) + 1 + min(e - RREC_DW, 6)];
+        }
+    };
+    double x0[LPL], x1[LPL];
+    fetch(1, x0);
+    fetch(2, x1);
+    for (int k = 1; k < mmax; ++k) {
+        const bool act = k < m;
+        double* sp = sIn[grp][k & 1];
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) sp[c + q * LANES] = x0[q];
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) x0[q] = x1[q];
+        fetch(k + 2, x1);
+        wave_lds_sync();
+        Phi f;
+        double Wv[9];
+        if (act) {
+            const RRec& rr = *reinterpret_cast<const RRec*>(sp);
+            const double dt = sp[RREC_DW];
+            // the velocity / position sums (integrationProcess, the order of preint_kernel)
+            double dvel[3];
+            if (!earth) {
+                for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + g3[i] * dt;
+            } else {
+                double cc3[3], dvcg[3];
+                cross3(iewn, v, cc3);
+                for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
+                for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + dvcg[i];
+            }
+            for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
+            for (int i = 0; i < 3; ++i) v[i] += dvel[i];
+            if (pns && c == 0)
+                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
+            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * rr.b[i];
+            for (int i = 0; i < 3; ++i) dv[i] += rr.b[i];
+
+            double cbb0[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cbb0[i] = rr.cbb0[i];
+            double sdth[3], sdv[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                sdth[i] = sp[RREC_DW + 1 + i] - dt * s0.bg[i];
+                sdv[i] = sp[RREC_DW + 4 + i] - dt * s0.ba[i];
+            }
+            const double sg = earth ? 1.0 : -1.0;
+            double gR[9];
+            for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double g = (gR[3 * a] * nacc) * gR[3 * b];
+                    g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+                    g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+                    Wv[3 * a + b] = g;
+                }
+            double S[9];
+            skew(sdv, S);
+            mm3(cbb0, S, f.C);
+            for (int i = 0; i < 9; ++i) f.D[i] = cbb0[i] * dt;
+            skew(sdth, S);
+            for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+            f.dt = dt;
+            f.f = 1 - dt / prm.corr_time;
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) {
+                const int cc = c + j * LANES;
+                double y[NS];
+                phi_mv(f, Pc[j], y);
+                if (cc < NS) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) sG[grp][cc * NS + i] = y[i];
+                }
+                phi_mv(f, Jc[j], y);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) Jc[j][i] = y[i];
+            }
+        }
+        wave_lds_sync();
+        if (act) {
+            const double a = 0.5 * f.dt;
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) {
+                const int ce = c + j * LANES;
+                const int cc = ce < NS ? ce : 0;
+                double K[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cc];
+                if (cc >= 3 && cc < 6) {
+                    K[3] = K[3] + a * Wv[cc - 3];
+                    K[4] = K[4] + a * Wv[3 + cc - 3];
+                    K[5] = K[5] + a * Wv[6 + cc - 3];
+                }
+#pragma unroll
+                for (int i = 6; i < NS; ++i)
+                    if (i == cc) K[i] = K[i] + a * wd(i);
+                const int r3 = cc - 3, r6 = cc - 6;
+                double phr[NS];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    phr[3 + b] = (cc == b) ? f.dt : (cc == 3 + b ? 1.0 : 0.0);
+                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
+                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
+                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
+                    phr[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
+                    phr[9 + b] = (cc == 6 + b) ? -f.dt : (cc == 9 + b ? f.f : 0.0);
+                    phr[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (cc == 12 + b ? f.f : 0.0);
+                }
+                double y[NS];
+                phi_mv(f, K, y);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[j][i] = y[i];
+                q_terms(a, Wv, wg, nbg, nba, phr, y, Pc[j]);
+            }
+        }
+    }
+    if (!live) return;
+    gvx_preint_result* o = out + seg;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+        const int cc = c + j * LANES;
+        if (cc < NS) {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                o->jacobian[i * NS + cc] = Jc[j][i];
+                o->covariance[cc * NS + i] = Pc[j][i];
+            }
+        }
+    }
+    if (c == 0)
+        for (int i = 0; i < 3; ++i) {
+            o->current.p[i] = p[i];
+            o->current.v[i] = v[i];
+            o->delta.p[i] = dp[i];
+            o->delta.v[i] = dv[i];
+        }
+}
+
+// preint_cov_kernel with the step's Phi / W blocks off the sequential path:
+// 16 lanes per segment (lane c owns column c of J and row c of P), and every 8
+// steps each lane of a segment's group forms ONE step's blocks -- the bias-
+// compensated sample, C = cbb0 skew(dv), D = cbb0 dt, W = gR N_v gR^T, the
+// RRec's rotated increments -- into LDS (StepRec), so the per-step chain keeps
+// only the velocity / position sums and the three column mat-vecs.  The blocks
+// are formed by the same operations as in preint_cov_kernel / preint_kernel, and
+// the column updates are the same code, so the outputs are the same bits
+// (tests/test_ba_gpu.py::test_preint_two_phase_bits_equal_one_phase).  The
+// 8-lane kernel above spent ~6.5 k cycles per step on one wave per SIMD (656
+// waves for 5,247 segments), most of them the per-lane scalar chain.
+// r04: row c of Phi is read from the record at a lane-dependent offset (no
+// selects), K's Q terms are LDS adds into the transpose (q_terms fuses the
+// rest) and the steps hand over through LDS with a wave fence, not s_barrier:
+// 321 -> 221 VALU instructions per step, but only 3-5 % of the launch -- the step
+// is bound by its dependent latency (PMC r04 v14: VALU active 30 % of a wave's
+// cycles at 1.3 waves per SIMD; timing probes: the record phases' loads 16 us,
+// the record phases altogether 24 us of ~240, profiles/r04_v17/).
+struct StepRec {
+    double dt, f;             // Phi's scalars (the layout of Phi, so phi_mv reads it in place)
+    double C[9], D[9], M[9];  // Phi(3:6, 6:9), Phi(3:6, 12:15), Phi(6:9, 6:9) = I - skew(dtheta)
+    double W[9];              // W(3:6, 3:6)
+    double a[3], b[3];        // RRec's velocity / delta-velocity increments
+    // row c of Phi, read by lane c at a lane-dependent offset instead of selected:
+    // S = {0,0,dt,0,0,f,0,0,-dt,0,0} (rows of dt I, f I, -dt I at 2-j, 5-j, 8-j),
+    // S1 = {0,0,1,0,0} (rows of I), Z = zeros
+    double S[11], S1[5], Z[3], pad;
+};
+static_assert(sizeof(Phi) == 29 * 8, "Phi is StepRec's prefix");
+constexpr int SREC_DW = sizeof(StepRec) / 8;  // 64
+constexpr int C16_CK = 8;  // steps per record chunk (one per lane of half a group): 23.6 KB of LDS per
+                           // wave, so every wave of a 5,247-segment batch is resident at once
+
+__global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_params prm, int n_seg,
+                                                          const gvx_imu* __restrict__ imu,
+                                                          const int32_t* __restrict__ seg_off,
+                                                          const gvx_state* __restrict__ state0,
+                                                          const double* __restrict__ iewn_in,
+                                                          const RRec* __restrict__ rrec,
+                                                          gvx_preint_result* __restrict__ out, double* __restrict__ pn) {
+    constexpr int LANES = 16, SPWL = 64 / LANES;
+    __shared__ StepRec sR[SPWL][C16_CK];
+    __shared__ double sG[SPWL][MS];
+    const int lane = threadIdx.x;
+    const int grp = lane / LANES, c = lane % LANES;
+    const int seg = blockIdx.x * SPWL + grp;
+    const bool live = seg < n_seg;
+    const int b0 = live ? seg_off[seg] : 0;
+    const int m = live ? seg_off[seg + 1] - b0 : 0;
+    int mmax = m;
+#pragma unroll
+    for (int o = LANES; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+    const bool earth = variant == GVX_PREINT_EARTH;
+    double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    gvx_state s0{};
+    double iewn[3] = {0, 0, 0};
+    if (live) {
+        s0 = state0[seg];
+        if (earth)
+            for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    }
+    double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        p[i] = s0.p[i];
+        v[i] = s0.v[i];
+    }
+    const double g3[3] = {0, 0, prm.gravity};
+    const double nacc = prm.acc_vrw * prm.acc_vrw;
+    const double ngyr = prm.gyr_arw * prm.gyr_arw;
+    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
+    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
+    const double g60 = earth ? -1.0 : 1.0;
+    const double wg = (g60 * ngyr) * g60;
+    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
+    const double wdc = wd(c);
+    constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
+    constexpr int oS = offsetof(StepRec, S) / 8, oS1 = offsetof(StepRec, S1) / 8, oZ = offsetof(StepRec, Z) / 8;
+    const int ph3 = c < 3 ? oS + 2 - c : (c < 6 ? oS1 + 2 - (c - 3) : oZ);
+    const int ph6 = (c >= 3 && c < 6) ? oC + 3 * (c - 3) : ((c >= 6 && c < 9) ? oM + 3 * (c - 6) : oZ);
+    const int ph9 = (c >= 6 && c < 9) ? oS + 8 - (c - 6) : ((c >= 9 && c < 12) ? oS + 5 - (c - 9) : oZ);
+    const int ph12 = (c >= 3 && c < 6) ? oD + 3 * (c - 3) : ((c >= 12 && c < NS) ? oS + 5 - (c - 12) : oZ);
+    double Jc[NS], Pc[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        Jc[i] = i == c ? 1.0 : 0.0;
+        Pc[i] = 0.0;
+    }
+    const RRec* rr0 = rrec + (live ? b0 - seg : 0);
+    const gvx_imu* im = imu + b0;
+    for (int kc = 1; kc < mmax; kc += C16_CK) {
+        // ---- this chunk's step records, one step per lane ----
+        {
+            const int k = kc + c;
+            if (c < C16_CK && k < m) {
+                const RRec& rr = rr0[k - 1];
+                const gvx_imu& sm = im[k];
+                StepRec r;
+                const double dt = sm.dt;
+                double cbb0[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) cbb0[i] = rr.cbb0[i];
+                double sdv[3], sdth[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    sdth[i] = sm.dtheta[i] - dt * s0.bg[i];
+                    sdv[i] = sm.dvel[i] - dt * s0.ba[i];
+                    r.a[i] = rr.a[i];
+                    r.b[i] = rr.b[i];
+                }
+                const double sg = earth ? 1.0 : -1.0;
+                double gR[9];
+                for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) {
+                        double g = (gR[3 * a] * nacc) * gR[3 * b];
+                        g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+                        g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+                        r.W[3 * a + b] = g;
+                    }
+                double S[9];
+                skew(sdv, S);
+                mm3(cbb0, S, r.C);
+                for (int i = 0; i < 9; ++i) r.D[i] = cbb0[i] * dt;
+                skew(sdth, S);
+                for (int i = 0; i < 9; ++i) r.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+                r.dt = dt;
+                r.f = 1 - dt / prm.corr_time;
+#pragma unroll
+                for (int i = 0; i < 11; ++i) r.S[i] = 0.0;
+                r.S[2] = dt;
+                r.S[5] = r.f;
+                r.S[8] = -dt;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) r.S1[i] = i == 2 ? 1.0 : 0.0;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) r.Z[i] = 0.0;
+                r.pad = 0.0;
+                double* dst = reinterpret_cast<double*>(&sR[grp][c]);
+                const double* w = reinterpret_cast<const double*>(&r);
+#pragma unroll
+                for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+            }
+        }
+        wave_lds_sync();
+        const int kend = min(kc + C16_CK, mmax);
+        for (int k = kc; k < kend; ++k) {
+            const bool act = k < m;
+            const StepRec& r = sR[grp][k - kc];
+            // Phi copied out of the record once per step (29 doubles): the three
+            // mat-vecs then wait on no LDS reads of their own (+8 %, profiles/r04_v20/)
+            const Phi f = *reinterpret_cast<const Phi*>(&r);
+            if (act) {
+                const double dt = r.dt;
+                // the velocity / position sums (integrationProcess, the order of preint_kernel)
+                double dvel[3];
+                if (!earth) {
+                    for (int i = 0; i < 3; ++i) dvel[i] = r.a[i] + g3[i] * dt;
+                } else {
+                    double cc3[3], dvcg[3];
+                    cross3(iewn, v, cc3);
+                    for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
+                    for (int i = 0; i < 3; ++i) dvel[i] = r.a[i] + dvcg[i];
+                }
+                for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
+                for (int i = 0; i < 3; ++i) v[i] += dvel[i];
+                if (pns && c == 0)
+                    *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
+                for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * r.b[i];
+                for (int i = 0; i < 3; ++i) dv[i] += r.b[i];
+                double y[NS];
+                phi_mv(f, Pc, y);
+                if (c < NS) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
+                }
+                // K's Q terms added where K is read from (LDS add after this lane's
+                // own column write; the same fp64 add as K[i] + a*w): the W block for
+                // lanes 3..5, the diagonal for lanes 6..14
+                {
+                    const double a = 0.5 * f.dt;
+                    if (c >= 3 && c < 6) {
+#pragma unroll
+                        for (int j = 0; j < 3; ++j)
+                            __hip_atomic_fetch_add(&sG[grp][(3 + j) * NS + c], a * r.W[3 * j + c - 3],
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else if (c >= 6 && c < NS) {
+                        __hip_atomic_fetch_add(&sG[grp][c * NS + c], a * wdc, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                phi_mv(f, Jc, y);
+#pragma unroll
+                for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            }
+            wave_lds_sync();
+            if (act) {
+                const double a = 0.5 * f.dt;
+                const int cl = c < NS ? c : 0;
+                double K[NS];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
+                const double* rw = reinterpret_cast<const double*>(&r);
+                double ph[NS];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    ph[3 + b] = rw[ph3 + b];
+                    ph[6 + b] = rw[ph6 + b];
+                    ph[9 + b] = rw[ph9 + b];
+                    ph[12 + b] = rw[ph12 + b];
+                }
+                double y[NS];
+                phi_mv(f, K, y);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[i] = y[i];
+                q_terms(a, r.W, wg, nbg, nba, ph, y, Pc);
+            }
+            wave_lds_sync();
+        }
+    }
+    if (!live) return;
+    gvx_preint_result* o = out + seg;
+    if (c < NS) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            o->jacobian[i * NS + c] = Jc[i];
+            o->covariance[c * NS + i] = Pc[i];
+        }
+    }
+    if (c == 0)
+        for (int i = 0; i < 3; ++i) {
+            o->current.p[i] = p[i];
+            o->current.v[i] = v[i];
+            o->delta.p[i] = dp[i];
+            o->delta.v[i] = dv[i];
+        }
+}
+
+}  // namespace
+
+hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
+                         const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
+                         const double* iewn, gvx_preint_result* out, double* pn) {
+    if (n_seg <= 0) return hipSuccess;
+    // Four-launch form when the per-step scratch can be sized without a round trip:
+    // the IMU allocation bounds the number of samples (hipMemGetAddressRange).
+    // A pointer into a large pooled block bounds nothing useful: above 1 GiB of
+    // scratch the single kernel runs.  GVX_PREINT_ONEPHASE=1 forces it (A/B and
+    // the bit-identity test; read per call).
+    const char* e1 = getenv("GVX_PREINT_ONEPHASE");
+    const bool one_phase = e1 && atoi(e1) != 0;
+    hipDeviceptr_t base = nullptr;
+    size_t range = 0;
+    if (!one_phase && hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)imu) == hipSuccess && range > 0) {
+        const size_t samples = (reinterpret_cast<const char*>(base) + range - reinterpret_cast<const char*>(imu)) /
+                               sizeof(gvx_imu);
+        const size_t bytes = samples * STEP_SCRATCH;
+        char* d = bytes <= (size_t(1) << 30) ? (char*)scratch(c, "preint_steps", bytes) : nullptr;
+        if (d) {
+            PreG* pre = reinterpret_cast<PreG*>(d);
+            QRec* qr = reinterpret_cast<QRec*>(d + samples * sizeof(PreG));
+            RRec* rr = reinterpret_cast<RRec*>(d + samples * (sizeof(PreG) + sizeof(QRec)));
+            hipLaunchKernelGGL(preint_pre_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, imu, seg_off,
+                               state0, iewn, pre);
+            hipLaunchKernelGGL(variant == GVX_PREINT_EARTH ? preint_chain_kernel<true> : preint_chain_kernel<false>,
+                               dim3((n_seg + 63) / 64), dim3(128), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
+                               (const PreG*)pre, qr, out);
+            hipLaunchKernelGGL(preint_rot_kernel, dim3(std::min(n_seg, c->n_cu * 8)), dim3(64), 0, c->stream, variant, n_seg, seg_off,
+                               state0, (const PreG*)pre, (const QRec*)qr, rr);
+            // the covariance pass: 16 lanes per segment with the step blocks formed
+            // 16 steps at a time off the sequential chain (GVX_PREINT_COV8=1: the
+            // 8-lane kernel that forms them per step on every lane, for A/B)
+            const char* e8 = getenv("GVX_PREINT_COV8");
+            if (e8 && atoi(e8) != 0)
+                hipLaunchKernelGGL(preint_cov_kernel<8>, dim3((n_seg + 7) / 8), dim3(64), 0, c->stream, variant, prm,
+                                   n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
+            else
+                hipLaunchKernelGGL(preint_cov16_kernel, dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, variant, prm,
+                                   n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
+            return hipGetLastError();
+        }
+    }
+    (void)hipGetLastError();  // a failed range query is not an error of this call
+    hipLaunchKernelGGL(preint_kernel, dim3((n_seg + SPW - 1) / SPW), dim3(64), 0, c->stream, variant, prm, n_seg, imu,
+                       seg_off, state0, iewn, out, pn);
+    return hipGetLastError();
+}
+
+}  // namespace gvx

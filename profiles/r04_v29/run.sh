@@ -1,0 +1,7 @@
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; O=gpurun_out/r04_v29; mkdir -p $O
+for v in ck8 ck12; do
+GVX_LIB=$PWD/ic-gvins_amd/gvx/variants/libgvx_$v.so timeout -k 10 600 python -u -m pytest tests/test_ba_gpu.py tests/test_factor_parity_gpu.py -x -q --timeout 200 --timeout-method thread > $O/tests_$v.log 2>&1 || { tail -30 $O/tests_$v.log; exit 1; }
+echo $v $(tail -1 $O/tests_$v.log)
+done
+bash tools/ab_run.sh r04_v29/ab 3 "tools/preint_loop.py" "(d['cold']['preint'], d['warm']['preint'], d['warm']['steps_per_s'])" base ck4 ck8 ck12
