@@ -216,7 +216,6 @@ __global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result*
     for (int e = gl; e < NS * NS; e += 16) A[e] = live ? s->covariance[e] : (e % (NS + 1) == 0 ? 1.0 : 0.0);
     if (gl < NS) perm[gl] = gl;
     __syncthreads();
-#pragma unroll
     for (int k = 0; k < NS; ++k) {
         int piv = k;
         double best = fabs(A[k * NS + k]);
@@ -245,44 +244,24 @@ __global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result*
         if (akk != 0.0 && gl > k && gl < NS) A[gl * NS + k] = A[gl * NS + k] / akk;
         __syncthreads();
         const int j = k + 1 + gl;  // trailing block column of this lane
-        if (j < NS) {
-            // every operand read before the first store (the rows are independent)
-            double l[NS], u[NS];
-            const double akj = A[k * NS + j];
-#pragma unroll
-            for (int i = k + 1; i < NS; ++i) {
-                l[i] = A[i * NS + k];
-                u[i] = A[i * NS + j];
-            }
-#pragma unroll
-            for (int i = k + 1; i < NS; ++i) A[i * NS + j] = u[i] - l[i] * akj;
-        }
+        if (j < NS)
+            for (int i = k + 1; i < NS; ++i) A[i * NS + j] = A[i * NS + j] - A[i * NS + k] * A[k * NS + j];
         __syncthreads();
     }
     // inverse from the LU: X = P, then L^-1 and U^-1 column by column (lane gl:
     // column gl; a column's entries depend only on that column and on A)
-    // (the column in registers: A is read-only here, so its reads issue early)
     if (gl < NS) {
         const int c = gl;
-        double xc[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) xc[i] = perm[i] == c ? 1.0 : 0.0;
-#pragma unroll
+        for (int i = 0; i < NS; ++i) X[i * NS + c] = perm[i] == c ? 1.0 : 0.0;
         for (int k = 0; k < NS; ++k)
-#pragma unroll
-            for (int i = k + 1; i < NS; ++i) xc[i] = xc[i] - A[i * NS + k] * xc[k];
-#pragma unroll
+            for (int i = k + 1; i < NS; ++i) X[i * NS + c] = X[i * NS + c] - A[i * NS + k] * X[k * NS + c];
         for (int k = NS - 1; k >= 0; --k) {
-            xc[k] = xc[k] / A[k * NS + k];
-#pragma unroll
-            for (int i = 0; i < k; ++i) xc[i] = xc[i] - A[i * NS + k] * xc[k];
+            X[k * NS + c] = X[k * NS + c] / A[k * NS + k];
+            for (int i = 0; i < k; ++i) X[i * NS + c] = X[i * NS + c] - A[i * NS + k] * X[k * NS + c];
         }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) X[i * NS + c] = xc[i];
     }
     __syncthreads();
     // Eigen llt_inplace<Lower>::unblocked on the lower triangle of X
-#pragma unroll
     for (int k = 0; k < NS; ++k) {
         double x = X[k * NS + k];
         if (k > 0) {
