@@ -439,7 +439,6 @@ struct PreG {                // StepPre terms of one step (scratch, per IMU step
     double qnn[4], qa[4], qb[4];  // Earth only
 };
 constexpr int PREG_DW = sizeof(PreG) / 8;  // 20
-constexpr int PREG_NORMAL_DW = 8;          // dtime, dvfb, qd
 struct QRec {                // the chains after step k
     double q[4], dqt[4];
 };
