@@ -425,9 +425,7 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
 //   preint_chain_kernel  one lane per SEGMENT (64 per wave): the two quaternion
 //                        chains alone, StepPre prefetched three steps ahead;
 //   preint_rot_kernel    one lane per STEP: the rotated increments of the
-//                        velocity updates and cbb0 from the chain values (only
-//                        before the 8-lane cov pass: preint_cov16_kernel forms
-//                        them in its record phase, rot_terms);
+//                        velocity updates and cbb0 from the chain values;
 //   preint_cov_kernel    16 lanes per segment: the velocity / position sums
 //                        (a few adds per step, on every lane of the group), J <-
 //                        Phi J and P <- Phi P Phi^T + Qk with Phi and W rebuilt
