@@ -72,9 +72,11 @@ gvx_status gvx_preint_integrate_dev(gvx_ctx* c, int32_t variant, const gvx_imu_p
     hipSetDevice(c->device);
     hipEvent_t ev{};
     prof_begin(c, "preint", &ev);
-    hipError_t e = launch_preint(c, variant, *prm, n_seg, d_imu, d_seg_off, d_state0, d_iewn, d_out, d_pn);
+    bool sqrt_done = false;
+    hipError_t e = launch_preint(c, variant, *prm, n_seg, d_imu, d_seg_off, d_state0, d_iewn, d_out, d_pn, &sqrt_done);
     prof_end(c, "preint", ev);
     if (e != hipSuccess) return hip_err(c, e, "preint kernel");
+    if (sqrt_done) return GVX_OK;  // formed in the covariance pass's epilogue
     prof_begin(c, "sqrt_info", &ev);
     e = launch_sqrt_info(c, n_seg, d_out);
     prof_end(c, "sqrt_info", ev);

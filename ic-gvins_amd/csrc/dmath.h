@@ -150,4 +150,115 @@ __device__ __forceinline__ void qlr_br(dq a, dq b, double* M) {
             M[3 * i + j] = av[i] * -bv[j] + L[3 * i] * R[j] + L[3 * i + 1] * R[3 + j] + L[3 * i + 2] * R[6 + j];
 }
 
+// sqrt_information_ = LLT(covariance_.inverse()).matrixL().transpose() of one
+// 15 x 15 covariance by a 16-lane group (lane gl) of a one-wave workgroup
+// (preintegration_earth.cc:39-40; factors.hip sqrt_info_kernel and the
+// covariance pass preint.hip preint_cov16_kernel share it): partial-pivot LU,
+// axpy-form substitutions for the inverse and the left-looking unblocked LLT,
+// each entry updated in the same k order as the sequential CPU restatement
+// (oracle/preint.c).  Lane gl owns column k+1+gl of the LU's trailing block,
+// column gl of the inverse (held in registers through both substitutions: a
+// column depends only on itself and on A) and row gl in the LLT.  A (the
+// covariance, row-major, on entry), X and perm are the group's LDS scratch;
+// the result is stored upper triangular (sqrt_info[i][j] = L[j][i]) to dst
+// unless dst is null.
+constexpr int SI_N = 15;
+__device__ __forceinline__ void sqrt_info_group(double* A, double* X, int* perm, int gl, double* dst) {
+    if (gl < SI_N) perm[gl] = gl;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SI_N; ++k) {
+        int piv = k;
+        double best = fabs(A[k * SI_N + k]);
+        for (int i = k + 1; i < SI_N; ++i) {
+            const double v = fabs(A[i * SI_N + k]);
+            if (v > best) {
+                best = v;
+                piv = i;
+            }
+        }
+        __syncthreads();
+        if (piv != k) {
+            if (gl < SI_N) {
+                const double t = A[k * SI_N + gl];
+                A[k * SI_N + gl] = A[piv * SI_N + gl];
+                A[piv * SI_N + gl] = t;
+            }
+            if (gl == 0) {
+                const int t = perm[k];
+                perm[k] = perm[piv];
+                perm[piv] = t;
+            }
+        }
+        __syncthreads();
+        const double akk = A[k * SI_N + k];
+        if (akk != 0.0 && gl > k && gl < SI_N) A[gl * SI_N + k] = A[gl * SI_N + k] / akk;
+        __syncthreads();
+        const int j = k + 1 + gl;  // trailing block column of this lane
+        if (j < SI_N) {
+            // every operand read before the first store (the rows are independent)
+            double l[SI_N], u[SI_N];
+            const double akj = A[k * SI_N + j];
+#pragma unroll
+            for (int i = k + 1; i < SI_N; ++i) {
+                l[i] = A[i * SI_N + k];
+                u[i] = A[i * SI_N + j];
+            }
+#pragma unroll
+            for (int i = k + 1; i < SI_N; ++i) A[i * SI_N + j] = u[i] - l[i] * akj;
+        }
+        __syncthreads();
+    }
+    // inverse from the LU: X = P, then L^-1 and U^-1 column by column (lane gl:
+    // column gl; a column's entries depend only on that column and on A)
+    // (the column in registers: A is read-only here, so its reads issue early)
+    if (gl < SI_N) {
+        const int c = gl;
+        double xc[SI_N];
+#pragma unroll
+        for (int i = 0; i < SI_N; ++i) xc[i] = perm[i] == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < SI_N; ++k)
+#pragma unroll
+            for (int i = k + 1; i < SI_N; ++i) xc[i] = xc[i] - A[i * SI_N + k] * xc[k];
+#pragma unroll
+        for (int k = SI_N - 1; k >= 0; --k) {
+            xc[k] = xc[k] / A[k * SI_N + k];
+#pragma unroll
+            for (int i = 0; i < k; ++i) xc[i] = xc[i] - A[i * SI_N + k] * xc[k];
+        }
+#pragma unroll
+        for (int i = 0; i < SI_N; ++i) X[i * SI_N + c] = xc[i];
+    }
+    __syncthreads();
+    // Eigen llt_inplace<Lower>::unblocked on the lower triangle of X
+#pragma unroll
+    for (int k = 0; k < SI_N; ++k) {
+        double x = X[k * SI_N + k];
+        if (k > 0) {
+            double sq = 0;
+            for (int j = 0; j < k; ++j) sq = sq + X[k * SI_N + j] * X[k * SI_N + j];
+            x = x - sq;
+        }
+        x = sqrt(x);
+        __syncthreads();
+        if (gl == 0) X[k * SI_N + k] = x;
+        if (gl > k && gl < SI_N) {
+            double v = X[gl * SI_N + k];
+            if (k > 0) {
+                double d = 0;
+                for (int j = 0; j < k; ++j) d = d + X[gl * SI_N + j] * X[k * SI_N + j];
+                v = v - d;
+            }
+            X[gl * SI_N + k] = v / x;
+        }
+        __syncthreads();
+    }
+    if (dst)
+        for (int e = gl; e < SI_N * SI_N; e += 16) {
+            const int i = e / SI_N, j = e - i * SI_N;
+            dst[e] = j >= i ? X[j * SI_N + i] : 0.0;
+        }
+}
+
 }  // namespace gvx

@@ -187,18 +187,14 @@ __device__ __forceinline__ void set3(double* J, int ld, int r, int c, const doub
 }
 
 // sqrt_information_ = LLT(covariance_.inverse()).matrixL().transpose()
-// (preintegration_earth.cc:39-40; the Normal variant likewise): partial-pivot
-// LU, axpy-form substitutions for the inverse and the left-looking unblocked
-// LLT, each entry updated in the same k order as the sequential CPU
-// restatement.  Four segments per wavefront, 16 lanes each (the per-step scalar
-// work -- pivot search, divisions, the LLT's dot products -- issued once for
-// four segments; one wave per segment spent most of its issue on idle lanes):
-// lane gl owns column k+1+gl of the LU's trailing block and column gl of the
-// inverse (the substitutions touch one column per lane, so they need no
-// barrier), and row gl in the LLT.  The reference recomputes the factor inside
-// every Evaluate; it depends on covariance_ alone, so it is formed once here
-// (after integration / at factor-set creation) with the same arithmetic and
-// stored upper triangular in gvx_preint_result::sqrt_info.
+// (preintegration_earth.cc:39-40; the Normal variant likewise) for factor
+// sets and integrate calls that do not run preint_cov16_kernel (which forms it
+// in its epilogue): four segments per wavefront, 16 lanes each (the per-step
+// scalar work -- pivot search, divisions, the LLT's dot products -- issued once
+// for four segments), by dmath.h sqrt_info_group.  The reference recomputes
+// the factor inside every Evaluate; it depends on covariance_ alone, so it is
+// formed once here with the same arithmetic and stored upper triangular in
+// gvx_preint_result::sqrt_info.
 constexpr int SQ_SEG = 4;  // segments per 64-lane workgroup
 __global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result* __restrict__ pre) {
     __shared__ double As[SQ_SEG][NS * NS];  // LU
@@ -206,110 +202,10 @@ __global__ void __launch_bounds__(64) sqrt_info_kernel(int n, gvx_preint_result*
     __shared__ int perms[SQ_SEG][NS];
     const int g = threadIdx.x >> 4, gl = threadIdx.x & 15;
     const int fi = blockIdx.x * SQ_SEG + g;
-    const bool live = fi < n;  // a spare group factors the identity (barriers below)
-    double* A = As[g];
-    double* X = Xs[g];
-    int* perm = perms[g];
+    const bool live = fi < n;  // a spare group factors the identity
     gvx_preint_result* s = pre + (live ? fi : 0);
-
-    // ---- sqrt_information_ = LLT(covariance_.inverse()).matrixL().transpose() ----
-    for (int e = gl; e < NS * NS; e += 16) A[e] = live ? s->covariance[e] : (e % (NS + 1) == 0 ? 1.0 : 0.0);
-    if (gl < NS) perm[gl] = gl;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        int piv = k;
-        double best = fabs(A[k * NS + k]);
-        for (int i = k + 1; i < NS; ++i) {
-            const double v = fabs(A[i * NS + k]);
-            if (v > best) {
-                best = v;
-                piv = i;
-            }
-        }
-        __syncthreads();
-        if (piv != k) {
-            if (gl < NS) {
-                const double t = A[k * NS + gl];
-                A[k * NS + gl] = A[piv * NS + gl];
-                A[piv * NS + gl] = t;
-            }
-            if (gl == 0) {
-                const int t = perm[k];
-                perm[k] = perm[piv];
-                perm[piv] = t;
-            }
-        }
-        __syncthreads();
-        const double akk = A[k * NS + k];
-        if (akk != 0.0 && gl > k && gl < NS) A[gl * NS + k] = A[gl * NS + k] / akk;
-        __syncthreads();
-        const int j = k + 1 + gl;  // trailing block column of this lane
-        if (j < NS) {
-            // every operand read before the first store (the rows are independent)
-            double l[NS], u[NS];
-            const double akj = A[k * NS + j];
-#pragma unroll
-            for (int i = k + 1; i < NS; ++i) {
-                l[i] = A[i * NS + k];
-                u[i] = A[i * NS + j];
-            }
-#pragma unroll
-            for (int i = k + 1; i < NS; ++i) A[i * NS + j] = u[i] - l[i] * akj;
-        }
-        __syncthreads();
-    }
-    // inverse from the LU: X = P, then L^-1 and U^-1 column by column (lane gl:
-    // column gl; a column's entries depend only on that column and on A)
-    // (the column in registers: A is read-only here, so its reads issue early)
-    if (gl < NS) {
-        const int c = gl;
-        double xc[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) xc[i] = perm[i] == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-#pragma unroll
-            for (int i = k + 1; i < NS; ++i) xc[i] = xc[i] - A[i * NS + k] * xc[k];
-#pragma unroll
-        for (int k = NS - 1; k >= 0; --k) {
-            xc[k] = xc[k] / A[k * NS + k];
-#pragma unroll
-            for (int i = 0; i < k; ++i) xc[i] = xc[i] - A[i * NS + k] * xc[k];
-        }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) X[i * NS + c] = xc[i];
-    }
-    __syncthreads();
-    // Eigen llt_inplace<Lower>::unblocked on the lower triangle of X
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        double x = X[k * NS + k];
-        if (k > 0) {
-            double sq = 0;
-            for (int j = 0; j < k; ++j) sq = sq + X[k * NS + j] * X[k * NS + j];
-            x = x - sq;
-        }
-        x = sqrt(x);
-        __syncthreads();
-        if (gl == 0) X[k * NS + k] = x;
-        if (gl > k && gl < NS) {
-            double v = X[gl * NS + k];
-            if (k > 0) {
-                double d = 0;
-                for (int j = 0; j < k; ++j) d = d + X[gl * NS + j] * X[k * NS + j];
-                v = v - d;
-            }
-            X[gl * NS + k] = v / x;
-        }
-        __syncthreads();
-    }
-    // sqrt_info[i][j] = L[j][i] for j >= i  (upper triangular)
-    if (live)
-        for (int e = gl; e < NS * NS; e += 16) {
-            const int i = e / NS, j = e - i * NS;
-            s->sqrt_info[e] = j >= i ? X[j * NS + i] : 0.0;
-        }
+    for (int e = gl; e < NS * NS; e += 16) As[g][e] = live ? s->covariance[e] : (e % (NS + 1) == 0 ? 1.0 : 0.0);
+    sqrt_info_group(As[g], Xs[g], perms[g], gl, live ? s->sqrt_info : nullptr);
 }
 
 // One factor per 16-lane group, 4 factors per 64-lane workgroup (one wave).

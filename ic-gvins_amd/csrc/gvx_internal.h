@@ -314,7 +314,8 @@ hipError_t launch_camera(gvx_ctx* c, int op, const CamArgs& a, const void* in0, 
 // ---- preint.hip / factors.hip ----
 hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
-                         const double* iewn, gvx_preint_result* out, double* pn);
+                         const double* iewn, gvx_preint_result* out, double* pn,
+                         bool* sqrt_info_done = nullptr);  // set when the covariance pass formed sqrt_info
 hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
                          const int32_t* offs, double* res, double* jac);
 hipError_t launch_sqrt_info(gvx_ctx* c, int n, gvx_preint_result* pre);

@@ -913,6 +913,10 @@ constexpr int SREC_DW = sizeof(StepRec) / 8;  // 64
 constexpr int C16_CK = 8;  // steps per record chunk (one per lane of half a group): 23.6 KB of LDS per
                            // wave, so every wave of a 5,247-segment batch is resident at once
 
+// per segment group in the record region: A and X (15 x 15 each) and perm
+constexpr int SI_GROUP_DW = 2 * NS * NS + 8;
+static_assert(4 * SI_GROUP_DW <= 4 * C16_CK * SREC_DW, "sqrt_info scratch fits the record region");
+template <bool SQRT_INFO>
 __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_params prm, int n_seg,
                                                           const gvx_imu* __restrict__ imu,
                                                           const int32_t* __restrict__ seg_off,
@@ -1113,13 +1117,28 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
             o->delta.p[i] = dp[i];
             o->delta.v[i] = dv[i];
         }
+    if constexpr (SQRT_INFO) {
+        // sqrt_information_ from P while it is in registers, in the record
+        // region (the same function as factors.hip sqrt_info_kernel, same bits):
+        // no fifth launch, no read-back of the covariance
+        wave_lds_sync();  // the last step's record reads are done
+        double* A = reinterpret_cast<double*>(&sR[0][0]) + grp * SI_GROUP_DW;
+        double* X = A + NS * NS;
+        int* perm = reinterpret_cast<int*>(X + NS * NS);
+        if (c < NS) {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) A[c * NS + i] = Pc[i];
+        }
+        sqrt_info_group(A, X, perm, c, o->sqrt_info);
+    }
 }
 
 }  // namespace
 
 hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int n_seg,
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
-                         const double* iewn, gvx_preint_result* out, double* pn) {
+                         const double* iewn, gvx_preint_result* out, double* pn, bool* sqrt_info_done) {
+    if (sqrt_info_done) *sqrt_info_done = false;
     if (n_seg <= 0) return hipSuccess;
     // Four-launch form when the per-step scratch can be sized without a round trip:
     // the IMU allocation bounds the number of samples (hipMemGetAddressRange).
@@ -1155,8 +1174,9 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                 hipLaunchKernelGGL(preint_cov_kernel<8>, dim3((n_seg + 7) / 8), dim3(64), 0, c->stream, variant, prm,
                                    n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
             } else {
-                hipLaunchKernelGGL(preint_cov16_kernel, dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, variant, prm,
-                                   n_seg, imu, seg_off, state0, iewn, (const PreG*)pre, (const QRec*)qr, out, pn);
+                hipLaunchKernelGGL(preint_cov16_kernel<true>, dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, variant,
+                                   prm, n_seg, imu, seg_off, state0, iewn, (const PreG*)pre, (const QRec*)qr, out, pn);
+                if (sqrt_info_done) *sqrt_info_done = true;
             }
             return hipGetLastError();
         }
