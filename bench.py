@@ -292,6 +292,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pre", action="store_true", help="skip the CLAHE preprocessing leg")
     ap.add_argument("--no-factors", action="store_true", help="skip the configs[3] factor leg of the default line")
+    ap.add_argument("--no-sequence", action="store_true",
+                    help="skip the configs[4] sequence leg of the default line (one sequence per GPU + the RCCL "
+                         "gather of the tracks to rank 0)")
+    ap.add_argument("--seq-frames", type=int, default=2000,
+                    help="configs[4] leg of the default line: frames per sequence (per GPU)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--gather", action="store_true", help="batch-replay: all-gather results every step")
     ap.add_argument("--mock", action="store_true", help="no GPU: exercise launch/aggregation logic only")
@@ -424,6 +429,10 @@ def main():
     # the same run: configs[3]'s factor batch (its own line under "factors")
     factors = None if args.no_factors else factor_leg(args, ctx, dev, dist, world, rank,
                                                       steps=max(10, args.steps // 2), window_extras=False)
+    # the north_star scaling workload, timed in the same run at every N: one
+    # configs[4] sequence per GPU replayed on the device, then every rank's
+    # per-frame tracks gathered to rank 0 over RCCL (its own line under "sequence")
+    seq = None if args.no_sequence else sequence_leg(args, ctx, dev, dist, world, rank, args.seq_frames)
     kept_frac = float(dNK.float().mean().item()) / N
     total_pairs = world * Pn * args.steps
     value = total_pairs / elapsed
@@ -492,6 +501,7 @@ def main():
             "single_pair": single,
             "host_buffers": pcie,
             "factors": factors,
+            "sequence": sequence_summary(seq) if seq else None,
             "dist_backend": dist.get_backend() if dist else None,
             "gather_check": gather_ok,
         }
@@ -1038,24 +1048,51 @@ def all_digests(tracks, counts, dist, cdev):
 
 
 def sequence_main(args):
+    """`--config 5`: the configs[4] sequence replay on its own, as the line's
+    headline (sequence_leg, with the per-family profile and the CPU baseline)."""
+    import gvx
+    dist, dev, world, rank, local = rank_setup(args)
+    ctx = gvx.Context(local)
+    line = sequence_leg(args, ctx, dev, dist, world, rank, args.frames, cpu=world == 1 and not args.no_cpu)
+    if rank == 0:
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def sequence_summary(line):
+    """The configs[4] fields the default line carries under "sequence" (the
+    north_star scaling workload: one sequence per GPU and the RCCL gather of every
+    rank's per-frame tracks to rank 0, timed inside the region)."""
+    keep = ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "frames_per_rank", "tracks_per_frame_mean",
+            "gathered_ranks", "gather_check", "gather_bytes_per_rank", "gather_ms", "all_digests", "dist_backend",
+            "host_enqueue_ms_per_frame", "scaling")
+    out = {k: line[k] for k in keep if k in line}
+    out["metric"] = line["metric"]
+    out["workload"] = line["config"]["workload"]
+    out["device_ms_per_frame"] = line["roofline"]["device_ms_per_frame"]
+    return out
+
+
+def sequence_leg(args, ctx, dev, dist, world, rank, n_frames, cpu=False):
     """configs[4]: one synthetic sequence per GPU (a moving
     camera over a textured plane, frames rendered into HBM before the timed
-    region).  Per frame, as Tracking::track does: the frame's pyramid once
-    (gvx_frame_put_dev), forward + backward LK of the tracked points from the
-    previous frame with a constant-velocity initial flow, FB + border +
-    compaction (gvx_klt_fb), and block-grid detection (gvx_detect) topping the
-    tracks up to N whenever they drop below it.  After the last frame every
-    rank's per-frame tracks go to rank 0 in one RCCL gather.  A step = one
-    frame per GPU; value = frames of all ranks / max-over-ranks time."""
+    region; rank r's seed is synth.SEED + 7919 r).  Per frame, as Tracking::track
+    does: CLAHE, the frame's pyramid once, forward + backward LK of the tracked
+    points from the previous frame with a constant-velocity initial flow, FB +
+    border + compaction, and block-grid detection topping the tracks up to N
+    whenever they drop below it.  After the last frame every rank's per-frame
+    tracks go to rank 0 in one RCCL gather (inside the timed region).  A step =
+    one frame per GPU; value = frames of all ranks / max-over-ranks time.
+    Returns the line on rank 0, None elsewhere."""
     import torch
     import gvx
     from gvx import synth
-    dist, dev, world, rank, local = rank_setup(args)
     W, H, N, L = args.width, args.height, args.features, args.levels
-    F = max(args.frames, args.warmup + 2)
+    F = max(n_frames, args.warmup + 2)
     frames, _ = synth.make_sequence(W, H, F, dev, seed=synth.SEED + 7919 * rank)
     torch.cuda.synchronize()
-    ctx = gvx.Context(local)
     from gvx.tracking import DeviceSequenceTracker, SequenceTracker
     kp = gvx.KltParams.default(max_level=L)
     dp = gvx.DetectParams.default(max_features=N)
@@ -1113,6 +1150,7 @@ def sequence_main(args):
         timed += 1
     t_enq = time.perf_counter() - t0  # host time to enqueue the timed frames
     ctx.sync()
+    t_g = time.perf_counter()
     if device_loop:
         # the records stay in HBM: RCCL gathers them device to device
         d_tracks, d_counts = tracker.rec_tracks, tracker.rec_counts
@@ -1120,10 +1158,12 @@ def sequence_main(args):
         d_tracks, d_counts = torch.from_numpy(tracks), torch.from_numpy(counts)
     gathered = gather_tracks(d_tracks, d_counts, dist, coll_device(dist, dev))
     torch.cuda.synchronize()
+    t_g = time.perf_counter() - t_g
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if device_loop:
+        tracker.close()
         tracks[:] = tracker.rec_tracks.cpu().numpy()  # for the line's statistics, after the timed region
         counts[:] = tracker.rec_counts.cpu().numpy()
     # every rank's digest of its own records (outside the timed region): rank 0
@@ -1148,66 +1188,72 @@ def sequence_main(args):
         fam = {f: ctx.profile_read(f) for f in ("clahe", "pyramid", "klt", "compact", "detect")}
         fam = {k: (v[0] * timed / k_prof, v[1]) for k, v in fam.items() if v[1] > 0}
         ctx.profile(False)
+        prof.close()
     else:
         fam = {f: ctx.profile_read(f) for f in ("clahe", "pyramid", "klt", "compact", "detect")}
         fam = {k: v for k, v in fam.items() if v[1] > 0}
         ctx.profile(False)
     elapsed = max_over_ranks(elapsed, dist, dev)
-    if rank == 0:
-        value = world * timed / elapsed
-        dev_ms = sum(v[0] for v in fam.values()) / timed
-        # the frame-pair unit with each frame read and its pyramid
-        # built once per sequence frame instead of twice
-        ap, sw, sh = 0, W, H
-        for _ in range(L):
-            sw, sh = (sw + 1) // 2, (sh + 1) // 2
-            ap += sw * sh
-        B = algorithmic_bytes(W, H, L, N) - W * H - 2 * ap + 2 * W * H  # + CLAHE: read + write the frame
-        achieved = B / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
-        cpu = None
-        if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=host_threads(), clahe=True)
-            cpu["sample"] += " (per sequence frame, detection not included)"
-        tr = counts[F - timed:]
-        print(json.dumps({
-            "metric": f"KLT sequence frames/sec @{W}x{H},{N} feat (configs[4])", "value": round(value, 2),
-            "unit": "frames/s", "n_gpus": world, "steps": timed, "warmup": warm,
-            "ms_per_step": round(elapsed / timed * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8/i32 windows, f32 solve",
-            "data": "synthetic sequences (moving camera over a band-limited texture, seed 20261015 + 7919*rank)",
-            "config": {"workload": f"configs[4]: one {F}-frame sequence per GPU, {W}x{H} mono, {N} feat, maxLevel "
-                                   f"{L}: per frame CLAHE + pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
-                                   f"RCCL gather of all per-frame tracks to rank 0",
-                       "loop": (("device-resident: one captured hipGraph launch per frame (gvx_track_frame_dev)"
-                                 if args.no_pipeline else
-                                 ("device-resident, pipelined: a graph tracking frames t..t+K-1 "
-                                  "(gvx_track_frame_dev + the track record, per frame) on the context stream beside a "
-                                  "graph preprocessing frames t+K..t+2K-1 on its side stream "
-                                  "(gvx_branch_begin/_end/_join), K = %d" % args.frame_batch))
-                                if device_loop else "host loop: SequenceTracker, host round trips per frame"),
-                       "frame_batch": args.frame_batch if device_loop and not args.no_pipeline else None,
-                       "parallelism": f"sequences sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
-                         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": None, "algorithmic_bytes_per_frame": B,
-                         "device_ms_per_frame": {k: round(v[0] / timed, 4) for k, v in fam.items()}},
-            "cpu_baseline": cpu,
-            "tracks_per_frame_mean": round(float(tr.mean()), 1),
-            "detect_frames": stats["detect_frames"] if not device_loop else None,
-            "host_overhead_frac": round(max(0.0, 1.0 - dev_ms / (elapsed / timed * 1e3)), 3) if dev_ms else None,
-            "host_enqueue_ms_per_frame": round(t_enq / timed * 1e3, 4),
-            "gathered_ranks": len(gathered) if gathered else 0,
-            "gather_check": bool(gathered and np.array_equal(gathered[0][0].numpy(), tracks)
-                                 and np.array_equal(gathered[0][1].numpy(), counts)
-                                 and all(int(c[F - timed:].min()) > 0 for _, c in gathered)
-                                 and all(records_digest(t.numpy(), c.numpy()) == d
-                                         for (t, c), d in zip(gathered, digests))),
-            "dist_backend": dist.get_backend() if dist else None,
-        }))
-    if dist:
-        dist.destroy_process_group()
-    ctx.close()
+    t_g = max_over_ranks(t_g, dist, dev)
+    del frames
+    if rank != 0:
+        return None
+    value = world * timed / elapsed
+    dev_ms = sum(v[0] for v in fam.values()) / timed
+    # the frame-pair unit with each frame read and its pyramid
+    # built once per sequence frame instead of twice
+    ap, sw, sh = 0, W, H
+    for _ in range(L):
+        sw, sh = (sw + 1) // 2, (sh + 1) // 2
+        ap += sw * sh
+    B = algorithmic_bytes(W, H, L, N) - W * H - 2 * ap + 2 * W * H  # + CLAHE: read + write the frame
+    achieved = B / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else None
+    cpu_line = None
+    if cpu:
+        cpu_line = cpu_baseline(W, H, N, L, args.cpu_budget / 2, threads=host_threads(), clahe=True)
+        cpu_line["sample"] += " (per sequence frame, detection not included)"
+    tr = counts[F - timed:]
+    return {
+        "metric": f"KLT sequence frames/sec @{W}x{H},{N} feat (configs[4])", "value": round(value, 2),
+        "unit": "frames/s", "n_gpus": world, "steps": timed, "warmup": warm,
+        "ms_per_step": round(elapsed / timed * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8/i32 windows, f32 solve",
+        "data": "synthetic sequences (moving camera over a band-limited texture, seed 20261015 + 7919*rank)",
+        "config": {"workload": f"configs[4]: one {F}-frame sequence per GPU, {W}x{H} mono, {N} feat, maxLevel "
+                               f"{L}: per frame CLAHE + pyramid + fwd/bwd LK + FB + compaction + detection top-up; "
+                               f"RCCL gather of all per-frame tracks to rank 0",
+                   "loop": (("device-resident: one captured hipGraph launch per frame (gvx_track_frame_dev)"
+                             if args.no_pipeline else
+                             ("device-resident, pipelined: a graph tracking frames t..t+K-1 "
+                              "(gvx_track_frame_dev + the track record, per frame) on the context stream beside a "
+                              "graph preprocessing frames t+K..t+2K-1 on its side stream "
+                              "(gvx_branch_begin/_end/_join), K = %d" % args.frame_batch))
+                            if device_loop else "host loop: SequenceTracker, host round trips per frame"),
+                   "frame_batch": args.frame_batch if device_loop and not args.no_pipeline else None,
+                   "parallelism": f"sequences sharded over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "kernel": "per-frame pipeline (latency-bound: one frame at a time)",
+                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": None, "algorithmic_bytes_per_frame": B,
+                     "device_ms_per_frame": {k: round(v[0] / timed, 4) for k, v in fam.items()}},
+        "cpu_baseline": cpu_line,
+        "frames_per_rank": F,
+        "tracks_per_frame_mean": round(float(tr.mean()), 1),
+        "detect_frames": stats["detect_frames"] if not device_loop else None,
+        "host_overhead_frac": round(max(0.0, 1.0 - dev_ms / (elapsed / timed * 1e3)), 3) if dev_ms else None,
+        "host_enqueue_ms_per_frame": round(t_enq / timed * 1e3, 4),
+        "gathered_ranks": len(gathered) if gathered else 0,
+        # the exchange: F x N x 2 f32 tracks + F counts per rank, one gather to rank 0
+        "gather_bytes_per_rank": int(4 * (F * N * 2 + F)),
+        "gather_ms": round(t_g * 1e3, 3),
+        "all_digests": [[d[0], d[1]] for d in digests],
+        "gather_check": bool(gathered and np.array_equal(gathered[0][0].numpy(), tracks)
+                             and np.array_equal(gathered[0][1].numpy(), counts)
+                             and all(int(c[F - timed:].min()) > 0 for _, c in gathered)
+                             and all(records_digest(t.numpy(), c.numpy()) == d
+                                     for (t, c), d in zip(gathered, digests))),
+        "dist_backend": dist.get_backend() if dist else None,
+    }
 
 
 def spawn_ranks(n):
@@ -1259,22 +1305,34 @@ def mock_main(args):
         time.sleep(step_s)
     if dist:
         dist.barrier()
-    gathered_ok = None
-    if args.config == 5:
-        F, N = 6, 4
-        tr = torch.full((F, N, 2), float(rank)) + torch.arange(F, dtype=torch.float32)[:, None, None]
-        cn = torch.full((F,), 3 + rank, dtype=torch.int32)
-        g = gather_tracks(tr, cn, dist, torch.device("cpu"))
-        if rank == 0:
-            gathered_ok = len(g) == world and all(
-                bool((gt[:, :, 0] == r + torch.arange(F)[:, None]).all()) and bool((gc == 3 + r).all())
-                for r, (gt, gc) in enumerate(g))
     elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+    # the configs[4] exchange (gather_tracks + all_digests), as the default line's
+    # "sequence" sub-object and --config 5 run it: each rank's records differ
+    F, N = 6, 4
+    tr = torch.full((F, N, 2), float(rank)) + torch.arange(F, dtype=torch.float32)[:, None, None]
+    cn = torch.full((F,), 3 + rank, dtype=torch.int32)
+    t1 = time.perf_counter()
+    for _ in range(F):
+        time.sleep(step_s / 4)
+    g = gather_tracks(tr, cn, dist, torch.device("cpu"))
+    seq_el = max_over_ranks(time.perf_counter() - t1, dist)
+    digests = all_digests(tr.numpy(), cn.numpy(), dist, torch.device("cpu"))
+    gathered_ok = None
     if rank == 0:
-        print(json.dumps({"metric": "mock", "value": world * args.pairs * args.steps / elapsed, "unit": "frames/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-                          "scaling": "weak", "elapsed_s": elapsed, "gathered_ok": gathered_ok}))
+        gathered_ok = len(g) == world and all(
+            bool((gt[:, :, 0] == r + torch.arange(F)[:, None]).all()) and bool((gc == 3 + r).all())
+            and records_digest(gt.numpy(), gc.numpy()) == d for r, ((gt, gc), d) in enumerate(zip(g, digests)))
+    if rank == 0:
+        line = {"metric": "mock", "value": world * args.pairs * args.steps / elapsed, "unit": "frames/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak", "elapsed_s": elapsed, "gathered_ok": gathered_ok}
+        if args.config != 5 and not args.no_sequence:
+            line["sequence"] = {"metric": "mock sequence", "value": world * F / seq_el, "unit": "frames/s",
+                                "n_gpus": world, "steps": F, "frames_per_rank": F, "gathered_ranks": len(g),
+                                "gather_check": gathered_ok, "all_digests": [[d[0], d[1]] for d in digests],
+                                "dist_backend": dist.get_backend() if dist else None, "scaling": "weak"}
+        print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
 

@@ -65,3 +65,22 @@ def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_bench_mock_default_line_sequence_gloo():
+    """The default line's "sequence" sub-object at world 2:
+    the configs[4] exchange -- every rank's records gathered to rank 0, checked
+    against the all-gathered per-rank digests -- aggregated over both ranks."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--mock", "--backend", "gloo", "--gpus", "2", "--steps", "4", "--warmup", "1", "--pairs", "8"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    s = json.loads(lines[0])["sequence"]
+    assert s["n_gpus"] == 2 and s["gathered_ranks"] == 2 and s["gather_check"] is True
+    assert s["dist_backend"] == "gloo" and len(s["all_digests"]) == 2
+    assert s["all_digests"][0] != s["all_digests"][1]
+    assert s["value"] > 0 and s["scaling"] == "weak"

@@ -40,10 +40,27 @@ def _run_two_ranks(extra, timeout=100):
 
 def test_batch_two_ranks_gather():
     """configs[1] batch at world 2 with the per-step results all-gather."""
-    d = _run_two_ranks(["--pairs", "16", "--steps", "4", "--warmup", "2", "--no-pre", "--no-factors", "--gather"])
+    d = _run_two_ranks(["--pairs", "16", "--steps", "4", "--warmup", "2", "--no-pre", "--no-factors", "--gather",
+                        "--no-sequence"])
     assert d["n_gpus"] == 2 and d["steps"] == 4 and d["scaling"] == "weak"
     assert abs(d["value"] - 2 * 16 * 4 / (d["ms_per_step"] * 4e-3)) < 1e-3 * d["value"]
     assert 0.5 < d["kept_fraction"] <= 1.0
+    assert d["sequence"] is None
+
+
+def test_default_line_sequence_two_ranks():
+    """The default line's "sequence" sub-object at world 2:
+    each rank replays its own configs[4] sequence inside the line's run, rank 0
+    receives both ranks' per-frame tracks, and every record set matches its
+    owner's digest."""
+    d = _run_two_ranks(["--pairs", "16", "--steps", "4", "--warmup", "2", "--no-pre", "--no-factors",
+                        "--seq-frames", "48"], timeout=160)
+    s = d["sequence"]
+    assert s["n_gpus"] == 2 and s["frames_per_rank"] == 48 and s["steps"] == 32  # warm-up 2 -> one K = 16 batch
+    assert s["gathered_ranks"] == 2 and s["gather_check"] is True and s["dist_backend"] == "gloo"
+    assert len(s["all_digests"]) == 2 and s["all_digests"][0] != s["all_digests"][1]  # distinct sequences
+    assert abs(s["value"] - 2 * s["steps"] / (s["ms_per_step"] * s["steps"] * 1e-3)) < 1e-3 * s["value"]
+    assert s["tracks_per_frame_mean"] > 75
 
 
 def test_sequence_two_ranks_track_gather():

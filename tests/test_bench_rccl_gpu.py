@@ -42,10 +42,24 @@ def _run_rccl(extra, timeout=110):
 
 def test_batch_results_all_gather_rccl():
     """configs[1] batch with the per-step device-tensor all_gather over RCCL."""
-    d = _run_rccl(["--pairs", "32", "--steps", "4", "--warmup", "2", "--no-pre", "--no-factors", "--gather"])
+    d = _run_rccl(["--pairs", "32", "--steps", "4", "--warmup", "2", "--no-pre", "--no-factors", "--gather",
+                   "--no-sequence"])
     assert d["dist_backend"] == "nccl"
     assert d["gather_check"] is True
     assert d["n_gpus"] == 1 and 0.5 < d["kept_fraction"] <= 1.0
+
+
+def test_default_line_sequence_rccl():
+    """The default line's "sequence" sub-object through
+    RCCL: the configs[4] replay and the device-to-device gather of its records,
+    as the driver's N-GPU run takes them."""
+    d = _run_rccl(["--pairs", "32", "--steps", "4", "--warmup", "2", "--no-pre", "--no-factors",
+                   "--seq-frames", "64"])
+    s = d["sequence"]
+    assert s["dist_backend"] == "nccl" and d["dist_backend"] == "nccl"
+    assert s["gathered_ranks"] == 1 and s["gather_check"] is True and len(s["all_digests"]) == 1
+    assert s["frames_per_rank"] == 64 and s["steps"] == 48 and s["value"] > 0
+    assert s["gather_bytes_per_rank"] == 4 * (64 * 150 * 2 + 64)
 
 
 def test_sequence_track_gather_rccl():
