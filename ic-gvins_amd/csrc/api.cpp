@@ -171,6 +171,11 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
         return GVX_ERR_HIP;
     }
     c->main = c->stream;
+    {
+        // A/B switches are read once, here (not per launch)
+        const char* e = std::getenv("GVX_PREINT_ONEPHASE");
+        if (e && std::atoi(e) != 0) c->preint_path = GVX_PREINT_PATH_ONEPHASE;
+    }
     *out = c;
     return GVX_OK;
 }

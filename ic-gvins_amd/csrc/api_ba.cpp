@@ -58,6 +58,14 @@ void gvx_earth_iewn(const double origin[3], const double local[3], double iewn[3
     iewn[2] = -WGS84_WIE * std::sin(lat);
 }
 
+gvx_status gvx_set_preint_path(gvx_ctx* c, int32_t path) {
+    if (!c) return GVX_ERR_INVALID;
+    if (path != GVX_PREINT_PATH_AUTO && path != GVX_PREINT_PATH_ONEPHASE)
+        return set_err(c, GVX_ERR_INVALID, "unknown preintegration path %d", path);
+    c->preint_path = path;
+    return GVX_OK;
+}
+
 gvx_status gvx_preint_integrate_dev(gvx_ctx* c, int32_t variant, const gvx_imu_params* prm,
                                     int32_t n_seg, const gvx_imu* d_imu, const int32_t* d_seg_off,
                                     const gvx_state* d_state0, const double* d_iewn,

@@ -87,6 +87,8 @@ struct gvx_ctx {
     bool capture_failed = false;
     // gvx_set_marg_solver
     int32_t marg_solver = GVX_MARG_SOLVER_FAST;
+    // gvx_set_preint_path (GVX_PREINT_ONEPHASE=1 at creation: the single kernel)
+    int32_t preint_path = GVX_PREINT_PATH_AUTO;
     // gvx_track_frame_dev: what the detection constants in "trk_static" were
     // built for (the buffer itself and the geometry)
     struct TrackStatic {

@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
     }
 }
 
-// ------------------------------------------------ four-launch preintegration
+// ------------------------------------------------ three-launch preintegration
 // preint_kernel's sequential part runs on every lane of a wave that serves 4
 // segments: the wave's issue time per step is the same whether it advances 4
 // segments or 64, and 5,247 segments give 1.3 k such waves for 1,024 SIMDs.
@@ -423,17 +423,13 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
 //   preint_pre_kernel    one lane per STEP (a workgroup per segment): the
 //                        StepPre terms -- every transcendental of the step;
 //   preint_chain_kernel  one lane per SEGMENT (64 per wave): the two quaternion
-//                        chains alone, StepPre prefetched three steps ahead;
-//   preint_rot_kernel    one lane per STEP: the rotated increments of the
-//                        velocity updates and cbb0 from the chain values (only
-//                        before the 8-lane cov pass: preint_cov16_kernel forms
-//                        them in its record phase, rot_terms);
-//   preint_cov_kernel    16 lanes per segment: the velocity / position sums
-//                        (a few adds per step, on every lane of the group), J <-
-//                        Phi J and P <- Phi P Phi^T + Qk with Phi and W rebuilt
-//                        from cbb0 and the IMU sample.
+//                        chains alone, StepPre prefetched ahead;
+//   preint_cov16_kernel  16 lanes per segment: the step records (rotated terms,
+//                        Phi, W) formed 8 steps at a time, one step per lane,
+//                        then the velocity / position sums, J <- Phi J and
+//                        P <- Phi P Phi^T + Qk per step, sqrt_info at the end.
 // Every value is formed by the same operations in the same order as in
-// preint_kernel, so the results are the same bits (tests/test_ba_gpu.py).
+// preint_kernel (tests/test_ba_gpu.py).
 struct PreG {                // StepPre terms of one step (scratch, per IMU step)
     double dtime;            // delta_time after the step
     double dvfb[3];
@@ -444,14 +440,7 @@ constexpr int PREG_DW = sizeof(PreG) / 8;  // 20
 struct QRec {                // the chains after step k
     double q[4], dqt[4];
 };
-struct RRec {                // rotated terms of step k
-    double cbb0[9];          // -R(dqt) (Normal) or -R(qb dqt) (Earth)
-    double a[3];             // velocity increment before gravity / Coriolis
-    double b[3];             // delta-velocity increment
-    double pad;
-};
-constexpr int RREC_DW = sizeof(RRec) / 8;  // 16
-constexpr size_t STEP_SCRATCH = sizeof(PreG) + sizeof(QRec) + sizeof(RRec);
+constexpr size_t STEP_SCRATCH = sizeof(PreG) + sizeof(QRec);  // per IMU sample
 
 __global__ void __launch_bounds__(64, 6) preint_pre_kernel(int variant, int n_seg, const gvx_imu* __restrict__ imu,
                                                         const int32_t* __restrict__ seg_off,
@@ -621,7 +610,8 @@ __global__ void __launch_bounds__(128) preint_chain_kernel(gvx_imu_params prm, i
     dq_store(dq_load(s0.q), o->q0);
 }
 
-// The rotated terms of step k (k >= 1) from the chain values: RRec's a, b and
+// The rotated terms of step k (k >= 1) from the chain values: the velocity and
+// delta-velocity increments a, b and
 // cbb0 (qs = the segment's QRec base, q0 = its start attitude for k = 1).
 __device__ __forceinline__ void rot_terms(bool earth, const PreG* __restrict__ gp, const QRec* __restrict__ qs, int k,
                                           const double* q0, double* ra, double* rb, double* cbb0) {
@@ -651,258 +641,41 @@ __device__ __forceinline__ void rot_terms(bool earth, const PreG* __restrict__ g
     for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
 }
 
-__global__ void __launch_bounds__(64) preint_rot_kernel(int variant, int n_seg, const int32_t* __restrict__ seg_off,
-                                                        const gvx_state* __restrict__ state0,
-                                                        const PreG* __restrict__ pre,
-                                                        const QRec* __restrict__ qrec, RRec* __restrict__ rrec) {
-    const bool earth = variant == GVX_PREINT_EARTH;
-    for (int seg = blockIdx.x; seg < n_seg; seg += gridDim.x) {  // waves loop over segments
-    const int b0 = seg_off[seg];
-    const int m = seg_off[seg + 1] - b0;
-    const size_t o0 = (size_t)(b0 - seg);
-    for (int k = 1 + threadIdx.x; k < m; k += 64) {
-        RRec r;
-        rot_terms(earth, pre + (o0 + k - 1), qrec + o0, k, state0[seg].q, r.a, r.b, r.cbb0);
-        r.pad = 0.0;
-        double* dst = reinterpret_cast<double*>(rrec + o0 + k - 1);
-        const double* w = reinterpret_cast<const double*>(&r);
-#pragma unroll
-        for (int i = 0; i < RREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
-    }
-    }
-}
 
-template <int LANES>
-__global__ void __launch_bounds__(64) preint_cov_kernel(int variant, gvx_imu_params prm, int n_seg,
-                                                        const gvx_imu* __restrict__ imu,
-                                                        const int32_t* __restrict__ seg_off,
-                                                        const gvx_state* __restrict__ state0,
-                                                        const double* __restrict__ iewn_in,
-                                                        const RRec* __restrict__ rrec,
-                                                        gvx_preint_result* __restrict__ out,
-                                                        double* __restrict__ pn) {
-    // LANES lanes per segment; lane c owns columns c, c + LANES, .. (< 15) of J
-    // and rows of P.  The per-step scalar work (the velocity / position sums, Phi
-    // and W) is issued once per wave for 64 / LANES segments.
-    constexpr int SPWL = 64 / LANES;
-    constexpr int CPL = (NS + LANES - 1) / LANES;  // columns per lane
-    constexpr int NIN = RREC_DW + 7;               // + the sample's dt, dtheta, dvel
-    constexpr int LPL = (NIN + LANES - 1) / LANES; // inputs loaded per lane per step
-    __shared__ double sIn[SPWL][2][LPL * LANES];
-    __shared__ double sG[SPWL][MS];
-    const int lane = threadIdx.x;
-    const int grp = lane / LANES, c = lane % LANES;
-    const int seg = blockIdx.x * SPWL + grp;
-    const bool live = seg < n_seg;
-    const int b0 = live ? seg_off[seg] : 0;
-    const int m = live ? seg_off[seg + 1] - b0 : 0;
-    int mmax = m;
-#pragma unroll
-    for (int o = LANES; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
-    const bool earth = variant == GVX_PREINT_EARTH;
-    double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
-    gvx_state s0{};
-    double iewn[3] = {0, 0, 0};
-    if (live) {
-        s0 = state0[seg];
-        if (earth)
-            for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
-    }
-    double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
-    for (int i = 0; i < 3; ++i) {
-        p[i] = s0.p[i];
-        v[i] = s0.v[i];
-    }
-    const double g3[3] = {0, 0, prm.gravity};
-    const double nacc = prm.acc_vrw * prm.acc_vrw;
-    const double ngyr = prm.gyr_arw * prm.gyr_arw;
-    const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
-    const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
-    const double g60 = earth ? -1.0 : 1.0;
-    const double wg = (g60 * ngyr) * g60;
-    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
-    double Jc[CPL][NS], Pc[CPL][NS];
-#pragma unroll
-    for (int j = 0; j < CPL; ++j)
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            Jc[j][i] = i == c + j * LANES ? 1.0 : 0.0;
-            Pc[j][i] = 0.0;
-        }
-    // input e of a step (e < 16: RRec double e; 16..22: the sample's double
-    // e - 15, i.e. dt, dtheta, dvel); lane c loads inputs c, c + LANES, ..
-    // never predicated (a clamped step; spare slots re-read an input), so the
-    // compiler's counters keep the prefetches in flight across the step
-    const double* src_r = reinterpret_cast<const double*>(rrec + (live ? b0 - seg : 0));
-    const double* src_im = reinterpret_cast<const double*>(imu + b0);
-    const int klast = m >= 2 ? m - 1 : 1;
-    auto fetch = [&](int k, double (&x)[LPL]) {
-        const int kk = min(k, klast);
-#pragma unroll
-        for (int q = 0; q < LPL; ++q) {
-            const int e = c + q * LANES;
-            x[q] = e < RREC_DW ? src_r[(size_t)(kk - 1) * RREC_DW + e]
-                               : src_im[(size_t)kk * (sizeof(gvx_imu) / 8) + 1 + min(e - RREC_DW, 6)];
-        }
-    };
-    double x0[LPL], x1[LPL];
-    fetch(1, x0);
-    fetch(2, x1);
-    for (int k = 1; k < mmax; ++k) {
-        const bool act = k < m;
-        double* sp = sIn[grp][k & 1];
-#pragma unroll
-        for (int q = 0; q < LPL; ++q) sp[c + q * LANES] = x0[q];
-#pragma unroll
-        for (int q = 0; q < LPL; ++q) x0[q] = x1[q];
-        fetch(k + 2, x1);
-        wave_lds_sync();
-        Phi f;
-        double Wv[9];
-        if (act) {
-            const RRec& rr = *reinterpret_cast<const RRec*>(sp);
-            const double dt = sp[RREC_DW];
-            // the velocity / position sums (integrationProcess, the order of preint_kernel)
-            double dvel[3];
-            if (!earth) {
-                for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + g3[i] * dt;
-            } else {
-                double cc3[3], dvcg[3];
-                cross3(iewn, v, cc3);
-                for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
-                for (int i = 0; i < 3; ++i) dvel[i] = rr.a[i] + dvcg[i];
-            }
-            for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
-            for (int i = 0; i < 3; ++i) v[i] += dvel[i];
-            if (pns && c == 0)
-                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
-            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * rr.b[i];
-            for (int i = 0; i < 3; ++i) dv[i] += rr.b[i];
-
-            double cbb0[9];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) cbb0[i] = rr.cbb0[i];
-            double sdth[3], sdv[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                sdth[i] = sp[RREC_DW + 1 + i] - dt * s0.bg[i];
-                sdv[i] = sp[RREC_DW + 4 + i] - dt * s0.ba[i];
-            }
-            const double sg = earth ? 1.0 : -1.0;
-            double gR[9];
-            for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
-            for (int a = 0; a < 3; ++a)
-                for (int b = 0; b < 3; ++b) {
-                    double g = (gR[3 * a] * nacc) * gR[3 * b];
-                    g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
-                    g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
-                    Wv[3 * a + b] = g;
-                }
-            double S[9];
-            skew(sdv, S);
-            mm3(cbb0, S, f.C);
-            for (int i = 0; i < 9; ++i) f.D[i] = cbb0[i] * dt;
-            skew(sdth, S);
-            for (int i = 0; i < 9; ++i) f.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
-            f.dt = dt;
-            f.f = 1 - dt / prm.corr_time;
-#pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                const int cc = c + j * LANES;
-                double y[NS];
-                phi_mv(f, Pc[j], y);
-                if (cc < NS) {
-#pragma unroll
-                    for (int i = 0; i < NS; ++i) sG[grp][cc * NS + i] = y[i];
-                }
-                phi_mv(f, Jc[j], y);
-#pragma unroll
-                for (int i = 0; i < NS; ++i) Jc[j][i] = y[i];
-            }
-        }
-        wave_lds_sync();
-        if (act) {
-            const double a = 0.5 * f.dt;
-#pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                const int ce = c + j * LANES;
-                const int cc = ce < NS ? ce : 0;
-                double K[NS];
-#pragma unroll
-                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cc];
-                if (cc >= 3 && cc < 6) {
-                    K[3] = K[3] + a * Wv[cc - 3];
-                    K[4] = K[4] + a * Wv[3 + cc - 3];
-                    K[5] = K[5] + a * Wv[6 + cc - 3];
-                }
-#pragma unroll
-                for (int i = 6; i < NS; ++i)
-                    if (i == cc) K[i] = K[i] + a * wd(i);
-                const int r3 = cc - 3, r6 = cc - 6;
-                double phr[NS];
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    phr[3 + b] = (cc == b) ? f.dt : (cc == 3 + b ? 1.0 : 0.0);
-                    const double cr = r3 == 0 ? f.C[b] : (r3 == 1 ? f.C[3 + b] : f.C[6 + b]);
-                    const double mr = r6 == 0 ? f.M[b] : (r6 == 1 ? f.M[3 + b] : f.M[6 + b]);
-                    const double dr = r3 == 0 ? f.D[b] : (r3 == 1 ? f.D[3 + b] : f.D[6 + b]);
-                    phr[6 + b] = (r3 >= 0 && r3 < 3) ? cr : ((r6 >= 0 && r6 < 3) ? mr : 0.0);
-                    phr[9 + b] = (cc == 6 + b) ? -f.dt : (cc == 9 + b ? f.f : 0.0);
-                    phr[12 + b] = (r3 >= 0 && r3 < 3) ? dr : (cc == 12 + b ? f.f : 0.0);
-                }
-                double y[NS];
-                phi_mv(f, K, y);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) Pc[j][i] = y[i];
-                q_terms(a, Wv, wg, nbg, nba, phr, y, Pc[j]);
-            }
-        }
-    }
-    if (!live) return;
-    gvx_preint_result* o = out + seg;
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-        const int cc = c + j * LANES;
-        if (cc < NS) {
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                o->jacobian[i * NS + cc] = Jc[j][i];
-                o->covariance[cc * NS + i] = Pc[j][i];
-            }
-        }
-    }
-    if (c == 0)
-        for (int i = 0; i < 3; ++i) {
-            o->current.p[i] = p[i];
-            o->current.v[i] = v[i];
-            o->delta.p[i] = dp[i];
-            o->delta.v[i] = dv[i];
-        }
-}
-
-// preint_cov_kernel with the step's Phi / W blocks off the sequential path:
-// 16 lanes per segment (lane c owns column c of J and row c of P), and every 8
-// steps each lane of a segment's group forms ONE step's blocks -- the bias-
-// compensated sample, C = cbb0 skew(dv), D = cbb0 dt, W = gR N_v gR^T, the
-// RRec's rotated increments -- into LDS (StepRec), so the per-step chain keeps
-// only the velocity / position sums and the three column mat-vecs.  The blocks
-// are formed by the same operations as in preint_cov_kernel / preint_kernel, and
-// the column updates are the same code, so the outputs are the same bits
-// (tests/test_ba_gpu.py::test_preint_two_phase_bits_equal_one_phase).  The
-// 8-lane kernel above spent ~6.5 k cycles per step on one wave per SIMD (656
-// waves for 5,247 segments), most of them the per-lane scalar chain.
-// r04: row c of Phi is read from the record at a lane-dependent offset (no
-// selects), K's Q terms are LDS adds into the transpose (q_terms fuses the
-// rest) and the steps hand over through LDS with a wave fence, not s_barrier:
-// 321 -> 221 VALU instructions per step, but only 3-5 % of the launch -- the step
-// is bound by its dependent latency (PMC r04 v14: VALU active 30 % of a wave's
-// cycles at 1.3 waves per SIMD; timing probes: the record phases' loads 16 us,
-// the record phases altogether 24 us of ~240, profiles/r04_v17/).
+// The covariance pass (r05): 16 lanes per segment, 4 segments per one-wave
+// workgroup; lane c owns column c of J and of P (P is symmetric, so also row c).
+// Every 8 steps the lanes c < 8 of a segment's group form ONE step's record each
+// into LDS (StepRec: Phi's blocks, W, the rotated increments, the lookups of
+// Phi's row c); then the 8 steps run in sequence.  A step is branch-free up to
+// its last assignment:
+//   * its whole record is read into registers at once (the broadcast blocks, the
+//     lane's row of Phi, the lane's W column of the Q term): one wait, not one
+//     per mat-vec;
+//   * G(:,c) = Phi P(:,c) is stored transposed -- lane c writes element i to
+//     row i of the segment's LDS tile (sT, 18 doubles a row: rows 16-B aligned,
+//     the 16 lanes' 8-byte stores contiguous and the b128 row reads of 16 lanes
+//     on 16 distinct 4-bank windows), so lane c then reads row c, i.e.
+//     K = G(c,:)^T, as seven ds_read_b128 + one b64 instead of fifteen
+//     strided reads;
+//   * K's Q terms (a W(:,c), the same fp64 adds as before) are LDS adds issued
+//     after a wave fence, their operands formed before the stores (no LDS
+//     round trip, no lgkmcnt(0) drain in the step);
+//   * J <- Phi J runs between the stores and the reads;
+//   * P'(:,c) = Phi K + a W phi_c (q_terms), assigned where the step is live.
+// Steps past a segment's m (ragged batches: the wave runs to the longest of its
+// four) read an identity record (dt = 0, f = 1, C = D = W = 0, M = I, a = b =
+// 0), which leaves J, the sums and the record outputs unchanged; P keeps its
+// value through the final assignment's predicate (an identity step would
+// otherwise hand back P^T).  The operations and their order are those of
+// preint_kernel (the one-phase form), so the two forms agree value for value
+// (tests/test_ba_gpu.py::test_preint_two_phase_equals_one_phase).
+// Reference: preintegration_earth.cc:266-303, preintegration_normal.cc:198-232
+// (updateJacobianAndCovariance), preintegration_earth.cc:205-260 (the sums).
 struct StepRec {
     double dt, f;             // Phi's scalars (the layout of Phi, so phi_mv reads it in place)
     double C[9], D[9], M[9];  // Phi(3:6, 6:9), Phi(3:6, 12:15), Phi(6:9, 6:9) = I - skew(dtheta)
     double W[9];              // W(3:6, 3:6)
-    double a[3], b[3];        // RRec's velocity / delta-velocity increments
+    double a[3], b[3];        // velocity / delta-velocity increments (before gravity / Coriolis)
     // row c of Phi, read by lane c at a lane-dependent offset instead of selected:
     // S = {0,0,dt,0,0,f,0,0,-dt,0,0} (rows of dt I, f I, -dt I at 2-j, 5-j, 8-j),
     // S1 = {0,0,1,0,0} (rows of I), Z = zeros
@@ -910,23 +683,124 @@ struct StepRec {
 };
 static_assert(sizeof(Phi) == 29 * 8, "Phi is StepRec's prefix");
 constexpr int SREC_DW = sizeof(StepRec) / 8;  // 64
-constexpr int C16_CK = 8;  // steps per record chunk (one per lane of half a group): 23.6 KB of LDS per
-                           // wave, so every wave of a 5,247-segment batch is resident at once
+constexpr int C16_CK = 8;   // steps per record chunk (one per lane of half a group)
+constexpr int TS = 18;      // sT row stride (doubles): 16-B aligned rows, conflict-free b128 row reads
+constexpr int TSEG = 288;   // sT doubles per segment: 15 rows of 18, padded to a multiple of 256 B
+static_assert(TSEG >= 16 * TS - 2 && (TSEG * 8) % 256 == 0, "sT layout");
+// records in LDS: RS doubles apart (528 B: the 8 lanes writing a chunk's records
+// hit 8 distinct 4-bank windows instead of one, 8-way), segments SEGR doubles
+// apart (36 banks: the broadcast b128 reads of two segments' lanes sharing a lane
+// group do not collide).  PMC r05 v3: 39 % of the LDS cycles were bank conflicts.
+constexpr int RS = SREC_DW + 2;
+constexpr int SEGR = C16_CK * RS + 2;
+static_assert((RS * 8) % 16 == 0 && (SEGR * 8) % 16 == 0, "16-B aligned records");
+// LDS per wave: 4 x 4,240 B of records + 4 x 2,304 B of transpose tiles = 26.2 KB,
+// so the 1,312 waves of a 5,247-segment batch are resident at once (6 per CU)
 
 // per segment group in the record region: A and X (15 x 15 each) and perm
 constexpr int SI_GROUP_DW = 2 * NS * NS + 8;
-static_assert(4 * SI_GROUP_DW <= 4 * C16_CK * SREC_DW, "sqrt_info scratch fits the record region");
-template <bool SQRT_INFO>
-__global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_params prm, int n_seg,
+static_assert(4 * SI_GROUP_DW <= 4 * SEGR, "sqrt_info scratch fits the record region");
+
+// The record of step k (k >= 1) of one segment: the rotated terms from the
+// chain values (QRec), the bias-compensated sample, Phi's blocks and W, formed
+// by the same operations as preint_kernel's step.
+template <bool EARTH>
+__device__ __forceinline__ void make_record(const gvx_imu_params& prm, const PreG* __restrict__ pg, const QRec* qr,
+                                            const gvx_imu& sm, const gvx_state& s0, int k, double nacc,
+                                            double* __restrict__ dst) {
+    // each field stored as it is formed (short live ranges: the step loop's J, P
+    // and sums stay in registers across the record phase)
+    const auto put2 = [&](int i, double x, double y) { *reinterpret_cast<double2*>(dst + i) = double2{x, y}; };
+    double cbb0[9], ra[3], rb[3];
+    rot_terms(EARTH, pg, qr, k, s0.q, ra, rb, cbb0);
+    constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
+    constexpr int oW = offsetof(StepRec, W) / 8, oA = offsetof(StepRec, a) / 8, oS = offsetof(StepRec, S) / 8;
+    static_assert(oC == 2 && oD == 11 && oM == 20 && oW == 29 && oA == 38 && oS == 44, "record layout");
+    const double dt = sm.dt;
+    const double f = 1 - dt / prm.corr_time;
+    double sdv[3], sdth[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        sdth[i] = sm.dtheta[i] - dt * s0.bg[i];
+        sdv[i] = sm.dvel[i] - dt * s0.ba[i];
+    }
+    double S[9], C[9], M[9];
+    skew(sdv, S);
+    mm3(cbb0, S, C);
+    skew(sdth, S);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
+    // dt, f, C[0..8], D[0..8], M[0..8] (doubles 0..28), W (29..37), a (38..40), b (41..43)
+    put2(0, dt, f);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) put2(oC + i, C[i], C[i + 1]);
+    put2(oC + 8, C[8], cbb0[0] * dt);
+#pragma unroll
+    for (int i = 1; i < 9; i += 2) put2(oD + i, cbb0[i] * dt, cbb0[i + 1] * dt);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) put2(oM + i, M[i], M[i + 1]);
+    const double sg = EARTH ? 1.0 : -1.0;  // gt(3:6, 3:6) = gR = sg * cbb0
+    double gR[9], W[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            double g = (gR[3 * a] * nacc) * gR[3 * b];
+            g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
+            g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
+            W[3 * a + b] = g;
+        }
+    put2(oM + 8, M[8], W[0]);
+#pragma unroll
+    for (int i = 1; i < 9; i += 2) put2(oW + i, W[i], W[i + 1]);
+    put2(oA, ra[0], ra[1]);
+    put2(oA + 2, ra[2], rb[0]);
+    put2(oA + 4, rb[1], rb[2]);
+    // S = {0,0,dt,0,0,f,0,0,-dt,0,0}, S1 = {0,0,1,0,0}, Z = 0, pad
+    put2(oS, 0.0, 0.0);
+    put2(oS + 2, dt, 0.0);
+    put2(oS + 4, 0.0, f);
+    put2(oS + 6, 0.0, 0.0);
+    put2(oS + 8, -dt, 0.0);
+    put2(oS + 10, 0.0, 0.0);
+    put2(oS + 12, 0.0, 1.0);
+    put2(oS + 14, 0.0, 0.0);
+    put2(oS + 16, 0.0, 0.0);
+    put2(oS + 18, 0.0, 0.0);
+}
+
+// the identity step (past a segment's m): Phi = I, W = 0, no increments
+__device__ __forceinline__ void identity_record(double* __restrict__ dst) {
+    double w[SREC_DW];
+#pragma unroll
+    for (int i = 0; i < SREC_DW; ++i) w[i] = 0.0;
+    w[offsetof(StepRec, f) / 8] = 1.0;
+    w[offsetof(StepRec, M) / 8] = 1.0;
+    w[offsetof(StepRec, M) / 8 + 4] = 1.0;
+    w[offsetof(StepRec, M) / 8 + 8] = 1.0;
+    w[offsetof(StepRec, S) / 8 + 5] = 1.0;
+    w[offsetof(StepRec, S1) / 8 + 2] = 1.0;
+#pragma unroll
+    for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+}
+
+template <bool EARTH>
+__global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm, int n_seg,
                                                           const gvx_imu* __restrict__ imu,
                                                           const int32_t* __restrict__ seg_off,
                                                           const gvx_state* __restrict__ state0,
                                                           const double* __restrict__ iewn_in,
                                                           const PreG* __restrict__ pre, const QRec* __restrict__ qrec,
                                                           gvx_preint_result* __restrict__ out, double* __restrict__ pn) {
+    // the kernel is written for ONE wave per workgroup: its LDS hand-overs are
+    // wave fences (in-order LDS within a wave), and sqrt_info_group's barriers
+    // are reached by every lane (dead groups factor the identity)
     constexpr int LANES = 16, SPWL = 64 / LANES;
-    __shared__ StepRec sR[SPWL][C16_CK];
-    __shared__ double sG[SPWL][MS];
+    static_assert(SPWL * LANES == 64, "one wave per workgroup");
+    __shared__ __attribute__((aligned(256))) double sRec[SPWL * SEGR];
+    __shared__ __attribute__((aligned(256))) double sT[SPWL][TSEG];
     const int lane = threadIdx.x;
     const int grp = lane / LANES, c = lane % LANES;
     const int seg = blockIdx.x * SPWL + grp;
@@ -936,15 +810,15 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
     int mmax = m;
 #pragma unroll
     for (int o = LANES; o < 64; o <<= 1) mmax = max(mmax, __shfl_xor(mmax, o));
-    const bool earth = variant == GVX_PREINT_EARTH;
-    double* pns = (pn && live && earth) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
+    double* pns = (pn && live && EARTH) ? pn + (size_t)(b0 - seg) * 4 : nullptr;
     gvx_state s0{};
     double iewn[3] = {0, 0, 0};
     if (live) {
         s0 = state0[seg];
-        if (earth)
+        if (EARTH)
             for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
     }
+    s0.q[3] = live ? s0.q[3] : 1.0;  // dead groups: a unit quaternion for rot_terms
     double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
     for (int i = 0; i < 3; ++i) {
         p[i] = s0.p[i];
@@ -955,16 +829,20 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
     const double ngyr = prm.gyr_arw * prm.gyr_arw;
     const double nbg = 2 * prm.gyr_bias_std * prm.gyr_bias_std / prm.corr_time;
     const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
-    const double g60 = earth ? -1.0 : 1.0;
+    const double g60 = EARTH ? -1.0 : 1.0;
     const double wg = (g60 * ngyr) * g60;
-    auto wd = [&](int i) { return i < 9 ? wg : (i < 12 ? nbg : nba); };
-    const double wdc = wd(c);
+    const double wdc = c < 9 ? wg : (c < 12 ? nbg : nba);
     constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
     constexpr int oS = offsetof(StepRec, S) / 8, oS1 = offsetof(StepRec, S1) / 8, oZ = offsetof(StepRec, Z) / 8;
+    constexpr int oW = offsetof(StepRec, W) / 8, oA = offsetof(StepRec, a) / 8;
+    // lane-dependent lookups into a record: row c of Phi (cols 3..14) and the W
+    // column of lane c's Q adds (lanes 3..5; the others read a zero)
     const int ph3 = c < 3 ? oS + 2 - c : (c < 6 ? oS1 + 2 - (c - 3) : oZ);
     const int ph6 = (c >= 3 && c < 6) ? oC + 3 * (c - 3) : ((c >= 6 && c < 9) ? oM + 3 * (c - 6) : oZ);
     const int ph9 = (c >= 6 && c < 9) ? oS + 8 - (c - 6) : ((c >= 9 && c < 12) ? oS + 5 - (c - 9) : oZ);
     const int ph12 = (c >= 3 && c < 6) ? oD + 3 * (c - 3) : ((c >= 12 && c < NS) ? oS + 5 - (c - 12) : oZ);
+    const int qw = (c >= 3 && c < 6) ? c - 3 : 0;
+    const bool qv = c >= 3 && c < 6, qd = c >= 6 && c < NS;
     double Jc[NS], Pc[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -974,163 +852,132 @@ __global__ void __launch_bounds__(64) preint_cov16_kernel(int variant, gvx_imu_p
     const PreG* pg0 = pre + (live ? b0 - seg : 0);
     const QRec* qr0 = qrec + (live ? b0 - seg : 0);
     const gvx_imu* im = imu + b0;
+    double* const tile = sT[grp];
     for (int kc = 1; kc < mmax; kc += C16_CK) {
         // ---- this chunk's step records, one step per lane ----
-        {
+        if (c < C16_CK) {
             const int k = kc + c;
-            if (c < C16_CK && k < m) {
-                const gvx_imu& sm = im[k];
-                StepRec r;
-                double cbb0[9];
-                // the rotated terms (what preint_rot_kernel stores for the 8-lane pass)
-                rot_terms(earth, pg0 + (k - 1), qr0, k, s0.q, r.a, r.b, cbb0);
-                const double dt = sm.dt;
-                double sdv[3], sdth[3];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    sdth[i] = sm.dtheta[i] - dt * s0.bg[i];
-                    sdv[i] = sm.dvel[i] - dt * s0.ba[i];
-                }
-                const double sg = earth ? 1.0 : -1.0;
-                double gR[9];
-                for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
-                for (int a = 0; a < 3; ++a)
-                    for (int b = 0; b < 3; ++b) {
-                        double g = (gR[3 * a] * nacc) * gR[3 * b];
-                        g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
-                        g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
-                        r.W[3 * a + b] = g;
-                    }
-                double S[9];
-                skew(sdv, S);
-                mm3(cbb0, S, r.C);
-                for (int i = 0; i < 9; ++i) r.D[i] = cbb0[i] * dt;
-                skew(sdth, S);
-                for (int i = 0; i < 9; ++i) r.M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
-                r.dt = dt;
-                r.f = 1 - dt / prm.corr_time;
-#pragma unroll
-                for (int i = 0; i < 11; ++i) r.S[i] = 0.0;
-                r.S[2] = dt;
-                r.S[5] = r.f;
-                r.S[8] = -dt;
-#pragma unroll
-                for (int i = 0; i < 5; ++i) r.S1[i] = i == 2 ? 1.0 : 0.0;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) r.Z[i] = 0.0;
-                r.pad = 0.0;
-                double* dst = reinterpret_cast<double*>(&sR[grp][c]);
-                const double* w = reinterpret_cast<const double*>(&r);
-#pragma unroll
-                for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
-            }
+            double* dst = sRec + grp * SEGR + c * RS;
+            if (k < m)
+                make_record<EARTH>(prm, pg0 + (k - 1), qr0, im[k], s0, k, nacc, dst);
+            else
+                identity_record(dst);
         }
         wave_lds_sync();
         const int kend = min(kc + C16_CK, mmax);
         for (int k = kc; k < kend; ++k) {
             const bool act = k < m;
-            const StepRec& r = sR[grp][k - kc];
-            // Phi copied out of the record once per step (29 doubles): the three
-            // mat-vecs then wait on no LDS reads of their own (+8 %, profiles/r04_v20/)
-            const Phi f = *reinterpret_cast<const Phi*>(&r);
-            if (act) {
-                const double dt = r.dt;
-                // the velocity / position sums (integrationProcess, the order of preint_kernel)
-                double dvel[3];
-                if (!earth) {
-                    for (int i = 0; i < 3; ++i) dvel[i] = r.a[i] + g3[i] * dt;
-                } else {
-                    double cc3[3], dvcg[3];
-                    cross3(iewn, v, cc3);
-                    for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
-                    for (int i = 0; i < 3; ++i) dvel[i] = r.a[i] + dvcg[i];
-                }
-                for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
-                for (int i = 0; i < 3; ++i) v[i] += dvel[i];
-                if (pns && c == 0)
-                    *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
-                for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * r.b[i];
-                for (int i = 0; i < 3; ++i) dv[i] += r.b[i];
-                double y[NS];
-                phi_mv(f, Pc, y);
-                if (c < NS) {
+            const double* rw = sRec + grp * SEGR + (k - kc) * RS;
+            // the record's Phi, increments and this lane's Q operands (one wait);
+            // W and row c of Phi are read after the hand-over, where they are used
+            const Phi f = *reinterpret_cast<const Phi*>(rw);
+            double ra[3], rb[3], wq[3];
 #pragma unroll
-                    for (int i = 0; i < NS; ++i) sG[grp][c * NS + i] = y[i];
-                }
-                // K's Q terms added where K is read from (LDS add after this lane's
-                // own column write; the same fp64 add as K[i] + a*w): the W block for
-                // lanes 3..5, the diagonal for lanes 6..14
-                {
-                    const double a = 0.5 * f.dt;
-                    if (c >= 3 && c < 6) {
-#pragma unroll
-                        for (int j = 0; j < 3; ++j)
-                            __hip_atomic_fetch_add(&sG[grp][(3 + j) * NS + c], a * r.W[3 * j + c - 3],
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else if (c >= 6 && c < NS) {
-                        __hip_atomic_fetch_add(&sG[grp][c * NS + c], a * wdc, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                phi_mv(f, Jc, y);
-#pragma unroll
-                for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            for (int i = 0; i < 3; ++i) {
+                ra[i] = rw[oA + i];
+                rb[i] = rw[oA + 3 + i];
+                wq[i] = rw[oW + 3 * i + qw];
             }
+            const double dt = f.dt;
+            const double a = 0.5 * dt;
+            // the velocity / position sums (integrationProcess, the order of preint_kernel)
+            double dvel[3];
+            if constexpr (!EARTH) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) dvel[i] = ra[i] + g3[i] * dt;
+            } else {
+                double cc3[3], dvcg[3];
+                cross3(iewn, v, cc3);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) dvcg[i] = (g3[i] - 2.0 * cc3[i]) * dt;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) dvel[i] = ra[i] + dvcg[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v[i] += dvel[i];
+            if (pns && c == 0 && act)
+                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
+#pragma unroll
+            for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * rb[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) dv[i] += rb[i];
+            // G(:,c) = Phi P(:,c), stored transposed (element i to row i); lane 15
+            // writes column 15, which no row read uses
+            double y[NS];
+            phi_mv(f, Pc, y);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) tile[i * TS + c] = y[i];
+            // K's Q terms: a W(3:6, c) into row c, cols 3..5 (lanes 3..5), a w_c
+            // onto the diagonal (lanes 6..14) -- after every lane's stores
+            double qa[3];
+#pragma unroll
+            for (int b = 0; b < 3; ++b) qa[b] = a * wq[b];
+            const double qdg = a * wdc;
             wave_lds_sync();
+            if (qv) {
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    __hip_atomic_fetch_add(&tile[c * TS + 3 + b], qa[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (qd) {
+                __hip_atomic_fetch_add(&tile[c * TS + c], qdg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            // J <- Phi J (no LDS: fills the hand-over's latency)
+            phi_mv(f, Jc, y);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            wave_lds_sync();
+            // K = row c of the tile = G(c,:)^T + a W(:,c); row 15 is padding
+            double K[NS], W[9], ph[NS];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) K[i] = tile[c * TS + i];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) W[i] = rw[oW + i];
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                ph[3 + b] = rw[ph3 + b];
+                ph[6 + b] = rw[ph6 + b];
+                ph[9 + b] = rw[ph9 + b];
+                ph[12 + b] = rw[ph12 + b];
+            }
             if (act) {
-                const double a = 0.5 * f.dt;
-                const int cl = c < NS ? c : 0;
-                double K[NS];
-#pragma unroll
-                for (int i = 0; i < NS; ++i) K[i] = sG[grp][i * NS + cl];
-                const double* rw = reinterpret_cast<const double*>(&r);
-                double ph[NS];
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    ph[3 + b] = rw[ph3 + b];
-                    ph[6 + b] = rw[ph6 + b];
-                    ph[9 + b] = rw[ph9 + b];
-                    ph[12 + b] = rw[ph12 + b];
-                }
-                double y[NS];
                 phi_mv(f, K, y);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Pc[i] = y[i];
-                q_terms(a, r.W, wg, nbg, nba, ph, y, Pc);
+                q_terms(a, W, wg, nbg, nba, ph, y, Pc);
             }
-            wave_lds_sync();
+            wave_lds_sync();  // the next step's stores after this step's reads
         }
     }
-    if (!live) return;
     gvx_preint_result* o = out + seg;
-    if (c < NS) {
+    if (live && c < NS) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             o->jacobian[i * NS + c] = Jc[i];
             o->covariance[c * NS + i] = Pc[i];
         }
     }
-    if (c == 0)
+    if (live && c == 0)
         for (int i = 0; i < 3; ++i) {
             o->current.p[i] = p[i];
             o->current.v[i] = v[i];
             o->delta.p[i] = dp[i];
             o->delta.v[i] = dv[i];
         }
-    if constexpr (SQRT_INFO) {
-        // sqrt_information_ from P while it is in registers, in the record
-        // region (the same function as factors.hip sqrt_info_kernel, same bits):
-        // no fifth launch, no read-back of the covariance
-        wave_lds_sync();  // the last step's record reads are done
-        double* A = reinterpret_cast<double*>(&sR[0][0]) + grp * SI_GROUP_DW;
-        double* X = A + NS * NS;
-        int* perm = reinterpret_cast<int*>(X + NS * NS);
-        if (c < NS) {
+    // sqrt_information_ from P while it is in registers, in the record region
+    // (the same function as factors.hip sqrt_info_kernel, same bits): no extra
+    // launch, no read-back of the covariance.  Dead groups factor the identity
+    // and store nothing, so every lane reaches every barrier.
+    wave_lds_sync();  // the last step's record reads are done
+    double* A = sRec + grp * SI_GROUP_DW;
+    double* X = A + NS * NS;
+    int* perm = reinterpret_cast<int*>(X + NS * NS);
+    if (c < NS) {
 #pragma unroll
-            for (int i = 0; i < NS; ++i) A[c * NS + i] = Pc[i];
-        }
-        sqrt_info_group(A, X, perm, c, o->sqrt_info);
+        for (int i = 0; i < NS; ++i) A[c * NS + i] = live ? Pc[i] : (i == c ? 1.0 : 0.0);
     }
+    sqrt_info_group(A, X, perm, c, live ? o->sqrt_info : nullptr);
 }
 
 }  // namespace
@@ -1140,16 +987,16 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                          const double* iewn, gvx_preint_result* out, double* pn, bool* sqrt_info_done) {
     if (sqrt_info_done) *sqrt_info_done = false;
     if (n_seg <= 0) return hipSuccess;
-    // Four-launch form when the per-step scratch can be sized without a round trip:
-    // the IMU allocation bounds the number of samples (hipMemGetAddressRange).
-    // A pointer into a large pooled block bounds nothing useful: above 1 GiB of
-    // scratch the single kernel runs.  GVX_PREINT_ONEPHASE=1 forces it (A/B and
-    // the bit-identity test; read per call).
-    const char* e1 = getenv("GVX_PREINT_ONEPHASE");
-    const bool one_phase = e1 && atoi(e1) != 0;
+    // Three-launch form when the per-step scratch can be sized without a round
+    // trip: the IMU allocation bounds the number of samples
+    // (hipMemGetAddressRange).  A pointer into a large pooled block bounds nothing
+    // useful: above 1 GiB of scratch the single kernel runs.
+    // gvx_set_preint_path(GVX_PREINT_PATH_ONEPHASE) forces it (A/B and the parity
+    // test of the two forms).
     hipDeviceptr_t base = nullptr;
     size_t range = 0;
-    if (!one_phase && hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)imu) == hipSuccess && range > 0) {
+    if (c->preint_path != GVX_PREINT_PATH_ONEPHASE &&
+        hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)imu) == hipSuccess && range > 0) {
         const size_t samples = (reinterpret_cast<const char*>(base) + range - reinterpret_cast<const char*>(imu)) /
                                sizeof(gvx_imu);
         const size_t bytes = samples * STEP_SCRATCH;
@@ -1157,27 +1004,17 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
         if (d) {
             PreG* pre = reinterpret_cast<PreG*>(d);
             QRec* qr = reinterpret_cast<QRec*>(d + samples * sizeof(PreG));
-            RRec* rr = reinterpret_cast<RRec*>(d + samples * (sizeof(PreG) + sizeof(QRec)));
+            const bool earth = variant == GVX_PREINT_EARTH;
             hipLaunchKernelGGL(preint_pre_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, imu, seg_off,
                                state0, iewn, pre);
-            hipLaunchKernelGGL(variant == GVX_PREINT_EARTH ? preint_chain_kernel<true> : preint_chain_kernel<false>,
+            hipLaunchKernelGGL(earth ? preint_chain_kernel<true> : preint_chain_kernel<false>,
                                dim3((n_seg + 63) / 64), dim3(128), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
                                (const PreG*)pre, qr, out);
-            // the covariance pass: 16 lanes per segment with the step blocks (and the
-            // rotated terms) formed 8 steps at a time off the sequential chain
-            // (GVX_PREINT_COV8=1: the rot pass, then the 8-lane kernel that forms the
-            // blocks per step on every lane, for A/B)
-            const char* e8 = getenv("GVX_PREINT_COV8");
-            if (e8 && atoi(e8) != 0) {
-                hipLaunchKernelGGL(preint_rot_kernel, dim3(std::min(n_seg, c->n_cu * 8)), dim3(64), 0, c->stream, variant,
-                                   n_seg, seg_off, state0, (const PreG*)pre, (const QRec*)qr, rr);
-                hipLaunchKernelGGL(preint_cov_kernel<8>, dim3((n_seg + 7) / 8), dim3(64), 0, c->stream, variant, prm,
-                                   n_seg, imu, seg_off, state0, iewn, (const RRec*)rr, out, pn);
-            } else {
-                hipLaunchKernelGGL(preint_cov16_kernel<true>, dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, variant,
-                                   prm, n_seg, imu, seg_off, state0, iewn, (const PreG*)pre, (const QRec*)qr, out, pn);
-                if (sqrt_info_done) *sqrt_info_done = true;
-            }
+            // the covariance pass, sqrt_info in its epilogue
+            hipLaunchKernelGGL(earth ? preint_cov16_kernel<true> : preint_cov16_kernel<false>,
+                               dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
+                               (const PreG*)pre, (const QRec*)qr, out, pn);
+            if (sqrt_info_done) *sqrt_info_done = true;
             return hipGetLastError();
         }
     }

@@ -34,6 +34,8 @@ class GvxError(RuntimeError):
 
 # gvx_set_marg_solver (include/gvx.h GVX_MARG_SOLVER_*)
 MARG_SOLVER_EXACT, MARG_SOLVER_FAST = 0, 1
+# gvx_set_preint_path (include/gvx.h GVX_PREINT_PATH_*)
+PREINT_PATH_AUTO, PREINT_PATH_ONEPHASE = 0, 1
 
 # gvx_klt_params.accum (include/gvx.h GVX_LK_ACCUM_*): LK's window-sum order
 LK_ACCUM_EXACT, LK_ACCUM_F32_SCALAR, LK_ACCUM_F32_SIMD4 = 0, 1, 2
@@ -234,6 +236,7 @@ def _declare(L):
         "gvx_schur_solve_dev": (i32, [P, i32, P, P, P, P, P, P, i64, i32, P, P, i32, i32, P, P, P, P]),
         "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
         "gvx_set_marg_solver": (i32, [P, i32]),
+        "gvx_set_preint_path": (i32, [P, i32]),
         "gvx_find_fundamental_ransac": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
         "gvx_copy_indexed_dev": (i32, [P, P, P, C.c_size_t, P, i32]),
         "gvx_track_record_dev": (i32, [P, P, P, i32, P, P, P, i32]),
@@ -845,6 +848,11 @@ class Context:
                                                 _ptr(joff), d_data, n_data, d_loss, size.size, _ptr(size),
                                                 _ptr(index), m, L, d_J0, d_e0, d_Hp, d_bp, d_eval, d_info),
                     "gvx_marginalize_dev")
+
+    def set_preint_path(self, path: int):
+        """gvx_set_preint_path: PREINT_PATH_AUTO (the three-launch form) or
+        PREINT_PATH_ONEPHASE (the single kernel; A/B and parity switch)."""
+        self._check(self._L.gvx_set_preint_path(self._h, path), "gvx_set_preint_path")
 
     def set_marg_solver(self, solver: int):
         """gvx_set_marg_solver: MARG_SOLVER_EXACT (Eigen's eigen-solver, bit-exact

@@ -484,6 +484,15 @@ gvx_status gvx_preint_integrate_dev(gvx_ctx* ctx, int32_t variant, const gvx_imu
                                     int32_t n_seg, const gvx_imu* d_imu, const int32_t* d_seg_off,
                                     const gvx_state* d_state0, const double* d_iewn,
                                     gvx_preint_result* d_out, double* d_pn);
+/* Which form gvx_preint_integrate[_dev] runs (default GVX_PREINT_PATH_AUTO:
+   the three-launch form -- per-step terms, the quaternion chains, the covariance
+   pass with sqrt_information_ in its epilogue -- whenever its scratch can be
+   sized; the single kernel otherwise).  GVX_PREINT_PATH_ONEPHASE forces the
+   single kernel: an A/B and parity switch, per context.  The environment
+   variable GVX_PREINT_ONEPHASE=1 sets it when the context is created. */
+#define GVX_PREINT_PATH_AUTO 0
+#define GVX_PREINT_PATH_ONEPHASE 1
+gvx_status gvx_set_preint_path(gvx_ctx* ctx, int32_t path);
 
 /* Earth::iewn(station, p) (common/earth.h:233-237), host-side helper used by
    resetState (preintegration_earth.cc:320). */
