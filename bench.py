@@ -175,6 +175,40 @@ def cpu_factor_baseline(prob, segs, states, iewn, params, poffs, threads, budget
                       f"preintegration, M=100, residuals + Jacobians), {threads} thread(s), {dt:.1f} s"}
 
 
+def cpu_preint_baseline(segs, states, iewn, threads, budget_s=2.0):
+    """Oracle preintegration (orc_preint_integrate: the reference's
+    integrationProcess + updateJacobianAndCovariance per sample, Eigen's dense
+    15 x 15 products restated in C) of configs[3]'s Earth segments, one segment
+    per call, independent segments on `threads` host threads at once (the
+    ctypes calls release the GIL), bounded to about budget_s seconds ->
+    preintegration steps/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # test-infrastructure import: cpu_baseline leg only
+    from concurrent.futures import ThreadPoolExecutor
+    from gvx import synth_ba
+    prm = orc.imu_params(*synth_ba.imu_params())
+    st = [orc.make_state(float(s["time"]), s["p"], s["q"], s["v"], s["bg"], s["ba"]) for s in states]
+    orc.PreintSeg(2, prm, segs[0], st[0], iewn[0])  # warm
+    t0 = time.perf_counter()
+
+    def worker(wi):
+        n = 0
+        k = wi
+        while time.perf_counter() - t0 < budget_s:
+            j = k % len(segs)
+            orc.PreintSeg(2, prm, segs[j], st[j], iewn[j])
+            n += len(segs[j]) - 1
+            k += 1
+        return n
+
+    with ThreadPoolExecutor(threads) as ex:
+        steps = sum(ex.map(worker, range(threads)))
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "preintegration steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} IMU steps of Earth segments (M = {len(segs[0])}) through orc_preint_integrate, "
+                      f"one segment per call, {threads} thread(s), {dt:.1f} s"}
+
+
 def traffic_for(workload):
     """PMC HBM bytes per step measured on this workload (tools/traffic.py)."""
     f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -690,8 +724,10 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     d_jac = torch.empty((n_r, 46), dtype=torch.float64, device=dev)
     n_p = (n_kf - 1) * reps
     d_pre = dev_t(np.tile(pre, reps).view(np.uint8))
-    d_pn = dev_t(pn)
-    d_pn_off = dev_t(np.tile(pn_off, reps))
+    # every replica its own copy of the pn_ samples (the streamed bytes the
+    # preintegration factor roofline counts)
+    d_pn = dev_t(np.tile(pn, (reps, 1)))
+    d_pn_off = dev_t(np.concatenate([pn_off + r * len(pn) for r in range(reps)]).astype(np.int32))
     d_poffs = dev_t(np.tile(poffs, (reps, 1)))
     d_pres = torch.empty((n_p, 15), dtype=torch.float64, device=dev)
     d_pjac = torch.empty((n_p, 480), dtype=torch.float64, device=dev)
@@ -772,6 +808,7 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     pf_ms = fam["preint_factor"][0] / steps
     B_pf = 8 * (16 + 225 + 225 + 4 * M + 7) + 8 * (15 + 15 * 32)  # SURVEY 8d, M = 100: 10,944 B
     B_rp = 15 * 8 + 5 * 4 + 48 * 8  # consts + offsets in, residual + 5 Jacobian blocks out
+    B_rp_survey = 504  # SURVEY 8d's per-factor figure (its Jacobian count, no offsets)
     achieved = B_rp * n_r / (rp_ms * 1e-3) / 1e9 if rp_ms > 0 else None
     line = None
     if rank == 0:
@@ -789,14 +826,19 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
                          "algorithmic_bytes_per_factor": B_rp,
+                         "survey_bytes_per_factor": B_rp_survey,
+                         "frac_at_survey_bytes": round(B_rp_survey * n_r / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if rp_ms > 0 else None,
                          "device_ms_per_step": {k: round(v[0] / steps, 4) for k, v in fam.items()}},
             "preint_factor_roofline": {"bound": "hbm", "kernel": "preint_factor_kernel",
                                        "achieved": round(pf_achieved, 1) if pf_achieved else None,
                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                        "frac": round(pf_achieved / HBM_PEAK_GBS, 4) if pf_achieved else None,
-                                       "algorithmic_bytes_per_factor": B_pf},
+                                       "algorithmic_bytes_per_factor": B_pf,
+                                       "pn_samples": "one copy per replica (streamed, not shared)"},
             "preint_steps_per_s": round(world * S * (M - 1) * k_i / el_i, 1),
             "preint_device_ms_per_launch": round(fam_i["preint"][0] / k_i, 4),
+            "preint_cpu_baseline": None,
             "problem_size": {"window_factors": n_w,
                              "device_launch_evals_per_s": round(world * n_w * k_w / el_w, 1),
                              "factor_set_prepare_evals_per_s": round(world * n_w * k_w / el_p, 1),
@@ -813,6 +855,15 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
                 ref["all_cores_value"] = allc["value"]
                 ref["all_cores_sample"] = allc["sample"]
             line["cpu_baseline"] = ref
+            # the integrate scan on the CPU (preintegration_earth.cc:205-303 per
+            # addNewImu), the same 99-step Earth segments: the reference's
+            # 4 threads and the box's CPU share
+            pre_ref = cpu_preint_baseline(segs, states, iewn, threads=4)
+            if nt != 4:
+                pre_all = cpu_preint_baseline(segs, states, iewn, threads=nt)
+                pre_ref["all_cores_value"] = pre_all["value"]
+                pre_ref["all_cores_sample"] = pre_all["sample"]
+            line["preint_cpu_baseline"] = pre_ref
     return line
 
 

@@ -175,6 +175,8 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
         // A/B switches are read once, here (not per launch)
         const char* e = std::getenv("GVX_PREINT_ONEPHASE");
         if (e && std::atoi(e) != 0) c->preint_path = GVX_PREINT_PATH_ONEPHASE;
+        const char* f = std::getenv("GVX_FACTORSET_D2H");
+        c->factorset_d2h = f && std::atoi(f) != 0;
     }
     *out = c;
     return GVX_OK;

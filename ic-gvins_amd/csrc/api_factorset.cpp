@@ -30,9 +30,15 @@ struct gvx_factor_set {
     int32_t* d_poffs = nullptr;
     double* d_params = nullptr;
     double* d_out = nullptr;  // reproj res | reproj jac | preint res | preint jac
-    // pinned host: gathered parameters and the results of the last prepare
+    // pinned host: gathered parameters and the results of the last prepare.
+    // h_out is mapped into the device's address space (dh_out): the kernels
+    // store the results straight into it over PCIe while they run, so a
+    // prepare has no device-to-host copy to wait for (out_mode 1; 0 = a device
+    // buffer and one D2H copy, the r04 form, kept for A/B: GVX_FACTORSET_D2H=1)
     double* h_params = nullptr;
     double* h_out = nullptr;
+    double* dh_out = nullptr;
+    int out_mode = 1;
     size_t out_doubles = 0;
     bool have_jac = false, prepared = false;
 };
@@ -129,8 +135,10 @@ gvx_status gvx_factor_set_create(gvx_ctx* c, int32_t n_blocks, const double* con
     size_t total = 0;
     for (size_t b : sz) total += align256(b);
     hipSetDevice(c->device);
+    s->out_mode = c->factorset_d2h ? 0 : 1;
     if (hipMalloc(&s->dev, total) != hipSuccess || hipHostMalloc(&s->h_params, sizeof(double) * s->n_params) != hipSuccess ||
-        hipHostMalloc(&s->h_out, sizeof(double) * (s->out_doubles + 1)) != hipSuccess) {
+        hipHostMalloc(&s->h_out, sizeof(double) * (s->out_doubles + 1), hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->dh_out, s->h_out, 0) != hipSuccess) {
         destroy(s);
         return set_err(c, GVX_ERR_OOM, "factor set (%zu bytes)", total);
     }
@@ -191,7 +199,7 @@ gvx_status gvx_factors_prepare(gvx_factor_set* s, int32_t with_jacobians) {
     hipError_t e = hipMemcpyAsync(s->d_params, s->h_params, sizeof(double) * s->n_params, hipMemcpyHostToDevice,
                                   c->stream);
     if (e != hipSuccess) return hip_err(c, e, "factor parameters H2D");
-    double* rres = s->d_out;
+    double* rres = s->out_mode == 1 ? s->dh_out : s->d_out;
     double* rjac = rres + (size_t)RP_RES * s->n_reproj;
     double* pres = rjac + (size_t)RP_JAC * s->n_reproj;
     double* pjac = pres + (size_t)PF_RES * s->n_preint;
@@ -201,8 +209,11 @@ gvx_status gvx_factors_prepare(gvx_factor_set* s, int32_t with_jacobians) {
                                               s->n_preint, s->d_pre, s->d_pn, s->d_pn_off, s->d_poffs, pres,
                                               jac ? pjac : nullptr, s->d_params);
     if (st) return st;
-    // one D2H of everything evaluated (the Jacobian regions only when computed)
-    if (jac) {
+    // one D2H of everything evaluated (the Jacobian regions only when computed),
+    // unless the kernels wrote it to the mapped host buffer themselves
+    if (s->out_mode == 1) {
+        e = hipSuccess;
+    } else if (jac) {
         e = hipMemcpyAsync(s->h_out, s->d_out, sizeof(double) * s->out_doubles, hipMemcpyDeviceToHost, c->stream);
     } else {
         e = hipMemcpyAsync(s->h_out, rres, sizeof(double) * RP_RES * s->n_reproj, hipMemcpyDeviceToHost, c->stream);

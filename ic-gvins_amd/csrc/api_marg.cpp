@@ -369,6 +369,10 @@ namespace {
 gvx_status run_lm(gvx_ctx* c, Lists& ls, const double* d_data, const double* d_D, int m, int L, double* d_delta,
                   double* d_S, int32_t* d_info) {
     const int r = L - m;
+    // the dense L x L H0 (and the 32-bit indexing of the H0 kernels) bound the
+    // window: GVX_SCHUR_MAX_L parameters, 2 GiB of H0
+    if (L > GVX_SCHUR_MAX_L)
+        return set_err(c, GVX_ERR_UNSUPPORTED, "schur solve: %d parameters (max %d)", L, GVX_SCHUR_MAX_L);
     const bool diag = diagonal_e(ls, m);
     if (!diag && m > GVX_EIG_MAX_N)
         return set_err(c, GVX_ERR_UNSUPPORTED, "schur solve: %d eliminated parameters with a non-diagonal Hee (max %d)",

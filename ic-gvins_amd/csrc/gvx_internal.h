@@ -89,6 +89,9 @@ struct gvx_ctx {
     int32_t marg_solver = GVX_MARG_SOLVER_FAST;
     // gvx_set_preint_path (GVX_PREINT_ONEPHASE=1 at creation: the single kernel)
     int32_t preint_path = GVX_PREINT_PATH_AUTO;
+    // factor sets created with a device result buffer and a D2H copy per prepare
+    // (GVX_FACTORSET_D2H=1 at creation; A/B against the mapped host buffer)
+    bool factorset_d2h = false;
     // gvx_track_frame_dev: what the detection constants in "trk_static" were
     // built for (the buffer itself and the geometry)
     struct TrackStatic {

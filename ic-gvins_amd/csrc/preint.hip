@@ -841,7 +841,10 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
     const int ph6 = (c >= 3 && c < 6) ? oC + 3 * (c - 3) : ((c >= 6 && c < 9) ? oM + 3 * (c - 6) : oZ);
     const int ph9 = (c >= 6 && c < 9) ? oS + 8 - (c - 6) : ((c >= 9 && c < 12) ? oS + 5 - (c - 9) : oZ);
     const int ph12 = (c >= 3 && c < 6) ? oD + 3 * (c - 3) : ((c >= 12 && c < NS) ? oS + 5 - (c - 12) : oZ);
-    const int qw = (c >= 3 && c < 6) ? c - 3 : 0;
+    // lane c's W column (c mod 3): the Q adds of lanes 3..5 and q_terms' W phi_c(3:6)
+    // (phi_c(3:6) has its one non-zero, dt for c < 3 or 1 for c < 6, at c mod 3)
+    const int qw = c % 3;
+    const int phs = ph3 + qw;
     const bool qv = c >= 3 && c < 6, qd = c >= 6 && c < NS;
     double Jc[NS], Pc[NS];
 #pragma unroll
@@ -878,6 +881,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
                 rb[i] = rw[oA + 3 + i];
                 wq[i] = rw[oW + 3 * i + qw];
             }
+            const double sc = rw[phs];
             const double dt = f.dt;
             const double a = 0.5 * dt;
             // the velocity / position sums (integrationProcess, the order of preint_kernel)
@@ -913,7 +917,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             // onto the diagonal (lanes 6..14) -- after every lane's stores
             double qa[3];
 #pragma unroll
-            for (int b = 0; b < 3; ++b) qa[b] = a * wq[b];
+            for (int b = 0; b < 3; ++b) qa[b] = a * wq[b];  // wq = W(3 + b, c - 3) for lanes 3..5
             const double qdg = a * wdc;
             wave_lds_sync();
             if (qv) {
@@ -923,29 +927,35 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             } else if (qd) {
                 __hip_atomic_fetch_add(&tile[c * TS + c], qdg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            // J <- Phi J (no LDS: fills the hand-over's latency)
-            phi_mv(f, Jc, y);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) Jc[i] = y[i];
             wave_lds_sync();
-            // K = row c of the tile = G(c,:)^T + a W(:,c); row 15 is padding
-            double K[NS], W[9], ph[NS];
+            // K = row c of the tile = G(c,:)^T + a W(:,c) (row 15 is padding) and
+            // row c of Phi, cols 6..14; issued before J's update, which runs
+            // while they land (sched_barrier: the compiler would sink it)
+            double K[NS], ph[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) K[i] = tile[c * TS + i];
 #pragma unroll
-            for (int i = 0; i < 9; ++i) W[i] = rw[oW + i];
-#pragma unroll
             for (int b = 0; b < 3; ++b) {
-                ph[3 + b] = rw[ph3 + b];
                 ph[6 + b] = rw[ph6 + b];
                 ph[9 + b] = rw[ph9 + b];
                 ph[12 + b] = rw[ph12 + b];
             }
+            __builtin_amdgcn_sched_barrier(0);
+            phi_mv(f, Jc, y);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) Jc[i] = y[i];
+            __builtin_amdgcn_sched_barrier(0);
             if (act) {
                 phi_mv(f, K, y);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Pc[i] = y[i];
-                q_terms(a, W, wg, nbg, nba, ph, y, Pc);
+                // q_terms with W phi_c(3:6) = sc W(:, c mod 3) (the other two terms
+                // of the sum are exact zeros)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Pc[3 + i] = __builtin_fma(a, wq[i] * sc, y[3 + i]);
+                const double ag = a * wg, abg = a * nbg, aba = a * nba;
+#pragma unroll
+                for (int i = 6; i < NS; ++i) Pc[i] = __builtin_fma(i < 9 ? ag : (i < 12 ? abg : aba), ph[i], y[i]);
             }
             wave_lds_sync();  // the next step's stores after this step's reads
         }

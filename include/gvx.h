@@ -605,7 +605,10 @@ gvx_status gvx_marginalize_dev(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres,
    failed Hee + D also sets info[1], since S is then never formed).  When either
    factorisation fails every entry of delta is NaN and gvx_schur_solve returns
    GVX_ERR_NUMERIC after writing delta, S and info (Ceres' linear solver
-   reports FAILURE and LM rejects the step). */
+   reports FAILURE and LM rejects the step).  The window holds at most
+   GVX_SCHUR_MAX_L local parameters (L; the dense H0 is L x L fp64, 2 GiB at the
+   bound): larger ones return GVX_ERR_UNSUPPORTED. */
+#define GVX_SCHUR_MAX_L 16384
 gvx_status gvx_schur_solve(gvx_ctx* ctx, int32_t n_fac, const int32_t* nres, const int32_t* blk_off,
                            const int32_t* blk, const int64_t* res_off, const int64_t* jac_off, const double* data,
                            int64_t n_data, int32_t nb, const int32_t* size, const int32_t* index, int32_t m,

@@ -71,6 +71,28 @@ def test_schur_solve_many_landmarks(ctx, orc):
     _check(ctx.schur_solve(p, D), p, D, 1e-9)
 
 
+def test_schur_solve_dev_many_landmarks(ctx, orc):
+    """The device-pointer entry on the diagonal-Hee path (m = 700 > 512, ADVICE
+    r04): the same delta as the host entry, bit for bit."""
+    import torch
+    p = synth_ba.lm_problem(synth_ba.make_marg_problem(orc.FactorEvaluator(), seed=11, n_kf=10, n_lm=700))
+    assert p["m"] == 700
+    L = p["L"]
+    H, _ = synth_ba.dense_normal_equations(p)
+    D = np.sqrt(1e-4 * np.maximum(np.diag(H), 1e-6))
+    g = ctx.schur_solve(p, D)
+    dev = torch.device("cuda")
+    d_data = torch.from_numpy(p["data"]).to(dev)
+    d_D = torch.from_numpy(D).to(dev)
+    d_delta = torch.zeros(L, dtype=torch.float64, device=dev)
+    d_info = torch.full((2,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.schur_solve_dev(p, d_data.data_ptr(), d_delta.data_ptr(), d_D=d_D.data_ptr(), d_info=d_info.data_ptr())
+    ctx.sync()
+    assert np.array_equal(d_delta.cpu().numpy(), g["delta"])
+    assert d_info.cpu().tolist() == [0, 0]
+
+
 def test_schur_solve_dev_matches_host(ctx, window):
     import torch
     p = window["prior over keyframes 0-8"]
