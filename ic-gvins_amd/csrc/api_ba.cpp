@@ -231,6 +231,13 @@ gvx_status gvx_factor_batch_eval_dev(gvx_ctx* c, int32_t n_reproj, const gvx_rep
     // second stream beside the reprojection one measured slower (both kernels
     // stretch: 0.162 -> 0.168 ms per configs[3] batch, r02 v17)
     hipError_t e = hipSuccess;
+    // a window that fills at most one workgroup per CU: both kinds in one launch
+    // (window_factor_kernel), so it costs the longer chain, not the sum
+    if (n_reproj > 0 && n_preint > 0 && window_factor_blocks(n_reproj, n_preint) <= c->n_cu) {
+        e = launch_window_factors(c, n_reproj, d_rc, d_roffs, d_rres, d_rjac, n_preint, d_pre, d_pn, d_pn_off, d_poffs,
+                                  d_pres, d_pjac, d_params);
+        return hip_err(c, e, "window factor kernel");
+    }
     if (n_reproj > 0) {
         e = launch_reproj(c, n_reproj, d_rc, d_params, d_roffs, d_rres, d_rjac);
         if (e != hipSuccess) return hip_err(c, e, "reproj kernel");

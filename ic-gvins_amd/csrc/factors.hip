@@ -52,14 +52,15 @@ __device__ __forceinline__ void put_2x7(const double* red, const double* L, cons
 constexpr int RP_THREADS = 128;
 constexpr int RP_OUT = 48;  // residual 2 + Jacobians 46
 
-__global__ void __launch_bounds__(RP_THREADS) reproj_kernel(int n, const gvx_reproj_const* __restrict__ cs,
-                                                             const double* __restrict__ params,
-                                                             const int32_t* __restrict__ offs,
-                                                             double* __restrict__ res,
-                                                             double* __restrict__ jac) {
-    __shared__ double stage[RP_THREADS * (RP_OUT + 1)];
+constexpr int RP_LDS = RP_THREADS * (RP_OUT + 1);  // doubles of the output staging
+// block `blk` of the reprojection batch (RP_THREADS threads): the body of
+// reproj_kernel and of window_factor_kernel's reprojection blocks
+__device__ __forceinline__ void reproj_body(int blk, double* __restrict__ stage, int n,
+                                            const gvx_reproj_const* __restrict__ cs,
+                                            const double* __restrict__ params, const int32_t* __restrict__ offs,
+                                            double* __restrict__ res, double* __restrict__ jac) {
     const int t = threadIdx.x;
-    const int base = blockIdx.x * RP_THREADS;
+    const int base = blk * RP_THREADS;
     const int i = base + t;
     double* out = stage + t * (RP_OUT + 1);
     if (i < n) {
@@ -180,6 +181,15 @@ __global__ void __launch_bounds__(RP_THREADS) reproj_kernel(int n, const gvx_rep
         }
 }
 
+__global__ void __launch_bounds__(RP_THREADS) reproj_kernel(int n, const gvx_reproj_const* __restrict__ cs,
+                                                             const double* __restrict__ params,
+                                                             const int32_t* __restrict__ offs,
+                                                             double* __restrict__ res,
+                                                             double* __restrict__ jac) {
+    __shared__ double stage[RP_LDS];
+    reproj_body(blockIdx.x, stage, n, cs, params, offs, res, jac);
+}
+
 // ------------------------------------------------------ preintegration factor
 __device__ __forceinline__ void set3(double* J, int ld, int r, int c, const double* B) {
     for (int i = 0; i < 3; ++i)
@@ -265,18 +275,24 @@ __device__ __forceinline__ double dpp_row_ror(double v) {
 // packed upper-triangular index of (r, c), c >= r, n = 15
 __device__ __forceinline__ int triu15(int r, int c) { return r * 15 - (r * (r - 1)) / 2 + (c - r); }
 
-__global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
-                                                           const double* __restrict__ pn,
-                                                           const int32_t* __restrict__ pn_off,
-                                                           const double* __restrict__ params,
-                                                           const int32_t* __restrict__ offs,
-                                                           double* __restrict__ res,
-                                                           double* __restrict__ jac) {
-    __shared__ double tile[2 * PN_INS * 128];  // pn_ chunks 0 / 1, then the Jr tiles
-    __shared__ double rec[PF_GROUPS * RC_STRIDE];
-    static_assert(PF_SLOTS * NS * PF_LD <= 2 * PN_INS * 128, "the tiles fit the pn_ staging");
-    const int grp = threadIdx.x / PF_L, lane = threadIdx.x % PF_L, tl = threadIdx.x;
-    const int f0 = blockIdx.x * PF_GROUPS;
+constexpr int PF_TILE = 2 * PN_INS * 128;        // doubles: pn_ chunks 0 / 1, then the Jr tiles
+constexpr int PF_REC = PF_GROUPS * RC_STRIDE;     // doubles: the factor records
+// the PF_GROUPS factors of group block `blk`, run by ONE wave (lanes tl = 0..63)
+// with its own LDS (tile, rec): the body of preint_factor_kernel and of
+// window_factor_kernel's preintegration waves.  Its two __syncthreads are
+// reached by every wave of a workgroup (no early exit, dead groups recompute a
+// valid factor and store nothing).
+__device__ __forceinline__ void preint_factor_body(int blk, double* __restrict__ tile, double* __restrict__ rec, int n,
+                                                   const gvx_preint_result* __restrict__ pre,
+                                                   const double* __restrict__ pn,
+                                                   const int32_t* __restrict__ pn_off,
+                                                   const double* __restrict__ params,
+                                                   const int32_t* __restrict__ offs, double* __restrict__ res,
+                                                   double* __restrict__ jac) {
+    static_assert(PF_SLOTS * NS * PF_LD <= PF_TILE, "the tiles fit the pn_ staging");
+    const int tl = threadIdx.x & 63;
+    const int grp = tl / PF_L, lane = tl % PF_L;
+    const int f0 = blk * PF_GROUPS;
     // dead groups (past n, or the partial group) recompute a valid factor and store nothing
     const int fi = min(f0 + min(grp, PF_GROUPS - 1), n - 1);
     const gvx_preint_result* s = pre + fi;
@@ -546,7 +562,7 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
         for (int i = 0; i < NS; ++i) Jr[i * PF_LD + 32] = r[i];
     // the whitening's A operands (sqrt_info rows / K) of the wave's four factors,
     // from the records' packed upper triangles (sqrt_info is upper triangular)
-    const int wl = threadIdx.x, wr = wl & 15, wk = wl >> 4;
+    const int wl = tl, wr = wl & 15, wk = wl >> 4;
     double SA[PF_GROUPS][4];
 #pragma unroll
     for (int f = 0; f < PF_GROUPS; ++f) {
@@ -627,7 +643,60 @@ __global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_prei
     }
 }
 
+__global__ void __launch_bounds__(64) preint_factor_kernel(int n, const gvx_preint_result* __restrict__ pre,
+                                                           const double* __restrict__ pn,
+                                                           const int32_t* __restrict__ pn_off,
+                                                           const double* __restrict__ params,
+                                                           const int32_t* __restrict__ offs,
+                                                           double* __restrict__ res,
+                                                           double* __restrict__ jac) {
+    __shared__ double tile[PF_TILE];
+    __shared__ double rec[PF_REC];
+    preint_factor_body(blockIdx.x, tile, rec, n, pre, pn, pn_off, params, offs, res, jac);
+}
+
+// A small window's two factor kinds in ONE launch (a Ceres window: 1,800
+// reprojection + 9 preintegration factors): workgroups [0, nbr) are
+// reprojection blocks, the rest carry two preintegration waves each, so the
+// window costs the longer of the two dependent chains instead of their sum
+// (two launches back to back: 29.7 us at r04).  The bodies are the same code
+// as the two kernels', so the results are the same bits.
+constexpr int WF_LDS = RP_LDS > 2 * (PF_TILE + PF_REC) ? RP_LDS : 2 * (PF_TILE + PF_REC);
+__global__ void __launch_bounds__(RP_THREADS) window_factor_kernel(
+    int nbr, int n_r, const gvx_reproj_const* __restrict__ cs, const int32_t* __restrict__ roffs,
+    double* __restrict__ rres, double* __restrict__ rjac, int n_p, const gvx_preint_result* __restrict__ pre,
+    const double* __restrict__ pn, const int32_t* __restrict__ pn_off, const int32_t* __restrict__ poffs,
+    double* __restrict__ pres, double* __restrict__ pjac, const double* __restrict__ params) {
+    static_assert(RP_THREADS == 128, "two preintegration waves per workgroup");
+    __shared__ double lds[WF_LDS];
+    if ((int)blockIdx.x < nbr) {
+        reproj_body(blockIdx.x, lds, n_r, cs, params, roffs, rres, rjac);
+    } else {
+        const int w = threadIdx.x >> 6;
+        double* tile = lds + w * (PF_TILE + PF_REC);
+        preint_factor_body(2 * ((int)blockIdx.x - nbr) + w, tile, tile + PF_TILE, n_p, pre, pn, pn_off, params, poffs,
+                           pres, pjac);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_window_factors(gvx_ctx* c, int n_r, const gvx_reproj_const* cs, const int32_t* roffs, double* rres,
+                                 double* rjac, int n_p, const gvx_preint_result* pre, const double* pn,
+                                 const int32_t* pn_off, const int32_t* poffs, double* pres, double* pjac,
+                                 const double* params) {
+    const int nbr = (n_r + RP_THREADS - 1) / RP_THREADS;
+    const int nbp = ((n_p + PF_GROUPS - 1) / PF_GROUPS + 1) / 2;
+    if (nbr + nbp == 0) return hipSuccess;
+    return launch_timed(c, "factor_window", window_factor_kernel, dim3(nbr + nbp), dim3(RP_THREADS), 0, nbr, n_r, cs,
+                        roffs, rres, rjac, n_p, pre, pn, pn_off, poffs, pres, pjac, params);
+}
+
+// the fused launch takes windows whose blocks fill at most this many workgroups
+// per CU (the batched launches beyond it: the two kernels are tuned apart)
+int window_factor_blocks(int n_r, int n_p) {
+    return (n_r + RP_THREADS - 1) / RP_THREADS + ((n_p + PF_GROUPS - 1) / PF_GROUPS + 1) / 2;
+}
 
 hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
                          const int32_t* offs, double* res, double* jac) {

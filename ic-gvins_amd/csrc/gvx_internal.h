@@ -321,6 +321,12 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                          const gvx_imu* imu, const int32_t* seg_off, const gvx_state* state0,
                          const double* iewn, gvx_preint_result* out, double* pn,
                          bool* sqrt_info_done = nullptr);  // set when the covariance pass formed sqrt_info
+// both factor kinds of a small window in one launch (factors.hip window_factor_kernel)
+hipError_t launch_window_factors(gvx_ctx* c, int n_r, const gvx_reproj_const* cs, const int32_t* roffs, double* rres,
+                                 double* rjac, int n_p, const gvx_preint_result* pre, const double* pn,
+                                 const int32_t* pn_off, const int32_t* poffs, double* pres, double* pjac,
+                                 const double* params);
+int window_factor_blocks(int n_r, int n_p);
 hipError_t launch_reproj(gvx_ctx* c, int n, const gvx_reproj_const* cs, const double* params,
                          const int32_t* offs, double* res, double* jac);
 hipError_t launch_sqrt_info(gvx_ctx* c, int n, gvx_preint_result* pre);

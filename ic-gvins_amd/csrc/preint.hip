@@ -413,22 +413,22 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
     }
 }
 
-// ------------------------------------------------ three-launch preintegration
+// ------------------------------------------------ two-launch preintegration
 // preint_kernel's sequential part runs on every lane of a wave that serves 4
 // segments: the wave's issue time per step is the same whether it advances 4
 // segments or 64, and 5,247 segments give 1.3 k such waves for 1,024 SIMDs.
 // Of that part only the two quaternion chains (cur.q and the delta rotation
 // dqt) and the velocity / position sums are truly sequential; the rotation
-// matrices and rotated increments of a step follow from the chain values.  So:
+// matrices and rotated increments of a step follow from the chain values, and
+// the chains themselves are products of per-step quaternions.  So:
 //   preint_pre_kernel    one lane per STEP (a workgroup per segment): the
-//                        StepPre terms -- every transcendental of the step;
-//   preint_chain_kernel  one lane per SEGMENT (64 per wave): the two quaternion
-//                        chains alone, StepPre prefetched ahead;
+//                        StepPre terms -- every transcendental of the step --
+//                        and the two chains as wave-wide prefix products;
 //   preint_cov16_kernel  16 lanes per segment: the step records (rotated terms,
 //                        Phi, W) formed 8 steps at a time, one step per lane,
 //                        then the velocity / position sums, J <- Phi J and
 //                        P <- Phi P Phi^T + Qk per step, sqrt_info at the end.
-// Every value is formed by the same operations in the same order as in
+// Every other value is formed by the same operations in the same order as in
 // preint_kernel (tests/test_ba_gpu.py).
 struct PreG {                // StepPre terms of one step (scratch, per IMU step)
     double dtime;            // delta_time after the step
@@ -442,17 +442,67 @@ struct QRec {                // the chains after step k
 };
 constexpr size_t STEP_SCRATCH = sizeof(PreG) + sizeof(QRec);  // per IMU sample
 
-__global__ void __launch_bounds__(64, 6) preint_pre_kernel(int variant, int n_seg, const gvx_imu* __restrict__ imu,
+// A quaternion through one DPP lane move (both dwords of each double); lanes
+// the move does not write (rows off ROWS, or a row shift's first lanes) take
+// the identity
+template <int CTRL, int ROWS>
+__device__ __forceinline__ dq dq_dpp(dq v) {
+    const auto mv = [](double x, double o) -> double {
+        const int lo = __builtin_amdgcn_update_dpp(__double2loint(o), __double2loint(x), CTRL, ROWS, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(__double2hiint(o), __double2hiint(x), CTRL, ROWS, 0xf, false);
+        return __hiloint2double(hi, lo);
+    };
+    return dq{mv(v.x, 0.0), mv(v.y, 0.0), mv(v.z, 0.0), mv(v.w, 1.0)};
+}
+// Inclusive prefix products of one quaternion per lane over the wave, in lane
+// order (Hillis-Steele: row shifts by 1, 2, 4, 8 inside each 16-lane row, then
+// the row totals by row_bcast:15 and row_bcast:31).  RIGHT: P_i = x_0 x_1 .. x_i
+// (later factors on the right); else P_i = x_i .. x_1 x_0.
+template <bool RIGHT>
+__device__ __forceinline__ dq wave_prefix_product(dq p) {
+    const auto comb = [](dq lower, dq self) { return RIGHT ? dq_mul(lower, self) : dq_mul(self, lower); };
+    p = comb(dq_dpp<0x111, 0xf>(p), p);
+    p = comb(dq_dpp<0x112, 0xf>(p), p);
+    p = comb(dq_dpp<0x114, 0xf>(p), p);
+    p = comb(dq_dpp<0x118, 0xf>(p), p);
+    p = comb(dq_dpp<0x142, 0xa>(p), p);
+    p = comb(dq_dpp<0x143, 0xc>(p), p);
+    return p;
+}
+__device__ __forceinline__ dq dq_readlane(dq v, int l) {
+    const auto rl = [&](double x) -> double {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                                __builtin_amdgcn_readlane(__double2loint(x), l));
+    };
+    return dq{rl(v.x), rl(v.y), rl(v.z), rl(v.w)};
+}
+
+// The per-step terms and the quaternion chains of one segment (one wave, lane =
+// step).  The chains are products: the reference's
+//     cur.q_k = normalize(qnn_k * cur.q_k-1 * qd_k)   (Normal: cur.q_k-1 * qd_k)
+//     dqt_k   = normalize(dqt_k-1 * qd_k)
+// normalise a product that is a unit quaternion up to rounding at every step,
+// so cur.q_k = normalize(L_k q0 R_k) and dqt_k = normalize(R_k) with the prefix
+// products R_k = qd_1 .. qd_k and L_k = qnn_k .. qnn_1 -- each a wave-wide scan
+// of the chunk's 64 steps (6 DPP stages) times the previous chunks' carry,
+// instead of a 99-step dependent chain on one lane per segment (the r04 chain
+// pass: 50 us per configs[3] batch, 1,200 cycles a step).  The two forms agree
+// to rounding (1e-15 relative on configs[3]; tests/test_ba_gpu.py holds the
+// whole integration to the oracle at 1e-10).
+template <bool EARTH>
+__global__ void __launch_bounds__(64, 6) preint_pre_kernel(int n_seg, const gvx_imu* __restrict__ imu,
                                                         const int32_t* __restrict__ seg_off,
                                                         const gvx_state* __restrict__ state0,
-                                                        const double* __restrict__ iewn_in, PreG* __restrict__ pre) {
+                                                        const double* __restrict__ iewn_in, PreG* __restrict__ pre,
+                                                        QRec* __restrict__ qrec, gvx_imu_params prm,
+                                                        gvx_preint_result* __restrict__ out) {
     const int seg = blockIdx.x;
     const int lane = threadIdx.x;
     const int b0 = seg_off[seg];
     const int m = seg_off[seg + 1] - b0;
     const gvx_imu* im = imu + b0;
     PreG* pg = pre + (b0 - seg);
-    const bool earth = variant == GVX_PREINT_EARTH;
+    QRec* qs = qrec + (b0 - seg);
     const gvx_state& s0 = state0[seg];
     double bg[3], ba[3], iewn[3] = {0, 0, 0};
     for (int i = 0; i < 3; ++i) {
@@ -461,153 +511,108 @@ __global__ void __launch_bounds__(64, 6) preint_pre_kernel(int variant, int n_se
     }
     const dq q0 = dq_load(s0.q);
     const dq q0i = dq_inv(q0);
-    if (earth)
+    if (EARTH)
         for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
+    gvx_preint_result* o = out + seg;
+    dq Rc = dq_make(1, 0, 0, 0), Lc = dq_make(1, 0, 0, 0);  // the previous chunks' products
     double base = 0.0;  // delta_time before the chunk
     for (int kc = 1; kc < m; kc += 64) {
         const int k = kc + lane;
+        const bool live = k < m;
         const int cnt = min(64, m - kc);
         // delta_time_ += dt in sample order: a running sum over the chunk's
         // samples (read lane by lane), lane k keeps its prefix
-        const double mydt = k < m ? im[k].dt : 0.0;
+        const double mydt = live ? im[k].dt : 0.0;
         double acc = base, dtime = 0.0;
         for (int i = 0; i < cnt; ++i) {
             acc += __shfl(mydt, i);
             if (lane == i) dtime = acc;
         }
         base = acc;
-        if (k >= m) continue;
-        const Imu pr = load_imu(im + k - 1, bg, ba);
-        const Imu ic = load_imu(im + k, bg, ba);
-        // the record's fields are stored as they are formed (short live ranges:
-        // the Earth terms need the registers)
-        double* dst = reinterpret_cast<double*>(pg + (k - 1));
-        const auto put2 = [&](int i, double a, double b) { *reinterpret_cast<double2*>(dst + i) = double2{a, b}; };
-        double c1[3], c2[3], c3[3], dth[3], dvfb[3];
-        cross3(ic.dth, ic.dv, c1);
-        cross3(pr.dth, ic.dv, c2);
-        cross3(pr.dv, ic.dth, c3);
-        for (int i = 0; i < 3; ++i) dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
-        put2(0, dtime, dvfb[0]);
-        put2(2, dvfb[1], dvfb[2]);
-        cross3(pr.dth, ic.dth, c1);
-        for (int i = 0; i < 3; ++i) dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
-        double qv[4];
-        dq_store(dq_from_rotvec(dth), qv);
-        put2(4, qv[0], qv[1]);
-        put2(6, qv[2], qv[3]);
-        if (earth) {
-            const double dt = ic.dt;
-            const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
-            dq_store(dq_from_rotvec(dnn), qv);
-            put2(8, qv[0], qv[1]);
-            put2(10, qv[2], qv[3]);
-            const double sc = -(dtime - 0.5 * dt);
-            const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
-            dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), qv);
-            put2(12, qv[0], qv[1]);
-            put2(14, qv[2], qv[3]);
-            const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
-            dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), qv);
-            put2(16, qv[0], qv[1]);
-            put2(18, qv[2], qv[3]);
-        }
-    }
-}
-
-// The quaternion chains, and every output field that does not depend on the
-// velocity / position sums or on J / P.
-template <bool EARTH>
-__global__ void __launch_bounds__(128) preint_chain_kernel(gvx_imu_params prm, int n_seg,
-                                                           const gvx_imu* __restrict__ imu,
-                                                           const int32_t* __restrict__ seg_off,
-                                                           const gvx_state* __restrict__ state0,
-                                                           const double* __restrict__ iewn_in,
-                                                           const PreG* __restrict__ pre, QRec* __restrict__ qrec,
-                                                           gvx_preint_result* __restrict__ out) {
-    // wave 0 runs the cur.q chain, wave 1 the dqt chain of the same 64 segments:
-    // the two chains are independent, and each wave issues half the work
-    const bool dwave = threadIdx.x >= 64;
-    const int seg = blockIdx.x * 64 + (threadIdx.x & 63);
-    if (seg >= n_seg) return;  // no barriers below
-    const int b0 = seg_off[seg];
-    const int m = seg_off[seg + 1] - b0;
-    const gvx_imu* im = imu + b0;
-    const double* pg = reinterpret_cast<const double*>(pre + (b0 - seg));
-    double* qs = reinterpret_cast<double*>(qrec + (b0 - seg)) + (dwave ? 4 : 0);
-    constexpr bool earth = EARTH;
-    constexpr int variant = EARTH ? GVX_PREINT_EARTH : GVX_PREINT_NORMAL;
-    const gvx_state s0 = state0[seg];
-    // the q chain reads qd and qnn (PreG doubles 4..11), the dqt chain qd
-    const bool two = earth && !dwave;
-    dq q = dwave ? dq_make(1, 0, 0, 0) : dq_load(s0.q);
-    // StepPre inputs in chunks of CK steps: chunk i+1 is loaded while chunk i
-    // runs and copied over at the chunk's end, so each load has CK steps of the
-    // chain to land (loads never predicated: a clamped index)
-    constexpr int CK = 4;
-    const int last = m >= 2 ? m - 2 : 0;
-    auto ldc = [&](int kc, double (&X)[CK][8]) {
-#pragma unroll
-        for (int j = 0; j < CK; ++j) {
-            const double* src = pg + (size_t)min(kc + j - 1, last) * PREG_DW + 4;
-            const double2 v0 = *reinterpret_cast<const double2*>(src);
-            const double2 v1 = *reinterpret_cast<const double2*>(src + 2);
-            X[j][0] = v0.x;
-            X[j][1] = v0.y;
-            X[j][2] = v1.x;
-            X[j][3] = v1.y;
-            if (two) {
-                const double2 v2 = *reinterpret_cast<const double2*>(src + 4);
-                const double2 v3 = *reinterpret_cast<const double2*>(src + 6);
-                X[j][4] = v2.x;
-                X[j][5] = v2.y;
-                X[j][6] = v3.x;
-                X[j][7] = v3.y;
+        dq qd = dq_make(1, 0, 0, 0), qnn = dq_make(1, 0, 0, 0);
+        if (live) {
+            const Imu pr = load_imu(im + k - 1, bg, ba);
+            const Imu ic = load_imu(im + k, bg, ba);
+            // the record's fields are stored as they are formed (short live ranges:
+            // the Earth terms need the registers)
+            double* dst = reinterpret_cast<double*>(pg + (k - 1));
+            const auto put2 = [&](int i, double a, double b) { *reinterpret_cast<double2*>(dst + i) = double2{a, b}; };
+            double c1[3], c2[3], c3[3], dth[3], dvfb[3];
+            cross3(ic.dth, ic.dv, c1);
+            cross3(pr.dth, ic.dv, c2);
+            cross3(pr.dv, ic.dth, c3);
+            for (int i = 0; i < 3; ++i) dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
+            put2(0, dtime, dvfb[0]);
+            put2(2, dvfb[1], dvfb[2]);
+            cross3(pr.dth, ic.dth, c1);
+            for (int i = 0; i < 3; ++i) dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
+            qd = dq_from_rotvec(dth);
+            put2(4, qd.x, qd.y);
+            put2(6, qd.z, qd.w);
+            if (EARTH) {
+                double qv[4];
+                const double dt = ic.dt;
+                const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
+                qnn = dq_from_rotvec(dnn);
+                put2(8, qnn.x, qnn.y);
+                put2(10, qnn.z, qnn.w);
+                const double sc = -(dtime - 0.5 * dt);
+                const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
+                dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), qv);
+                put2(12, qv[0], qv[1]);
+                put2(14, qv[2], qv[3]);
+                const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
+                dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), qv);
+                put2(16, qv[0], qv[1]);
+                put2(18, qv[2], qv[3]);
             }
         }
-    };
-    auto step = [&](int k, const double (&r)[8]) {
-        const dq qd = dq_load(r);
-        if (two)
-            q = dq_renorm(dq_mul(dq_mul(dq_load(r + 4), q), qd));
-        else  // Normal cur.q, and dqt in both variants
-            q = dq_renorm(dq_mul(q, qd));
-        *reinterpret_cast<double4*>(qs + (size_t)(k - 1) * 8) = double4{q.x, q.y, q.z, q.w};
-    };
-    double X[CK][8], Y[CK][8];
-    if (m > 1) ldc(1, X);
-    for (int kc = 1; kc < m; kc += CK) {
-        ldc(kc + CK, Y);
-#pragma unroll
-        for (int j = 0; j < CK; ++j)
-            if (kc + j < m) step(kc + j, X[j]);
-#pragma unroll
-        for (int j = 0; j < CK; ++j)
-#pragma unroll
-            for (int i = 0; i < 8; ++i) X[j][i] = Y[j][i];
+        // the chains after step k: R_k = Rc qd_kc .. qd_k, L_k = qnn_k .. qnn_kc Lc
+        // (steps past m carry the identity: they follow every live step)
+        const dq R = dq_mul(Rc, wave_prefix_product<true>(qd));
+        const dq dqt = dq_renorm(R);
+        dq q;
+        if constexpr (EARTH) {
+            const dq L = dq_mul(wave_prefix_product<false>(qnn), Lc);
+            q = dq_renorm(dq_mul(dq_mul(L, q0), R));
+            Lc = dq_renorm(dq_readlane(L, 63));
+        } else {
+            q = dq_renorm(dq_mul(q0, R));
+        }
+        Rc = dq_readlane(dqt, 63);
+        if (live) {
+            double* qd_ = reinterpret_cast<double*>(qs + (k - 1));
+            *reinterpret_cast<double4*>(qd_) = double4{q.x, q.y, q.z, q.w};
+            *reinterpret_cast<double4*>(qd_ + 4) = double4{dqt.x, dqt.y, dqt.z, dqt.w};
+        }
+        if (k == m - 1) {  // the segment's last step
+            dq_store(q, o->current.q);
+            dq_store(dqt, o->delta.q);
+            o->delta_time = dtime;
+        }
     }
-    gvx_preint_result* o = out + seg;
-    if (dwave) {
+    if (lane == 0) {
+        if (m <= 1) {
+            dq_store(q0, o->current.q);
+            dq_store(dq_make(1, 0, 0, 0), o->delta.q);
+            o->delta_time = 0.0;
+        }
+        o->variant = EARTH ? GVX_PREINT_EARTH : GVX_PREINT_NORMAL;
+        o->m = m;
+        o->start_time = im[0].time;
+        o->end_time = m > 1 ? im[m - 1].time : im[0].time;
+        o->current.time = m > 1 ? im[m - 1].time : s0.time;
         o->delta.time = 0;
-        dq_store(q, o->delta.q);
-        return;
+        for (int i = 0; i < 3; ++i) {
+            o->current.bg[i] = s0.bg[i];
+            o->current.ba[i] = s0.ba[i];
+            o->delta.bg[i] = s0.bg[i];
+            o->delta.ba[i] = s0.ba[i];
+            o->gravity[i] = i == 2 ? prm.gravity : 0.0;
+            o->iewn[i] = EARTH ? iewn_in[3 * seg + i] : 0.0;
+        }
+        dq_store(q0, o->q0);
     }
-    dq_store(q, o->current.q);
-    o->variant = variant;
-    o->m = m;
-    o->delta_time = m > 1 ? pg[(size_t)(m - 2) * PREG_DW] : 0.0;
-    o->start_time = im[0].time;
-    o->end_time = m > 1 ? im[m - 1].time : im[0].time;
-    o->current.time = m > 1 ? im[m - 1].time : s0.time;
-    for (int i = 0; i < 3; ++i) {
-        o->current.bg[i] = s0.bg[i];
-        o->current.ba[i] = s0.ba[i];
-        o->delta.bg[i] = s0.bg[i];
-        o->delta.ba[i] = s0.ba[i];
-        o->gravity[i] = i == 2 ? prm.gravity : 0.0;
-        o->iewn[i] = earth ? iewn_in[3 * seg + i] : 0.0;
-    }
-    dq_store(dq_load(s0.q), o->q0);
 }
 
 // The rotated terms of step k (k >= 1) from the chain values: the velocity and
@@ -997,7 +1002,7 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
                          const double* iewn, gvx_preint_result* out, double* pn, bool* sqrt_info_done) {
     if (sqrt_info_done) *sqrt_info_done = false;
     if (n_seg <= 0) return hipSuccess;
-    // Three-launch form when the per-step scratch can be sized without a round
+    // Two-launch form when the per-step scratch can be sized without a round
     // trip: the IMU allocation bounds the number of samples
     // (hipMemGetAddressRange).  A pointer into a large pooled block bounds nothing
     // useful: above 1 GiB of scratch the single kernel runs.
@@ -1015,11 +1020,10 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
             PreG* pre = reinterpret_cast<PreG*>(d);
             QRec* qr = reinterpret_cast<QRec*>(d + samples * sizeof(PreG));
             const bool earth = variant == GVX_PREINT_EARTH;
-            hipLaunchKernelGGL(preint_pre_kernel, dim3(n_seg), dim3(64), 0, c->stream, variant, n_seg, imu, seg_off,
-                               state0, iewn, pre);
-            hipLaunchKernelGGL(earth ? preint_chain_kernel<true> : preint_chain_kernel<false>,
-                               dim3((n_seg + 63) / 64), dim3(128), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
-                               (const PreG*)pre, qr, out);
+            // the per-step terms and the quaternion chains (wave scans), then the
+            // covariance pass
+            hipLaunchKernelGGL(earth ? preint_pre_kernel<true> : preint_pre_kernel<false>, dim3(n_seg), dim3(64), 0,
+                               c->stream, n_seg, imu, seg_off, state0, iewn, pre, qr, prm, out);
             // the covariance pass, sqrt_info in its epilogue
             hipLaunchKernelGGL(earth ? preint_cov16_kernel<true> : preint_cov16_kernel<false>,
                                dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,

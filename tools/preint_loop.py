@@ -20,7 +20,7 @@ dev = torch.device("cuda", 0)
 ctx = gvx.Context(0)
 prob = synth_ba.make_ba_problem()
 n_kf = prob["poses"].shape[0]
-reps = -(-(1 << 20) // len(prob["consts"]))
+reps = int(os.environ.get("PREINT_REPS", 0)) or -(-(1 << 20) // len(prob["consts"]))  # 583 (5,247 segments)
 rng = np.random.default_rng(synth_ba.SEED if hasattr(synth_ba, "SEED") else 20261015)
 M = 100
 segs = [synth_ba.make_imu_segment(rng, M, t0=0.5 * k) for k in range(n_kf - 1)]

@@ -20,3 +20,5 @@ for n, v in d.items():
 print(sys.argv[2], ' | '.join(out))
 PY
 done
+# the chain / pre / cov launches at a tenth of the segments (latency- vs throughput-bound)
+(cd /tmp && export TMPDIR=/tmp && PREINT_REPS=58 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/tr_small -- python3 $R/tools/preint_loop.py > $O/tr_small.json 2> $O/tr_small.err)
