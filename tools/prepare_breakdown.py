@@ -6,13 +6,20 @@ the gaps between consecutive operations of one prepare.
 import csv
 import glob
 import statistics
+import re
 import sys
+
+
+def kname(n):
+    """short kernel name: the identifier before the argument list"""
+    m = re.search(r"([A-Za-z_][A-Za-z_0-9]*(<[^()]*>)?)\(", n)
+    return m.group(1) if m else n[:40]
 
 root = sys.argv[1]
 ops = []
 for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].split("::")[-1]))
+        ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kname(r["Kernel_Name"])))
 for f in glob.glob(f"{root}/**/*memory_copy_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r["Direction"]))

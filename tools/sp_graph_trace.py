@@ -10,7 +10,14 @@ import csv
 import glob
 import os
 import statistics
+import re
 import sys
+
+
+def kname(n):
+    """short kernel name: the identifier before the argument list"""
+    m = re.search(r"([A-Za-z_][A-Za-z_0-9]*(<[^()]*>)?)\(", n)
+    return m.group(1) if m else n[:40]
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,7 +27,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
     ops = []
     for f in glob.glob(f"{sys.argv[2]}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].split("::")[-1]))
+            ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kname(r["Kernel_Name"])))
     ops.sort()
     gaps = [b[0] - a[1] for a, b in zip(ops, ops[1:])]
     cut = max(range(len(gaps)), key=lambda i: gaps[i]) + 1  # the pause
