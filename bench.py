@@ -773,7 +773,10 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
         return el, fam
 
     el, fam = timed(step, steps)
-    el_i, fam_i = timed(integ, max(1, steps // 4))
+    # the integrate call is ~0.3 ms: time enough launches that the shader clock
+    # has ramped and the host-side bracket is a small part of the span
+    k_i = max(40, steps)
+    el_i, fam_i = timed(integ, k_i)
 
     # one window at problem size (1800 + 9 factors, latency-bound): device-pointer
     # launches, and the two-phase FactorSet prepare (block gather, H2D, both
@@ -801,7 +804,6 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
                          np.vectorize(bidx.get)(poffs).astype(np.int32))
     el_p, _ = timed(lambda: fset.prepare(True), k_w)
     fset.close()
-    k_i = max(1, steps // 4)
     evals = world * (n_r + n_p) * steps
     value = evals / el
     rp_ms = fam["reproj"][0] / steps

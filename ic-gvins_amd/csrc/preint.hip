@@ -430,17 +430,20 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
 //                        P <- Phi P Phi^T + Qk per step, sqrt_info at the end.
 // Every other value is formed by the same operations in the same order as in
 // preint_kernel (tests/test_ba_gpu.py).
-struct PreG {                // StepPre terms of one step (scratch, per IMU step)
-    double dtime;            // delta_time after the step
-    double dvfb[3];
-    double qd[4];
-    double qnn[4], qa[4], qb[4];  // Earth only
+// What the covariance pass needs of step k (scratch, one record per IMU step,
+// written by preint_pre_kernel): the bias-compensated sample, the rotation whose
+// negated matrix is cbb0 and the rotated velocity / delta-velocity increments
+// (the reference's integrationProcess terms, preintegration_earth.cc:205-260,
+// preintegration_normal.cc:183-214).
+struct CovIn {
+    double dt, sdth[3], sdv[3];
+    double qc[4];  // cbb0 = -R(qc): qc = dqt_k (Normal), q0^-1 q(-dtime iewn) q0 dqt_k (Earth)
+    double a[3], b[3];
+    double pad;
 };
-constexpr int PREG_DW = sizeof(PreG) / 8;  // 20
-struct QRec {                // the chains after step k
-    double q[4], dqt[4];
-};
-constexpr size_t STEP_SCRATCH = sizeof(PreG) + sizeof(QRec);  // per IMU sample
+constexpr int COVIN_DW = sizeof(CovIn) / 8;  // 18 (144 B)
+static_assert(sizeof(CovIn) % 16 == 0, "16-B records (LDS-DMA pieces)");
+constexpr size_t STEP_SCRATCH = sizeof(CovIn);  // per IMU sample
 
 // A quaternion through one DPP lane move (both dwords of each double); lanes
 // the move does not write (rows off ROWS, or a row shift's first lanes) take
@@ -469,6 +472,15 @@ __device__ __forceinline__ dq wave_prefix_product(dq p) {
     p = comb(dq_dpp<0x143, 0xc>(p), p);
     return p;
 }
+// lane i - 1's quaternion (DPP wave_shr:1); lane 0 takes `first`
+__device__ __forceinline__ dq dq_wave_shr1(dq v, dq first) {
+    const auto mv = [](double x, double o) -> double {
+        const int lo = __builtin_amdgcn_update_dpp(__double2loint(o), __double2loint(x), 0x138, 0xf, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(__double2hiint(o), __double2hiint(x), 0x138, 0xf, 0xf, false);
+        return __hiloint2double(hi, lo);
+    };
+    return dq{mv(v.x, first.x), mv(v.y, first.y), mv(v.z, first.z), mv(v.w, first.w)};
+}
 __device__ __forceinline__ dq dq_readlane(dq v, int l) {
     const auto rl = [&](double x) -> double {
         return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
@@ -490,19 +502,18 @@ __device__ __forceinline__ dq dq_readlane(dq v, int l) {
 // to rounding (1e-15 relative on configs[3]; tests/test_ba_gpu.py holds the
 // whole integration to the oracle at 1e-10).
 template <bool EARTH>
-__global__ void __launch_bounds__(64, 6) preint_pre_kernel(int n_seg, const gvx_imu* __restrict__ imu,
+__global__ void __launch_bounds__(64, EARTH ? 4 : 6) preint_pre_kernel(int seg0, const gvx_imu* __restrict__ imu,
                                                         const int32_t* __restrict__ seg_off,
                                                         const gvx_state* __restrict__ state0,
-                                                        const double* __restrict__ iewn_in, PreG* __restrict__ pre,
-                                                        QRec* __restrict__ qrec, gvx_imu_params prm,
+                                                        const double* __restrict__ iewn_in,
+                                                        CovIn* __restrict__ cin, gvx_imu_params prm,
                                                         gvx_preint_result* __restrict__ out) {
-    const int seg = blockIdx.x;
+    const int seg = seg0 + blockIdx.x;
     const int lane = threadIdx.x;
     const int b0 = seg_off[seg];
     const int m = seg_off[seg + 1] - b0;
     const gvx_imu* im = imu + b0;
-    PreG* pg = pre + (b0 - seg);
-    QRec* qs = qrec + (b0 - seg);
+    CovIn* cs = cin + (b0 - seg);
     const gvx_state& s0 = state0[seg];
     double bg[3], ba[3], iewn[3] = {0, 0, 0};
     for (int i = 0; i < 3; ++i) {
@@ -515,6 +526,7 @@ __global__ void __launch_bounds__(64, 6) preint_pre_kernel(int n_seg, const gvx_
         for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
     gvx_preint_result* o = out + seg;
     dq Rc = dq_make(1, 0, 0, 0), Lc = dq_make(1, 0, 0, 0);  // the previous chunks' products
+    dq qlast = q0;  // the attitude after the previous chunk's last step (Rc: its delta)
     double base = 0.0;  // delta_time before the chunk
     for (int kc = 1; kc < m; kc += 64) {
         const int k = kc + lane;
@@ -530,41 +542,31 @@ __global__ void __launch_bounds__(64, 6) preint_pre_kernel(int n_seg, const gvx_
         }
         base = acc;
         dq qd = dq_make(1, 0, 0, 0), qnn = dq_make(1, 0, 0, 0);
+        double dvfb[3] = {0, 0, 0}, sdv2 = 0.0, dt = 0.0;
+        double* dst = reinterpret_cast<double*>(cs + (k - 1));
+        const auto put2 = [&](int i, double a, double b) { *reinterpret_cast<double2*>(dst + i) = double2{a, b}; };
         if (live) {
             const Imu pr = load_imu(im + k - 1, bg, ba);
             const Imu ic = load_imu(im + k, bg, ba);
-            // the record's fields are stored as they are formed (short live ranges:
-            // the Earth terms need the registers)
-            double* dst = reinterpret_cast<double*>(pg + (k - 1));
-            const auto put2 = [&](int i, double a, double b) { *reinterpret_cast<double2*>(dst + i) = double2{a, b}; };
-            double c1[3], c2[3], c3[3], dth[3], dvfb[3];
+            dt = ic.dt;
+            double c1[3], c2[3], c3[3], dth[3];
             cross3(ic.dth, ic.dv, c1);
             cross3(pr.dth, ic.dv, c2);
             cross3(pr.dv, ic.dth, c3);
             for (int i = 0; i < 3; ++i) dvfb[i] = ic.dv[i] + 0.5 * c1[i] + 1.0 / 12.0 * (c2[i] + c3[i]);
-            put2(0, dtime, dvfb[0]);
-            put2(2, dvfb[1], dvfb[2]);
             cross3(pr.dth, ic.dth, c1);
             for (int i = 0; i < 3; ++i) dth[i] = ic.dth[i] + 1.0 / 12.0 * c1[i];
+            // the step's own increments go out first (short live ranges across
+            // the scans; load_imu's dth / dv are already bias-compensated:
+            // compensationBias)
+            put2(0, dt, ic.dth[0]);
+            put2(2, ic.dth[1], ic.dth[2]);
+            put2(4, ic.dv[0], ic.dv[1]);
+            sdv2 = ic.dv[2];
             qd = dq_from_rotvec(dth);
-            put2(4, qd.x, qd.y);
-            put2(6, qd.z, qd.w);
             if (EARTH) {
-                double qv[4];
-                const double dt = ic.dt;
                 const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
                 qnn = dq_from_rotvec(dnn);
-                put2(8, qnn.x, qnn.y);
-                put2(10, qnn.z, qnn.w);
-                const double sc = -(dtime - 0.5 * dt);
-                const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
-                dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), qv);
-                put2(12, qv[0], qv[1]);
-                put2(14, qv[2], qv[3]);
-                const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
-                dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), qv);
-                put2(16, qv[0], qv[1]);
-                put2(18, qv[2], qv[3]);
             }
         }
         // the chains after step k: R_k = Rc qd_kc .. qd_k, L_k = qnn_k .. qnn_kc Lc
@@ -579,11 +581,45 @@ __global__ void __launch_bounds__(64, 6) preint_pre_kernel(int n_seg, const gvx_
         } else {
             q = dq_renorm(dq_mul(q0, R));
         }
+        // the rotated terms of step k from the chain values after step k - 1
+        // (lane k - 1, or the previous chunk's last step; q0 / identity at k = 1)
+        const dq qprev = dq_wave_shr1(q, qlast), dprev = dq_wave_shr1(dqt, Rc);
         Rc = dq_readlane(dqt, 63);
+        qlast = dq_readlane(q, 63);
         if (live) {
-            double* qd_ = reinterpret_cast<double*>(qs + (k - 1));
-            *reinterpret_cast<double4*>(qd_) = double4{q.x, q.y, q.z, q.w};
-            *reinterpret_cast<double4*>(qd_ + 4) = double4{dqt.x, dqt.y, dqt.z, dqt.w};
+            double Rm[9], ra[3], rb[3];
+            dq qc;
+            if constexpr (!EARTH) {
+                dq_rot(qprev, Rm);
+                mv3(Rm, dvfb, ra);
+                dq_rot(dprev, Rm);
+                mv3(Rm, dvfb, rb);
+                qc = dqt;
+            } else {
+                // ra = 0.5 (I + R(qnn)) R(qprev) dvfb, rb = R(qa dprev) dvfb, qc = qb dqt
+                // (qa, qb: the Earth-rotation corrections at mid-step and at the
+                // step's end, conjugated into the segment's start frame)
+                double x[3], y[3];
+                dq_rot(qprev, Rm);
+                mv3(Rm, dvfb, x);
+                dq_rot(qnn, Rm);
+                mv3(Rm, x, y);
+                for (int i = 0; i < 3; ++i) ra[i] = 0.5 * (x[i] + y[i]);
+                const double sc = -(dtime - 0.5 * dt);
+                const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
+                const dq qa = dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0);
+                dq_rot(dq_mul(qa, dprev), Rm);
+                mv3(Rm, dvfb, rb);
+                const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
+                const dq qb = dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0);
+                qc = dq_mul(qb, dqt);
+            }
+            put2(6, sdv2, qc.x);
+            put2(8, qc.y, qc.z);
+            put2(10, qc.w, ra[0]);
+            put2(12, ra[1], ra[2]);
+            put2(14, rb[0], rb[1]);
+            put2(16, rb[2], 0.0);
         }
         if (k == m - 1) {  // the segment's last step
             dq_store(q, o->current.q);
@@ -614,38 +650,6 @@ __global__ void __launch_bounds__(64, 6) preint_pre_kernel(int n_seg, const gvx_
         dq_store(q0, o->q0);
     }
 }
-
-// The rotated terms of step k (k >= 1) from the chain values: the velocity and
-// delta-velocity increments a, b and
-// cbb0 (qs = the segment's QRec base, q0 = its start attitude for k = 1).
-__device__ __forceinline__ void rot_terms(bool earth, const PreG* __restrict__ gp, const QRec* __restrict__ qs, int k,
-                                          const double* q0, double* ra, double* rb, double* cbb0) {
-    const PreG& g = *gp;
-    const dq qprev = k > 1 ? dq_load(qs[k - 2].q) : dq_load(q0);
-    const dq dprev = k > 1 ? dq_load(qs[k - 2].dqt) : dq_make(1, 0, 0, 0);
-    const dq dcur = dq_load(qs[k - 1].dqt);
-    double dvfb[3] = {g.dvfb[0], g.dvfb[1], g.dvfb[2]};
-    double R[9];
-    if (!earth) {
-        dq_rot(qprev, R);
-        mv3(R, dvfb, ra);
-        dq_rot(dprev, R);
-        mv3(R, dvfb, rb);
-        dq_rot(dcur, R);
-    } else {
-        double T[9], M1[9];
-        dq_rot(dq_load(g.qnn), T);
-        for (int i = 0; i < 9; ++i) M1[i] = 0.5 * (((i % 4) == 0 ? 1.0 : 0.0) + T[i]);
-        dq_rot(qprev, R);
-        mm3(M1, R, T);
-        mv3(T, dvfb, ra);
-        dq_rot(dq_mul(dq_load(g.qa), dprev), R);
-        mv3(R, dvfb, rb);
-        dq_rot(dq_mul(dq_load(g.qb), dcur), R);
-    }
-    for (int i = 0; i < 9; ++i) cbb0[i] = -R[i];
-}
-
 
 // The covariance pass (r05): 16 lanes per segment, 4 segments per one-wave
 // workgroup; lane c owns column c of J and of P (P is symmetric, so also row c).
@@ -688,7 +692,7 @@ struct StepRec {
 };
 static_assert(sizeof(Phi) == 29 * 8, "Phi is StepRec's prefix");
 constexpr int SREC_DW = sizeof(StepRec) / 8;  // 64
-constexpr int C16_CK = 8;   // steps per record chunk (one per lane of half a group)
+constexpr int C16_CK = 6;   // steps per record chunk (one per lane c < 6 of a group)
 constexpr int TS = 18;      // sT row stride (doubles): 16-B aligned rows, conflict-free b128 row reads
 constexpr int TSEG = 288;   // sT doubles per segment: 15 rows of 18, padded to a multiple of 256 B
 static_assert(TSEG >= 16 * TS - 2 && (TSEG * 8) % 256 == 0, "sT layout");
@@ -699,36 +703,49 @@ static_assert(TSEG >= 16 * TS - 2 && (TSEG * 8) % 256 == 0, "sT layout");
 constexpr int RS = SREC_DW + 2;
 constexpr int SEGR = C16_CK * RS + 2;
 static_assert((RS * 8) % 16 == 0 && (SEGR * 8) % 16 == 0, "16-B aligned records");
-// LDS per wave: 4 x 4,240 B of records + 4 x 2,304 B of transpose tiles = 26.2 KB,
-// so the 1,312 waves of a 5,247-segment batch are resident at once (6 per CU)
+// the next chunk's CovIn records are staged by LDS-DMA (global_load_lds, 16 B a
+// lane) while the current chunk's steps run: the record phase reads LDS, not
+// HBM (the r05 v12 stamps put a chunk's record phase at ~8,800 cycles, most of
+// it the global round trip and the rotated terms, now formed in the pre pass)
+// One DMA instruction (64 lanes x 16 B) per segment: a segment's staging slot
+// is 1 KB, its 6 records (864 B) in the first 54 pieces, so each instruction's
+// source base and m are the segment's own (uniform, scalar registers)
+constexpr int STG_SEG = 128;                                // doubles per segment slot
+constexpr int STG_PIECES = C16_CK * COVIN_DW * 8 / 16;      // 16-B pieces staged per segment (54)
+static_assert(STG_PIECES <= 64 && C16_CK * COVIN_DW <= STG_SEG, "a chunk's records fit one DMA instruction");
+constexpr int STG_INS = 4;                                  // DMA instructions per chunk (one per segment)
+// LDS per wave: 4 x 3,184 B of records + 4 x 2,304 B of transpose tiles + 4 x
+// 864 B of staging = 25.4 KB, so the 1,312 waves of a 5,247-segment batch are
+// resident at once (6 per CU)
 
 // per segment group in the record region: A and X (15 x 15 each) and perm
 constexpr int SI_GROUP_DW = 2 * NS * NS + 8;
-static_assert(4 * SI_GROUP_DW <= 4 * SEGR, "sqrt_info scratch fits the record region");
+constexpr int C16_LDS_REC = (4 * SEGR + 31) / 32 * 32, C16_LDS_T = 4 * TSEG, C16_LDS_STG = STG_INS * 128;
+static_assert(4 * SI_GROUP_DW <= C16_LDS_REC + C16_LDS_T, "sqrt_info scratch fits the record + tile region");
+static_assert(C16_LDS_REC % 32 == 0 && C16_LDS_T % 32 == 0, "256-B aligned sub-regions");
 
-// The record of step k (k >= 1) of one segment: the rotated terms from the
-// chain values (QRec), the bias-compensated sample, Phi's blocks and W, formed
-// by the same operations as preint_kernel's step.
+// The record of step k (k >= 1) of one segment from its staged CovIn (in LDS):
+// cbb0 = -R(qc), Phi's blocks and W, formed by the same operations as
+// preint_kernel's step.
 template <bool EARTH>
-__device__ __forceinline__ void make_record(const gvx_imu_params& prm, const PreG* __restrict__ pg, const QRec* qr,
-                                            const gvx_imu& sm, const gvx_state& s0, int k, double nacc,
+__device__ __forceinline__ void make_record(const gvx_imu_params& prm, const double* __restrict__ ci, double nacc,
                                             double* __restrict__ dst) {
     // each field stored as it is formed (short live ranges: the step loop's J, P
     // and sums stay in registers across the record phase)
     const auto put2 = [&](int i, double x, double y) { *reinterpret_cast<double2*>(dst + i) = double2{x, y}; };
-    double cbb0[9], ra[3], rb[3];
-    rot_terms(EARTH, pg, qr, k, s0.q, ra, rb, cbb0);
     constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
     constexpr int oW = offsetof(StepRec, W) / 8, oA = offsetof(StepRec, a) / 8, oS = offsetof(StepRec, S) / 8;
     static_assert(oC == 2 && oD == 11 && oM == 20 && oW == 29 && oA == 38 && oS == 44, "record layout");
-    const double dt = sm.dt;
+    constexpr int iDT = offsetof(CovIn, dt) / 8, iTH = offsetof(CovIn, sdth) / 8, iDV = offsetof(CovIn, sdv) / 8;
+    constexpr int iQC = offsetof(CovIn, qc) / 8, iA = offsetof(CovIn, a) / 8, iB = offsetof(CovIn, b) / 8;
+    const double dt = ci[iDT];
     const double f = 1 - dt / prm.corr_time;
-    double sdv[3], sdth[3];
+    const double sdth[3] = {ci[iTH], ci[iTH + 1], ci[iTH + 2]};
+    const double sdv[3] = {ci[iDV], ci[iDV + 1], ci[iDV + 2]};
+    double cbb0[9];
+    dq_rot(dq_load(ci + iQC), cbb0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        sdth[i] = sm.dtheta[i] - dt * s0.bg[i];
-        sdv[i] = sm.dvel[i] - dt * s0.ba[i];
-    }
+    for (int i = 0; i < 9; ++i) cbb0[i] = -cbb0[i];
     double S[9], C[9], M[9];
     skew(sdv, S);
     mm3(cbb0, S, C);
@@ -760,9 +777,9 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const Pre
     put2(oM + 8, M[8], W[0]);
 #pragma unroll
     for (int i = 1; i < 9; i += 2) put2(oW + i, W[i], W[i + 1]);
-    put2(oA, ra[0], ra[1]);
-    put2(oA + 2, ra[2], rb[0]);
-    put2(oA + 4, rb[1], rb[2]);
+    put2(oA, ci[iA], ci[iA + 1]);
+    put2(oA + 2, ci[iA + 2], ci[iB]);
+    put2(oA + 4, ci[iB + 1], ci[iB + 2]);
     // S = {0,0,dt,0,0,f,0,0,-dt,0,0}, S1 = {0,0,1,0,0}, Z = 0, pad
     put2(oS, 0.0, 0.0);
     put2(oS + 2, dt, 0.0);
@@ -791,25 +808,53 @@ __device__ __forceinline__ void identity_record(double* __restrict__ dst) {
     for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
 }
 
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
+constexpr int VMCNT0 = 0x0F70;
+
+// 16 B per lane from global memory into LDS (lane l's piece at lds + 16 l):
+// the LDS-DMA form of global_load_lds_dwordx4, issued from inline asm.  Through
+// the builtin the compiler tracks the in-flight DMA as an LDS write and makes
+// the next LDS access of the step loop wait for it (vmcnt(0): a full HBM round
+// trip a chunk, r05 v17); hidden from it, the DMA is waited for only where the
+// kernel says so (s_waitcnt vmcnt(0) before the staging is read).  Waits the
+// compiler inserts for its own loads can only over-count an extra unknown
+// operation, never under-count it.
+__device__ __forceinline__ void dma16(const double* src, const double* lds) {
+    typedef __attribute__((address_space(3))) const void* lptr;
+    const uint32_t l = (uint32_t)(uintptr_t)(lptr)lds;
+    uint32_t saved;  // m0 is reserved to the compiler: restored, not clobbered
+    __asm__ volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "v"(src), "s"(l)
+        : "memory");
+}
+
 template <bool EARTH>
-__global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm, int n_seg,
+__global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm, int seg0, int seg_end,
                                                           const gvx_imu* __restrict__ imu,
                                                           const int32_t* __restrict__ seg_off,
                                                           const gvx_state* __restrict__ state0,
                                                           const double* __restrict__ iewn_in,
-                                                          const PreG* __restrict__ pre, const QRec* __restrict__ qrec,
+                                                          const CovIn* __restrict__ cin,
                                                           gvx_preint_result* __restrict__ out, double* __restrict__ pn) {
     // the kernel is written for ONE wave per workgroup: its LDS hand-overs are
     // wave fences (in-order LDS within a wave), and sqrt_info_group's barriers
     // are reached by every lane (dead groups factor the identity)
     constexpr int LANES = 16, SPWL = 64 / LANES;
     static_assert(SPWL * LANES == 64, "one wave per workgroup");
-    __shared__ __attribute__((aligned(256))) double sRec[SPWL * SEGR];
-    __shared__ __attribute__((aligned(256))) double sT[SPWL][TSEG];
+    // records | transpose tiles in one buffer (sqrt_info's scratch spans both
+    // after the step loop); the DMA staging in its own: a distinct LDS object
+    // lets the compiler see that the step loop's LDS reads do not alias the
+    // in-flight DMA, so they do not wait for it (vmcnt)
+    __shared__ __attribute__((aligned(256))) double sLds[C16_LDS_REC + C16_LDS_T];
+    __shared__ __attribute__((aligned(16))) double sStg[C16_LDS_STG];  // the next chunk's CovIn records
+    double* const sRec = sLds;
     const int lane = threadIdx.x;
     const int grp = lane / LANES, c = lane % LANES;
-    const int seg = blockIdx.x * SPWL + grp;
-    const bool live = seg < n_seg;
+    const int wseg = seg0 + blockIdx.x * SPWL;  // the wave's first segment
+    const int seg = wseg + grp;
+    const bool live = seg < seg_end;
     const int b0 = live ? seg_off[seg] : 0;
     const int m = live ? seg_off[seg + 1] - b0 : 0;
     int mmax = m;
@@ -823,7 +868,6 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
         if (EARTH)
             for (int i = 0; i < 3; ++i) iewn[i] = iewn_in[3 * seg + i];
     }
-    s0.q[3] = live ? s0.q[3] : 1.0;  // dead groups: a unit quaternion for rot_terms
     double p[3], v[3], dp[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
     for (int i = 0; i < 3; ++i) {
         p[i] = s0.p[i];
@@ -857,20 +901,87 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
         Jc[i] = i == c ? 1.0 : 0.0;
         Pc[i] = 0.0;
     }
-    const PreG* pg0 = pre + (live ? b0 - seg : 0);
-    const QRec* qr0 = qrec + (live ? b0 - seg : 0);
-    const gvx_imu* im = imu + b0;
-    double* const tile = sT[grp];
+    double* const tile = sLds + C16_LDS_REC + grp * TSEG;
+    // LDS-DMA of a chunk's CovIn records (steps kc .. kc + C16_CK - 1 of the four
+    // segments) into sStg: 16-B piece pc of the wave's staging is piece pc % P of
+    // segment pc / P's chunk (P = 54); pieces of steps past a segment's m (or of
+    // dead groups) re-read a valid record and are never used
+    // the four segments' first CovIn record and m (uniform: scalar registers;
+    // per-lane copies kept across the step loop were spilled, and their
+    // reloads serialised every record phase: 4,800 cycles, r05 v17 stamps)
+    const int m0s = __builtin_amdgcn_readlane(m, 0), m1s = __builtin_amdgcn_readlane(m, LANES);
+    const int m2s = __builtin_amdgcn_readlane(m, 2 * LANES), m3s = __builtin_amdgcn_readlane(m, 3 * LANES);
+    const int wb = __builtin_amdgcn_readlane(b0, 0) - wseg;  // dead groups: record 0
+    const int b1s = m1s > 0 ? __builtin_amdgcn_readlane(b0, LANES) - (wseg + 1) : 0;
+    const int b2s = m2s > 0 ? __builtin_amdgcn_readlane(b0, 2 * LANES) - (wseg + 2) : 0;
+    const int b3s = m3s > 0 ? __builtin_amdgcn_readlane(b0, 3 * LANES) - (wseg + 3) : 0;
+    // piece `lane` of a slot: record (2 lane) / 18 of the chunk, double
+    // (2 lane) % 18 inside it; records 0 .. m-2 hold steps 1 .. m-1
+    const auto piece = [&](int kc, int bg, int mg) {
+        const int rec = max(min(kc - 1 + (2 * lane) / COVIN_DW, mg - 2), 0);
+        return reinterpret_cast<const double*>(cin + (bg + rec)) + (2 * lane) % COVIN_DW;
+    };
+    if (1 < mmax && lane < STG_PIECES) {
+        dma16(piece(1, m0s > 0 ? wb : 0, m0s), sStg);
+        dma16(piece(1, b1s, m1s), sStg + STG_SEG);
+        dma16(piece(1, b2s, m2s), sStg + 2 * STG_SEG);
+        dma16(piece(1, b3s, m3s), sStg + 3 * STG_SEG);
+    }
+    // pn rows (dt, p) of the chunk's steps: lane c < C16_CK keeps step kc + c's
+    // and stores it during the next chunk's record phase, after that chunk's
+    // DMA has been waited for (a store issued inside the step loop would hold up
+    // the next chunk's vmcnt(0) wait by a full write round trip)
+    double prow[4] = {0, 0, 0, 0};
+    int prk = 0;  // the step prow belongs to (0: none)
+    const auto store_prow = [&]() {
+        if (pns && c < C16_CK && prk >= 1 && prk < m)
+            *reinterpret_cast<double4*>(pns + 4 * (prk - 1)) = double4{prow[0], prow[1], prow[2], prow[3]};
+    };
+    // The previous chunk's pn rows, then the next chunk's DMA, every operand
+    // formed first: the kernel is VGPR-bound and some operands are spilled, and
+    // a reload issued after a DMA waits (vmcnt(0)) for that DMA's round trip
+    // (r05 v17 stamps: 4,800 cycles a chunk when the four issues were
+    // interleaved with reloads).
+    const auto stage_and_store = [&](int kc) {
+        const int kn = kc + C16_CK;
+        const bool dma = kn < mmax && lane < STG_PIECES;
+        const double* s0p = piece(kn, m0s > 0 ? wb : 0, m0s);
+        const double* s1p = piece(kn, b1s, m1s);
+        const double* s2p = piece(kn, b2s, m2s);
+        const double* s3p = piece(kn, b3s, m3s);
+        const bool st = pns && c < C16_CK && prk >= 1 && prk < m;
+        double* pdst = st ? pns + 4 * (prk - 1) : pn;
+        const double4 pv{prow[0], prow[1], prow[2], prow[3]};
+        if (st) *reinterpret_cast<double4*>(pdst) = pv;
+        __builtin_amdgcn_sched_barrier(0);
+        if (dma) {
+            dma16(s0p, sStg);
+            dma16(s1p, sStg + STG_SEG);
+            dma16(s2p, sStg + 2 * STG_SEG);
+            dma16(s3p, sStg + 3 * STG_SEG);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
     for (int kc = 1; kc < mmax; kc += C16_CK) {
-        // ---- this chunk's step records, one step per lane ----
+        // ---- this chunk's step records, one step per lane, from the staged CovIn ----
+        // the chunk's DMA has landed (the intrinsic, not asm: the compiler then
+        // knows nothing of its own is outstanding either, and puts no waits for
+        // older reloads inside the step loop, where they would catch the next DMA)
+        __builtin_amdgcn_s_waitcnt(VMCNT0);
+        wave_lds_sync();
         if (c < C16_CK) {
             const int k = kc + c;
             double* dst = sRec + grp * SEGR + c * RS;
             if (k < m)
-                make_record<EARTH>(prm, pg0 + (k - 1), qr0, im[k], s0, k, nacc, dst);
+                make_record<EARTH>(prm, sStg + grp * STG_SEG + c * COVIN_DW, nacc, dst);
             else
                 identity_record(dst);
         }
+        // the staging is read: the next chunk's records land there while this
+        // chunk's steps run
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage_and_store(kc);
+        prk = kc + c;
         wave_lds_sync();
         const int kend = min(kc + C16_CK, mmax);
         for (int k = kc; k < kend; ++k) {
@@ -906,8 +1017,12 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             for (int i = 0; i < 3; ++i) p[i] += dt * v[i] + 0.5 * dt * dvel[i];
 #pragma unroll
             for (int i = 0; i < 3; ++i) v[i] += dvel[i];
-            if (pns && c == 0 && act)
-                *reinterpret_cast<double4*>(pns + 4 * (k - 1)) = double4{dt, p[0], p[1], p[2]};
+            if (pns && k - kc == c) {
+                prow[0] = dt;
+                prow[1] = p[0];
+                prow[2] = p[1];
+                prow[3] = p[2];
+            }
 #pragma unroll
             for (int i = 0; i < 3; ++i) dp[i] += dt * dv[i] + 0.5 * dt * rb[i];
 #pragma unroll
@@ -965,6 +1080,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             wave_lds_sync();  // the next step's stores after this step's reads
         }
     }
+    store_prow();
     gvx_preint_result* o = out + seg;
     if (live && c < NS) {
 #pragma unroll
@@ -1017,17 +1133,25 @@ hipError_t launch_preint(gvx_ctx* c, int variant, const gvx_imu_params& prm, int
         const size_t bytes = samples * STEP_SCRATCH;
         char* d = bytes <= (size_t(1) << 30) ? (char*)scratch(c, "preint_steps", bytes) : nullptr;
         if (d) {
-            PreG* pre = reinterpret_cast<PreG*>(d);
-            QRec* qr = reinterpret_cast<QRec*>(d + samples * sizeof(PreG));
+            const CovIn* ci = reinterpret_cast<CovIn*>(d);
             const bool earth = variant == GVX_PREINT_EARTH;
-            // the per-step terms and the quaternion chains (wave scans), then the
-            // covariance pass
-            hipLaunchKernelGGL(earth ? preint_pre_kernel<true> : preint_pre_kernel<false>, dim3(n_seg), dim3(64), 0,
-                               c->stream, n_seg, imu, seg_off, state0, iewn, pre, qr, prm, out);
-            // the covariance pass, sqrt_info in its epilogue
-            hipLaunchKernelGGL(earth ? preint_cov16_kernel<true> : preint_cov16_kernel<false>,
-                               dim3((n_seg + 3) / 4), dim3(64), 0, c->stream, prm, n_seg, imu, seg_off, state0, iewn,
-                               (const PreG*)pre, (const QRec*)qr, out, pn);
+            // the per-step terms and the quaternion chains (wave scans) of
+            // segments [s0, s1), then their covariance pass (sqrt_info in its
+            // epilogue)
+            const auto pre = [&](hipStream_t st, int s0, int s1) {
+                hipLaunchKernelGGL(earth ? preint_pre_kernel<true> : preint_pre_kernel<false>, dim3(s1 - s0), dim3(64),
+                                   0, st, s0, imu, seg_off, state0, iewn, (CovIn*)ci, prm, out);
+            };
+            const auto cov = [&](hipStream_t st, int s0, int s1) {
+                hipLaunchKernelGGL(earth ? preint_cov16_kernel<true> : preint_cov16_kernel<false>,
+                                   dim3((s1 - s0 + 3) / 4), dim3(64), 0, st, prm, s0, s1, imu, seg_off, state0, iewn,
+                                   ci, out, pn);
+            };
+            // (r05 v15: splitting a batch in two, the first half's covariance pass
+            // on a second stream beside the second half's pre pass, was 4 %
+            // slower: the covariance waves are not latency-bound enough to share)
+            pre(c->stream, 0, n_seg);
+            cov(c->stream, 0, n_seg);
             if (sqrt_info_done) *sqrt_info_done = true;
             return hipGetLastError();
         }

@@ -3,7 +3,7 @@
 PROBE: s_memtime at the step's start, after the G stores, after the K reads
 landed, and at the end, written by lane 0 of each segment over its pn_
 sample): median shader cycles of each phase per step, and of the gap from one
-step's end to the next step's start (the record phase every 8 steps).  Each
+step's end to the next step's start (the record phase every STAMP_CK steps, default 6).  Each
 stamp waits for the outstanding LDS operations, so phases include drains.
 Run with GVX_LIB=.../libgvx_stamp.so; PREINT_REPS as preint_loop.py."""
 import json
@@ -22,8 +22,9 @@ for seg in (0, 1, pl.S // 2, pl.S - 1):
     t = pn[seg]
     ph = np.diff(t, axis=1)  # t1-t0, t2-t1, t3-t2
     gap = t[1:, 0] - t[:-1, 3]
-    chunk = gap[np.arange(len(gap)) % 8 == 7]  # steps 8j -> 8j+1: the record phase between them
-    plain = gap[np.arange(len(gap)) % 8 != 7]
+    CK = int(os.environ.get("STAMP_CK", "6"))  # steps per record chunk
+    chunk = gap[np.arange(len(gap)) % CK == CK - 1]  # the record phase between chunks
+    plain = gap[np.arange(len(gap)) % CK != CK - 1]
     out[str(seg)] = {"start_to_stores": float(np.median(ph[:, 0])), "stores_to_K": float(np.median(ph[:, 1])),
                      "K_to_end": float(np.median(ph[:, 2])), "gap_in_chunk": float(np.median(plain)),
                      "gap_record_phase": float(np.median(chunk)),
