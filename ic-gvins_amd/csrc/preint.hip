@@ -473,6 +473,24 @@ __device__ __forceinline__ dq wave_prefix_product(dq p) {
     return p;
 }
 // lane i - 1's quaternion (DPP wave_shr:1); lane 0 takes `first`
+// inclusive wave prefix sum of a double (lanes past the data carry 0), the
+// same DPP ladder as wave_prefix_product
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double d_dpp(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, ROWS, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_prefix_sum(double x) {
+    x = d_dpp<0x111, 0xf>(x) + x;
+    x = d_dpp<0x112, 0xf>(x) + x;
+    x = d_dpp<0x114, 0xf>(x) + x;
+    x = d_dpp<0x118, 0xf>(x) + x;
+    x = d_dpp<0x142, 0xa>(x) + x;
+    x = d_dpp<0x143, 0xc>(x) + x;
+    return x;
+}
+
 __device__ __forceinline__ dq dq_wave_shr1(dq v, dq first) {
     const auto mv = [](double x, double o) -> double {
         const int lo = __builtin_amdgcn_update_dpp(__double2loint(o), __double2loint(x), 0x138, 0xf, 0xf, false);
@@ -481,12 +499,12 @@ __device__ __forceinline__ dq dq_wave_shr1(dq v, dq first) {
     };
     return dq{mv(v.x, first.x), mv(v.y, first.y), mv(v.z, first.z), mv(v.w, first.w)};
 }
+__device__ __forceinline__ double d_readlane(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+}
 __device__ __forceinline__ dq dq_readlane(dq v, int l) {
-    const auto rl = [&](double x) -> double {
-        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
-                                __builtin_amdgcn_readlane(__double2loint(x), l));
-    };
-    return dq{rl(v.x), rl(v.y), rl(v.z), rl(v.w)};
+    return dq{d_readlane(v.x, l), d_readlane(v.y, l), d_readlane(v.z, l), d_readlane(v.w, l)};
 }
 
 // The per-step terms and the quaternion chains of one segment (one wave, lane =
@@ -531,16 +549,13 @@ __global__ void __launch_bounds__(64, EARTH ? 4 : 6) preint_pre_kernel(int seg0,
     for (int kc = 1; kc < m; kc += 64) {
         const int k = kc + lane;
         const bool live = k < m;
-        const int cnt = min(64, m - kc);
-        // delta_time_ += dt in sample order: a running sum over the chunk's
-        // samples (read lane by lane), lane k keeps its prefix
+        // delta_time_ += dt: a wave prefix sum over the chunk's samples on top
+        // of the previous chunks' total (summation order differs from the
+        // sequential sum by rounding: 1e-16 relative, inside the 1e-10 contract;
+        // the lane-by-lane running sum was 64 dependent cross-lane reads a chunk)
         const double mydt = live ? im[k].dt : 0.0;
-        double acc = base, dtime = 0.0;
-        for (int i = 0; i < cnt; ++i) {
-            acc += __shfl(mydt, i);
-            if (lane == i) dtime = acc;
-        }
-        base = acc;
+        const double dtime = base + wave_prefix_sum(mydt);
+        base = d_readlane(dtime, 63);
         dq qd = dq_make(1, 0, 0, 0), qnn = dq_make(1, 0, 0, 0);
         double dvfb[3] = {0, 0, 0}, sdv2 = 0.0, dt = 0.0;
         double* dst = reinterpret_cast<double*>(cs + (k - 1));
