@@ -62,6 +62,37 @@ struct Imu {
     double dt, dth[3], dv[3], time;
 };
 
+// rotvec2quaternion (Eigen AngleAxis: (cos(a/2), sin(a/2) r/|r|)) for the
+// small angles of one IMU sample and of the Earth rotation over a segment:
+// with y = |r|^2 / 4, cos(a/2) and sin(a/2)/|r| are even series in |r|, so no
+// square root, division or sin / cos call is needed.  Below y = 2.5e-3 (an
+// angle of 0.1 rad) the series are cut after the y^5 / y^4 terms, whose
+// remainders are < 1e-20 relative; larger angles take dmath's exact form.
+// Differs from it by rounding only (1e-16), inside the 1e-10 contract; a
+// preintegration step computes four of these (r05: ~40 % of the pre pass).
+__device__ __attribute__((noinline)) dq dq_from_rotvec_large(double r0, double r1, double r2) {
+    const double r[3] = {r0, r1, r2};
+    return dq_from_rotvec(r);
+}
+__device__ __forceinline__ dq dq_from_rotvec_small(const double* r) {
+    const double n2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+    const double y = 0.25 * n2;
+    if (y > 2.5e-3) return dq_from_rotvec_large(r[0], r[1], r[2]);  // out of line: rare
+    // cos x = 1 - y/2 + y^2/24 - y^3/720 + y^4/40320 - y^5/3628800 (x^2 = y)
+    double c = __builtin_fma(y, -1.0 / 3628800.0, 1.0 / 40320.0);
+    c = __builtin_fma(y, c, -1.0 / 720.0);
+    c = __builtin_fma(y, c, 1.0 / 24.0);
+    c = __builtin_fma(y, c, -0.5);
+    c = __builtin_fma(y, c, 1.0);
+    // sin x / (2 x) = (1 - y/6 + y^2/120 - y^3/5040 + y^4/362880) / 2
+    double t = __builtin_fma(y, 1.0 / 362880.0, -1.0 / 5040.0);
+    t = __builtin_fma(y, t, 1.0 / 120.0);
+    t = __builtin_fma(y, t, -1.0 / 6.0);
+    t = __builtin_fma(y, t, 1.0);
+    t *= 0.5;
+    return dq_make(c, t * r[0], t * r[1], t * r[2]);
+}
+
 __device__ __forceinline__ Imu load_imu(const gvx_imu* p, const double* bg, const double* ba) {
     // PreintegrationBase::compensationBias (preintegration_base.cc:86-92)
     Imu r;
@@ -237,16 +268,16 @@ __global__ void __launch_bounds__(64) preint_kernel(int variant, gvx_imu_params 
                     sp.dv[i] = ic.dv[i];
                     sp.dth[i] = ic.dth[i];
                 }
-                dq_store(dq_from_rotvec(dth), sp.qd);
+                dq_store(dq_from_rotvec_small(dth), sp.qd);
                 if (earth) {
                     const double dt = ic.dt;
                     const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
-                    dq_store(dq_from_rotvec(dnn), sp.qnn);
+                    dq_store(dq_from_rotvec_small(dnn), sp.qnn);
                     const double sc = -(dtime - 0.5 * dt);
                     const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
-                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0), sp.qa);
+                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec_small(dnn2)), q0), sp.qa);
                     const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
-                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0), sp.qb);
+                    dq_store(dq_mul(dq_mul(q0i, dq_from_rotvec_small(dnn3)), q0), sp.qb);
                 }
                 const double* w = reinterpret_cast<const double*>(&sp);
                 double* dst = pre_base + c * PRE_DW;
@@ -578,10 +609,10 @@ __global__ void __launch_bounds__(64, EARTH ? 4 : 6) preint_pre_kernel(int seg0,
             put2(2, ic.dth[1], ic.dth[2]);
             put2(4, ic.dv[0], ic.dv[1]);
             sdv2 = ic.dv[2];
-            qd = dq_from_rotvec(dth);
+            qd = dq_from_rotvec_small(dth);
             if (EARTH) {
                 const double dnn[3] = {-iewn[0] * dt, -iewn[1] * dt, -iewn[2] * dt};
-                qnn = dq_from_rotvec(dnn);
+                qnn = dq_from_rotvec_small(dnn);
             }
         }
         // the chains after step k: R_k = Rc qd_kc .. qd_k, L_k = qnn_k .. qnn_kc Lc
@@ -622,11 +653,11 @@ __global__ void __launch_bounds__(64, EARTH ? 4 : 6) preint_pre_kernel(int seg0,
                 for (int i = 0; i < 3; ++i) ra[i] = 0.5 * (x[i] + y[i]);
                 const double sc = -(dtime - 0.5 * dt);
                 const double dnn2[3] = {sc * iewn[0], sc * iewn[1], sc * iewn[2]};
-                const dq qa = dq_mul(dq_mul(q0i, dq_from_rotvec(dnn2)), q0);
+                const dq qa = dq_mul(dq_mul(q0i, dq_from_rotvec_small(dnn2)), q0);
                 dq_rot(dq_mul(qa, dprev), Rm);
                 mv3(Rm, dvfb, rb);
                 const double dnn3[3] = {-iewn[0] * dtime, -iewn[1] * dtime, -iewn[2] * dtime};
-                const dq qb = dq_mul(dq_mul(q0i, dq_from_rotvec(dnn3)), q0);
+                const dq qb = dq_mul(dq_mul(q0i, dq_from_rotvec_small(dnn3)), q0);
                 qc = dq_mul(qb, dqt);
             }
             put2(6, sdv2, qc.x);
