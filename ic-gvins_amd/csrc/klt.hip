@@ -373,6 +373,79 @@ __device__ __forceinline__ void j_pairs(const uint32_t (&r0)[2], const uint32_t 
     }
 }
 
+// A J row of a unit cached between iterations as its even byte pairs, each byte
+// times 128 in a uint16 half ("spread": h[k] = (b[2k], b[2k+1]) * 128, k = 0..3):
+// the even pairs of an iteration are then free and each odd pair is one
+// alignbit of two neighbours (3 operations a row, not 7 perms; the spread
+// itself is formed once per reload, by 4 perms with run-time selectors straight
+// from the loaded dwords and a packed shift).  Iterations mostly reuse the rows
+// (sub-pixel steps).  With the bytes at 128 (not 256) the bilinear sum
+// X = 128 (sum + 2^8) is exactly half of j_pairs' X, so the descaled value
+// (sum + 2^8) >> 9 is X >> 16: one perm takes it for two pixels, no shift.
+__device__ __forceinline__ uint32_t spread_pair(const uint32_t (&h)[4], int t) {
+    return (t & 1) ? shift_pair(h[t >> 1], h[(t >> 1) + 1]) : h[t >> 1];
+}
+// h from 12 loaded bytes {z:y:x} at byte offset sh (0..3): bytes sh .. sh+7
+__device__ __forceinline__ void spread_row(uint32_t x, uint32_t y, uint32_t z, uint32_t sh, uint32_t (&h)[4]) {
+    const uint32_t d = sh * 0x01000100u;
+    const auto half = [](uint32_t v) {
+        return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2us, v) >> (unsigned short)1);
+    };
+    h[0] = half(__builtin_amdgcn_perm(y, x, 0x010c000cu + d));
+    h[1] = half(__builtin_amdgcn_perm(y, x, 0x030c020cu + d));
+    h[2] = half(__builtin_amdgcn_perm(z, y, 0x010c000cu + d));
+    h[3] = half(__builtin_amdgcn_perm(z, y, 0x030c020cu + d));
+}
+// the same from an 8-byte row already aligned
+__device__ __forceinline__ void spread_row2(const uint32_t (&r)[2], uint32_t (&h)[4]) {
+    spread_row(r[0], r[1], r[1], 0, h);
+}
+__device__ __forceinline__ void j_pairs_h(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t W0, uint32_t W1,
+                                          uint32_t (&jp)[4]) {
+    constexpr uint32_t RND = 1u << (W_BITS - 6 + 7);
+    uint32_t X[8];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) X[t] = udot2(spread_pair(h1, t), W1, udot2k(spread_pair(h0, t), W0, RND));
+    X[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jp[k] = __builtin_amdgcn_perm(X[2 * k + 1], X[2 * k], 0x07060302u);  // (X0 >> 16, X1 >> 16)
+}
+// the signed form (w11 < 0) from the spread rows: plain bytes are the pairs >> 7
+__device__ __forceinline__ void j_pairs_h_signed(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t W0,
+                                                 uint32_t W1, uint32_t (&jp)[4]) {
+    constexpr int RND = 1 << (W_BITS - 6);
+    const auto plain = [](uint32_t v) {
+        return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2us, v) >> (unsigned short)7);
+    };
+    int jv[8];
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+        jv[t] = dot2(plain(spread_pair(h1, t)), W1, dot2k(plain(spread_pair(h0, t)), W0, RND)) >> (W_BITS - 5);
+    jv[7] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
+}
+// match_unit on spread rows (the exact iteration path)
+template <bool SIGNED>
+__device__ __forceinline__ void match_unit_h(const Unit& u, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
+                                             uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2) {
+    uint32_t jp[4];
+    if constexpr (SIGNED)
+        j_pairs_h_signed(h0, h1, W0, W1, jp);
+    else
+        j_pairs_h(h0, h1, W0, W1, jp);
+    const uint32_t d0 = psub16(jp[0], u.iv[0]);
+    int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const uint32_t d = psub16(jp[k], u.iv[k]);
+        s1 = dot2(d, u.ix[k], s1);
+        s2 = dot2(d, u.iy[k], s2);
+    }
+    b1 += valid ? s1 : 0;
+    b2 += valid ? s2 : 0;
+}
+
 template <bool ERR, bool SIGNED = false>
 __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
                                            uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
@@ -755,7 +828,9 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
         // pixel the window stays on the same pixel grid and only the bilinear
         // weights change, so the rows are reused instead of loaded again
         int cinx = INT_MIN, ciny = INT_MIN;
-        uint32_t jr0[U][2], jr1[U][2];
+        // the exact path keeps the spread form (jh), the fp32 orders the bytes (jr)
+        constexpr int JW = ACC == 0 ? 4 : 2;
+        uint32_t jr0[U][JW], jr1[U][JW];
         // one exit, at the bottom: every loop-carried value is updated in place
         // (with the early exits the register allocator copied all of them -- the
         // cached J rows, the position, the previous step -- on every iteration)
@@ -801,15 +876,28 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                     }
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
-                        jr0[s][0] = __builtin_amdgcn_alignbyte(w0[s].y, w0[s].x, sh[s]);
-                        jr0[s][1] = __builtin_amdgcn_alignbyte(w0[s].z, w0[s].y, sh[s]);
-                        jr1[s][0] = __builtin_amdgcn_alignbyte(w1[s].y, w1[s].x, sh[s]);
-                        jr1[s][1] = __builtin_amdgcn_alignbyte(w1[s].z, w1[s].y, sh[s]);
+                        if constexpr (ACC == 0) {
+                            spread_row(w0[s].x, w0[s].y, w0[s].z, sh[s], jr0[s]);
+                            spread_row(w1[s].x, w1[s].y, w1[s].z, sh[s], jr1[s]);
+                        } else {
+                            jr0[s][0] = __builtin_amdgcn_alignbyte(w0[s].y, w0[s].x, sh[s]);
+                            jr0[s][1] = __builtin_amdgcn_alignbyte(w0[s].z, w0[s].y, sh[s]);
+                            jr1[s][0] = __builtin_amdgcn_alignbyte(w1[s].y, w1[s].x, sh[s]);
+                            jr1[s][1] = __builtin_amdgcn_alignbyte(w1[s].z, w1[s].y, sh[s]);
+                        }
                     }
                 } else {
 #pragma unroll
-                    for (int s = 0; s < U; ++s)
-                        load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, jr0[s], jr1[s]);
+                    for (int s = 0; s < U; ++s) {
+                        if constexpr (ACC == 0) {
+                            uint32_t r0[2], r1[2];
+                            load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
+                            spread_row2(r0, jr0[s]);
+                            spread_row2(r1, jr1[s]);
+                        } else {
+                            load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, jr0[s], jr1[s]);
+                        }
+                    }
                 }
                 cinx = inx;
                 ciny = iny;
@@ -821,13 +909,13 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
                         if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                        match_unit<false, true>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                        match_unit_h<true>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2);
                     }
                 } else {
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
                         if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                        match_unit<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                        match_unit_h<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2);
                     }
                 }
                 group_sums_f32<G>(b1, b2, fb1, fb2);
@@ -910,7 +998,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 // (the fp32-order instances are LDS-limited: 16 KB per two-point wave)
 template <int PPW, int ACC>
 constexpr int klt_occupancy() {
-    return PPW == 1 ? 4 : ACC ? 2 : 5;
+    return PPW == 1 ? 4 : ACC ? 2 : 4;
 }
 template <int PPW, int ACC>
 __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
