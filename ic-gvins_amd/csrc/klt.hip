@@ -256,10 +256,14 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
         const uint32_t Wr = rr ? W1 : W0;
+        // the derivatives are formed times 4 (|4 dI| <= 16320 fits int16; the
+        // constants absorb the factor): the interpolated 4 (sum + 2^13) then
+        // holds CV_DESCALE(sum, 14) in its high half, and one perm packs two
+        // pixels' Ix (or Iy) without the two shifts
         uint32_t T0[5], T1[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            T0[k] = pmad16(padd16(E[rr][k], E[rr + 2][k]), 3, pmul16(E[rr + 1][k], 10));
+            T0[k] = pmad16(padd16(E[rr][k], E[rr + 2][k]), 12, pmul16(E[rr + 1][k], 40));
             T1[k] = psub16(E[rr + 2][k], E[rr][k]);
         }
         // derivative pairs at columns (2k+1, 2k+2), k = 0..3
@@ -267,7 +271,7 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             DX[k] = psub16(T0[k + 1], T0[k]);
-            DY[k] = pmad16(padd16(T1[k + 1], T1[k]), 3, pmul16(shift_pair(T1[k], T1[k + 1]), 10));
+            DY[k] = pmad16(padd16(T1[k + 1], T1[k]), 12, pmul16(shift_pair(T1[k], T1[k + 1]), 40));
         }
         if (!interior) {
             // derivatives are zero outside the image (BORDER_CONSTANT padding of
@@ -291,8 +295,8 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
             const uint32_t py = (t & 1) ? shift_pair(DY[k], DY[k + 1]) : DY[k];
             if (rr == 0) {
                 iv[t] = dot2k(pv, Wr, RNDV);
-                ix[t] = dot2k(px, Wr, RNDD);
-                iy[t] = dot2k(py, Wr, RNDD);
+                ix[t] = dot2k(px, Wr, 4 * RNDD);
+                iy[t] = dot2k(py, Wr, 4 * RNDD);
             } else {
                 iv[t] = dot2(pv, Wr, iv[t]);
                 ix[t] = dot2(px, Wr, ix[t]);
@@ -304,8 +308,12 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
     for (int k = 0; k < 4; ++k) {
         const int h = 2 * k + 1 < 7 ? 2 * k + 1 : 0;
         u.iv[k] = pack16(iv[2 * k] >> (W_BITS - 5), 2 * k + 1 < 7 ? iv[h] >> (W_BITS - 5) : 0);
-        u.ix[k] = pack16(ix[2 * k] >> W_BITS, 2 * k + 1 < 7 ? ix[h] >> W_BITS : 0);
-        u.iy[k] = pack16(iy[2 * k] >> W_BITS, 2 * k + 1 < 7 ? iy[h] >> W_BITS : 0);
+        // (4 sum) >> 16 = sum >> 14 (arithmetic), the high halves of the two
+        // pixels; the missing 8th pixel of the last pair is 0
+        u.ix[k] = 2 * k + 1 < 7 ? __builtin_amdgcn_perm((uint32_t)ix[h], (uint32_t)ix[2 * k], 0x07060302u)
+                                : __builtin_amdgcn_perm(0u, (uint32_t)ix[2 * k], 0x07060302u);
+        u.iy[k] = 2 * k + 1 < 7 ? __builtin_amdgcn_perm((uint32_t)iy[h], (uint32_t)iy[2 * k], 0x07060302u)
+                                : __builtin_amdgcn_perm(0u, (uint32_t)iy[2 * k], 0x07060302u);
     }
     int s11 = dot2k(u.ix[0], u.ix[0], 0), s12 = dot2k(u.ix[0], u.iy[0], 0), s22 = dot2k(u.iy[0], u.iy[0], 0);
 #pragma unroll
