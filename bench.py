@@ -753,14 +753,16 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
         ctx.preint_integrate_dev(2, synth_ba.imu_params(), S, d_imu.data_ptr(), d_seg_off.data_ptr(),
                                  d_states.data_ptr(), d_iewn.data_ptr(), d_out.data_ptr(), d_pnall.data_ptr())
 
-    def timed(fn, k):
-        for _ in range(args.warmup):
+    def timed(fn, k, warm=None, prof=True):
+        # prof: per-family device times by events on every launch (off for the
+        # ~35 us single-window calls, whose wall time the events would inflate)
+        for _ in range(args.warmup if warm is None else warm):
             fn()
         ctx.sync()
         if dist:
             dist.barrier()
         ctx.profile_reset()
-        ctx.profile(True)
+        ctx.profile(prof)
         t0 = time.perf_counter()
         for _ in range(k):
             fn()
@@ -776,7 +778,7 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     # the integrate call is ~0.3 ms: time enough launches that the shader clock
     # has ramped and the host-side bracket is a small part of the span
     k_i = max(40, steps)
-    el_i, fam_i = timed(integ, k_i)
+    el_i, fam_i = timed(integ, k_i, warm=max(20, args.warmup))
 
     # one window at problem size (1800 + 9 factors, latency-bound): device-pointer
     # launches, and the two-phase FactorSet prepare (block gather, H2D, both
@@ -788,8 +790,10 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
                                   n_kf - 1, d_pre.data_ptr(), d_pn.data_ptr(), d_pn_off.data_ptr(),
                                   d_poffs.data_ptr(), d_pres.data_ptr(), d_pjac.data_ptr(), d_params.data_ptr())
 
-    k_w = max(50, steps)
-    el_w, _ = timed(window, k_w)
+    # ~35 us calls: hundreds of them, after enough warm-up calls that the clocks
+    # and the host path have settled (50 calls gave 40-46 us where 2,000 give 34)
+    k_w = max(500, steps)
+    el_w, _ = timed(window, k_w, warm=max(100, args.warmup), prof=False)
     # parameter blocks as views of the packed vector (the layout the offsets index)
     starts = sorted({int(v) for v in prob["offs"].ravel()} | {int(v) for v in poffs.ravel()})
     sizes = {}
@@ -802,7 +806,7 @@ def factor_leg(args, ctx, dev, dist, world, rank, steps, window_extras=True):
     fset = gvx.FactorSet(ctx, blocks, prob["consts"].astype(gvx.REPROJ_DTYPE),
                          np.vectorize(bidx.get)(prob["offs"]).astype(np.int32), pre, pn, pn_off,
                          np.vectorize(bidx.get)(poffs).astype(np.int32))
-    el_p, _ = timed(lambda: fset.prepare(True), k_w)
+    el_p, _ = timed(lambda: fset.prepare(True), k_w, warm=max(100, args.warmup), prof=False)
     fset.close()
     evals = world * (n_r + n_p) * steps
     value = evals / el
