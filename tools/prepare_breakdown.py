@@ -24,13 +24,14 @@ for f in glob.glob(f"{root}/**/*memory_copy_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         ops.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r["Direction"]))
 ops.sort()
-# the last 100 prepares: H2D, kernels, D2H ... group from each H2D
-idx = [i for i, o in enumerate(ops) if o[2].startswith("copy") and "HOST_TO_DEVICE" in o[2].upper()]
-groups = []
-for a, b in zip(idx, idx[1:] + [len(ops)]):
-    groups.append(ops[a:b])
-groups = [g for g in groups[-100:] if len(g) >= 3]
-names = [o[2] for o in groups[0]]
+# the last 100 prepares: the op sequence repeats with period L (copies and
+# kernels of one prepare: mapped results are a parameter upload and one kernel,
+# the D2H form adds the result copy); L is the shortest period of the tail
+names_all = [o[2] for o in ops]
+L = next(L for L in range(1, 16) if all(names_all[-i] == names_all[-i - L] for i in range(1, 3 * L + 1)))
+tail = ops[len(ops) - (len(ops) // L) * L:]
+groups = [tail[k:k + L] for k in range(0, len(tail), L)][-100:]
+names = [o[2] for o in groups[-1]]
 print("ops per prepare:", names)
 for j, n in enumerate(names):
     d = statistics.median((g[j][1] - g[j][0]) / 1000 for g in groups if len(g) == len(names))
