@@ -792,9 +792,16 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const dou
     dq_rot(dq_load(ci + iQC), cbb0);
 #pragma unroll
     for (int i = 0; i < 9; ++i) cbb0[i] = -cbb0[i];
+    // C = cbb0 skew(dv), by skew's two non-zeros per column (a product and a fused
+    // multiply-add per entry instead of mm3's three products against a zero)
     double S[9], C[9], M[9];
-    skew(sdv, S);
-    mm3(cbb0, S, C);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double* r = cbb0 + 3 * i;
+        C[3 * i] = __builtin_fma(r[1], sdv[2], -(r[2] * sdv[1]));
+        C[3 * i + 1] = __builtin_fma(r[2], sdv[0], -(r[0] * sdv[2]));
+        C[3 * i + 2] = __builtin_fma(r[0], sdv[1], -(r[1] * sdv[0]));
+    }
     skew(sdth, S);
 #pragma unroll
     for (int i = 0; i < 9; ++i) M[i] = ((i % 4) == 0 ? 1.0 : 0.0) - S[i];
@@ -807,22 +814,11 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const dou
     for (int i = 1; i < 9; i += 2) put2(oD + i, cbb0[i] * dt, cbb0[i + 1] * dt);
 #pragma unroll
     for (int i = 0; i < 8; i += 2) put2(oM + i, M[i], M[i + 1]);
-    const double sg = EARTH ? 1.0 : -1.0;  // gt(3:6, 3:6) = gR = sg * cbb0
-    double gR[9], W[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) gR[i] = sg * cbb0[i];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            double g = (gR[3 * a] * nacc) * gR[3 * b];
-            g = g + (gR[3 * a + 1] * nacc) * gR[3 * b + 1];
-            g = g + (gR[3 * a + 2] * nacc) * gR[3 * b + 2];
-            W[3 * a + b] = g;
-        }
-    put2(oM + 8, M[8], W[0]);
-#pragma unroll
-    for (int i = 1; i < 9; i += 2) put2(oW + i, W[i], W[i + 1]);
+    // W = gR (nacc I) gR^T with gR = +-R(qc) a rotation: nacc I up to rounding
+    // (1e-16), so the record carries no W; the step adds a nacc on P's diagonal
+    // like the gyro and bias terms (covariance kernel, wdc and wq)
+    (void)nacc;
+    put2(oM + 8, M[8], 0.0);
     put2(oA, ci[iA], ci[iA + 1]);
     put2(oA + 2, ci[iA + 2], ci[iB]);
     put2(oA + 4, ci[iB + 1], ci[iB + 2]);
@@ -926,7 +922,9 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
     const double nba = 2 * prm.acc_bias_std * prm.acc_bias_std / prm.corr_time;
     const double g60 = EARTH ? -1.0 : 1.0;
     const double wg = (g60 * ngyr) * g60;
-    const double wdc = c < 9 ? wg : (c < 12 ? nbg : nba);
+    // the diagonal Q term of lane c's row (W = nacc I, see make_record); lanes
+    // 0..2 have none
+    const double wdc = c < 3 ? 0.0 : (c < 6 ? nacc : (c < 9 ? wg : (c < 12 ? nbg : nba)));
     constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
     constexpr int oS = offsetof(StepRec, S) / 8, oS1 = offsetof(StepRec, S1) / 8, oZ = offsetof(StepRec, Z) / 8;
     constexpr int oW = offsetof(StepRec, W) / 8, oA = offsetof(StepRec, a) / 8;
@@ -940,7 +938,11 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
     // (phi_c(3:6) has its one non-zero, dt for c < 3 or 1 for c < 6, at c mod 3)
     const int qw = c % 3;
     const int phs = ph3 + qw;
-    const bool qv = c >= 3 && c < 6, qd = c >= 6 && c < NS;
+    const bool qdl = c >= 3 && c < NS;  // lanes with a diagonal Q add
+    // lane c's W column (c mod 3) of q_terms: nacc at row c mod 3
+    double wq[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) wq[i] = i == qw ? nacc : 0.0;
     double Jc[NS], Pc[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -1036,12 +1038,11 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             // the record's Phi, increments and this lane's Q operands (one wait);
             // W and row c of Phi are read after the hand-over, where they are used
             const Phi f = *reinterpret_cast<const Phi*>(rw);
-            double ra[3], rb[3], wq[3];
+            double ra[3], rb[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 ra[i] = rw[oA + i];
                 rb[i] = rw[oA + 3 + i];
-                wq[i] = rw[oW + 3 * i + qw];
             }
             const double sc = rw[phs];
             const double dt = f.dt;
@@ -1079,20 +1080,11 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             phi_mv(f, Pc, y);
 #pragma unroll
             for (int i = 0; i < NS; ++i) tile[i * TS + c] = y[i];
-            // K's Q terms: a W(3:6, c) into row c, cols 3..5 (lanes 3..5), a w_c
-            // onto the diagonal (lanes 6..14) -- after every lane's stores
-            double qa[3];
-#pragma unroll
-            for (int b = 0; b < 3; ++b) qa[b] = a * wq[b];  // wq = W(3 + b, c - 3) for lanes 3..5
+            // K's Q term: a w_c onto the diagonal of row c (lanes 3..14; W = nacc I,
+            // so lanes 3..5 add a nacc there) -- after every lane's stores
             const double qdg = a * wdc;
             wave_lds_sync();
-            if (qv) {
-#pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    __hip_atomic_fetch_add(&tile[c * TS + 3 + b], qa[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else if (qd) {
-                __hip_atomic_fetch_add(&tile[c * TS + c], qdg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
+            if (qdl) __hip_atomic_fetch_add(&tile[c * TS + c], qdg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             wave_lds_sync();
             // K = row c of the tile = G(c,:)^T + a W(:,c) (row 15 is padding) and
             // row c of Phi, cols 6..14; issued before J's update, which runs
