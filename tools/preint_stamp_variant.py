@@ -24,12 +24,8 @@ rep("""            if (pns && k - kc == c) {
             }
 """, """            double st0 = (double)__builtin_amdgcn_s_memtime();  // STAMP PROBE
 """)
-rep("""            double qa[3];
-#pragma unroll
-            for (int b = 0; b < 3; ++b) qa[b] = a * wq[b];""", """            double st1 = (double)__builtin_amdgcn_s_memtime();  // STAMP PROBE
-            double qa[3];
-#pragma unroll
-            for (int b = 0; b < 3; ++b) qa[b] = a * wq[b];""")
+rep("""            const double qdg = a * wdc;""", """            double st1 = (double)__builtin_amdgcn_s_memtime();  // STAMP PROBE
+            const double qdg = a * wdc;""")
 rep("""            __builtin_amdgcn_sched_barrier(0);
             phi_mv(f, Jc, y);""", """            __builtin_amdgcn_sched_barrier(0);
             double st2 = (double)__builtin_amdgcn_s_memtime() + K[0] * 0.0;  // STAMP PROBE (after K landed)
