@@ -822,32 +822,39 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const dou
     put2(oA, ci[iA], ci[iA + 1]);
     put2(oA + 2, ci[iA + 2], ci[iB]);
     put2(oA + 4, ci[iB + 1], ci[iB + 2]);
-    // S = {0,0,dt,0,0,f,0,0,-dt,0,0}, S1 = {0,0,1,0,0}, Z = 0, pad
-    put2(oS, 0.0, 0.0);
-    put2(oS + 2, dt, 0.0);
-    put2(oS + 4, 0.0, f);
-    put2(oS + 6, 0.0, 0.0);
-    put2(oS + 8, -dt, 0.0);
-    put2(oS + 10, 0.0, 0.0);
-    put2(oS + 12, 0.0, 1.0);
-    put2(oS + 14, 0.0, 0.0);
-    put2(oS + 16, 0.0, 0.0);
-    put2(oS + 18, 0.0, 0.0);
+    // S = {0,0,dt,0,0,f,0,0,-dt,0,0}: its three step values (the constant rest
+    // of S, S1 = {0,0,1,0,0}, Z = 0 and the pad are written once per slot,
+    // record_constants: 10 b128 stores a record fewer)
+    dst[oS + 2] = dt;
+    dst[oS + 5] = f;
+    dst[oS + 8] = -dt;
 }
 
 // the identity step (past a segment's m): Phi = I, W = 0, no increments
+// (S's three step values and everything before S; the rest is record_constants')
 __device__ __forceinline__ void identity_record(double* __restrict__ dst) {
-    double w[SREC_DW];
+    constexpr int oS = offsetof(StepRec, S) / 8;
+    double w[oS];
 #pragma unroll
-    for (int i = 0; i < SREC_DW; ++i) w[i] = 0.0;
+    for (int i = 0; i < oS; ++i) w[i] = 0.0;
     w[offsetof(StepRec, f) / 8] = 1.0;
     w[offsetof(StepRec, M) / 8] = 1.0;
     w[offsetof(StepRec, M) / 8 + 4] = 1.0;
     w[offsetof(StepRec, M) / 8 + 8] = 1.0;
-    w[offsetof(StepRec, S) / 8 + 5] = 1.0;
-    w[offsetof(StepRec, S1) / 8 + 2] = 1.0;
 #pragma unroll
-    for (int i = 0; i < SREC_DW; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+    for (int i = 0; i < oS; i += 2) *reinterpret_cast<double2*>(dst + i) = double2{w[i], w[i + 1]};
+    dst[oS + 2] = 0.0;
+    dst[oS + 5] = 1.0;
+    dst[oS + 8] = 0.0;
+}
+// the constant part of a record slot's lookups: S = {0,0,*,0,0,*,0,0,*,0,0},
+// S1 = {0,0,1,0,0}, Z = 0 and the pad, written once per slot before the steps
+__device__ __forceinline__ void record_constants(double* __restrict__ dst) {
+    constexpr int oS = offsetof(StepRec, S) / 8, oS1 = offsetof(StepRec, S1) / 8;
+    static_assert(oS % 2 == 0 && SREC_DW - oS == 20, "S .. pad: 10 pairs");
+#pragma unroll
+    for (int i = oS; i < SREC_DW; i += 2)
+        *reinterpret_cast<double2*>(dst + i) = double2{i == oS1 + 2 ? 1.0 : 0.0, i + 1 == oS1 + 2 ? 1.0 : 0.0};
 }
 
 // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maxima)
@@ -969,6 +976,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
         const int rec = max(min(kc - 1 + (2 * lane) / COVIN_DW, mg - 2), 0);
         return reinterpret_cast<const double*>(cin + (bg + rec)) + (2 * lane) % COVIN_DW;
     };
+    if (c < C16_CK) record_constants(sRec + grp * SEGR + c * RS);
     if (1 < mmax && lane < STG_PIECES) {
         dma16(piece(1, m0s > 0 ? wb : 0, m0s), sStg);
         dma16(piece(1, b1s, m1s), sStg + STG_SEG);
