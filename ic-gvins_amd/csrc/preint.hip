@@ -131,6 +131,47 @@ struct Phi {
     double M[9];         // Phi(6:9, 6:9) = I - skew(dtheta); Phi(6:9, 9:12) = -dt I
 };
 
+// Phi with its (6:9, 6:9) block as dtheta (the covariance pass's record prefix:
+// 24 doubles a step instead of 29 in registers and 12 b128 reads instead of 15)
+struct PhiT {
+    double dt, f;
+    double C[9], D[9];
+    double th[3], pad;
+};
+// phi_mv with M = I - skew(th) formed in the products: its entries are exact
+// (0 - (-x) = x, 1 - 0 = 1), 1 * v6 is v6 and fma(1, v7, s) rounds like
+// s + v7, so the result has the same bits as phi_mv's
+__device__ __forceinline__ void phi_mv_t(const PhiT& f, const double* v, double* y) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = __builtin_fma(f.dt, v[3 + i], v[i]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double s = v[3 + a];
+        s = __builtin_fma(f.C[3 * a], v[6], s);
+        s = __builtin_fma(f.C[3 * a + 1], v[7], s);
+        s = __builtin_fma(f.C[3 * a + 2], v[8], s);
+        s = __builtin_fma(f.D[3 * a], v[12], s);
+        s = __builtin_fma(f.D[3 * a + 1], v[13], s);
+        s = __builtin_fma(f.D[3 * a + 2], v[14], s);
+        y[3 + a] = s;
+    }
+    // rows of I - skew(th): (1, th2, -th1), (-th2, 1, th0), (th1, -th0, 1)
+    double s = v[6];
+    s = __builtin_fma(f.th[2], v[7], s);
+    s = __builtin_fma(-f.th[1], v[8], s);
+    y[6] = __builtin_fma(-f.dt, v[9], s);
+    s = -f.th[2] * v[6];
+    s = s + v[7];
+    s = __builtin_fma(f.th[0], v[8], s);
+    y[7] = __builtin_fma(-f.dt, v[10], s);
+    s = f.th[1] * v[6];
+    s = __builtin_fma(-f.th[0], v[7], s);
+    s = s + v[8];
+    y[8] = __builtin_fma(-f.dt, v[11], s);
+#pragma unroll
+    for (int i = 9; i < NS; ++i) y[i] = f.f * v[i];
+}
+
 __device__ __forceinline__ void phi_mv(const Phi& f, const double* v, double* y) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) y[i] = __builtin_fma(f.dt, v[3 + i], v[i]);
@@ -727,10 +768,12 @@ __global__ void __launch_bounds__(64, EARTH ? 4 : 6) preint_pre_kernel(int seg0,
 // Reference: preintegration_earth.cc:266-303, preintegration_normal.cc:198-232
 // (updateJacobianAndCovariance), preintegration_earth.cc:205-260 (the sums).
 struct StepRec {
-    double dt, f;             // Phi's scalars (the layout of Phi, so phi_mv reads it in place)
-    double C[9], D[9], M[9];  // Phi(3:6, 6:9), Phi(3:6, 12:15), Phi(6:9, 6:9) = I - skew(dtheta)
-    double W[9];              // W(3:6, 3:6)
+    double dt, f;             // PhiT's scalars (the layout of PhiT, so the step reads it in place)
+    double C[9], D[9];        // Phi(3:6, 6:9), Phi(3:6, 12:15)
+    double th[3], pad0;       // dtheta: Phi(6:9, 6:9) = I - skew(dtheta) (phi_mv_t forms its rows)
+    double M[9], pad1;        // I - skew(dtheta), for lanes 6..8's row lookups
     double a[3], b[3];        // velocity / delta-velocity increments (before gravity / Coriolis)
+    double pad2[4];
     // row c of Phi, read by lane c at a lane-dependent offset instead of selected:
     // S = {0,0,dt,0,0,f,0,0,-dt,0,0} (rows of dt I, f I, -dt I at 2-j, 5-j, 8-j),
     // S1 = {0,0,1,0,0} (rows of I), Z = zeros
@@ -780,8 +823,10 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const dou
     // and sums stay in registers across the record phase)
     const auto put2 = [&](int i, double x, double y) { *reinterpret_cast<double2*>(dst + i) = double2{x, y}; };
     constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
-    constexpr int oW = offsetof(StepRec, W) / 8, oA = offsetof(StepRec, a) / 8, oS = offsetof(StepRec, S) / 8;
-    static_assert(oC == 2 && oD == 11 && oM == 20 && oW == 29 && oA == 38 && oS == 44, "record layout");
+    constexpr int oA = offsetof(StepRec, a) / 8, oS = offsetof(StepRec, S) / 8;
+    constexpr int oT = offsetof(StepRec, th) / 8;
+    static_assert(oC == 2 && oD == 11 && oT == 20 && oM == 24 && oA == 34 && oS == 44 && sizeof(PhiT) == 24 * 8,
+                  "record layout");
     constexpr int iDT = offsetof(CovIn, dt) / 8, iTH = offsetof(CovIn, sdth) / 8, iDV = offsetof(CovIn, sdv) / 8;
     constexpr int iQC = offsetof(CovIn, qc) / 8, iA = offsetof(CovIn, a) / 8, iB = offsetof(CovIn, b) / 8;
     const double dt = ci[iDT];
@@ -819,6 +864,8 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const dou
     // like the gyro and bias terms (covariance kernel, wdc and wq)
     (void)nacc;
     put2(oM + 8, M[8], 0.0);
+    put2(oT, sdth[0], sdth[1]);
+    put2(oT + 2, sdth[2], 0.0);
     put2(oA, ci[iA], ci[iA + 1]);
     put2(oA + 2, ci[iA + 2], ci[iB]);
     put2(oA + 4, ci[iB + 1], ci[iB + 2]);
@@ -934,7 +981,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
     const double wdc = c < 3 ? 0.0 : (c < 6 ? nacc : (c < 9 ? wg : (c < 12 ? nbg : nba)));
     constexpr int oC = offsetof(StepRec, C) / 8, oD = offsetof(StepRec, D) / 8, oM = offsetof(StepRec, M) / 8;
     constexpr int oS = offsetof(StepRec, S) / 8, oS1 = offsetof(StepRec, S1) / 8, oZ = offsetof(StepRec, Z) / 8;
-    constexpr int oW = offsetof(StepRec, W) / 8, oA = offsetof(StepRec, a) / 8;
+    constexpr int oA = offsetof(StepRec, a) / 8;
     // lane-dependent lookups into a record: row c of Phi (cols 3..14) and the W
     // column of lane c's Q adds (lanes 3..5; the others read a zero)
     const int ph3 = c < 3 ? oS + 2 - c : (c < 6 ? oS1 + 2 - (c - 3) : oZ);
@@ -1045,7 +1092,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             const double* rw = sRec + grp * SEGR + (k - kc) * RS;
             // the record's Phi, increments and this lane's Q operands (one wait);
             // W and row c of Phi are read after the hand-over, where they are used
-            const Phi f = *reinterpret_cast<const Phi*>(rw);
+            const PhiT f = *reinterpret_cast<const PhiT*>(rw);
             double ra[3], rb[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
@@ -1085,7 +1132,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             // G(:,c) = Phi P(:,c), stored transposed (element i to row i); lane 15
             // writes column 15, which no row read uses
             double y[NS];
-            phi_mv(f, Pc, y);
+            phi_mv_t(f, Pc, y);
 #pragma unroll
             for (int i = 0; i < NS; ++i) tile[i * TS + c] = y[i];
             // K's Q term: a w_c onto the diagonal of row c (lanes 3..14; W = nacc I,
@@ -1107,12 +1154,12 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
                 ph[12 + b] = rw[ph12 + b];
             }
             __builtin_amdgcn_sched_barrier(0);
-            phi_mv(f, Jc, y);
+            phi_mv_t(f, Jc, y);
 #pragma unroll
             for (int i = 0; i < NS; ++i) Jc[i] = y[i];
             __builtin_amdgcn_sched_barrier(0);
             if (act) {
-                phi_mv(f, K, y);
+                phi_mv_t(f, K, y);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Pc[i] = y[i];
                 // q_terms with W phi_c(3:6) = sc W(:, c mod 3) (the other two terms
