@@ -814,10 +814,11 @@ static_assert(4 * SI_GROUP_DW <= C16_LDS_REC + C16_LDS_T, "sqrt_info scratch fit
 static_assert(C16_LDS_REC % 32 == 0 && C16_LDS_T % 32 == 0, "256-B aligned sub-regions");
 
 // The record of step k (k >= 1) of one segment from its staged CovIn (in LDS):
-// cbb0 = -R(qc), Phi's blocks and W, formed by the same operations as
-// preint_kernel's step.
+// cbb0 = -R(qc), Phi's blocks (C by skew's structure, fused), dtheta and the
+// increments.  No W: gR (nacc I) gR^T of a rotation is nacc I up to rounding,
+// which the step adds on P's diagonal (wdc, wq).
 template <bool EARTH>
-__device__ __forceinline__ void make_record(const gvx_imu_params& prm, const double* __restrict__ ci, double nacc,
+__device__ __forceinline__ void make_record(const gvx_imu_params& prm, const double* __restrict__ ci,
                                             double* __restrict__ dst) {
     // each field stored as it is formed (short live ranges: the step loop's J, P
     // and sums stay in registers across the record phase)
@@ -862,7 +863,6 @@ __device__ __forceinline__ void make_record(const gvx_imu_params& prm, const dou
     // W = gR (nacc I) gR^T with gR = +-R(qc) a rotation: nacc I up to rounding
     // (1e-16), so the record carries no W; the step adds a nacc on P's diagonal
     // like the gyro and bias terms (covariance kernel, wdc and wq)
-    (void)nacc;
     put2(oM + 8, M[8], 0.0);
     put2(oT, sdth[0], sdth[1]);
     put2(oT + 2, sdth[2], 0.0);
@@ -1076,7 +1076,7 @@ __global__ void __launch_bounds__(64, 2) preint_cov16_kernel(gvx_imu_params prm,
             const int k = kc + c;
             double* dst = sRec + grp * SEGR + c * RS;
             if (k < m)
-                make_record<EARTH>(prm, sStg + grp * STG_SEG + c * COVIN_DW, nacc, dst);
+                make_record<EARTH>(prm, sStg + grp * STG_SEG + c * COVIN_DW, dst);
             else
                 identity_record(dst);
         }
