@@ -322,6 +322,15 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
         s12 = dot2(u.ix[k], u.iy[k], s12);
         s22 = dot2(u.iy[k], u.iy[k], s22);
     }
+    // an invalid unit (k >= 63: lane 31's second unit) gets zero gradients, so its
+    // products vanish in every iteration without a per-iteration select
+    if (!u.valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u.ix[k] = 0u;
+            u.iy[k] = 0u;
+        }
+    }
     a11 = u.valid ? s11 : 0;
     a12 = u.valid ? s12 : 0;
     a22 = u.valid ? s22 : 0;
@@ -534,6 +543,22 @@ __device__ __forceinline__ void group_sums_f32(int v0, int v1, float& f0, float&
     const uint32_t l = (uint32_t)group_sum<G>((int)(((uint32_t)v0 & 1023u) | (((uint32_t)v1 & 1023u) << 16)));
     f0 = (float)__builtin_fma((double)h0, 1024.0, (double)(l & 0xffffu));
     f1 = (float)__builtin_fma((double)h1, 1024.0, (double)(l >> 16));
+}
+// The same sums when no lane's value reaches 2^31 / G in magnitude (2^26 for a
+// 32-lane group; the usual case: the mismatch shrinks as the iterations
+// converge): the group sum then stays below 2^31, so one int32 chain per sum
+// and the int -> fp32 conversion (round to nearest even, as the fp64 route) give
+// the same bits with 2 chains instead of 3 and no fp64 (wave-uniform choice)
+template <int G>
+__device__ __forceinline__ void group_sums_f32_fast(int v0, int v1, float& f0, float& f1) {
+    constexpr int LIM = (int)((1u << 31) / G);
+    const bool big = (v0 >= LIM || v0 <= -LIM) || (v1 >= LIM || v1 <= -LIM);
+    if (__builtin_amdgcn_ballot_w64(big) == 0) {
+        f0 = (float)group_sum<G>(v0);
+        f1 = (float)group_sum<G>(v1);
+    } else {
+        group_sums_f32<G>(v0, v1, f0, f1);
+    }
 }
 template <int G>
 __device__ __forceinline__ float group_sum_f32(int v) {
@@ -917,16 +942,16 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
                         if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                        match_unit_h<true>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2);
+                        match_unit_h<true>(u[s], jr0[s], jr1[s], J0, J1, true, b1, b2);  // invalid: Ix = Iy = 0
                     }
                 } else {
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
                         if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                        match_unit_h<false>(u[s], jr0[s], jr1[s], J0, J1, s < U - 1 || u[s].valid, b1, b2);
+                        match_unit_h<false>(u[s], jr0[s], jr1[s], J0, J1, true, b1, b2);
                     }
                 }
-                group_sums_f32<G>(b1, b2, fb1, fb2);
+                group_sums_f32_fast<G>(b1, b2, fb1, fb2);
             } else {
                 wave_lds_sync();  // the previous readers of the region are done
 #pragma unroll
