@@ -803,8 +803,18 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
         }
         float A11, A12, A22;
         if constexpr (ACC == 0) {
-            group_sums_f32<G>(a11, a12, A11, A12);
-            A22 = group_sum_f32<G>(a22);
+            // the structure tensor: three int32 chains when every lane's partial
+            // is below 2^31 / G (same bits as the split fp64 route, as for b)
+            constexpr int LIM = (int)((1u << 31) / G);
+            const bool big = (a11 >= LIM) || (a22 >= LIM) || (a12 >= LIM || a12 <= -LIM);  // a11, a22 >= 0
+            if (__builtin_amdgcn_ballot_w64(big) == 0) {
+                A11 = (float)group_sum<G>(a11);
+                A12 = (float)group_sum<G>(a12);
+                A22 = (float)group_sum<G>(a22);
+            } else {
+                group_sums_f32<G>(a11, a12, A11, A12);
+                A22 = group_sum_f32<G>(a22);
+            }
         } else {
             // Ix*Ix and Ix*Iy first, then Iy*Iy (exact int products < 2^24: the
             // float conversion is exact, as OpenCV's fx*fx of converted values)
