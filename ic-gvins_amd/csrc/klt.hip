@@ -885,8 +885,9 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             // 0) with its position as it was.  The body still runs (no divergent
             // branch around it: see the reloads below) at a position clamped into
             // the padded level, and its result is discarded by the selects.
-            const bool oob = (int)fnx < -WIN || (int)fnx >= W || (int)fny < -WIN || (int)fny >= H;
-            const int inx = min(max((int)fnx, -WIN), W - 1), iny = min(max((int)fny, -WIN), H - 1);
+            const int fxi = (int)fnx, fyi = (int)fny;
+            const int inx = min(max(fxi, -WIN), W - 1), iny = min(max(fyi, -WIN), H - 1);
+            const bool oob = inx != fxi || iny != fyi;  // the clamp moved it: off the level
             uint32_t J0, J1;
             weights(nextx - fnx, nexty - fny, J0, J1);
             int b1 = 0, b2 = 0, es = 0;
