@@ -1028,6 +1028,428 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
     }
 }
 
+// ---- three points per wave (PPW 3, exact order) ----
+// Point group g holds lanes 21g .. 21g+20 (lane 63 shadows lane 62 and belongs to
+// no sum).  Lane gl of a group owns three vertically adjacent units: window
+// rows 3(gl/3) .. 3(gl/3)+2 of segment gl%3.  Three units share their
+// derivative rows (4 instead of 6) and their J rows (4 instead of 6), and the
+// per-point scalar work is issued once for three points.
+constexpr int G3 = 21;
+__device__ __forceinline__ int grp3(int lane) { return lane < G3 ? 0 : lane < 2 * G3 ? 1 : 2; }
+
+// inclusive prefix sum over the wave, modulo 2^32 (DPP row shifts, then the row
+// broadcasts of lanes 15 and 31)
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+    return v;
+}
+// the total of v over the lane's point group: the inclusive scan at the group's
+// last lane minus the exclusive scan at its first, both read by ds_bpermute
+// (ga = 4 * first lane).  Modulo 2^32, so exact whenever the total fits int32.
+__device__ __forceinline__ int gsum3(int v, int ga) {
+    const uint32_t s = wave_scan((uint32_t)v);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(ga + 4 * (G3 - 1), (int)s);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(ga, (int)(s - (uint32_t)v));
+    return (int)(e - b);
+}
+// group_sums_f32 / group_sums_f32_fast / group_sum_f32 over the 21-lane groups
+// (the packed lo halves stay below 2^16 over the whole wave: 63 * 1023)
+__device__ __forceinline__ void gsums_f32_3(int v0, int v1, float& f0, float& f1, int ga) {
+    const int h0 = gsum3(v0 >> 10, ga), h1 = gsum3(v1 >> 10, ga);
+    const uint32_t l = (uint32_t)gsum3((int)(((uint32_t)v0 & 1023u) | (((uint32_t)v1 & 1023u) << 16)), ga);
+    f0 = (float)__builtin_fma((double)h0, 1024.0, (double)(l & 0xffffu));
+    f1 = (float)__builtin_fma((double)h1, 1024.0, (double)(l >> 16));
+}
+constexpr int LIM3 = (int)((1u << 31) / G3);
+__device__ __forceinline__ void gsums_f32_fast3(int v0, int v1, float& f0, float& f1, int ga) {
+    const bool big = (v0 >= LIM3 || v0 <= -LIM3) || (v1 >= LIM3 || v1 <= -LIM3);
+    if (__builtin_amdgcn_ballot_w64(big) == 0) {
+        f0 = (float)gsum3(v0, ga);
+        f1 = (float)gsum3(v1, ga);
+    } else {
+        gsums_f32_3(v0, v1, f0, f1, ga);
+    }
+}
+__device__ __forceinline__ float gsum_f32_3(int v, int ga) {
+    const int h = gsum3(v >> 10, ga), l = gsum3(v & 1023, ga);
+    return (float)__builtin_fma((double)h, 1024.0, (double)l);
+}
+
+// fill_win by the wave's active lanes (the groups still on this level): the one
+// tile of the wave serves the groups in turn
+__device__ __forceinline__ void fill_win_active(uint32_t* win, const Plane& P, int W, int H, int x0, int y0,
+                                                int rows) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    const int n = __builtin_popcountll(ex);
+    const int first = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u));
+    wave_lds_sync();  // earlier reads of the tile are done
+#pragma unroll 1
+    for (int i = first; i < rows * WIN_DW; i += n) {
+        const int r = i >> 3, q = i & 7;
+        const int ro = P.o0 + refl(y0 + r, H) * P.pitch;
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(P.rs, ro + refl(x0 + 4 * q + b, W), 0, 0) << (8 * b);
+        win[i] = v;
+    }
+    wave_lds_sync();
+}
+
+// A lane's three units from its six source rows d[r] (bytes X .. X+11, X =
+// ipx + 7 seg - 1, of rows y0 - 1 + r, y0 = ipy + 3 rb): the Scharr rows at
+// window rows 3rb .. 3rb+3 are formed once each; unit j takes derivative rows j
+// (weights W0) and j+1 (W1), exactly as extract_unit does for one unit.  Each
+// finished unit goes to its LDS slot; the structure-tensor partials of the
+// three are summed into a11 / a12 / a22.
+__device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X, int y0, int W, int H,
+                                               bool interior, uint32_t W0, uint32_t W1, v4u* ust, int& a11,
+                                               int& a12, int& a22) {
+    constexpr int RNDV = 1 << (W_BITS - 6), RNDD = 1 << (W_BITS - 1);
+    uint32_t E[6][5];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) E[r][k] = bpair(d[r], 2 * k);
+    uint32_t cm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool lo = (unsigned)(X + 2 * k + 1) < (unsigned)W;
+        const bool hi = (unsigned)(X + 2 * k + 2) < (unsigned)W;
+        cm[k] = (lo ? 0xffffu : 0u) | (hi ? 0xffff0000u : 0u);
+    }
+    int iv[7], ix[7], iy[7];
+    a11 = a12 = a22 = 0;
+#pragma unroll
+    for (int dd = 0; dd < 4; ++dd) {
+        // derivative row dd (times 4, as extract_unit)
+        uint32_t T0[5], T1[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            T0[k] = pmad16(padd16(E[dd][k], E[dd + 2][k]), 12, pmul16(E[dd + 1][k], 40));
+            T1[k] = psub16(E[dd + 2][k], E[dd][k]);
+        }
+        uint32_t DX[4], DY[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            DX[k] = psub16(T0[k + 1], T0[k]);
+            DY[k] = pmad16(padd16(T1[k + 1], T1[k]), 12, pmul16(shift_pair(T1[k], T1[k + 1]), 40));
+        }
+        if (!interior) {
+            const bool row_in = (unsigned)(y0 + dd) < (unsigned)H;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t m = row_in ? cm[k] : 0u;
+                DX[k] &= m;
+                DY[k] &= m;
+            }
+        }
+        // both output rows that use derivative row dd read I from source row dd+1
+#pragma unroll
+        for (int rr = 1; rr >= 0; --rr) {
+            // rr = 1: the second half of unit dd-1 (W1); rr = 0: the first half of unit dd (W0)
+            if (rr == 1 && dd == 0) continue;
+            if (rr == 0 && dd == 3) continue;
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                const int k = t >> 1;
+                const uint32_t pv = (t & 1) ? E[dd + 1][k + 1] : bpair(d[dd + 1], t + 1);
+                const uint32_t px = (t & 1) ? shift_pair(DX[k], DX[k + 1]) : DX[k];
+                const uint32_t py = (t & 1) ? shift_pair(DY[k], DY[k + 1]) : DY[k];
+                if (rr == 0) {
+                    iv[t] = dot2k(pv, W0, RNDV);
+                    ix[t] = dot2k(px, W0, 4 * RNDD);
+                    iy[t] = dot2k(py, W0, 4 * RNDD);
+                } else {
+                    iv[t] = dot2(pv, W1, iv[t]);
+                    ix[t] = dot2(px, W1, ix[t]);
+                    iy[t] = dot2(py, W1, iy[t]);
+                }
+            }
+            if (rr == 1) {
+                // unit dd-1 is complete
+                Unit u;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int h = 2 * k + 1 < 7 ? 2 * k + 1 : 0;
+                    u.iv[k] = pack16(iv[2 * k] >> (W_BITS - 5), 2 * k + 1 < 7 ? iv[h] >> (W_BITS - 5) : 0);
+                    u.ix[k] = 2 * k + 1 < 7 ? __builtin_amdgcn_perm((uint32_t)ix[h], (uint32_t)ix[2 * k], 0x07060302u)
+                                            : __builtin_amdgcn_perm(0u, (uint32_t)ix[2 * k], 0x07060302u);
+                    u.iy[k] = 2 * k + 1 < 7 ? __builtin_amdgcn_perm((uint32_t)iy[h], (uint32_t)iy[2 * k], 0x07060302u)
+                                            : __builtin_amdgcn_perm(0u, (uint32_t)iy[2 * k], 0x07060302u);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    a11 = dot2(u.ix[k], u.ix[k], a11);
+                    a12 = dot2(u.ix[k], u.iy[k], a12);
+                    a22 = dot2(u.iy[k], u.iy[k], a22);
+                }
+                unit_put(ust, dd - 1, u);
+            }
+        }
+    }
+}
+
+// lk_group for three points per wave (exact order only): the same algorithm and
+// the same selects, with the units, rows and sums of the triple layout.
+__device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
+                                          const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
+                                          float p0y, float& nx, float& ny, int& status, float& err, uint32_t* win,
+                                          v4u* units) {
+    int rb, seg, ga;
+    {
+        const int lane = lane_v(), g = grp3(lane), gl = min(lane - G3 * g, G3 - 1);  // lane 63 shadows lane 62
+        rb = gl / 3;
+        seg = gl - 3 * rb;
+        ga = 4 * G3 * g;
+    }
+    v4u* ust = units + lane_v();
+    const float halfw = (float)((WIN - 1) * 0.5f);
+    const int max_level = lay.nlev - 1;
+    status = 1;
+    err = 0.f;
+    for (int l = max_level; l >= 0; --l) {
+        const int W = lay.w[l], H = lay.h[l];
+        const bool raw = l == 0 && p0.raw;
+        const int pitch = l == 0 ? p0.pitch : lay.pitch[l];
+        const int o0 = l == 0 ? p0.o0 : PAD * pitch + PAD;
+        const Plane PI = make_plane(l == 0 ? p0.i : I + lay.off[l], o0, pitch);
+        const Plane PJ = make_plane(l == 0 ? p0.j : J + lay.off[l], o0, pitch);
+        const int lane_off = __mul24(3 * rb, pitch) + 7 * seg;
+        const float sc = ldexpf(1.f, -l);
+        float prevx = p0x * sc, prevy = p0y * sc;
+        float nextx, nexty;
+        if (l == max_level) {
+            if (cfg.use_initial_flow) {
+                nextx = nx * sc;
+                nexty = ny * sc;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = nx * 2.f;
+            nexty = ny * 2.f;
+        }
+        nx = nextx;
+        ny = nexty;
+        prevx -= halfw;
+        prevy -= halfw;
+        const float fpx = floorf(prevx), fpy = floorf(prevy);
+        const int ipx = (int)fpx, ipy = (int)fpy;
+        if (ipx < -WIN || ipx >= W || ipy < -WIN || ipy >= H) {
+            if (l == 0) {
+                status = 0;
+                err = 0.f;
+            }
+            continue;
+        }
+        uint32_t W0, W1;
+        weights(prevx - fpx, prevy - fpy, W0, W1);
+        int a11, a12, a22;
+        {
+            uint32_t d[6][3];
+            const bool fast = !raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H);
+            if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
+                const int off = lane_off + (PI.o0 + (ipy - 1) * PI.pitch + ipx - 1);
+                const int al = off & ~3;
+                const uint32_t sh = (uint32_t)off & 3u;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) brow<3>(PI, al, sh, r * PI.pitch, d[r]);
+            } else {
+                // a border window in the wave: every group's rows from the tile, one group at a time
+                // (d defined before the selects: a select against an undefined value may fold away)
+                const int g = grp3(lane_v());
+#pragma unroll
+                for (int r = 0; r < 6; ++r) d[r][0] = d[r][1] = d[r][2] = 0u;
+#pragma unroll
+                for (int gs = 0; gs < 3; ++gs) {
+                    if (__builtin_amdgcn_ballot_w64(g == gs) == 0) continue;  // group gs is off this level
+                    const int gx = __builtin_amdgcn_readlane(ipx, G3 * gs), gy = __builtin_amdgcn_readlane(ipy, G3 * gs);
+                    fill_win_active(win, PI, W, H, gx - 1, gy - 1, WIN + 3);
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) {
+                        uint32_t t[3];
+                        read_win<3>(win, 3 * rb + r, 7 * seg, t);
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) d[r][q] = g == gs ? t[q] : d[r][q];
+                    }
+                }
+            }
+            const bool interior = ipx >= 0 && ipx + WIN + 1 <= W && ipy >= 0 && ipy + WIN + 1 <= H;
+            extract_triple(d, ipx + 7 * seg - 1, ipy + 3 * rb, W, H, interior, W0, W1, ust, a11, a12, a22);
+        }
+        float A11, A12, A22;
+        {
+            const bool big = (a11 >= LIM3) || (a22 >= LIM3) || (a12 >= LIM3 || a12 <= -LIM3);  // a11, a22 >= 0
+            if (__builtin_amdgcn_ballot_w64(big) == 0) {
+                A11 = (float)gsum3(a11, ga);
+                A12 = (float)gsum3(a12, ga);
+                A22 = (float)gsum3(a22, ga);
+            } else {
+                gsums_f32_3(a11, a12, A11, A12, ga);
+                A22 = gsum_f32_3(a22, ga);
+            }
+        }
+        A11 *= FLT_SCALE;
+        A12 *= FLT_SCALE;
+        A22 *= FLT_SCALE;
+        float D = A11 * A22 - A12 * A12;
+        const float minEig =
+            __fdiv_rn(A22 + A11 - __fsqrt_rn((A11 - A22) * (A11 - A22) + 4.f * A12 * A12), (float)(2 * WIN * WIN));
+        if (minEig < cfg.min_eig || D < __FLT_EPSILON__) {
+            if (l == 0) {
+                status = 0;
+                err = 0.f;
+            }
+            continue;
+        }
+        D = __fdiv_rn(1.f, D);
+
+        nextx -= halfw;
+        nexty -= halfw;
+        float pdx = 0.f, pdy = 0.f;
+        int cinx = INT_MIN, ciny = INT_MIN;
+        uint32_t jr[4][4];  // the lane's four J rows as spread byte pairs
+        bool more = cfg.max_iter > 0;
+        int j = 0;
+        while (more) {
+            const float fnx = floorf(nextx), fny = floorf(nexty);
+            const int fxi = (int)fnx, fyi = (int)fny;
+            const int inx = min(max(fxi, -WIN), W - 1), iny = min(max(fyi, -WIN), H - 1);
+            const bool oob = inx != fxi || iny != fyi;  // the clamp moved it: off the level
+            uint32_t J0, J1;
+            weights(nextx - fnx, nexty - fny, J0, J1);
+            if (__builtin_amdgcn_ballot_w64(inx != cinx || iny != ciny)) {
+                const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+                if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
+                    const int off = lane_off + (PJ.o0 + iny * PJ.pitch + inx);
+                    const int al = off & ~3;
+                    const uint32_t sh = (uint32_t)off & 3u;
+                    v3u w[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) w[r] = __builtin_amdgcn_raw_buffer_load_b96(PJ.rs, al, r * PJ.pitch, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) spread_row(w[r].x, w[r].y, w[r].z, sh, jr[r]);
+                } else {
+                    const int g = grp3(lane_v());
+                    uint32_t nj[4][4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) nj[r][0] = nj[r][1] = nj[r][2] = nj[r][3] = 0u;
+#pragma unroll
+                    for (int gs = 0; gs < 3; ++gs) {
+                        if (__builtin_amdgcn_ballot_w64(g == gs) == 0) continue;
+                        const int gx = __builtin_amdgcn_readlane(inx, G3 * gs), gy = __builtin_amdgcn_readlane(iny, G3 * gs);
+                        fill_win_active(win, PJ, W, H, gx, gy, WIN + 1);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            uint32_t t[2], h[4];
+                            read_win<2>(win, 3 * rb + r, 7 * seg, t);
+                            spread_row2(t, h);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) nj[r][q] = g == gs ? h[q] : nj[r][q];
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) jr[r][q] = nj[r][q];
+                }
+                cinx = inx;
+                ciny = iny;
+            }
+            int b1 = 0, b2 = 0;
+            if (__builtin_amdgcn_ballot_w64((int)J1 < 0)) {
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    Unit u;
+                    unit_get(ust, s, u);
+                    match_unit_h<true>(u, jr[s], jr[s + 1], J0, J1, true, b1, b2);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    Unit u;
+                    unit_get(ust, s, u);
+                    match_unit_h<false>(u, jr[s], jr[s + 1], J0, J1, true, b1, b2);
+                }
+            }
+            float fb1, fb2;
+            gsums_f32_fast3(b1, b2, fb1, fb2, ga);
+            fb1 *= FLT_SCALE;
+            fb2 *= FLT_SCALE;
+            const float dx = (A12 * fb2 - A22 * fb1) * D;
+            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            const float tx = nextx + dx, ty = nexty + dy;
+            const bool conv = __builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps;
+            const bool osc = !conv && j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f;
+            const float ux = osc ? (tx + halfw) - dx * 0.5f : tx + halfw;
+            const float uy = osc ? (ty + halfw) - dy * 0.5f : ty + halfw;
+            nx = oob ? nx : ux;
+            ny = oob ? ny : uy;
+            nextx = oob ? nextx : tx;
+            nexty = oob ? nexty : ty;
+            status = (oob && l == 0) ? 0 : status;
+            pdx = dx;
+            pdy = dy;
+            more = !oob && !conv && !osc && ++j < cfg.max_iter;
+        }
+        if (status && l == 0) {
+            const float exf = nx - halfw, eyf = ny - halfw;
+            const float fex = floorf(exf), fey = floorf(eyf);
+            const int inx = (int)fex, iny = (int)fey;
+            if (inx < -WIN || inx >= W || iny < -WIN || iny >= H) {
+                status = 0;
+                continue;
+            }
+            if (!cfg.want_err) continue;
+            uint32_t J0, J1;
+            weights(exf - fex, eyf - fey, J0, J1);
+            int b1 = 0, b2 = 0, es = 0;
+            {
+                uint32_t r[4][2];
+                const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+                if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
+                    const int off = lane_off + (PJ.o0 + iny * PJ.pitch + inx);
+                    const int al = off & ~3;
+                    const uint32_t sh = (uint32_t)off & 3u;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) brow<2>(PJ, al, sh, q * PJ.pitch, r[q]);
+                } else {
+                    const int g = grp3(lane_v());
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) r[q][0] = r[q][1] = 0u;
+#pragma unroll
+                    for (int gs = 0; gs < 3; ++gs) {
+                        if (__builtin_amdgcn_ballot_w64(g == gs) == 0) continue;
+                        const int gx = __builtin_amdgcn_readlane(inx, G3 * gs), gy = __builtin_amdgcn_readlane(iny, G3 * gs);
+                        fill_win_active(win, PJ, W, H, gx, gy, WIN + 1);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            uint32_t t[2];
+                            read_win<2>(win, 3 * rb + q, 7 * seg, t);
+                            r[q][0] = g == gs ? t[0] : r[q][0];
+                            r[q][1] = g == gs ? t[1] : r[q][1];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    Unit u;
+                    unit_get(ust, s, u);
+                    match_unit<true, true>(u, r[s], r[s + 1], J0, J1, true, b1, b2, es);
+                }
+            }
+            err = __fdiv_rn((float)gsum3(es, ga) * 1.f, (float)(32 * WIN * WIN));
+        }
+    }
+}
+
 // One launch for a batch of pairs: PPW points per wavefront, the points of a
 // wave always from one pair (wave-uniform plane bases); ceil(n_pts / PPW)
 // waves per pair, the spare groups of a pair's last wave recompute its last
@@ -1044,14 +1466,20 @@ template <int PPW, int ACC>
 constexpr int klt_occupancy() {
     return PPW == 1 ? 4 : ACC ? 2 : 4;
 }
+// border tiles per wave: one per point group; the three-point layout shares one
+// (its groups take turns), so its LDS stays within 160 KB / 16 waves
+template <int PPW>
+constexpr int klt_tiles() {
+    return PPW == 3 ? 1 : PPW;
+}
 template <int PPW, int ACC>
 __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
                                                   const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
                                                   int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
                                                   float* __restrict__ next_xy, float* __restrict__ back_xy,
                                                   uint8_t* __restrict__ flags, float* __restrict__ err_out) {
-    constexpr int G = 64 / PPW;
-    __shared__ uint32_t wins[KLT_WPB * PPW][(WIN + 3) * WIN_DW];  // per-group border tiles
+    static_assert(PPW == 3 ? ACC == 0 : (PPW == 1 || PPW == 2), "three points per wave: exact order only");
+    __shared__ uint32_t wins[KLT_WPB * klt_tiles<PPW>()][(WIN + 3) * WIN_DW];  // border tiles
     __shared__ v4u units[KLT_WPB][3 * PPW * 64];                  // per-lane window values
     // fp32-order window sums: one region per point group
     __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC_FLOATS];
@@ -1068,11 +1496,20 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
     // the group's point (a spare group of a pair's last wave recomputes the last
     // point); rebuilt from the lane id where needed
     auto point = [&](bool& writer) -> int64_t {
-        const int lane = lane_v(), pt_raw = (wg - pair * wpp) * PPW + lane / G;
-        writer = pt_raw < npt && (lane & (G - 1)) == 0;
+        const int lane = lane_v();
+        int grp, gl;
+        if constexpr (PPW == 3) {
+            grp = grp3(lane);
+            gl = lane - G3 * grp;  // 21 on lane 63: no group's writer
+        } else {
+            grp = lane / (64 / PPW);
+            gl = lane & (64 / PPW - 1);
+        }
+        const int pt_raw = (wg - pair * wpp) * PPW + grp;
+        writer = pt_raw < npt && gl == 0;
         return (int64_t)pair * a.n_pts + (pt_raw < npt ? pt_raw : npt - 1);
     };
-    uint32_t(*wv_wins)[(WIN + 3) * WIN_DW] = wins + wv * PPW;
+    uint32_t(*wv_wins)[(WIN + 3) * WIN_DW] = wins + wv * klt_tiles<PPW>();
     v4u* wv_units = units[wv];
     float(*wv_accs)[ACC_FLOATS] = accs + (ACC ? wv * PPW : 0);
     const uint8_t* I = pyr_prev + pair * prev_stride;
@@ -1092,10 +1529,14 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
         nx = init_xy[2 * gp];
         ny = init_xy[2 * gp + 1];
         if constexpr (ACC != 0) {
+            constexpr int G = 64 / PPW;
             const int lane = lane_v();
             acc_clear<ACC, G>(wv_accs[lane / G], lane & (G - 1));
         }
-        lk_group<PPW, ACC>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, wv_wins, wv_units, wv_accs);
+        if constexpr (PPW == 3)
+            lk_group3(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, wv_wins[0], wv_units);
+        else
+            lk_group<PPW, ACC>(I, J, pf, lay, cfg, p0x, p0y, nx, ny, st, e, wv_wins, wv_units, wv_accs);
     }
     if (a.mode == 0) {
         gp = point(writer);
@@ -1118,7 +1559,10 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
     float e2 = 0.f;
     cfg.use_initial_flow = 1;
     cfg.want_err = 0;  // the backward error is not reported
-    lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, wv_wins, wv_units, wv_accs);
+    if constexpr (PPW == 3)
+        lk_group3(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, wv_wins[0], wv_units);
+    else
+        lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, wv_wins, wv_units, wv_accs);
     gp = point(writer);
     if (writer) {
         const float p0x = pxy[2 * gp], p0y = pxy[2 * gp + 1];
@@ -1174,6 +1618,11 @@ __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* 
 // the slowest wave (41 vs 54 us per frame), built for 4 waves per SIMD (no
 // spills; at most 4 waves per SIMD below the threshold: 36.8 -> 35.8 us per
 // sequence frame, 50.3 -> 49.0 us per pair, r02 v18).
+// KLT_PPW_BATCH 3: batches in the three-point layout (exact order only; the
+// fp32 orders keep two).
+#ifndef KLT_PPW_BATCH
+#define KLT_PPW_BATCH 3
+#endif
 static int klt_ppw(int64_t total_points) { return total_points <= 4096 ? 1 : 2; }
 
 template <int PPW, int ACC>
@@ -1195,6 +1644,9 @@ static void launch_klt_acc(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, c
     if (klt_ppw((int64_t)a.n_pairs * a.n_pts) == 1)
         launch_klt_ppw<1, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
                                next_xy, back_xy, flags, err);
+    else if (ACC == 0 && KLT_PPW_BATCH == 3)
+        launch_klt_ppw<3, 0>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                             next_xy, back_xy, flags, err);
     else
         launch_klt_ppw<2, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
                                next_xy, back_xy, flags, err);

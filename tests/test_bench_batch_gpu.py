@@ -3,8 +3,9 @@
 bench.py's step is one gvx_klt_fb_batch_init_dev over 256 synthetic pairs
 (bench.KltWorkload: synth.make_batch(256, ..., seed=synth.SEED, distinct=16),
 the predictions in their own buffer, tracked points to a separate one).  At
-38,400 / 128,000 points per launch that is the two-points-per-wave LK instance
-(klt.hip: more than 4,096 points -> PPW = 2) on the configs' own geometry.
+38,400 / 128,000 points per launch that is the batched LK instance (klt.hip:
+more than 4,096 points -> three points per wave in the exact order, two in the
+fp32 orders) on the configs' own geometry.
 Here the same object runs the same launch and sampled pairs are compared
 BIT-EXACT with the restatement (oracle.klt_fb, pyramids built once per image,
 as the batched path does) in the three window-sum orders: next, back, flags
@@ -50,7 +51,7 @@ def _assert_same(a, b, what):
 @pytest.mark.parametrize("mode", MODES)
 def test_bench_launch_bit_exact(ctx, orc, gvx_mod, w, h, n, L, mode):
     wl = _workload(w, h, n)
-    assert wl.n_pairs * n > 4096  # the two-points-per-wave instance
+    assert wl.n_pairs * n > 4096  # the batched (three / two points per wave) instance
     wl.N.fill_(np.nan)
     wl.NK.fill_(-1)
     wl.step(ctx, gvx_mod.KltParams.default(max_level=L, accum=mode))

@@ -194,11 +194,12 @@ def test_frame_put_dev_matches_host_put(ctx, gvx_mod):
     ctx.frame_drop(22)
 
 
-@pytest.mark.parametrize("n_pairs,n_pts", [(64, 149), (3, 2731)])
-def test_batch_two_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
-    """Launches of > 4096 points take the two-points-per-wave LK; odd point
-    counts leave a spare lane group in each pair's last wave.  Border points
-    included (the LDS tile gather runs per lane group)."""
+@pytest.mark.parametrize("n_pairs,n_pts", [(64, 149), (3, 2731), (30, 150)])
+def test_batch_three_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
+    """Launches of > 4096 points take the three-points-per-wave LK (the exact
+    order); point counts that are not multiples of 3 leave one or two spare
+    lane groups in each pair's last wave.  Border points included (the groups
+    take turns on the wave's LDS tile)."""
     w, h = 320, 140
     rng = np.random.default_rng(n_pairs + n_pts)
     I = np.stack([synth.make_image(w, h, rng) for _ in range(n_pairs)])
@@ -209,6 +210,28 @@ def test_batch_two_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
     init = (prev + rng.uniform(-1.0, 1.0, prev.shape)).astype(np.float32)
     g = ctx.klt_fb_batch(I, J, prev, init)
     for i in range(0, n_pairs, max(1, n_pairs // 8)):
+        o = orc.klt_fb(I[i], J[i], prev[i], init[i], reuse_pyramids=True)
+        _assert_same(g["next"][i], o["next"], f"pair {i} next")
+        _assert_same(g["back"][i], o["back"], f"pair {i} back")
+        flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
+        _assert_same(g["flags"][i], flags, f"pair {i} flags")
+        _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
+
+
+def test_batch_three_points_per_wave_configs1(ctx, orc, gvx_mod):
+    """configs[1] geometry (1280x560, 150 points, 3 levels) in a batch that takes
+    the three-point layout, with border points at level 0 (read in place) in
+    every pair: forward, backward, flags and kept indices bit-exact."""
+    P, W, H, N = 30, 1280, 560, 150
+    rng = np.random.default_rng(20261018)
+    I = np.stack([synth.make_image(W, H, rng) for _ in range(P)])
+    J = np.stack([np.roll(I[i], (2, -1), axis=(0, 1)) for i in range(P)])
+    prev = np.stack([np.concatenate([_border_points(W, H, 30, rng),
+                                     rng.uniform([0, 0], [W, H], (N - 30, 2)).astype(np.float32)])
+                     for _ in range(P)])
+    init = (prev + rng.uniform(-2.0, 2.0, prev.shape)).astype(np.float32)
+    g = ctx.klt_fb_batch(I, J, prev, init)
+    for i in (0, 13, P - 1):
         o = orc.klt_fb(I[i], J[i], prev[i], init[i], reuse_pyramids=True)
         _assert_same(g["next"][i], o["next"], f"pair {i} next")
         _assert_same(g["back"][i], o["back"], f"pair {i} back")
