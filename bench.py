@@ -523,6 +523,14 @@ def main():
                          "traffic": round(tr["bytes_per_step"]) if tr else None,
                          "traffic_unit": "HBM bytes per step (PMC 2*FETCH_SIZE+WRITE_SIZE)",
                          "traffic_source": tr["source"] if tr else None,
+                         "convention": ("effective bandwidth (SURVEY 8d): B counts the int16x2 Scharr planes "
+                                        "written and read; this build forms Scharr in registers and never "
+                                        "stores them, so frac passes 1 above 454 k pairs/s; measured_frac is "
+                                        "the PMC traffic over the same span"),
+                         "measured_gbs": round(tr["bytes_per_step"] / (span_ms * 1e-3) / 1e9, 1)
+                         if tr and span_ms > 0 else None,
+                         "measured_frac": round(tr["bytes_per_step"] / (span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if tr and span_ms > 0 else None,
                          "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()},
                          "overlap": pipelined},

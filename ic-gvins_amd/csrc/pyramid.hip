@@ -78,25 +78,39 @@ __global__ void __launch_bounds__(256) level0_kernel(const uint8_t* __restrict__
 // start inside its first dword, 0 or 2).
 template <int SH>
 __device__ __forceinline__ uint2 hsum4(const uint32_t* row, int g) {
+    static_assert(SH == 0 || SH == 2, "row starts at byte 0 or 2 of its first dword");
     const uint32_t* p = row + 2 * g;
     const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
-    uint32_t d0, d1, d2;
-    if (SH == 0) {
-        d0 = w0;
-        d1 = w1;
-        d2 = w2;
+    constexpr uint32_t K = 0x04060401u;  // taps 1 4 6 4 on bytes 0..3, the fifth tap added
+    uint32_t a0, a1, a2, a3, t0, t1, t2, t3;  // the four outputs' first four bytes and fifth byte
+    if constexpr (SH == 0) {
+        // outputs read bytes 0..4, 2..6, 4..8, 6..10
+        a0 = w0;
+        a1 = __builtin_amdgcn_alignbyte(w1, w0, 2);
+        a2 = w1;
+        a3 = __builtin_amdgcn_alignbyte(w2, w1, 2);
+        t0 = w1 & 0xffu;
+        t1 = (w1 >> 16) & 0xffu;
+        t2 = w2 & 0xffu;
+        t3 = (w2 >> 16) & 0xffu;
     } else {
+        // outputs read bytes 2..6, 4..8, 6..10, 8..12: the odd outputs' windows are
+        // whole loaded dwords, so only the even ones realign (2 alignbytes a row,
+        // not 5)
         const uint32_t w3 = p[3];
-        d0 = __builtin_amdgcn_alignbyte(w1, w0, SH);
-        d1 = __builtin_amdgcn_alignbyte(w2, w1, SH);
-        d2 = __builtin_amdgcn_alignbyte(w3, w2, SH);
+        a0 = __builtin_amdgcn_alignbyte(w1, w0, 2);
+        a1 = w1;
+        a2 = __builtin_amdgcn_alignbyte(w2, w1, 2);
+        a3 = w2;
+        t0 = (w1 >> 16) & 0xffu;
+        t1 = w2 & 0xffu;
+        t2 = (w2 >> 16) & 0xffu;
+        t3 = w3 & 0xffu;
     }
-    constexpr uint32_t K = 0x04060401u;  // taps 1 4 6 4 on bytes 0..3
-    const uint32_t e1 = __builtin_amdgcn_alignbyte(d1, d0, 2), e3 = __builtin_amdgcn_alignbyte(d2, d1, 2);
-    const uint32_t o0 = __builtin_amdgcn_udot4(d0, K, d1 & 0xffu, false);
-    const uint32_t o1 = __builtin_amdgcn_udot4(e1, K, (d1 >> 16) & 0xffu, false);
-    const uint32_t o2 = __builtin_amdgcn_udot4(d1, K, d2 & 0xffu, false);
-    const uint32_t o3 = __builtin_amdgcn_udot4(e3, K, (d2 >> 16) & 0xffu, false);
+    const uint32_t o0 = __builtin_amdgcn_udot4(a0, K, t0, false);
+    const uint32_t o1 = __builtin_amdgcn_udot4(a1, K, t1, false);
+    const uint32_t o2 = __builtin_amdgcn_udot4(a2, K, t2, false);
+    const uint32_t o3 = __builtin_amdgcn_udot4(a3, K, t3, false);
     return make_uint2(o0 | (o1 << 16), o2 | (o3 << 16));
 }
 
@@ -215,9 +229,19 @@ __device__ __forceinline__ Gather make_gather(int x0, int w) {
 }
 __device__ __forceinline__ bool lane_in(uint64_t m) { return (m >> __lane_id()) & 1u; }
 // 16 source bytes of row y (REFLECT_101) for this lane
+// Interior strips load through a buffer view of the source whose base sits
+// SRC_BIAS bytes before pixel (0,0) (padded sources are read up to 20 bytes
+// left of it, in their ring): the lane's column is a fixed voffset and the row a
+// wave-uniform soffset, so a row load costs no VALU address arithmetic.
+constexpr int SRC_BIAS = 64;
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
 template <bool GATHER>
 __device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pitch, int h, int x, const Gather& g,
-                                           int y) {
+                                           int y, const __amdgpu_buffer_rsrc_t& srs) {
+    if constexpr (!GATHER) {
+        const v4u_t w = __builtin_amdgcn_raw_buffer_load_b128(srs, x + SRC_BIAS, refl(y, h) * pitch, 0);
+        return make_uint4(w.x, w.y, w.z, w.w);
+    }
     const uint8_t* row = S + (int64_t)refl(y, h) * pitch;
     if constexpr (GATHER) {
         const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x + g.dx);  // 4-byte aligned
@@ -344,6 +368,8 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     const int xs = src.raw ? x0 : min(x0, w0 + 16);
     Gather g{};
     if constexpr (GATHER) g = make_gather(x0, w0);
+    const __amdgpu_buffer_rsrc_t srs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(S - SRC_BIAS), (short)0, 0x7fffffff, 0x00020000);
     const bool own_lane = lane >= 2 && lane < 62;
     const int w1 = L.w[0], h1 = L.h[0], p1 = L.pitch[0];
     const int c1 = (ST_COLS / 2) * st;            // level-1 column of lane 2, byte 0
@@ -378,7 +404,7 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     uint2 hr[5];
     uint32_t g2[5] = {0, 0, 0, 0, 0}, g3[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16<GATHER>(S, sp, h0, xs, g, 2 * r1s - 2 + k));
+    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16<GATHER>(S, sp, h0, xs, g, 2 * r1s - 2 + k, srs));
     // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % RS;
     // they are fetched PF iterations ahead (2*PF rows x 1 KB in flight per wave).
     // PF = 4 at 4 waves per SIMD (99 VGPRs) measured 0.230 ms per 512 images
@@ -393,8 +419,8 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     uint4 pa[RS], pb[RS];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-        pa[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 1, ylast));
-        pb[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 2, ylast));
+        pa[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 1, ylast), srs);
+        pb[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 2, ylast), srs);
     }
     // Loads are issued unconditionally and stores branch only on wave-uniform
     // row conditions (rows of the band, mirrored ring rows): on gfx9 stores and
@@ -409,8 +435,8 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
         const int r1 = r1s + k;
         hr[3] = hsum_row(pa[slot]);
         hr[4] = hsum_row(pb[slot]);
-        pa[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 1, ylast));
-        pb[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 2, ylast));
+        pa[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 1, ylast), srs);
+        pb[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 2, ylast), srs);
         // level-1 row r1
         uint32_t l1 = hibytes(vsum2(hr[0].x, hr[1].x, hr[2].x, hr[3].x, hr[4].x),
                               vsum2(hr[0].y, hr[1].y, hr[2].y, hr[3].y, hr[4].y));
