@@ -1038,7 +1038,12 @@ constexpr int G3 = 21;
 __device__ __forceinline__ int grp3(int lane) { return lane < G3 ? 0 : lane < 2 * G3 ? 1 : 2; }
 
 // inclusive prefix sum over the wave, modulo 2^32 (DPP row shifts, then the row
-// broadcasts of lanes 15 and 31)
+// broadcasts of lanes 15 and 31).  Groups that have left the loop are disabled
+// lanes: a DPP read of a disabled lane is invalid, so the write is skipped and
+// the add takes `old` = 0.  Such lanes contribute nothing, and a group is a
+// contiguous run of lanes, so the difference gsum3 takes inside an active group
+// is exact whatever the other groups are doing (checked by a lane-level model
+// of the scan over random activity patterns).
 __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
