@@ -1106,6 +1106,24 @@ __device__ __forceinline__ void fill_win_active(uint32_t* win, const Plane& P, i
     wave_lds_sync();
 }
 
+// The J side of match_unit_h for unit slot s: b1 += sum J Ix, b2 += sum J Iy over
+// its pixels (the gradients read from the slot; I is not needed)
+template <bool SIGNED>
+__device__ __forceinline__ void match_grad_h(const v4u* ust, int s, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
+                                             uint32_t W0, uint32_t W1, int& b1, int& b2) {
+    const v4u gx = ust[(3 * s + 1) * 64], gy = ust[(3 * s + 2) * 64];
+    uint32_t jp[4];
+    if constexpr (SIGNED)
+        j_pairs_h_signed(h0, h1, W0, W1, jp);
+    else
+        j_pairs_h(h0, h1, W0, W1, jp);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        b1 = dot2(jp[k], gx[k], b1);
+        b2 = dot2(jp[k], gy[k], b2);
+    }
+}
+
 // A lane's three units from its six source rows d[r] (bytes X .. X+11, X =
 // ipx + 7 seg - 1, of rows y0 - 1 + r, y0 = ipy + 3 rb): the Scharr rows at
 // window rows 3rb .. 3rb+3 are formed once each; unit j takes derivative rows j
@@ -1114,7 +1132,7 @@ __device__ __forceinline__ void fill_win_active(uint32_t* win, const Plane& P, i
 // three are summed into a11 / a12 / a22.
 __device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X, int y0, int W, int H,
                                                bool interior, uint32_t W0, uint32_t W1, v4u* ust, int& a11,
-                                               int& a12, int& a22) {
+                                               int& a12, int& a22, int& c1, int& c2) {
     constexpr int RNDV = 1 << (W_BITS - 6), RNDD = 1 << (W_BITS - 1);
     uint32_t E[6][5];
 #pragma unroll
@@ -1130,6 +1148,7 @@ __device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X,
     }
     int iv[7], ix[7], iy[7];
     a11 = a12 = a22 = 0;
+    c1 = c2 = 0;
 #pragma unroll
     for (int dd = 0; dd < 4; ++dd) {
         // derivative row dd (times 4, as extract_unit)
@@ -1193,6 +1212,8 @@ __device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X,
                     a11 = dot2(u.ix[k], u.ix[k], a11);
                     a12 = dot2(u.ix[k], u.iy[k], a12);
                     a22 = dot2(u.iy[k], u.iy[k], a22);
+                    c1 = dot2(u.iv[k], u.ix[k], c1);
+                    c2 = dot2(u.iv[k], u.iy[k], c2);
                 }
                 unit_put(ust, dd - 1, u);
             }
@@ -1256,7 +1277,7 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
         }
         uint32_t W0, W1;
         weights(prevx - fpx, prevy - fpy, W0, W1);
-        int a11, a12, a22;
+        int a11, a12, a22, c1, c2;
         {
             uint32_t d[6][3];
             const bool fast = !raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H);
@@ -1287,7 +1308,7 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
                 }
             }
             const bool interior = ipx >= 0 && ipx + WIN + 1 <= W && ipy >= 0 && ipy + WIN + 1 <= H;
-            extract_triple(d, ipx + 7 * seg - 1, ipy + 3 * rb, W, H, interior, W0, W1, ust, a11, a12, a22);
+            extract_triple(d, ipx + 7 * seg - 1, ipy + 3 * rb, W, H, interior, W0, W1, ust, a11, a12, a22, c1, c2);
         }
         float A11, A12, A22;
         {
@@ -1368,21 +1389,16 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
                 cinx = inx;
                 ciny = iny;
             }
-            int b1 = 0, b2 = 0;
+            // b = sum (J - I) I' = sum J I' - sum I I': the second sum is the level's
+            // constant (c1, c2), so an iteration forms only the J products (exact
+            // integers either way; the lane partial is the same value)
+            int b1 = -c1, b2 = -c2;
             if (__builtin_amdgcn_ballot_w64((int)J1 < 0)) {
 #pragma unroll
-                for (int s = 0; s < 3; ++s) {
-                    Unit u;
-                    unit_get(ust, s, u);
-                    match_unit_h<true>(u, jr[s], jr[s + 1], J0, J1, true, b1, b2);
-                }
+                for (int s = 0; s < 3; ++s) match_grad_h<true>(ust, s, jr[s], jr[s + 1], J0, J1, b1, b2);
             } else {
 #pragma unroll
-                for (int s = 0; s < 3; ++s) {
-                    Unit u;
-                    unit_get(ust, s, u);
-                    match_unit_h<false>(u, jr[s], jr[s + 1], J0, J1, true, b1, b2);
-                }
+                for (int s = 0; s < 3; ++s) match_grad_h<false>(ust, s, jr[s], jr[s + 1], J0, J1, b1, b2);
             }
             float fb1, fb2;
             gsums_f32_fast3(b1, b2, fb1, fb2, ga);
