@@ -442,27 +442,22 @@ __device__ __forceinline__ void j_pairs_h_signed(const uint32_t (&h0)[4], const 
 #pragma unroll
     for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
 }
-// match_unit on spread rows (the exact iteration path)
+// the J side of match_unit_h: b1 += sum J Ix, b2 += sum J Iy (the I side is the
+// level's constant, subtracted once)
 template <bool SIGNED>
-__device__ __forceinline__ void match_unit_h(const Unit& u, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
-                                             uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2) {
+__device__ __forceinline__ void match_grad_u(const Unit& u, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
+                                             uint32_t W0, uint32_t W1, int& b1, int& b2) {
     uint32_t jp[4];
     if constexpr (SIGNED)
         j_pairs_h_signed(h0, h1, W0, W1, jp);
     else
         j_pairs_h(h0, h1, W0, W1, jp);
-    const uint32_t d0 = psub16(jp[0], u.iv[0]);
-    int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-        const uint32_t d = psub16(jp[k], u.iv[k]);
-        s1 = dot2(d, u.ix[k], s1);
-        s2 = dot2(d, u.iy[k], s2);
+    for (int k = 0; k < 4; ++k) {
+        b1 = dot2(jp[k], u.ix[k], b1);
+        b2 = dot2(jp[k], u.iy[k], b2);
     }
-    b1 += valid ? s1 : 0;
-    b2 += valid ? s2 : 0;
 }
-
 template <bool ERR, bool SIGNED = false>
 __device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
                                            uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
@@ -784,6 +779,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
         uint32_t W0, W1;
         weights(prevx - fpx, prevy - fpy, W0, W1);
         int a11 = 0, a12 = 0, a22 = 0;
+        int c1 = 0, c2 = 0;  // the exact order's per-level I side of b (see lk_group3)
         {
             const bool fast = !raw || (ipx >= 4 && ipx + 30 <= W && ipy >= 1 && ipy + 23 <= H);
             if (!fast) fill_win<G>(win, PI, W, H, ipx - 1, ipy - 1, WIN + 3, gl);
@@ -798,6 +794,13 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 a11 += t11;
                 a12 += t12;
                 a22 += t22;
+                if constexpr (ACC == 0) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {  // invalid units: Ix = Iy = 0
+                        c1 = dot2(u[s].iv[k], u[s].ix[k], c1);
+                        c2 = dot2(u[s].iv[k], u[s].iy[k], c2);
+                    }
+                }
                 if constexpr (PPW > 1) unit_put(ust, s, u[s]);  // one unit per lane: kept in registers
             }
         }
@@ -890,7 +893,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             const bool oob = inx != fxi || iny != fyi;  // the clamp moved it: off the level
             uint32_t J0, J1;
             weights(nextx - fnx, nexty - fny, J0, J1);
-            int b1 = 0, b2 = 0, es = 0;
+            int b1 = -c1, b2 = -c2;  // b = sum J I' - sum I I' (exact order; c = 0 otherwise)
             // reload decisions are wave-uniform (ballots): a group whose position did
             // not move reloads the same rows, and a border window of either group
             // sends both groups through their LDS tiles (the tile path is correct for
@@ -953,13 +956,13 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
                         if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                        match_unit_h<true>(u[s], jr0[s], jr1[s], J0, J1, true, b1, b2);  // invalid: Ix = Iy = 0
+                        match_grad_u<true>(u[s], jr0[s], jr1[s], J0, J1, b1, b2);  // invalid: Ix = Iy = 0
                     }
                 } else {
 #pragma unroll
                     for (int s = 0; s < U; ++s) {
                         if constexpr (PPW > 1) unit_get(ust, s, u[s]);
-                        match_unit_h<false>(u[s], jr0[s], jr1[s], J0, J1, true, b1, b2);
+                        match_grad_u<false>(u[s], jr0[s], jr1[s], J0, J1, b1, b2);
                     }
                 }
                 group_sums_f32_fast<G>(b1, b2, fb1, fb2);
