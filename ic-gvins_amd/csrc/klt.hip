@@ -801,7 +801,9 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                         c2 = dot2(u[s].iv[k], u[s].iy[k], c2);
                     }
                 }
-                if constexpr (PPW > 1) unit_put(ust, s, u[s]);  // one unit per lane: kept in registers
+                // one unit per lane, or the fp32 orders (their occupancy is set by LDS, not
+                // registers): kept in registers
+                if constexpr (PPW > 1 && ACC == 0) unit_put(ust, s, u[s]);
             }
         }
         float A11, A12, A22;
@@ -970,7 +972,6 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 wave_lds_sync();  // the previous readers of the region are done
 #pragma unroll
                 for (int s = 0; s < U; ++s) {
-                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
                     float p1[7], p2[7];
                     match_unit_f32(u[s], jr0[s], jr1[s], J0, J1, p1, p2);
                     if (u[s].valid) {
@@ -1022,7 +1023,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                 for (int s = 0; s < U; ++s) {
                     uint32_t r0[2], r1[2];
                     load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
-                    if constexpr (PPW > 1) unit_get(ust, s, u[s]);
+                    if constexpr (PPW > 1 && ACC == 0) unit_get(ust, s, u[s]);
                     match_unit<true, true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
                 }
             }
@@ -1484,11 +1485,16 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
 #ifndef KLT_WPB
 #define KLT_WPB 1
 #endif
-// minimum waves per SIMD the register allocation must allow
-// (the fp32-order instances are LDS-limited: 16 KB per two-point wave)
+// minimum waves per SIMD the register allocation must allow.  The fp32-order
+// instances are bound by their chains' latency, so by occupancy: their units stay
+// in registers (10 KB of LDS per two-point wave instead of 16), for 3 waves per
+// SIMD instead of 2
+#ifndef KLT_ACC_OCC
+#define KLT_ACC_OCC 3
+#endif
 template <int PPW, int ACC>
 constexpr int klt_occupancy() {
-    return PPW == 1 ? 4 : ACC ? 2 : 4;
+    return PPW == 1 ? 4 : ACC ? KLT_ACC_OCC : 4;
 }
 // border tiles per wave: one per point group; the three-point layout shares one
 // (its groups take turns), so its LDS stays within 160 KB / 16 waves
@@ -1504,7 +1510,7 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
                                                   uint8_t* __restrict__ flags, float* __restrict__ err_out) {
     static_assert(PPW == 3 ? ACC == 0 : (PPW == 1 || PPW == 2), "three points per wave: exact order only");
     __shared__ uint32_t wins[KLT_WPB * klt_tiles<PPW>()][(WIN + 3) * WIN_DW];  // border tiles
-    __shared__ v4u units[KLT_WPB][3 * PPW * 64];                  // per-lane window values
+    __shared__ v4u units[KLT_WPB][ACC ? 1 : 3 * PPW * 64];        // per-lane window values (exact order)
     // fp32-order window sums: one region per point group
     __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC_FLOATS];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
