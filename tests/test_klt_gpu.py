@@ -218,6 +218,29 @@ def test_batch_three_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
         _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
 
 
+def test_single_call_three_points_per_wave_with_err(ctx, orc, gvx_mod):
+    """One pair with more than 4,096 points takes the three-point layout through
+    gvx_calc_optical_flow_pyr_lk, whose level-0 error output is the layout's err
+    path (the batch calls never ask for it): next, status and err bit-exact."""
+    W, H, N = 640, 480, 4500
+    rng = np.random.default_rng(4500)
+    I = synth.make_image(W, H, rng)
+    J = np.roll(I, (2, -1), axis=(0, 1))
+    prev = np.concatenate([_border_points(W, H, 300, rng),
+                           rng.uniform([0, 0], [W, H], (N - 300, 2)).astype(np.float32)])
+    init = (prev + rng.uniform(-1.5, 1.5, prev.shape)).astype(np.float32)
+    p = gvx_mod.KltParams.default()
+    ctx.frame_put(41, I, p)
+    ctx.frame_put(42, J, p)
+    g_next, g_st, g_err = ctx.calc_optical_flow_pyr_lk(41, 42, prev, init, p)
+    o_next, o_st, o_err = orc.calc_optical_flow_pyr_lk(I, J, prev, init)
+    _assert_same(g_st, o_st, "status")
+    _assert_same(g_next, o_next, "next")
+    _assert_same(g_err, o_err, "err")
+    ctx.frame_drop(41)
+    ctx.frame_drop(42)
+
+
 def test_batch_three_points_per_wave_configs1(ctx, orc, gvx_mod):
     """configs[1] geometry (1280x560, 150 points, 3 levels) in a batch that takes
     the three-point layout, with border points at level 0 (read in place) in
