@@ -8,13 +8,17 @@
 //  * the Scharr derivative planes are never materialised: each window's
 //    derivative is computed in registers from the padded pyramid (zero outside
 //    the image, as OpenCV's BORDER_CONSTANT derivative padding);
-//  * one point per 64-lane wavefront: lane k < 63 owns the 7-pixel "unit"
-//    (window row k/3, segment k%3) of the 21x21 window; window rows are read
-//    with aligned dword loads and realigned with v_alignbyte;
+//  * the 21x21 window is 63 seven-pixel "units" (window row k/3, segment k%3):
+//    one point per 64-lane wavefront (lane k owns unit k) for launches of up to
+//    4,096 points, three per wave for larger ones in the exact order (21 lanes a
+//    point, three vertically adjacent units a lane: lk_group3), two per wave in
+//    the fp32 orders; window rows are read with aligned dword loads and
+//    realigned with v_alignbyte;
 //  * window values are kept as packed int16 pairs and the bilinear weights,
 //    gradients and mismatch products run on v_dot2_i32_i16; every per-pixel
-//    quantity is an exact integer, and the window sums are exact 64-bit DPP
-//    wave reductions -- so the fp32 2x2 solve sees bit-identical inputs to
+//    quantity is an exact integer, and the window sums are exact (int32 DPP
+//    reductions, or a split fp64 route when a lane's partial could overflow) --
+//    so the fp32 2x2 solve sees bit-identical inputs to
 //    the CPU restatement (oracle/klt.c), whose LK outputs are matched bit-exactly.
 #include <hip/hip_runtime.h>
 
