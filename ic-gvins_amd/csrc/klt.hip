@@ -340,24 +340,12 @@ __device__ __forceinline__ void extract_unit(Unit& u, const uint32_t (&d)[4][3],
     a22 = u.valid ? s22 : 0;
 }
 
-// Mismatch of one unit against J at integer offset (jx, jy) with weights
-// (W0, W1): accumulates b1 += diff*Ix, b2 += diff*Iy (or es += |diff| for ERR).
-// r0 / r1: bytes jx+7*seg .. +7 of rows jy+row and jy+row+1.
-// Bytes (b[T], b[T+1]) of the 8-byte value {d1:d0} as the HIGH bytes of two
-// uint16 halves (b*256), for the unsigned dot2 below.
-template <int T>
-__device__ __forceinline__ uint32_t byte_pair_hi(uint32_t d0, uint32_t d1) {
-    return __builtin_amdgcn_perm(d1, d0, 0x000c000cu | ((uint32_t)T << 8) | ((uint32_t)(T + 1) << 24));
-}
-// The J window values of a unit as packed int16 pairs (pixel 2k, 2k+1; pair 3
-// high = 0): CV_DESCALE(w00 J00 + w01 J01 + w10 J10 + w11 J11, W_BITS - 5).
-// The sum runs on v_dot2_u32_u16 with the bytes scaled by 256 (b*256 <= 65280
-// and w <= 2^14 are uint16; X = 256 (sum + 2^8) < 2^30), so the value is X >> 17:
-// one v_perm takes the high halves of two pixels' X and one packed shift by 1
-// finishes both (2 operations per pixel pair instead of 2 shifts and a pack).
-// Only for w11 >= 0: w11 = 2^14 - w00 - w01 - w10 of three separately rounded
-// weights is -1 or -2 when a*b*2^14 is below ~1.5, and such iterations take
-// j_pairs_signed (the signed v_dot2_i32_i16 on plain bytes).
+// The J window values of a unit from its two raw J rows r0 / r1 (bytes
+// jx+7*seg .. +7 of rows jy+row and jy+row+1) as packed int16 pairs (pixel 2k,
+// 2k+1; pair 3 high = 0): CV_DESCALE(w00 J00 + w01 J01 + w10 J10 + w11 J11,
+// W_BITS - 5) on the signed v_dot2_i32_i16 (any w11, also the -1 / -2 that three
+// separately rounded weights can leave it at).  The iterations use the spread
+// rows below; this form serves the level-0 error.
 __device__ __forceinline__ void j_pairs_signed(const uint32_t (&r0)[2], const uint32_t (&r1)[2], uint32_t W0,
                                                uint32_t W1, uint32_t (&jp)[4]) {
     constexpr int RND = 1 << (W_BITS - 6);
@@ -375,34 +363,15 @@ __device__ __forceinline__ void j_pairs_signed(const uint32_t (&r0)[2], const ui
 #pragma unroll
     for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
 }
-__device__ __forceinline__ void j_pairs(const uint32_t (&r0)[2], const uint32_t (&r1)[2], uint32_t W0, uint32_t W1,
-                                        uint32_t (&jp)[4]) {
-    constexpr uint32_t RND = 1u << (W_BITS - 6 + 8);
-    uint32_t X[8];
-    X[0] = udot2(byte_pair_hi<0>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<0>(r0[0], r0[1]), W0, RND));
-    X[1] = udot2(byte_pair_hi<1>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<1>(r0[0], r0[1]), W0, RND));
-    X[2] = udot2(byte_pair_hi<2>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<2>(r0[0], r0[1]), W0, RND));
-    X[3] = udot2(byte_pair_hi<3>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<3>(r0[0], r0[1]), W0, RND));
-    X[4] = udot2(byte_pair_hi<4>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<4>(r0[0], r0[1]), W0, RND));
-    X[5] = udot2(byte_pair_hi<5>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<5>(r0[0], r0[1]), W0, RND));
-    X[6] = udot2(byte_pair_hi<6>(r1[0], r1[1]), W1, udot2k(byte_pair_hi<6>(r0[0], r0[1]), W0, RND));
-    X[7] = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t hi = __builtin_amdgcn_perm(X[2 * k + 1], X[2 * k], 0x07060302u);  // (X0 >> 16, X1 >> 16)
-        jp[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2us, hi) >> (unsigned short)1);
-    }
-}
-
 // A J row of a unit cached between iterations as its even byte pairs, each byte
 // times 128 in a uint16 half ("spread": h[k] = (b[2k], b[2k+1]) * 128, k = 0..3):
 // the even pairs of an iteration are then free and each odd pair is one
 // alignbit of two neighbours (3 operations a row, not 7 perms; the spread
 // itself is formed once per reload, by 4 perms with run-time selectors straight
 // from the loaded dwords and a packed shift).  Iterations mostly reuse the rows
-// (sub-pixel steps).  With the bytes at 128 (not 256) the bilinear sum
-// X = 128 (sum + 2^8) is exactly half of j_pairs' X, so the descaled value
-// (sum + 2^8) >> 9 is X >> 16: one perm takes it for two pixels, no shift.
+// (sub-pixel steps).  With the bytes at 128 the bilinear sum is
+// X = 128 (sum + 2^8), so the descaled value (sum + 2^8) >> 9 is X >> 16: one
+// perm takes it for two pixels, no shift (the unsigned v_dot2_u32_u16: w11 >= 0).
 __device__ __forceinline__ uint32_t spread_pair(const uint32_t (&h)[4], int t) {
     return (t & 1) ? shift_pair(h[t >> 1], h[(t >> 1) + 1]) : h[t >> 1];
 }
@@ -446,8 +415,8 @@ __device__ __forceinline__ void j_pairs_h_signed(const uint32_t (&h0)[4], const 
 #pragma unroll
     for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
 }
-// the J side of match_unit_h: b1 += sum J Ix, b2 += sum J Iy (the I side is the
-// level's constant, subtracted once)
+// an iteration's products of one unit: b1 += sum J Ix, b2 += sum J Iy (the I
+// side of b = sum (J - I) I' is the level's constant, subtracted once)
 template <bool SIGNED>
 __device__ __forceinline__ void match_grad_u(const Unit& u, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
                                              uint32_t W0, uint32_t W1, int& b1, int& b2) {
@@ -462,38 +431,22 @@ __device__ __forceinline__ void match_grad_u(const Unit& u, const uint32_t (&h0)
         b2 = dot2(jp[k], u.iy[k], b2);
     }
 }
-template <bool ERR, bool SIGNED = false>
-__device__ __forceinline__ void match_unit(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
-                                           uint32_t W0, uint32_t W1, bool valid, int& b1, int& b2, int& es) {
+// the level-0 error's part of one unit: es += sum |J - I| over its pixels
+__device__ __forceinline__ void unit_abs_err(const Unit& u, const uint32_t (&r0)[2], const uint32_t (&r1)[2],
+                                             uint32_t W0, uint32_t W1, bool valid, int& es) {
     uint32_t jp[4];
-    if constexpr (SIGNED)
-        j_pairs_signed(r0, r1, W0, W1, jp);
-    else
-        j_pairs(r0, r1, W0, W1, jp);
-    if (ERR) {
-        int e = 0;
+    j_pairs_signed(r0, r1, W0, W1, jp);
+    int e = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t d = psub16(jp[k], u.iv[k]);  // diff pair
-            const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
-            e += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
-        }
-        es += valid ? e : 0;
-    } else {
-        const uint32_t d0 = psub16(jp[0], u.iv[0]);
-        int s1 = dot2k(d0, u.ix[0], 0), s2 = dot2k(d0, u.iy[0], 0);
-#pragma unroll
-        for (int k = 1; k < 4; ++k) {
-            const uint32_t d = psub16(jp[k], u.iv[k]);
-            s1 = dot2(d, u.ix[k], s1);
-            s2 = dot2(d, u.iy[k], s2);
-        }
-        b1 += valid ? s1 : 0;
-        b2 += valid ? s2 : 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t d = psub16(jp[k], u.iv[k]);  // diff pair
+        const int dlo = (int)(short)(d & 0xffff), dhi = (int)(short)(d >> 16);
+        e += (dlo < 0 ? -dlo : dlo) + (k < 3 ? (dhi < 0 ? -dhi : dhi) : 0);
     }
+    es += valid ? e : 0;
 }
 
-// match_unit's products for the fp32 orders: p1[t] = (float)(diff*Ix),
+// a unit's products for the fp32 orders: p1[t] = (float)(diff*Ix),
 // p2[t] = (float)(diff*Iy) of the unit's 7 pixels (OpenCV converts the int32
 // products, `ib1 += (itemtype)(diff*dIptr[0])`; |diff*Ix| < 2^25, round to
 // nearest even like the CPU's int -> float conversion).
@@ -1019,7 +972,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
             if (!cfg.want_err) continue;
             uint32_t J0, J1;
             weights(exf - fex, eyf - fey, J0, J1);
-            int b1 = 0, b2 = 0, es = 0;
+            int es = 0;
             {
                 const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
                 if (!fast) fill_win<G>(win, PJ, W, H, inx, iny, WIN + 1, gl);
@@ -1028,7 +981,7 @@ __device__ __forceinline__ void lk_group(const uint8_t* __restrict__ I, const ui
                     uint32_t r0[2], r1[2];
                     load_j_unit(u[s], PJ, lane_off[s], inx, iny, fast, win, r0, r1);
                     if constexpr (PPW > 1 && ACC == 0) unit_get(ust, s, u[s]);
-                    match_unit<true, true>(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, b1, b2, es);
+                    unit_abs_err(u[s], r0, r1, J0, J1, s < U - 1 || u[s].valid, es);
                 }
             }
             err = __fdiv_rn((float)group_sum<G>(es) * 1.f, (float)(32 * WIN * WIN));
@@ -1439,7 +1392,7 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
             if (!cfg.want_err) continue;
             uint32_t J0, J1;
             weights(exf - fex, eyf - fey, J0, J1);
-            int b1 = 0, b2 = 0, es = 0;
+            int es = 0;
             {
                 uint32_t r[4][2];
                 const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
@@ -1471,7 +1424,7 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
                 for (int s = 0; s < 3; ++s) {
                     Unit u;
                     unit_get(ust, s, u);
-                    match_unit<true, true>(u, r[s], r[s + 1], J0, J1, true, b1, b2, es);
+                    unit_abs_err(u, r[s], r[s + 1], J0, J1, true, es);
                 }
             }
             err = __fdiv_rn((float)gsum3(es, ga) * 1.f, (float)(32 * WIN * WIN));
