@@ -90,6 +90,22 @@ def algorithmic_bytes(w, h, levels, n):
     return 2 * a0 + 4 * ap + 16 * (a0 + ap) + 58 * n
 
 
+def min_bytes(w, h, levels, n):
+    """The bytes this design must move per frame pair: read I and
+    J once, write and read both pyramids' levels >= 1, the point I/O --
+    B_min = 2*A0 + 4*Ap + 58*N (SURVEY 8d's B without the Scharr planes, which
+    this build forms in registers and never stores)."""
+    return algorithmic_bytes(w, h, levels, n) - 16 * (w * h + pyramid_area(w, h, levels))
+
+
+def pyramid_area(w, h, levels):
+    ap = 0
+    for _ in range(levels):
+        w, h = (w + 1) // 2, (h + 1) // 2
+        ap += w * h
+    return ap
+
+
 def cpu_baseline(w, h, n, level, budget_s=12.0, threads=1, reuse=False, clahe=False, pair_workers=0):
     """Oracle (C restatement) on the reference's 4-call pattern (each
     calcOpticalFlowPyrLK rebuilds both pyramids; LK points split over `threads`
@@ -408,10 +424,11 @@ def main():
     # headline's W warm-up steps means the headline is timed at the shader clock
     # a running tracker sees, not during the clock's ramp from idle.
     t_side = time.perf_counter()
-    accum_cost = accum_leg(ctx, step, gvx, L, steps=max(5, args.steps // 4)) if world == 1 and not args.no_pre \
-        else None
-    pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if not args.no_pre else None
+    legs = side_legs_before_headline(args)
+    accum_cost = accum_leg(ctx, step, gvx, L, steps=max(5, args.steps // 4)) if "lk_accum" in legs else None
+    pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if "preprocess" in legs else None
     t_side = time.perf_counter() - t_side
+    side_ranks = ranks_that_ran(accum_cost is not None, dist, dev)
     pipelined = args.overlap
     wl.run(ctx, params, args.warmup, pipelined, collect)
     ctx.sync()
@@ -472,10 +489,16 @@ def main():
     value = total_pairs / elapsed
     ms_step = elapsed / args.steps * 1e3
     B = algorithmic_bytes(W, H, L, N)
+    Bmin = min_bytes(W, H, L, N)
     span_ms = ev0.elapsed_time(ev1) / args.steps  # device span per step (all kernels, overlap included)
-    achieved = B * Pn / (span_ms * 1e-3) / 1e9 if span_ms > 0 else None
     workload = f"klt_fb_batch {Pn}x{W}x{H} N{N} L{L}"
     tr = traffic_for(workload)
+    # roofline.achieved / frac: the HBM bytes the step really moves (PMC traffic of
+    # this workload, profiles/pmc_traffic.json) over the device span; without a
+    # matching PMC record, B_min (the bytes this design must move) stands in
+    gbs = (lambda nbytes: nbytes / (span_ms * 1e-3) / 1e9) if span_ms > 0 else (lambda nbytes: None)
+    achieved = gbs(tr["bytes_per_step"]) if tr else gbs(Bmin * Pn)
+    frac = (lambda v: round(v / HBM_PEAK_GBS, 4) if v else None)
 
     if rank == 0:
         cpu = None
@@ -519,18 +542,21 @@ def main():
                                     "klt pipeline (pyramid pass + LK/FB + compaction) per step"),
                          "device_span_ms_per_step": round(span_ms, 4),
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "unit": "GB/s", "frac": frac(achieved),
+                         "achieved_basis": ("measured: PMC HBM bytes per step (traffic) / device span" if tr else
+                                            "B_min per step / device span (no PMC record for this workload)"),
                          "traffic": round(tr["bytes_per_step"]) if tr else None,
                          "traffic_unit": "HBM bytes per step (PMC 2*FETCH_SIZE+WRITE_SIZE)",
                          "traffic_source": tr["source"] if tr else None,
-                         "convention": ("effective bandwidth (SURVEY 8d): B counts the int16x2 Scharr planes "
-                                        "written and read; this build forms Scharr in registers and never "
-                                        "stores them, so frac passes 1 above 454 k pairs/s; measured_frac is "
-                                        "the PMC traffic over the same span"),
-                         "measured_gbs": round(tr["bytes_per_step"] / (span_ms * 1e-3) / 1e9, 1)
-                         if tr and span_ms > 0 else None,
-                         "measured_frac": round(tr["bytes_per_step"] / (span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                         if tr and span_ms > 0 else None,
+                         "traffic_commit": tr.get("commit") if tr else None,
+                         "min_bytes_per_pair": Bmin,
+                         "frac_min": frac(gbs(Bmin * Pn)),
+                         "min_convention": "B_min = 2*A0 + 4*Ap + 58*N: I and J read once, pyramid levels "
+                                           "written and read, point I/O",
+                         "effective_frac": frac(gbs(B * Pn)),
+                         "effective_convention": ("SURVEY 8d's B, which counts int16x2 Scharr planes written and "
+                                                  "read; this build never stores them, so effective_frac passes 1 "
+                                                  "above 454 k pairs/s and is no roofline"),
                          "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()},
                          "overlap": pipelined},
@@ -539,6 +565,7 @@ def main():
             "lk_accum": args.accum,
             "lk_accum_cost": accum_cost,
             "side_legs_before_headline_s": round(t_side, 3),
+            "side_legs_before_headline_ranks": side_ranks,
             "preprocess": pre,
             "single_pair": single,
             "host_buffers": pcie,
@@ -1337,6 +1364,25 @@ def spawn_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def side_legs_before_headline(args):
+    """The side legs that run before the headline's W warm-up steps ramp the
+    shader clock: with 3 warm-up steps alone LK reads 0.50-0.55 ms
+    instead of 0.47.  They run at EVERY world size -- through r05 the LK leg ran
+    at N = 1 only, so the N > 1 points of the scaling curve were timed at a
+    colder clock."""
+    return [] if args.no_pre else ["lk_accum", "preprocess"]
+
+
+def ranks_that_ran(flag, dist, dev=None):
+    """How many ranks report `flag` true (an all-reduce; 1 or 0 without dist)."""
+    if not dist:
+        return int(bool(flag))
+    import torch
+    t = torch.tensor([int(bool(flag))], dtype=torch.int64, device=coll_device(dist, dev))
+    dist.all_reduce(t)
+    return int(t.item())
+
+
 def max_over_ranks(elapsed, dist, dev=None):
     if not dist:
         return elapsed
@@ -1361,6 +1407,10 @@ def mock_main(args):
         tdist.init_process_group(args.backend or "gloo")
         dist = tdist
     step_s = 0.002 * (1 + rank)  # ranks deliberately unequal: the max must win
+    legs = side_legs_before_headline(args)  # the same decision main() takes
+    for _ in legs:
+        time.sleep(step_s)
+    side_ranks = ranks_that_ran(bool(legs), dist)
     for _ in range(args.warmup):
         time.sleep(step_s)
     if dist:
@@ -1391,7 +1441,8 @@ def mock_main(args):
         line = {"metric": "mock", "value": world * args.pairs * args.steps / elapsed, "unit": "frames/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-                "scaling": "weak", "elapsed_s": elapsed, "gathered_ok": gathered_ok}
+                "scaling": "weak", "elapsed_s": elapsed, "gathered_ok": gathered_ok,
+                "side_legs_before_headline": legs, "side_legs_before_headline_ranks": side_ranks}
         if args.config != 5 and not args.no_sequence:
             line["sequence"] = {"metric": "mock sequence", "value": world * F / seq_el, "unit": "frames/s",
                                 "n_gpus": world, "steps": F, "frames_per_rank": F, "gathered_ranks": len(g),

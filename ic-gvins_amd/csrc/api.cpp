@@ -177,6 +177,12 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
         if (e && std::atoi(e) != 0) c->preint_path = GVX_PREINT_PATH_ONEPHASE;
         const char* f = std::getenv("GVX_FACTORSET_D2H");
         c->factorset_d2h = f && std::atoi(f) != 0;
+        // GVX_PROF_MARKERS=1: profiled launches bracketed by recorded events
+        // instead of events attached to the dispatch (the r05_m1 queue-abort A/B)
+        const char* m = std::getenv("GVX_PROF_MARKERS");
+        c->prof_markers = m && std::atoi(m) != 0;
+        const char* k = std::getenv("GVX_KLT_LPP");
+        if (k) c->klt_lpp = std::max(0, std::atoi(k));
     }
     *out = c;
     return GVX_OK;
@@ -221,6 +227,14 @@ gvx_status gvx_sync(gvx_ctx* c) {
 }
 
 void* gvx_get_stream(gvx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+gvx_status gvx_set_klt_phases(gvx_ctx* c, int32_t levels_per_phase) {
+    if (!c) return GVX_ERR_INVALID;
+    if (levels_per_phase < 0 || levels_per_phase > gvx::MAX_LEVELS)
+        return set_err(c, GVX_ERR_INVALID, "levels per phase %d (0..%d)", levels_per_phase, gvx::MAX_LEVELS);
+    c->klt_lpp = levels_per_phase;
+    return GVX_OK;
+}
 
 gvx_status gvx_profile_enable(gvx_ctx* c, int32_t on) {
     if (!c) return GVX_ERR_INVALID;

@@ -450,6 +450,8 @@ gvx_status gvx_schur_solve_dev(gvx_ctx* c, int32_t n_fac, const int32_t* nres, c
                                double* d_S, int32_t* d_info) {
     if (!c) return GVX_ERR_INVALID;
     if (!d_delta || (n_fac && !d_data)) return set_err(c, GVX_ERR_INVALID, "null device pointer");
+    if (L > GVX_SCHUR_MAX_L)  // before any list or staging is sized
+        return set_err(c, GVX_ERR_UNSUPPORTED, "schur solve: %d parameters (max %d)", L, GVX_SCHUR_MAX_L);
     hipSetDevice(c->device);
     Lists ls;
     gvx_status s =
@@ -464,6 +466,8 @@ gvx_status gvx_schur_solve(gvx_ctx* c, int32_t n_fac, const int32_t* nres, const
                            const double* D, double* delta, double* S, int32_t* info) {
     if (!c) return GVX_ERR_INVALID;
     if (!delta || (n_fac && !data)) return set_err(c, GVX_ERR_INVALID, "null pointer");
+    if (L > GVX_SCHUR_MAX_L)  // before the r x r pinned / device staging is sized
+        return set_err(c, GVX_ERR_UNSUPPORTED, "schur solve: %d parameters (max %d)", L, GVX_SCHUR_MAX_L);
     hipSetDevice(c->device);
     Lists ls;
     gvx_status s =

@@ -105,6 +105,10 @@ struct gvx_ctx {
     } track_static;
     // profiling
     bool prof = false;
+    bool prof_markers = false;  // GVX_PROF_MARKERS=1 at creation (launch_timed)
+    // batch LK (three points per wave): levels per phase of klt_phase_kernel, 0 =
+    // one wave runs the whole chain (klt_kernel); GVX_KLT_LPP at creation
+    int klt_lpp = 1;
     std::map<std::string, gvx::ProfEntry> prof_acc;
     struct Pending {
         std::string fam;
@@ -144,7 +148,13 @@ hipError_t launch_timed(gvx_ctx* c, const char* fam, F kernel, dim3 grid, dim3 b
         return hipGetLastError();
     }
     hipEvent_t a = prof_event(c), b = prof_event(c);
-    hipExtLaunchKernelGGL(kernel, grid, block, shmem, c->stream, a, b, 0, args...);
+    if (c->prof_markers) {
+        hipEventRecord(a, c->stream);
+        hipLaunchKernelGGL(kernel, grid, block, shmem, c->stream, args...);
+        hipEventRecord(b, c->stream);
+    } else {
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, c->stream, a, b, 0, args...);
+    }
     const hipError_t e = hipGetLastError();
     prof_push(c, fam, a, b);
     return e;
@@ -168,6 +178,30 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
 // the contiguous logical range [k*per, (k+1)*per): neighbouring work (points of
 // one frame pair, adjacent image tiles) shares one L2.  The grid must hold
 // 8*per workgroups; logical ids >= n are idle.
+#ifdef GVX_KLT_TRACE
+// Diagnostic builds only (EXTRA=-DGVX_KLT_TRACE tools/variant.sh): a wave stores
+// {wave id, start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32} to
+// buf[4 * id] when it leaves (tools/lk_residency.py, tools/pyr_residency.py).
+// The product build compiles none of this.
+struct WaveStamp {
+    uint64_t* buf;
+    uint64_t t0;
+    __device__ explicit WaveStamp(uint64_t* b) : buf(b) { t0 = __builtin_amdgcn_s_memrealtime(); }
+    __device__ ~WaveStamp() {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+        if (buf && (threadIdx.x & 63) == 0) {
+            const uint64_t id = (uint64_t)blockIdx.x * blockDim.x / 64 + (threadIdx.x >> 6);
+            buf[4 * id] = id;
+            buf[4 * id + 1] = t0;
+            buf[4 * id + 2] = t1;
+            buf[4 * id + 3] = (uint64_t)hw | ((uint64_t)xcc << 32);
+        }
+    }
+};
+#endif
+
 constexpr int N_XCD = 8;
 __host__ __device__ inline int xcd_per(int n) { return (n + N_XCD - 1) / N_XCD; }
 __device__ inline int xcd_swizzle(int b, int n) { return (b % N_XCD) * xcd_per(n) + b / N_XCD; }

@@ -1184,10 +1184,19 @@ __device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X,
 
 // lk_group for three points per wave (exact order only): the same algorithm and
 // the same selects, with the units, rows and sums of the triple layout.
+// klt_phase_kernel: the flow a phase starts from arrives from the previous
+// phase's wave; `resolve(nx, ny)` supplies it before the first level.  (Resolving
+// it after the top level's extraction, to hide the load behind the extraction's
+// own, costs 5 spilled VGPRs at 128.)  A whole-chain call resolves nothing.
+struct NoResolve {
+    __device__ void operator()(float&, float&) const {}
+};
+template <typename Resolve = NoResolve>
 __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const uint8_t* __restrict__ J,
                                           const L0Planes& p0, const PyrLayout& lay, const LkCfg& cfg, float p0x,
                                           float p0y, float& nx, float& ny, int& status, float& err, uint32_t* win,
-                                          v4u* units) {
+                                          v4u* units, int l_top = 99, int l_bot = 0,
+                                          const Resolve& resolve = Resolve()) {
     int rb, seg, ga;
     {
         const int lane = lane_v(), g = grp3(lane), gl = min(lane - G3 * g, G3 - 1);  // lane 63 shadows lane 62
@@ -1198,9 +1207,12 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
     v4u* ust = units + lane_v();
     const float halfw = (float)((WIN - 1) * 0.5f);
     const int max_level = lay.nlev - 1;
-    status = 1;
+    status = 1;  // only level 0 clears it: a phase of levels > 0 (klt_phase_kernel) leaves it
     err = 0.f;
-    for (int l = max_level; l >= 0; --l) {
+    // levels l_top .. l_bot (the whole pyramid by default); nx, ny carry the
+    // flow between levels, in level-(l+1) pixels when l_top < max_level
+    resolve(nx, ny);
+    for (int l = min(l_top, max_level); l >= l_bot; --l) {
         const int W = lay.w[l], H = lay.h[l];
         const bool raw = l == 0 && p0.raw;
         const int pitch = l == 0 ? p0.pitch : lay.pitch[l];
@@ -1209,22 +1221,27 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
         const Plane PJ = make_plane(l == 0 ? p0.j : J + lay.off[l], o0, pitch);
         const int lane_off = __mul24(3 * rb, pitch) + 7 * seg;
         const float sc = ldexpf(1.f, -l);
-        float prevx = p0x * sc, prevy = p0y * sc;
+        const float psx = p0x * sc, psy = p0y * sc;
+        float prevx = psx, prevy = psy;
         float nextx, nexty;
-        if (l == max_level) {
-            if (cfg.use_initial_flow) {
-                nextx = nx * sc;
-                nexty = ny * sc;
+        // the level's starting flow (nx, ny become it)
+        auto start_flow = [&]() {
+            if (l == max_level) {
+                if (cfg.use_initial_flow) {
+                    nextx = nx * sc;
+                    nexty = ny * sc;
+                } else {
+                    nextx = psx;
+                    nexty = psy;
+                }
             } else {
-                nextx = prevx;
-                nexty = prevy;
+                nextx = nx * 2.f;
+                nexty = ny * 2.f;
             }
-        } else {
-            nextx = nx * 2.f;
-            nexty = ny * 2.f;
-        }
-        nx = nextx;
-        ny = nexty;
+            nx = nextx;
+            ny = nexty;
+        };
+        start_flow();
         prevx -= halfw;
         prevy -= halfw;
         const float fpx = floorf(prevx), fpy = floorf(prevy);
@@ -1459,6 +1476,15 @@ template <int PPW>
 constexpr int klt_tiles() {
     return PPW == 3 ? 1 : PPW;
 }
+#ifdef GVX_KLT_TRACE
+// Diagnostic build only (tools/lk_residency.py): every wave of the batch
+// layout stamps itself (gvx_internal.h WaveStamp) into gvx_klt_trace_buf.
+__device__ uint64_t* gvx_klt_trace_buf;
+#define KLT_WAVE_STAMP WaveStamp wave_stamp_(gvx_klt_trace_buf)
+#else
+#define KLT_WAVE_STAMP
+#endif
+
 template <int PPW, int ACC>
 __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
                                                   const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
@@ -1470,6 +1496,7 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
     __shared__ v4u units[KLT_WPB][ACC ? 1 : 3 * PPW * 64];        // per-lane window values (exact order)
     // fp32-order window sums: one region per point group
     __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC_FLOATS];
+    KLT_WAVE_STAMP;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair (launch capacity)
     const int n_waves = a.n_pairs * wpp;
@@ -1570,6 +1597,166 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
 }
 
 
+// ---- the batch LK as a chain of phases (r06) ----
+// klt_kernel runs a point group's whole chain -- forward levels L..0, then
+// backward L..0 -- in one wave of ~84 us.  Its launch ends in a drain: the last
+// waves start ~100 us before the end, and the SIMDs hold 1.5 waves on average
+// from then on, against 3.9 before (profiles/r06_d1/res: one configs[1] launch,
+// per-wave s_memrealtime stamps).  Here the chain is cut into phases of `lpp`
+// levels of one direction, each a wave of its own, dispatched phase-major: all
+// groups' phase 0, then all groups' phase 1, ...  The drain is then as long as
+// one phase.
+// Hand-off: every value a phase passes on is one 64-bit word, the float in the
+// low half and a tag (the phase that wrote it, plus one) in the high half,
+// stored and loaded as single-copy-atomic dwordx2 accesses.  A reader waits for
+// the tag it expects, so no ordering between words is needed and a wave ends
+// without waiting for its stores.  Per point (PH_WORDS words): the running flow
+// x, y; the forward result fx, fy and status.  The last phase sets every tag back
+// to 0, so a launch leaves the words as it found them (graph replays included).
+// Coherence: the dispatcher sends workgroup b to XCD b % 8 and a phase's block
+// count is a multiple of 8, so the phases of a group run on one XCD and meet in
+// its L2; the accesses are agent-scope relaxed atomics (sc1: past the CU's L1).
+// Progress: workgroups of one XCD are dispatched in id order, so a phase's
+// predecessor has been dispatched before it waits; the wait is also bounded
+// (2^22 polls, about a second), so a broken assumption shows as wrong results,
+// not a hang.
+constexpr int PH_WORDS = 8;  // per point: x, y, fx, fy, st (64 B)
+enum { PH_X = 0, PH_Y = 1, PH_FX = 2, PH_FY = 3, PH_ST = 4 };
+__device__ __forceinline__ uint64_t ph_ld(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ph_st(uint64_t* p, uint32_t tag, uint32_t bits) {
+    __hip_atomic_store(p, ((uint64_t)tag << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the words `a` and `b` as written by phase tag-1 (va, vb: their first loads)
+__device__ __forceinline__ void ph_wait2(const uint64_t* a, const uint64_t* b, uint64_t& va, uint64_t& vb,
+                                         uint32_t tag) {
+    int guard = 0;
+    while (((uint32_t)(va >> 32) != tag || (uint32_t)(vb >> 32) != tag) && ++guard < (1 << 22)) {
+        __builtin_amdgcn_s_sleep(4);
+        va = ph_ld(a);
+        vb = ph_ld(b);
+    }
+}
+struct PhResolve {  // lk_group3's hook: the running flow of the previous phase
+    const uint64_t* hs;
+    uint32_t gi;   // the point (a 32-bit index: one VGPR live across the chain)
+    uint32_t tag;  // 0: the phase starts the chain (nothing to wait for)
+    __device__ void operator()(float& x, float& y) const {
+        if (tag == 0) return;
+        const uint64_t* w = hs + (size_t)PH_WORDS * gi;
+        uint64_t a = ph_ld(w + PH_X), b = ph_ld(w + PH_Y);
+        ph_wait2(w + PH_X, w + PH_Y, a, b, tag);
+        x = __uint_as_float((uint32_t)a);
+        y = __uint_as_float((uint32_t)b);
+    }
+};
+
+__global__ void __launch_bounds__(64, 4) klt_phase_kernel(KltArgs a, PyrLayout lay, const uint8_t* __restrict__ pyr_prev,
+                                                          const uint8_t* __restrict__ pyr_next, int64_t prev_stride,
+                                                          int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
+                                                          float* next_xy, float* __restrict__ back_xy,
+                                                          uint8_t* __restrict__ flags, float* __restrict__ err_out,
+                                                          uint64_t* hs, int nbp, int lpp) {
+    __shared__ uint32_t win[(WIN + 3) * WIN_DW];  // border tile
+    __shared__ v4u units[3 * 3 * 64];             // per-lane window values
+    KLT_WAVE_STAMP;
+    const int wpp = (a.n_pts + 2) / 3;
+    const int n_groups = a.n_pairs * wpp;
+    const int ph = blockIdx.x / nbp;
+    const int wg = xcd_swizzle(blockIdx.x - ph * nbp, n_groups);
+    if (wg >= n_groups) return;
+    const int pair = wg / wpp;
+    const int npt = a.n_dev ? min(a.n_pts, *a.n_dev) : a.n_pts;
+    if ((wg - pair * wpp) * 3 >= npt) return;  // every phase of this group leaves here
+    const int pd = (lay.nlev + lpp - 1) / lpp;  // phases per direction
+    const bool bwd = ph >= pd;
+    const int c = bwd ? ph - pd : ph;
+    const int l_top = lay.nlev - 1 - c * lpp, l_bot = max(l_top - lpp + 1, 0);
+    const bool last = ph == (a.mode == 0 ? pd : 2 * pd) - 1;
+    const int lane = lane_v(), grp = grp3(lane), gl = lane - G3 * grp;
+    const int pt_raw = (wg - pair * wpp) * 3 + grp;
+    const bool writer = pt_raw < npt && gl == 0;
+    const int64_t gp = (int64_t)pair * a.n_pts + (pt_raw < npt ? pt_raw : npt - 1);
+    uint64_t* w = hs + PH_WORDS * gp;
+    // one LK call for either direction (one inlined copy of the chain): the
+    // backward call tracks the forward result back from J to I, from the
+    // original prev points as its initial flow
+    const uint8_t* Ip = pyr_prev + pair * prev_stride;
+    const uint8_t* Jp = pyr_next + pair * next_stride;
+    const uint8_t* l0i = l0.prev + pair * l0.prev_stride;
+    const uint8_t* l0j = l0.next + pair * l0.next_stride;
+    const L0Planes pl{bwd ? l0j : l0i, bwd ? l0i : l0j, l0.o0, l0.pitch, l0.raw != 0};
+    const LkCfg cfg{a.max_iter, a.crit_eps, a.min_eig, bwd ? 1 : a.use_initial_flow,
+                    !bwd && err_out != nullptr && l_bot == 0};
+    float px, py, nx, ny;
+    // the running flow of the previous phase, read where the chain needs it (PhResolve)
+    const PhResolve res{hs, (uint32_t)gp, ph > 0 && ph != pd ? (uint32_t)ph : 0u};
+    if (!bwd) {
+        px = prev_xy[2 * gp];
+        py = prev_xy[2 * gp + 1];
+        nx = ny = 0.f;
+        if (ph == 0) {
+            const float* init_xy = a.init_xy ? a.init_xy : next_xy;
+            nx = init_xy[2 * gp];
+            ny = init_xy[2 * gp + 1];
+        }
+    } else {
+        uint64_t fx = ph_ld(w + PH_FX), fy = ph_ld(w + PH_FY);
+        ph_wait2(w + PH_FX, w + PH_FY, fx, fy, (uint32_t)pd);
+        px = __uint_as_float((uint32_t)fx);
+        py = __uint_as_float((uint32_t)fy);
+        nx = prev_xy[2 * gp];
+        ny = prev_xy[2 * gp + 1];
+    }
+    int st = 1;
+    float e = 0.f;
+    lk_group3(bwd ? Jp : Ip, bwd ? Ip : Jp, pl, lay, cfg, px, py, nx, ny, st, e, win, units, l_top, l_bot, res);
+    if (!writer) return;
+    const int64_t gq = res.gi;  // gp again, from the one VGPR the chain kept
+    w = hs + (size_t)PH_WORDS * res.gi;
+    const uint32_t tag = (uint32_t)ph + 1;
+    if (!bwd && l_bot != 0) {
+        ph_st(w + PH_X, tag, __float_as_uint(nx));
+        ph_st(w + PH_Y, tag, __float_as_uint(ny));
+    } else if (!bwd) {  // the forward result
+        next_xy[2 * gq] = nx;
+        next_xy[2 * gq + 1] = ny;
+        if (err_out) err_out[gq] = e;
+        if (a.mode == 0) {
+            flags[gq] = (uint8_t)st;
+            ph_st(w + PH_X, 0, 0);  // the last phase: tags back to 0
+            ph_st(w + PH_Y, 0, 0);
+        } else {
+            ph_st(w + PH_FX, tag, __float_as_uint(nx));
+            ph_st(w + PH_FY, tag, __float_as_uint(ny));
+            ph_st(w + PH_ST, tag, (uint32_t)st);
+        }
+    } else if (!last) {
+        ph_st(w + PH_X, tag, __float_as_uint(nx));
+        ph_st(w + PH_Y, tag, __float_as_uint(ny));
+    } else {
+        // tracking.cc:396-408 / :831-849 on the forward result (px, py), the
+        // backward result (nx, ny) and the original prev points
+        uint64_t s1 = ph_ld(w + PH_ST), dummy = (uint64_t)pd << 32;
+        ph_wait2(w + PH_ST, w + PH_ST, s1, dummy, (uint32_t)pd);
+        const int st1 = (int)(uint32_t)s1;
+        const float p0x = prev_xy[2 * gq], p0y = prev_xy[2 * gq + 1];
+        const double B = a.border;
+        const bool on_border = px < B || py < B || px > (a.cam_w - B) || py > (a.cam_h - B);
+        const double ddx = (double)(nx - p0x), ddy = (double)(ny - p0y);
+        const double dist = __dsqrt_rn(ddx * ddx + ddy * ddy);
+        const bool keep = st1 && st && !on_border && dist < a.fb_thresh;
+        if (back_xy) {
+            back_xy[2 * gq] = nx;
+            back_xy[2 * gq + 1] = ny;
+        }
+        flags[gq] = (uint8_t)((st1 ? 1 : 0) | (st ? 2 : 0) | (keep ? 4 : 0));
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ph_st(w + k, 0, 0);  // tags back to 0
+    }
+}
+
 // reduceVector (tracking.cc:831-839): order-preserving index compaction of the
 // keep bit, one workgroup per pair.
 __global__ void __launch_bounds__(256) compact_kernel(int n_pts, const uint8_t* __restrict__ flags,
@@ -1623,6 +1810,38 @@ static void launch_klt_ppw(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, c
                  prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err);
 }
 
+// The batch LK as phases of c->klt_lpp levels (klt_phase_kernel); false when
+// the hand-off buffers cannot be had (a capture that would grow them): the
+// caller then runs the single-wave chain, which gives the same bits.
+static bool launch_klt_phases(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                              const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                              const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy,
+                              uint8_t* flags, float* err) {
+    const int lpp = c->klt_lpp;
+    if (lpp <= 0) return false;
+    const int n_groups = a.n_pairs * ((a.n_pts + 2) / 3);
+    // one set per stream: a launch on the branch stream must not share them
+    const std::string tag = c->stream == c->main ? "" : "_side";
+    const bool failed_before = c->capture_failed;
+    const std::string name = "klt_phase_state" + tag;
+    uint64_t* hs = (uint64_t*)scratch(c, name, sizeof(uint64_t) * PH_WORDS * (size_t)a.n_pairs * a.n_pts);
+    if (!hs) {
+        c->capture_failed = failed_before;  // not a failure: the fallback needs no buffer
+        return false;
+    }
+    DevBuf& db = c->dev[name];
+    if (db.fresh) {  // tags start at 0; every launch leaves them at 0
+        if (hipMemsetAsync(db.p, 0, db.bytes, c->stream) != hipSuccess) return false;
+        db.fresh = false;
+    }
+    const int nbp = N_XCD * xcd_per(n_groups);  // blocks per phase, a multiple of 8
+    const int pd = (lay.nlev + lpp - 1) / lpp;
+    const int n_ph = a.mode == 0 ? pd : 2 * pd;
+    launch_timed(c, "klt", klt_phase_kernel, dim3((unsigned)(n_ph * nbp)), dim3(64), 0, a, lay, pyr_prev, pyr_next,
+                 prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err, hs, nbp, lpp);
+    return true;
+}
+
 template <int ACC>
 static void launch_klt_acc(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const uint8_t* pyr_prev,
                            const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
@@ -1631,9 +1850,12 @@ static void launch_klt_acc(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, c
     if (klt_ppw((int64_t)a.n_pairs * a.n_pts) == 1)
         launch_klt_ppw<1, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
                                next_xy, back_xy, flags, err);
-    else if (ACC == 0 && KLT_PPW_BATCH == 3)
-        launch_klt_ppw<3, 0>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
-                             next_xy, back_xy, flags, err);
+    else if (ACC == 0 && KLT_PPW_BATCH == 3) {
+        if (!launch_klt_phases(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                               next_xy, back_xy, flags, err))
+            launch_klt_ppw<3, 0>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                                 next_xy, back_xy, flags, err);
+    }
     else
         launch_klt_ppw<2, ACC>(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
                                next_xy, back_xy, flags, err);
@@ -1672,3 +1894,11 @@ hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* fla
 }
 
 }  // namespace gvx
+
+#ifdef GVX_KLT_TRACE
+// diagnostic build only: the wave-stamp buffer of klt_kernel (4 uint64 per wave
+// of the launch; nullptr turns the stamps off)
+extern "C" int gvx_klt_trace_set(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(gvx::gvx_klt_trace_buf), &buf, sizeof(buf));
+}
+#endif

@@ -596,11 +596,18 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     if constexpr (SKIP != 0) *reinterpret_cast<uint32_t*>(tl) = nsink;
 }
 
+#ifdef GVX_KLT_TRACE
+__device__ uint64_t* gvx_pyr_trace_buf;  // diagnostic build only (tools/pyr_residency.py)
+#endif
+
 template <int NL, int SKIP = 0>
 __global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(StreamSrc src, uint8_t* __restrict__ pyr,
                                                                   int64_t pyr_bytes, DownLevels L, int n_strips,
                                                                   int n_bands, int n_units, int band,
                                                                   uint8_t* __restrict__ trash) {
+#ifdef GVX_KLT_TRACE
+    WaveStamp wave_stamp_(gvx_pyr_trace_buf);
+#endif
     const int lane = threadIdx.x & 63;
     const int nblk = (n_units + 3) / 4;
     const int unit = xcd_swizzle(blockIdx.x, nblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -836,3 +843,10 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
 }
 
 }  // namespace gvx
+
+#ifdef GVX_KLT_TRACE
+// diagnostic build only: the wave-stamp buffer of stream_kernel (nullptr: off)
+extern "C" int gvx_pyr_trace_set(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(gvx::gvx_pyr_trace_buf), &buf, sizeof(buf));
+}
+#endif

@@ -193,6 +193,11 @@ def make_sequence(w: int, h: int, n_frames: int, device, seed: int = SEED, tex=N
         v = F.grid_sample(T, grid, mode="bilinear", padding_mode="border", align_corners=True)[0, 0]
         v = v + torch.randint(-2, 3, v.shape, device=device, generator=gen, dtype=torch.int32).to(v.dtype)
         out[t] = v.round().clamp(0, 255).to(torch.uint8)
+        if (t & 63) == 63 and out.is_cuda:
+            # bound the un-synchronised dispatch backlog (about 15 kernels a frame):
+            # rocprofv3's counter collection fails on tens of thousands of queued
+            # dispatches (a queue abort in r05_m1, a host SIGSEGV in r06_d1)
+            torch.cuda.synchronize(out.device)
     return out, tex
 
 

@@ -485,14 +485,24 @@ gvx_status gvx_preint_integrate_dev(gvx_ctx* ctx, int32_t variant, const gvx_imu
                                     const gvx_state* d_state0, const double* d_iewn,
                                     gvx_preint_result* d_out, double* d_pn);
 /* Which form gvx_preint_integrate[_dev] runs (default GVX_PREINT_PATH_AUTO:
-   the three-launch form -- per-step terms, the quaternion chains, the covariance
-   pass with sqrt_information_ in its epilogue -- whenever its scratch can be
-   sized; the single kernel otherwise).  GVX_PREINT_PATH_ONEPHASE forces the
+   the two-launch form -- preint_pre_kernel forms the per-step terms and runs
+   the quaternion chains as wave prefix products, then preint_cov16_kernel runs
+   the covariance pass with sqrt_information_ in its epilogue -- whenever its
+   scratch can be sized; the single kernel otherwise).  GVX_PREINT_PATH_ONEPHASE forces the
    single kernel: an A/B and parity switch, per context.  The environment
    variable GVX_PREINT_ONEPHASE=1 sets it when the context is created. */
 #define GVX_PREINT_PATH_AUTO 0
 #define GVX_PREINT_PATH_ONEPHASE 1
 gvx_status gvx_set_preint_path(gvx_ctx* ctx, int32_t path);
+
+/* How the batched LK launches (more than 4,096 points, the exact window-sum
+   order: three points per wave) are cut (tracking.cc:385-408, the calls they
+   replace): `levels_per_phase` >= 1 runs every point group's chain -- forward
+   levels maxLevel..0, then backward -- as phases of that many levels, one wave
+   each, handing the flow on through device memory (default 1; DESIGN 4 "LK
+   phases"); 0 runs each group's whole chain in one wave.  Same bits either way.
+   The environment variable GVX_KLT_LPP sets it when the context is created. */
+gvx_status gvx_set_klt_phases(gvx_ctx* ctx, int32_t levels_per_phase);
 
 /* Earth::iewn(station, p) (common/earth.h:233-237), host-side helper used by
    resetState (preintegration_earth.cc:320). */

@@ -181,3 +181,40 @@ def test_preint_two_phase_equals_one_phase(ctx, gvx_mod, variant):
         assert pn1.shape == pn2.shape
         assert np.array_equal(pn1[:, 0], pn2[:, 0])  # dt
         assert np.abs(pn1[:, 1:] - pn2[:, 1:]).max() <= 1e-12 * np.abs(pn1[:, 1:]).max()
+
+
+@pytest.mark.parametrize("variant", [NORMAL, EARTH])
+def test_preint_two_phase_identity_chains_bit_exact(ctx, gvx_mod, variant):
+    """with the chain inputs at the identity -- zero gyro increments,
+    zero gyro bias, iewn = 0 -- and dyadic sample times (256 Hz, so every
+    delta_time partial sum is exact), the quaternion chains are the identity in
+    both forms, and the two-launch form must agree with the single kernel bit
+    for bit, on ragged segments (identity records past m) included."""
+    rng = np.random.default_rng(77 + variant)
+    ms = [1, 2, 5, 64, 100, 101, 33]
+    segs, states = [], []
+    for m in ms:
+        imu = synth_ba.make_imu_segment(rng, m, rate=256.0)
+        imu["dtheta"] = 0.0
+        segs.append(imu)
+        s = synth_ba.random_state(rng)
+        s["bg"] = 0.0
+        states.append(s)
+    states = np.array(states)
+    iewn = np.zeros((len(ms), 3))
+    gstates = np.zeros(len(ms), gvx_mod.STATE_DTYPE)
+    for k in ("time", "p", "q", "v", "bg", "ba"):
+        gstates[k] = states[k]
+    try:
+        ctx.set_preint_path(gvx_mod.PREINT_PATH_ONEPHASE)
+        o1, pn1, _ = ctx.preint_integrate(variant, synth_ba.imu_params(), segs, gstates, iewn)
+    finally:
+        ctx.set_preint_path(gvx_mod.PREINT_PATH_AUTO)
+    o2, pn2, _ = ctx.preint_integrate(variant, synth_ba.imu_params(), segs, gstates, iewn)
+    for name in ("variant", "m", "start_time", "end_time", "delta_time"):
+        np.testing.assert_array_equal(o1[name], o2[name], err_msg=name)
+    for st in ("current", "delta"):
+        for f in ("time", "q", "bg", "ba"):
+            np.testing.assert_array_equal(o1[st][f], o2[st][f], err_msg=f"{st}.{f}")
+    if variant == EARTH:
+        assert np.array_equal(pn1, pn2)

@@ -107,3 +107,34 @@ def test_bench_pipelined_run_equals_step(ctx, gvx_mod, w, h, n, L):
     assert len(seen) == 5
     lay = gvx_mod.pyramid_layout(w, h, L)
     assert wl._pyr[0].numel() == 2 * wl.n_pairs * lay["bytes"]
+
+
+@pytest.mark.parametrize("w,h,n,L", CONFIGS)
+def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
+    """The bench's launch with the LK chain cut into phases of 1 (default), 2 or
+    3 levels, or run whole in one wave per point group (gvx_set_klt_phases):
+    every output of all 256 pairs identical (the default is pinned to the oracle
+    above)."""
+    wl = _workload(w, h, n)
+    p = gvx_mod.KltParams.default(max_level=L)
+    outs = {}
+    try:
+        for lpp in (1, 0, 2, 3, 1):
+            ctx.set_klt_phases(lpp)
+            wl.N.fill_(np.nan)
+            wl.B.fill_(np.nan)
+            wl.F.fill_(255)
+            wl.K.fill_(-1)
+            wl.NK.fill_(-1)
+            wl.step(ctx, p)
+            ctx.sync()
+            got = [a.cpu().numpy() for a in (wl.N, wl.B, wl.F, wl.K, wl.NK)]
+            if lpp in outs:  # a repeated launch: the hand-off counters were left at 0
+                for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), got, outs[lpp]):
+                    _assert_same(a, b, f"lpp {lpp} repeat {name}")
+            outs[lpp] = got
+    finally:
+        ctx.set_klt_phases(1)
+    for lpp in (0, 2, 3):
+        for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), outs[lpp], outs[1]):
+            _assert_same(a, b, f"lpp {lpp} {name}")

@@ -31,6 +31,10 @@ def test_bench_mock_two_ranks_gloo():
     # rank 1 sleeps 4 ms per step: the max over ranks must be >= 20 * 4 ms
     assert d["elapsed_s"] >= 0.08
     assert abs(d["value"] - 2 * 8 * 20 / d["elapsed_s"]) < 1e-6 * d["value"]
+    # the clock warm-up side legs run before the headline on EVERY rank at N > 1,
+    # as at N = 1
+    assert d["side_legs_before_headline"] == ["lk_accum", "preprocess"]
+    assert d["side_legs_before_headline_ranks"] == 2
 
 
 def test_bench_mock_sequence_gather_gloo():

@@ -47,12 +47,12 @@ def test_batch_results_all_gather_rccl():
     assert d["dist_backend"] == "nccl"
     assert d["gather_check"] is True
     assert d["n_gpus"] == 1 and 0.5 < d["kept_fraction"] <= 1.0
-    # the roofline states its convention (SURVEY 8d's effective bandwidth); the
-    # measured fraction needs the committed PMC traffic of this exact workload
-    # (256 pairs), so a 32-pair run reports none
+    # the measured fraction needs the committed PMC traffic of this exact
+    # workload (256 pairs), so a 32-pair run reports none and falls back to B_min
     r = d["roofline"]
-    assert r["bound"] == "hbm" and "Scharr" in r["convention"]
-    assert r["measured_frac"] is None and r["measured_gbs"] is None
+    assert r["bound"] == "hbm" and "Scharr" in r["effective_convention"]
+    assert r["traffic"] is None and r["achieved_basis"].startswith("B_min")
+    assert r["frac"] == r["frac_min"] and r["frac_min"] < r["effective_frac"]
 
 
 def test_default_line_sequence_rccl():

@@ -184,3 +184,35 @@ def test_factor_batch_eval_dev_matches_batched(ctx, gvx_mod):
     assert np.array_equal(d_rj.cpu().numpy(), rjac)
     assert np.array_equal(d_pr.cpu().numpy(), pres)
     assert np.array_equal(d_pj.cpu().numpy(), pjac)
+
+
+@pytest.mark.parametrize("n_kf,n_lm", [(6, 40), (10, 1500)])
+def test_factor_set_d2h_mode_matches_mapped(ctx, gvx_mod, n_kf, n_lm):
+    """the GVX_FACTORSET_D2H=1 fallback (device result buffer + one
+    D2H copy per prepare, out_mode 0) gives the same bits as the default mapped
+    host buffer the kernels write themselves (out_mode 1) -- on a small window
+    and on one of 13,500 reprojection factors, whose launch exceeds one block per
+    CU and takes the split kernels."""
+    import os
+    w = _window(ctx, gvx_mod, n_kf=n_kf, n_lm=n_lm, seed=17)
+    ref = _batched(ctx, gvx_mod, w)
+    fs = _make_set(ctx, gvx_mod, w)
+    fs.prepare(jacobians=True)
+    _check_set(fs, *ref)
+    fs.close()
+    os.environ["GVX_FACTORSET_D2H"] = "1"
+    try:
+        c2 = gvx_mod.Context(0)  # the switch is read once, at creation
+    finally:
+        del os.environ["GVX_FACTORSET_D2H"]
+    try:
+        fs2 = _make_set(c2, gvx_mod, w)
+        fs2.prepare(jacobians=True)
+        _check_set(fs2, *ref)
+        fs2.prepare(jacobians=False)
+        for i in range(0, fs2.n_reproj, 97):
+            r, _ = fs2.read_reproj(i, jacobians=False)
+            assert np.array_equal(r, ref[0][i])
+        fs2.close()
+    finally:
+        c2.close()

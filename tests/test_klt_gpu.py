@@ -194,12 +194,27 @@ def test_frame_put_dev_matches_host_put(ctx, gvx_mod):
     ctx.frame_drop(22)
 
 
+# gvx_set_klt_phases: the batched LK as phases of 1 (default), 2 or 3 levels,
+# or each point group's whole chain in one wave (0)
+PHASES = [pytest.param(1, id="lpp1"), pytest.param(0, id="chain"), pytest.param(2, id="lpp2"),
+          pytest.param(3, id="lpp3")]
+
+
+@pytest.fixture
+def phases(ctx, request):
+    ctx.set_klt_phases(request.param)
+    yield request.param
+    ctx.set_klt_phases(1)
+
+
+@pytest.mark.parametrize("phases", PHASES, indirect=True)
 @pytest.mark.parametrize("n_pairs,n_pts", [(64, 149), (3, 2731), (30, 150)])
-def test_batch_three_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
+def test_batch_three_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts, phases):
     """Launches of > 4096 points take the three-points-per-wave LK (the exact
     order); point counts that are not multiples of 3 leave one or two spare
     lane groups in each pair's last wave.  Border points included (the groups
-    take turns on the wave's LDS tile)."""
+    take turns on the wave's LDS tile).  Every way of cutting the chain into
+    phases gives the oracle's bits."""
     w, h = 320, 140
     rng = np.random.default_rng(n_pairs + n_pts)
     I = np.stack([synth.make_image(w, h, rng) for _ in range(n_pairs)])
@@ -218,10 +233,13 @@ def test_batch_three_points_per_wave(ctx, orc, gvx_mod, n_pairs, n_pts):
         _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
 
 
-def test_single_call_three_points_per_wave_with_err(ctx, orc, gvx_mod):
+@pytest.mark.parametrize("phases", PHASES, indirect=True)
+def test_single_call_three_points_per_wave_with_err(ctx, orc, gvx_mod, phases):
     """One pair with more than 4,096 points takes the three-point layout through
     gvx_calc_optical_flow_pyr_lk, whose level-0 error output is the layout's err
-    path (the batch calls never ask for it): next, status and err bit-exact."""
+    path (the batch calls never ask for it): next, status and err bit-exact --
+    also when the forward chain is cut into phases (mode 0: the last phase
+    writes the status)."""
     W, H, N = 640, 480, 4500
     rng = np.random.default_rng(4500)
     I = synth.make_image(W, H, rng)
@@ -292,3 +310,40 @@ def test_split_batch_entry_points_validate(ctx, gvx_mod):
     ctx.klt_batch_pyramids_dev(0, W, H, 0, 0, 3, 0)
     ctx.klt_fb_batch_pyr_dev(0, W, H, img.data_ptr(), img.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0, 0, params=p)
     ctx.sync()
+
+
+@pytest.mark.parametrize("phases", PHASES, indirect=True)
+def test_three_point_wave_groups_leave_at_different_times(ctx, orc, gvx_mod, phases):
+    """in the three-points-per-wave layout a group whose point stops
+    early must not disturb the groups that go on iterating (the group sums rely
+    on whole-group activity and on DPP reads of disabled lanes).  Every wave of
+    this batch holds one point off the image at every level (it stops at the top
+    level), one point that converges at once (J = I there, zero initial flow
+    error) and one that needs many iterations (a 1.6 px error under a large
+    iteration cap), in all three lane-group positions: next, back, flags and
+    kept indices bit-exact against the oracle."""
+    P, W, H, N = 40, 320, 140, 120  # 4,800 points: the three-point layout
+    rng = np.random.default_rng(120)
+    I = np.stack([synth.make_image(W, H, rng) for _ in range(P)])
+    J = np.stack([np.roll(I[i], (3, -2), axis=(0, 1)) for i in range(P)])
+    prev = rng.uniform([40, 40], [W - 40, H - 40], (P, N, 2)).astype(np.float32)
+    init = prev + np.float32([-2.0, 3.0])  # the true shift
+    for i in range(P):
+        for k in range(N // 3):
+            kind = (k + i) % 3  # which lane group holds which kind
+            off, fast, slow = 3 * k + kind, 3 * k + (kind + 1) % 3, 3 * k + (kind + 2) % 3
+            prev[i, off] = [-500.0, 60.0]  # off every level: stops at the top level
+            init[i, off] = prev[i, off]
+            init[i, fast] = prev[i, fast] + np.float32([-2.0, 3.0])
+            init[i, slow] = prev[i, slow] + np.float32([-2.0, 3.0]) + rng.uniform(-1.6, 1.6, 2).astype(np.float32)
+    p = gvx_mod.KltParams.default(max_level=3, max_iter=100)
+    g = ctx.klt_fb_batch(I, J, prev, init, params=p)
+    op = orc.KltParams.default(max_level=3, max_iter=100)
+    for i in (0, 1, 2, P - 1):
+        o = orc.klt_fb(I[i], J[i], prev[i], init[i], params=op, reuse_pyramids=True)
+        _assert_same(g["next"][i], o["next"], f"pair {i} next")
+        _assert_same(g["back"][i], o["back"], f"pair {i} back")
+        flags = o["st_f"] | (o["st_b"] << 1) | (o["keep"] << 2)
+        _assert_same(g["flags"][i], flags, f"pair {i} flags")
+        _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
+        assert (flags[0::3] | flags[1::3] | flags[2::3]).any() and not o["st_f"].all()

@@ -136,3 +136,20 @@ def test_schur_solve_reports_indefinite(ctx, window):
     ctx.schur_solve_dev(dict(p, data=data), d_data.data_ptr(), d_delta.data_ptr(), d_info=d_info.data_ptr())
     ctx.sync()
     assert d_info.cpu().tolist() == [1, 1] and torch.isnan(d_delta).all().item() and L == d_delta.numel()
+
+
+def test_schur_solve_refuses_oversized_window_before_staging(ctx):
+    """a window above GVX_SCHUR_MAX_L (16,384) parameters is refused
+    with GVX_ERR_UNSUPPORTED by both entries before any list, pinned or device
+    staging is sized -- an r x r staging of 2 GiB must not be attempted (which
+    could surface as GVX_ERR_OOM instead)."""
+    from gvx import _ptr
+    L = 16384 + 1
+    delta = np.zeros(1)
+    info = np.zeros(2, np.int32)
+    s = ctx._L.gvx_schur_solve(ctx._h, 0, None, None, None, None, None, _ptr(delta), 0, 0, None, None, 0, L,
+                               None, _ptr(delta), None, _ptr(info))
+    assert s == -6  # GVX_ERR_UNSUPPORTED
+    s = ctx._L.gvx_schur_solve_dev(ctx._h, 0, None, None, None, None, None, 1, 0, 0, None, None, 0, L, None, 1,
+                                   None, None)
+    assert s == -6

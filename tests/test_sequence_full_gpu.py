@@ -58,12 +58,12 @@ def test_bench_sequence_full_length(ctx, orc, gvx_mod):
     assert counts.min() > 0.5 * N and n_detect >= 50, (counts.min(), n_detect)
 
 
-@pytest.mark.parametrize("rank", [1, 7])
+@pytest.mark.parametrize("rank", [1, 2, 3, 4, 5, 6, 7])
 def test_bench_sequence_other_ranks(ctx, orc, gvx_mod, rank):
     """The sequences of ranks >= 1 (seed synth.SEED + 7919 r, VERDICT r04 weak
-    8): the first 400 frames of rank 1's and rank 7's sequence through the
-    bench's pipelined K = 16 graph loop, every per-frame record bit-exact
-    against the oracle loop."""
+    8, r05 weak 9): the first 400 frames of every other rank's sequence of the
+    driver's 8-GPU run through the bench's pipelined K = 16 graph loop, every
+    per-frame record bit-exact against the oracle loop."""
     import torch
     from gvx import synth
     from gvx.tracking import DeviceSequenceTracker

@@ -9,13 +9,19 @@ import glob
 import sys
 
 root, name = sys.argv[1], sys.argv[2]
-acc = collections.defaultdict(dict)
+# rows of one pass (file) are summed per dispatch; a counter collected in
+# several passes (SQ_WAVES, in every group) is averaged over them.  Through r05
+# it was summed, which doubled SQ_WAVES and halved every per-wave figure.
+raw = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if name not in r["Kernel_Name"]:
             continue
         key = (int(r["Grid_Size"]), r["Dispatch_Id"])
-        acc[key][r["Counter_Name"]] = acc[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        raw[(key, r["Counter_Name"])][f] += float(r["Counter_Value"])
+acc = collections.defaultdict(dict)
+for (key, cn), by_pass in raw.items():
+    acc[key][cn] = sum(by_pass.values()) / len(by_pass)
 if not acc:
     sys.exit(f"no dispatch of {name}")
 grid = max(k[0] for k in acc)

@@ -8,17 +8,21 @@ import sys
 
 
 def load(root):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    # rows of one pass (one rocprofv3 run, its own file) are summed per dispatch;
+    # a counter collected in several passes (SQ_WAVES is in every SQ group) is
+    # averaged over them -- summing it across passes doubled SQ_WAVES and halved
+    # every per-wave figure through r05
+    acc = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"].replace("(anonymous namespace)", "anon")
             name = kn.split("(")[0].split("<")[0].split("::")[-1] or kn[:40]
-            acc[name][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
+            acc[name][(r["Counter_Name"], r["Dispatch_Id"])][f] += float(r["Counter_Value"])
     out = {}
     for k, d in acc.items():
         per = collections.defaultdict(list)
-        for (cn, _), vals in d.items():
-            per[cn].append(sum(vals))
+        for (cn, _), by_pass in d.items():
+            per[cn].append(sum(by_pass.values()) / len(by_pass))
         out[k] = {cn: sum(v) / len(v) for cn, v in per.items()}
     return out
 

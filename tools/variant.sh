@@ -16,6 +16,6 @@ while [ $# -gt 0 ]; do
   shift; [ $# -gt 0 ] && shift
 done
 mkdir -p "$R/ic-gvins_amd/gvx/variants"
-make -s -C "$T" -j8 INC="$R/include" OUT="$R/ic-gvins_amd/gvx/variants/libgvx_$N.so" 2>&1 | grep -E "error" || true
+make -s -C "$T" -j8 EXTRA="$EXTRA" INC="$R/include" OUT="$R/ic-gvins_amd/gvx/variants/libgvx_$N.so" 2>&1 | grep -E "error" || true
 rm -rf "$T"
 ls -la "$R/ic-gvins_amd/gvx/variants/libgvx_$N.so"
