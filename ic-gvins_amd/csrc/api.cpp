@@ -166,7 +166,20 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
     gvx_ctx* c = new gvx_ctx();
     c->device = device;
     c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    {
+        const char* sp = std::getenv("GVX_SIDE_LOW_PRIO");
+        c->side_low_prio = sp ? std::atoi(sp) : 0;
+    }
+    hipError_t se;
+    if (c->side_low_prio) {
+        int least = 0, greatest = 0;
+        se = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (se == hipSuccess)
+            se = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->side_low_prio == 2 ? least : greatest);
+    } else {
+        se = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    }
+    if (se != hipSuccess) {
         delete c;
         return GVX_ERR_HIP;
     }
@@ -183,6 +196,12 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
         c->prof_markers = m && std::atoi(m) != 0;
         const char* k = std::getenv("GVX_KLT_LPP");
         if (k) c->klt_lpp = std::max(0, std::atoi(k));
+        const char* sk = std::getenv("GVX_KLT_SUPER");
+        if (sk) c->klt_super = std::max(8, std::atoi(sk));
+        const char* pw = std::getenv("GVX_PYR_WPB");
+        if (pw) c->pyr_wpb = std::atoi(pw) == 4 ? 4 : 1;
+        const char* po = std::getenv("GVX_PYR_ORDER");
+        if (po) c->pyr_order = std::atoi(po) != 0;
     }
     *out = c;
     return GVX_OK;
@@ -228,11 +247,14 @@ gvx_status gvx_sync(gvx_ctx* c) {
 
 void* gvx_get_stream(gvx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-gvx_status gvx_set_klt_phases(gvx_ctx* c, int32_t levels_per_phase) {
+gvx_status gvx_set_klt_phases(gvx_ctx* c, int32_t levels_per_phase, int32_t groups_per_chunk) {
     if (!c) return GVX_ERR_INVALID;
     if (levels_per_phase < 0 || levels_per_phase > gvx::MAX_LEVELS)
         return set_err(c, GVX_ERR_INVALID, "levels per phase %d (0..%d)", levels_per_phase, gvx::MAX_LEVELS);
+    if (groups_per_chunk < 0 || (groups_per_chunk > 0 && groups_per_chunk < 8))
+        return set_err(c, GVX_ERR_INVALID, "groups per chunk %d (0 or >= 8)", groups_per_chunk);
     c->klt_lpp = levels_per_phase;
+    if (groups_per_chunk) c->klt_super = groups_per_chunk;
     return GVX_OK;
 }
 

@@ -128,7 +128,15 @@ gvx_status gvx_branch_begin(gvx_ctx* c) {
     hipSetDevice(c->device);
     if (!c->side) {
         if (c->capturing) return set_err(c, GVX_ERR_INVALID, "open a first branch outside a capture");
-        hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+        hipError_t e;
+        if (c->side_low_prio) {  // the branch yields to the context stream (GVX_SIDE_LOW_PRIO)
+            int least = 0, greatest = 0;
+            e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+            if (e == hipSuccess)
+                e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, c->side_low_prio == 2 ? greatest : least);
+        } else {
+            e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+        }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
         if (e != hipSuccess) return hip_err(c, e, "branch stream");

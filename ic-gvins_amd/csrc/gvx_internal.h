@@ -109,6 +109,14 @@ struct gvx_ctx {
     // batch LK (three points per wave): levels per phase of klt_phase_kernel, 0 =
     // one wave runs the whole chain (klt_kernel); GVX_KLT_LPP at creation
     int klt_lpp = 1;
+    int klt_super = 4096;  // groups per superchunk of klt_phase_kernel (GVX_KLT_SUPER)
+    // pyramid pass (stream_kernel): waves per workgroup (1 or 4) and work order
+    // (1: edge strips first); GVX_PYR_WPB / GVX_PYR_ORDER at creation (A/B)
+    int pyr_wpb = 1, pyr_order = 0;
+    // GVX_SIDE_LOW_PRIO=1 at creation: the branch stream at the lowest priority,
+    // the context stream at the highest (work on the branch fills the gaps); 2:
+    // the other way round; 0 (default): both at the default priority
+    int side_low_prio = 0;
     std::map<std::string, gvx::ProfEntry> prof_acc;
     struct Pending {
         std::string fam;

@@ -1657,19 +1657,31 @@ __global__ void __launch_bounds__(64, 4) klt_phase_kernel(KltArgs a, PyrLayout l
                                                           int64_t next_stride, Level0 l0, const float* __restrict__ prev_xy,
                                                           float* next_xy, float* __restrict__ back_xy,
                                                           uint8_t* __restrict__ flags, float* __restrict__ err_out,
-                                                          uint64_t* hs, int nbp, int lpp) {
+                                                          uint64_t* hs, int sc, int lpp) {
     __shared__ uint32_t win[(WIN + 3) * WIN_DW];  // border tile
     __shared__ v4u units[3 * 3 * 64];             // per-lane window values
     KLT_WAVE_STAMP;
     const int wpp = (a.n_pts + 2) / 3;
     const int n_groups = a.n_pairs * wpp;
-    const int ph = blockIdx.x / nbp;
-    const int wg = xcd_swizzle(blockIdx.x - ph * nbp, n_groups);
-    if (wg >= n_groups) return;
+    const int pd = (lay.nlev + lpp - 1) / lpp;  // phases per direction
+    const int n_ph = a.mode == 0 ? pd : 2 * pd;
+    // superchunks of sc groups, each dispatched phase-major; the last one holds
+    // the remaining groups on 8 * xcd_per(remainder) blocks per phase
+    const int span = n_ph * sc, n_full = n_groups / sc;
+    int q = blockIdx.x / span, r = blockIdx.x - q * span, blk = sc;
+    if (q >= n_full) {
+        q = n_full;
+        r = blockIdx.x - n_full * span;
+        blk = N_XCD * xcd_per(n_groups - n_full * sc);
+    }
+    const int ph = r / blk;
+    const int g0 = q * sc, gs = min(sc, n_groups - g0);
+    const int lg = xcd_swizzle(r - ph * blk, gs);  // block b runs on XCD b % 8 in every phase
+    if (lg >= gs) return;
+    const int wg = g0 + lg;
     const int pair = wg / wpp;
     const int npt = a.n_dev ? min(a.n_pts, *a.n_dev) : a.n_pts;
     if ((wg - pair * wpp) * 3 >= npt) return;  // every phase of this group leaves here
-    const int pd = (lay.nlev + lpp - 1) / lpp;  // phases per direction
     const bool bwd = ph >= pd;
     const int c = bwd ? ph - pd : ph;
     const int l_top = lay.nlev - 1 - c * lpp, l_bot = max(l_top - lpp + 1, 0);
@@ -1834,11 +1846,16 @@ static bool launch_klt_phases(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay
         if (hipMemsetAsync(db.p, 0, db.bytes, c->stream) != hipSuccess) return false;
         db.fresh = false;
     }
-    const int nbp = N_XCD * xcd_per(n_groups);  // blocks per phase, a multiple of 8
+    // superchunks of sc groups (a multiple of 8), each run phase-major: a group's
+    // phases are sc waves apart in dispatch order, so its level-0 windows are
+    // still near in the caches when its backward pass reads them again
+    const int sc = std::min(std::max(8, c->klt_super / 8 * 8), N_XCD * xcd_per(n_groups));
     const int pd = (lay.nlev + lpp - 1) / lpp;
     const int n_ph = a.mode == 0 ? pd : 2 * pd;
-    launch_timed(c, "klt", klt_phase_kernel, dim3((unsigned)(n_ph * nbp)), dim3(64), 0, a, lay, pyr_prev, pyr_next,
-                 prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err, hs, nbp, lpp);
+    const int n_full = n_groups / sc, rem = n_groups - n_full * sc;
+    const int64_t grid = (int64_t)n_ph * ((int64_t)n_full * sc + (rem ? N_XCD * xcd_per(rem) : 0));
+    launch_timed(c, "klt", klt_phase_kernel, dim3((unsigned)grid), dim3(64), 0, a, lay, pyr_prev, pyr_next,
+                 prev_pair_stride, next_pair_stride, l0, prev_xy, next_xy, back_xy, flags, err, hs, sc, lpp);
     return true;
 }
 

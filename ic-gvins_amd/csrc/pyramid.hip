@@ -600,20 +600,38 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
 __device__ uint64_t* gvx_pyr_trace_buf;  // diagnostic build only (tools/pyr_residency.py)
 #endif
 
-template <int NL, int SKIP = 0>
-__global__ void __launch_bounds__(256, STREAM_OCC) stream_kernel(StreamSrc src, uint8_t* __restrict__ pyr,
+// Work order (edge_first, r06): the edge strips (REFLECT_101 gathers, side
+// bands) take ~52 us per wave at configs[1], an interior strip ~38 us
+// (profiles/r06_l2/res_pyr).  Units are dispatched edge strips first, each
+// strip's units image by image and band by band (vertical neighbours, which
+// share their warm-up rows, in one XCD's L2), so the launch drains on the short
+// interior waves.  edge_first = 0: strip-major within a band, the r05 order.
+// WPB waves per workgroup: 1 frees a finished wave's slot at once (a 4-wave
+// workgroup held its slots until its slowest wave ended, 17 us apart on average).
+template <int NL, int SKIP = 0, int WPB = 1>
+__global__ void __launch_bounds__(64 * WPB, STREAM_OCC) stream_kernel(StreamSrc src, uint8_t* __restrict__ pyr,
                                                                   int64_t pyr_bytes, DownLevels L, int n_strips,
                                                                   int n_bands, int n_units, int band,
-                                                                  uint8_t* __restrict__ trash) {
+                                                                  uint8_t* __restrict__ trash, int edge_first) {
 #ifdef GVX_KLT_TRACE
     WaveStamp wave_stamp_(gvx_pyr_trace_buf);
 #endif
     const int lane = threadIdx.x & 63;
-    const int nblk = (n_units + 3) / 4;
-    const int unit = xcd_swizzle(blockIdx.x, nblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nblk = (n_units + WPB - 1) / WPB;
+    const int unit = xcd_swizzle(blockIdx.x, nblk) * WPB + (WPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0);
     if (unit >= n_units) return;
-    const int st = unit % n_strips, rest = unit / n_strips;
-    const int bd = rest % n_bands, img = rest / n_bands;
+    int st, bd, img;
+    if (edge_first) {
+        const int per = n_units / n_strips, k = unit / per, rest = unit - k * per;
+        st = k == 0 ? 0 : k == 1 ? n_strips - 1 : k - 1;
+        img = rest / n_bands;
+        bd = rest - img * n_bands;
+    } else {
+        st = unit % n_strips;
+        const int rest = unit / n_strips;
+        bd = rest % n_bands;
+        img = rest / n_bands;
+    }
     uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
     // wave-uniform strip classes: source columns past an edge of an unpadded
     // level 0 (lanes 0 / 63 read x0 = 480*st - 20 / 480*st + 484, 16 bytes), and
@@ -660,13 +678,16 @@ hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrL
     const int band = stream_band(n_strips, D.h[0], n_img, c->n_cu);
     const int n_bands = (D.h[0] + band - 1) / band;
     const int n_units = n_strips * n_bands * n_img;
-    const int nblk = (n_units + 3) / 4;
     // the lanes without an output store to their wave's trash line: the kernel
     // must not run without it (a scratch buffer cannot grow inside a capture)
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
     if (!trash) return hipErrorOutOfMemory;
-    return launch_timed(c, "pyramid", stream_kernel<NL>, dim3(N_XCD * xcd_per(nblk)), dim3(256), 0, src, dst,
-                        lay.bytes, D, n_strips, n_bands, n_units, band, trash);
+    if (c->pyr_wpb == 4)
+        return launch_timed(c, "pyramid", stream_kernel<NL, 0, 4>, dim3(N_XCD * xcd_per((n_units + 3) / 4)),
+                            dim3(256), 0, src, dst, lay.bytes, D, n_strips, n_bands, n_units, band, trash,
+                            c->pyr_order);
+    return launch_timed(c, "pyramid", stream_kernel<NL, 0, 1>, dim3(N_XCD * xcd_per(n_units)), dim3(64), 0, src,
+                        dst, lay.bytes, D, n_strips, n_bands, n_units, band, trash, c->pyr_order);
 }
 
 

@@ -237,7 +237,7 @@ def _declare(L):
         "gvx_sym_eigen": (i32, [P, i32, P, i32, P, P, C.POINTER(i32)]),
         "gvx_set_marg_solver": (i32, [P, i32]),
         "gvx_set_preint_path": (i32, [P, i32]),
-        "gvx_set_klt_phases": (i32, [P, i32]),
+        "gvx_set_klt_phases": (i32, [P, i32, i32]),
         "gvx_find_fundamental_ransac": (i32, [P, i32, P, P, P, f64, f64, i32, P, P, P]),
         "gvx_copy_indexed_dev": (i32, [P, P, P, C.c_size_t, P, i32]),
         "gvx_track_record_dev": (i32, [P, P, P, i32, P, P, P, i32]),
@@ -850,10 +850,11 @@ class Context:
                                                 _ptr(index), m, L, d_J0, d_e0, d_Hp, d_bp, d_eval, d_info),
                     "gvx_marginalize_dev")
 
-    def set_klt_phases(self, levels_per_phase: int):
+    def set_klt_phases(self, levels_per_phase: int, groups_per_chunk: int = 0):
         """gvx_set_klt_phases: the batched LK as phases of that many levels, one
-        wave each (default 1), or 0 = one wave per point group's whole chain."""
-        self._check(self._L.gvx_set_klt_phases(self._h, levels_per_phase), "gvx_set_klt_phases")
+        wave each (default 1), or 0 = one wave per point group's whole chain;
+        superchunks of groups_per_chunk groups (0 = unchanged, default 4096)."""
+        self._check(self._L.gvx_set_klt_phases(self._h, levels_per_phase, groups_per_chunk), "gvx_set_klt_phases")
 
     def set_preint_path(self, path: int):
         """gvx_set_preint_path: PREINT_PATH_AUTO (the two-launch form: the per-step

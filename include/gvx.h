@@ -500,9 +500,12 @@ gvx_status gvx_set_preint_path(gvx_ctx* ctx, int32_t path);
    replace): `levels_per_phase` >= 1 runs every point group's chain -- forward
    levels maxLevel..0, then backward -- as phases of that many levels, one wave
    each, handing the flow on through device memory (default 1; DESIGN 4 "LK
-   phases"); 0 runs each group's whole chain in one wave.  Same bits either way.
-   The environment variable GVX_KLT_LPP sets it when the context is created. */
-gvx_status gvx_set_klt_phases(gvx_ctx* ctx, int32_t levels_per_phase);
+   phases"); 0 runs each group's whole chain in one wave.  The groups are
+   dispatched in superchunks of `groups_per_chunk` (rounded down to a multiple
+   of 8; 0 keeps the current value, default 4096), each superchunk phase by
+   phase.  Same bits either way.  The environment variables GVX_KLT_LPP and
+   GVX_KLT_SUPER set them when the context is created. */
+gvx_status gvx_set_klt_phases(gvx_ctx* ctx, int32_t levels_per_phase, int32_t groups_per_chunk);
 
 /* Earth::iewn(station, p) (common/earth.h:233-237), host-side helper used by
    resetState (preintegration_earth.cc:320). */

@@ -111,16 +111,16 @@ def test_bench_pipelined_run_equals_step(ctx, gvx_mod, w, h, n, L):
 
 @pytest.mark.parametrize("w,h,n,L", CONFIGS)
 def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
-    """The bench's launch with the LK chain cut into phases of 1 (default), 2 or
-    3 levels, or run whole in one wave per point group (gvx_set_klt_phases):
-    every output of all 256 pairs identical (the default is pinned to the oracle
-    above)."""
+    """The bench's launch with the LK chain cut into phases of 1 (default), 2, 3
+    or 4 levels, dispatched in superchunks of 8 to all groups, or run whole in one
+    wave per point group (gvx_set_klt_phases): every output of all 256 pairs
+    identical (the default is pinned to the oracle above)."""
     wl = _workload(w, h, n)
     p = gvx_mod.KltParams.default(max_level=L)
     outs = {}
     try:
-        for lpp in (1, 0, 2, 3, 1):
-            ctx.set_klt_phases(lpp)
+        for lpp, sc in ((1, 4096), (0, 0), (2, 0), (3, 0), (1, 8), (2, 1000), (4, 100000), (1, 4096)):
+            ctx.set_klt_phases(lpp, sc)
             wl.N.fill_(np.nan)
             wl.B.fill_(np.nan)
             wl.F.fill_(255)
@@ -129,12 +129,12 @@ def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
             wl.step(ctx, p)
             ctx.sync()
             got = [a.cpu().numpy() for a in (wl.N, wl.B, wl.F, wl.K, wl.NK)]
-            if lpp in outs:  # a repeated launch: the hand-off counters were left at 0
-                for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), got, outs[lpp]):
+            if (lpp, sc) in outs:  # a repeated launch: the hand-off tags were left at 0
+                for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), got, outs[(lpp, sc)]):
                     _assert_same(a, b, f"lpp {lpp} repeat {name}")
-            outs[lpp] = got
+            outs[(lpp, sc)] = got
     finally:
-        ctx.set_klt_phases(1)
-    for lpp in (0, 2, 3):
-        for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), outs[lpp], outs[1]):
-            _assert_same(a, b, f"lpp {lpp} {name}")
+        ctx.set_klt_phases(1, 4096)
+    for key, o in outs.items():
+        for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), o, outs[(1, 4096)]):
+            _assert_same(a, b, f"lpp/superchunk {key} {name}")

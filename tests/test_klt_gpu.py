@@ -202,9 +202,9 @@ PHASES = [pytest.param(1, id="lpp1"), pytest.param(0, id="chain"), pytest.param(
 
 @pytest.fixture
 def phases(ctx, request):
-    ctx.set_klt_phases(request.param)
+    ctx.set_klt_phases(request.param, 64)  # small superchunks: several per launch, a ragged last one
     yield request.param
-    ctx.set_klt_phases(1)
+    ctx.set_klt_phases(1, 4096)
 
 
 @pytest.mark.parametrize("phases", PHASES, indirect=True)
