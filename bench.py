@@ -235,6 +235,20 @@ def traffic_for(workload):
     return d if d.get("workload") == workload else None
 
 
+def issue_for(workload):
+    """LK's VALU-issue fraction on this workload (tools/issue.py: one PMC pass,
+    profiles/pmc_issue.json), or None."""
+    f = os.path.join(ROOT, "profiles", "pmc_issue.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return {k: d[k] for k in ("valu_busy", "resident_waves_per_simd", "max_waves_per_simd", "valu_insts_per_wave",
+                              "clock_ghz", "source", "commit") if k in d}
+
+
 def host_threads():
     """CPU share for the baseline: the affinity mask, capped at 16 (the GPU box's
     per-GPU CPU share; os.cpu_count() reports the whole machine there)."""
@@ -371,9 +385,9 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="open the process group even at world size 1 (run under torch.distributed.run): the "
                          "collectives of --gather / configs[4] / max-over-ranks then go through RCCL")
-    ap.add_argument("--overlap", action="store_true",
-                    help="configs[1]/[2]: batch t+1's pyramid pass on a side stream beside batch t's LK (default: "
-                         "back to back; the overlap measured slower, DESIGN.md 8)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="configs[1]/[2]: pyramid pass and LK back to back (default: batch t+1's pyramid pass on a "
+                         "side stream beside batch t's LK -- each fills the other's drain, DESIGN.md 4 / 5)")
     ap.add_argument("--accum", default="exact", choices=tuple(ACCUM_MODES),
                     help="LK window-sum order (gvx_klt_params.accum): exact integer sums (default), or "
                          "OpenCV 4.x's fp32 scalar-loop / CV_SIMD128 orders")
@@ -427,9 +441,12 @@ def main():
     legs = side_legs_before_headline(args)
     accum_cost = accum_leg(ctx, step, gvx, L, steps=max(5, args.steps // 4)) if "lk_accum" in legs else None
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if "preprocess" in legs else None
+    pipelined = args.overlap
+    if "settle" in legs:
+        wl.run(ctx, params, SETTLE_STEPS, pipelined)
+        ctx.sync()
     t_side = time.perf_counter() - t_side
     side_ranks = ranks_that_ran(accum_cost is not None, dist, dev)
-    pipelined = args.overlap
     wl.run(ctx, params, args.warmup, pipelined, collect)
     ctx.sync()
     torch.cuda.synchronize()
@@ -557,6 +574,7 @@ def main():
                          "effective_convention": ("SURVEY 8d's B, which counts int16x2 Scharr planes written and "
                                                   "read; this build never stores them, so effective_frac passes 1 "
                                                   "above 454 k pairs/s and is no roofline"),
+                         "klt_issue": issue_for(workload),
                          "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()},
                          "overlap": pipelined},
@@ -566,6 +584,8 @@ def main():
             "lk_accum_cost": accum_cost,
             "side_legs_before_headline_s": round(t_side, 3),
             "side_legs_before_headline_ranks": side_ranks,
+            "side_legs_before_headline": legs,
+            "settle_steps": SETTLE_STEPS if "settle" in legs else 0,
             "preprocess": pre,
             "single_pair": single,
             "host_buffers": pcie,
@@ -1367,10 +1387,16 @@ def spawn_ranks(n):
 def side_legs_before_headline(args):
     """The side legs that run before the headline's W warm-up steps ramp the
     shader clock: with 3 warm-up steps alone LK reads 0.50-0.55 ms
-    instead of 0.47.  They run at EVERY world size -- through r05 the LK leg ran
+    instead of 0.47.  The last, "settle", runs SETTLE_STEPS of the headline's own
+    steps: the clock settles to the pyramid-beside-LK load over ~20 ms
+    (profiles/r06_c1: pipelined steps 0.53 -> 0.47 ms over the first 20).  They
+    run at EVERY world size -- through r05 the LK leg ran
     at N = 1 only, so the N > 1 points of the scaling curve were timed at a
     colder clock."""
-    return [] if args.no_pre else ["lk_accum", "preprocess"]
+    return [] if args.no_pre else ["lk_accum", "preprocess", "settle"]
+
+
+SETTLE_STEPS = 40  # the headline's own (pipelined) steps, untimed, after the other side legs
 
 
 def ranks_that_ran(flag, dist, dev=None):

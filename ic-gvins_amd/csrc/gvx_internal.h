@@ -108,7 +108,7 @@ struct gvx_ctx {
     bool prof_markers = false;  // GVX_PROF_MARKERS=1 at creation (launch_timed)
     // batch LK (three points per wave): levels per phase of klt_phase_kernel, 0 =
     // one wave runs the whole chain (klt_kernel); GVX_KLT_LPP at creation
-    int klt_lpp = 1;
+    int klt_lpp = 0;
     int klt_super = 4096;  // groups per superchunk of klt_phase_kernel (GVX_KLT_SUPER)
     // pyramid pass (stream_kernel): waves per workgroup (1 or 4) and work order
     // (1: edge strips first); GVX_PYR_WPB / GVX_PYR_ORDER at creation (A/B)

@@ -1605,7 +1605,12 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
 // per-wave s_memrealtime stamps).  Here the chain is cut into phases of `lpp`
 // levels of one direction, each a wave of its own, dispatched phase-major: all
 // groups' phase 0, then all groups' phase 1, ...  The drain is then as long as
-// one phase.
+// one phase.  Measured (profiles/r06_l2, r06_l3): it is, but a phase wave costs
+// more than its share of the chain (+15-18 % wave time in all: its start-up, the
+// hand-off, level-0 windows re-read from HBM by the backward phases), so the net
+// is -1.7 % at 4 levels per phase (forward / backward) and a loss at 1-2; beside
+// the next batch's pyramid pass (bench.py's default) the whole-chain kernel wins,
+// because the pyramid waves fill its drain.  So gvx_set_klt_phases defaults to 0.
 // Hand-off: every value a phase passes on is one 64-bit word, the float in the
 // low half and a tag (the phase that wrote it, plus one) in the high half,
 // stored and loaded as single-copy-atomic dwordx2 accesses.  A reader waits for

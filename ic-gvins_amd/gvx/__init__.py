@@ -852,7 +852,7 @@ class Context:
 
     def set_klt_phases(self, levels_per_phase: int, groups_per_chunk: int = 0):
         """gvx_set_klt_phases: the batched LK as phases of that many levels, one
-        wave each (default 1), or 0 = one wave per point group's whole chain;
+        wave each, or 0 (default) = one wave per point group's whole chain;
         superchunks of groups_per_chunk groups (0 = unchanged, default 4096)."""
         self._check(self._L.gvx_set_klt_phases(self._h, levels_per_phase, groups_per_chunk), "gvx_set_klt_phases")
 

@@ -499,8 +499,8 @@ gvx_status gvx_set_preint_path(gvx_ctx* ctx, int32_t path);
    order: three points per wave) are cut (tracking.cc:385-408, the calls they
    replace): `levels_per_phase` >= 1 runs every point group's chain -- forward
    levels maxLevel..0, then backward -- as phases of that many levels, one wave
-   each, handing the flow on through device memory (default 1; DESIGN 4 "LK
-   phases"); 0 runs each group's whole chain in one wave.  The groups are
+   each, handing the flow on through device memory (DESIGN 4 "LK phases");
+   0 (default) runs each group's whole chain in one wave.  The groups are
    dispatched in superchunks of `groups_per_chunk` (rounded down to a multiple
    of 8; 0 keeps the current value, default 4096), each superchunk phase by
    phase.  Same bits either way.  The environment variables GVX_KLT_LPP and

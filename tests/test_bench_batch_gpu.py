@@ -111,15 +111,15 @@ def test_bench_pipelined_run_equals_step(ctx, gvx_mod, w, h, n, L):
 
 @pytest.mark.parametrize("w,h,n,L", CONFIGS)
 def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
-    """The bench's launch with the LK chain cut into phases of 1 (default), 2, 3
-    or 4 levels, dispatched in superchunks of 8 to all groups, or run whole in one
-    wave per point group (gvx_set_klt_phases): every output of all 256 pairs
-    identical (the default is pinned to the oracle above)."""
+    """The bench's launch with each point group's chain in one wave (the
+    default) or cut into phases of 1, 2, 3 or 4 levels, dispatched in
+    superchunks of 8 up to all groups (gvx_set_klt_phases): every output of all
+    256 pairs identical (the default is pinned to the oracle above)."""
     wl = _workload(w, h, n)
     p = gvx_mod.KltParams.default(max_level=L)
     outs = {}
     try:
-        for lpp, sc in ((1, 4096), (0, 0), (2, 0), (3, 0), (1, 8), (2, 1000), (4, 100000), (1, 4096)):
+        for lpp, sc in ((0, 4096), (1, 0), (2, 0), (3, 0), (1, 8), (2, 1000), (4, 100000), (0, 4096)):
             ctx.set_klt_phases(lpp, sc)
             wl.N.fill_(np.nan)
             wl.B.fill_(np.nan)
@@ -134,7 +134,7 @@ def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
                     _assert_same(a, b, f"lpp {lpp} repeat {name}")
             outs[(lpp, sc)] = got
     finally:
-        ctx.set_klt_phases(1, 4096)
+        ctx.set_klt_phases(0, 4096)
     for key, o in outs.items():
-        for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), o, outs[(1, 4096)]):
+        for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), o, outs[(0, 4096)]):
             _assert_same(a, b, f"lpp/superchunk {key} {name}")

@@ -33,7 +33,7 @@ def test_bench_mock_two_ranks_gloo():
     assert abs(d["value"] - 2 * 8 * 20 / d["elapsed_s"]) < 1e-6 * d["value"]
     # the clock warm-up side legs run before the headline on EVERY rank at N > 1,
     # as at N = 1
-    assert d["side_legs_before_headline"] == ["lk_accum", "preprocess"]
+    assert d["side_legs_before_headline"] == ["lk_accum", "preprocess", "settle"]
     assert d["side_legs_before_headline_ranks"] == 2
 
 

@@ -194,9 +194,9 @@ def test_frame_put_dev_matches_host_put(ctx, gvx_mod):
     ctx.frame_drop(22)
 
 
-# gvx_set_klt_phases: the batched LK as phases of 1 (default), 2 or 3 levels,
-# or each point group's whole chain in one wave (0)
-PHASES = [pytest.param(1, id="lpp1"), pytest.param(0, id="chain"), pytest.param(2, id="lpp2"),
+# gvx_set_klt_phases: each point group's whole chain in one wave (0, the
+# default), or the batched LK as phases of 1, 2 or 3 levels
+PHASES = [pytest.param(0, id="chain"), pytest.param(1, id="lpp1"), pytest.param(2, id="lpp2"),
           pytest.param(3, id="lpp3")]
 
 
@@ -204,7 +204,7 @@ PHASES = [pytest.param(1, id="lpp1"), pytest.param(0, id="chain"), pytest.param(
 def phases(ctx, request):
     ctx.set_klt_phases(request.param, 64)  # small superchunks: several per launch, a ragged last one
     yield request.param
-    ctx.set_klt_phases(1, 4096)
+    ctx.set_klt_phases(0, 4096)
 
 
 @pytest.mark.parametrize("phases", PHASES, indirect=True)
