@@ -316,8 +316,40 @@ class KltWorkload:
                                  self.N.data_ptr(), self.B.data_ptr(), self.F.data_ptr(), self.K.data_ptr(),
                                  self.NK.data_ptr(), params=params)
 
-    def run(self, ctx, params, k, pipelined, after_step=None):
-        """k steps; after_step() (if any) is called after each step's LK is enqueued."""
+    # ---- the same steps on two contexts (two streams, no cross-stream waits):
+    # steps take turns on several contexts, each with its own output buffers, so
+    # one stream's pyramid pass and another's LK share the GPU as they come
+    def _outs(self, i):
+        """Output buffers of context i >= 1 of a multi-context run (0: self's)."""
+        import torch
+        if not hasattr(self, "_ox"):
+            self._ox = {}
+        if i not in self._ox:
+            self._ox[i] = dict(N=torch.empty_like(self.Q), B=torch.empty_like(self.Q), F=torch.empty_like(self.F),
+                               K=torch.empty_like(self.K), NK=torch.empty_like(self.NK))
+        return self._ox[i]
+
+    def step_into(self, ctx, params, o):
+        ctx.klt_fb_batch_init_dev(self.n_pairs, self.w, self.h, self.I.data_ptr(), self.J.data_ptr(), self.n,
+                                  self.P.data_ptr(), self.Q.data_ptr(), o["N"].data_ptr(), o["B"].data_ptr(),
+                                  o["F"].data_ptr(), o["K"].data_ptr(), o["NK"].data_ptr(), params=params)
+
+    def run(self, ctx, params, k, pipelined, after_step=None, more=()):
+        """k steps; after_step() (if any) is called after each step's LK is enqueued.
+        more: further contexts -- step t then runs on context t % (1 + len(more)),
+        each with its own output buffers and its own stream, with no waits between
+        the streams (every step reads only the resident inputs)."""
+        if more:
+            ctxs = (ctx,) + tuple(more)
+            for t in range(k):
+                i = t % len(ctxs)
+                if i:
+                    self.step_into(ctxs[i], params, self._outs(i))
+                else:
+                    self.step(ctx, params)
+                if after_step:
+                    after_step()
+            return
         if not pipelined:
             for _ in range(k):
                 self.step(ctx, params)
@@ -385,6 +417,11 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="open the process group even at world size 1 (run under torch.distributed.run): the "
                          "collectives of --gather / configs[4] / max-over-ranks then go through RCCL")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="configs[1]/[2]: contexts (one stream each) the steps take turns on, with no waits between "
+                         "the streams, so one step's pyramid pass and another's LK share the GPU as they come "
+                         "(default 3); 1 = one context, its branch stream carrying batch t+1's pyramid pass beside "
+                         "batch t's LK (or back to back with --no-overlap)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="configs[1]/[2]: pyramid pass and LK back to back (default: batch t+1's pyramid pass on a "
                          "side stream beside batch t's LK -- each fills the other's drain, DESIGN.md 4 / 5)")
@@ -442,33 +479,51 @@ def main():
     accum_cost = accum_leg(ctx, step, gvx, L, steps=max(5, args.steps // 4)) if "lk_accum" in legs else None
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if "preprocess" in legs else None
     pipelined = args.overlap
+    more = tuple(gvx.Context(local) for _ in range(max(1, args.streams) - 1))
     if "settle" in legs:
-        wl.run(ctx, params, SETTLE_STEPS, pipelined)
-        ctx.sync()
+        wl.run(ctx, params, SETTLE_STEPS, pipelined, more=more)
+        for c in (ctx,) + more:
+            c.sync()
     t_side = time.perf_counter() - t_side
     side_ranks = ranks_that_ran(accum_cost is not None, dist, dev)
-    wl.run(ctx, params, args.warmup, pipelined, collect)
+    wl.run(ctx, params, args.warmup, pipelined, collect, more=more)
+    for c in more:
+        c.sync()
     ctx.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    ctx.profile_reset()
-    ctx.profile(True)
+    for c in (ctx,) + more:
+        c.profile_reset()
+        c.profile(True)
     # HIP events on the context stream around the K steps: the device span of the
-    # whole pipeline (the side branch joins back into this stream every step)
+    # whole run (the side branch joins back into this stream every step; the
+    # other contexts' streams wait for ev0 and are waited for before ev1)
     cstream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(cstream)
-    wl.run(ctx, params, args.steps, pipelined, collect)
+    others = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in more]
+    for s_ in others:
+        s_.wait_event(ev0)
+    wl.run(ctx, params, args.steps, pipelined, collect, more=more)
+    for s_ in others:
+        e_ = torch.cuda.Event()
+        e_.record(s_)
+        cstream.wait_event(e_)
     ev1.record(cstream)
-    ctx.sync()
+    for c in (ctx,) + more:
+        c.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     fam = {f: ctx.profile_read(f) for f in ("pyramid", "klt", "compact")}
     ctx.profile(False)
+    for c in more:
+        fam = {f: tuple(a + b for a, b in zip(v, c.profile_read(f))) for f, v in fam.items()}
+        c.profile(False)
+        c.close()
     elapsed = max_over_ranks(elapsed, dist, dev)
     single = single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps=max(200, 5 * args.steps)) \
         if world == 1 and not args.no_pre else None
@@ -554,7 +609,9 @@ def main():
                                    f"maxLevel {L}, win 21, fwd+bwd LK + FB + compaction",
                        "pairs_per_gpu_per_step": Pn, "parallelism": f"pairs sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm",
-                         "kernel": ("klt pipeline per step: batch t+1's pyramid pass beside batch t's LK/FB + "
+                         "kernel": ("klt pipeline (pyramid pass + LK/FB + compaction) per step, steps taking turns "
+                                    "on %d streams" % (1 + len(more)) if more else
+                                    "klt pipeline per step: batch t+1's pyramid pass beside batch t's LK/FB + "
                                     "compaction" if pipelined else
                                     "klt pipeline (pyramid pass + LK/FB + compaction) per step"),
                          "device_span_ms_per_step": round(span_ms, 4),
@@ -577,7 +634,7 @@ def main():
                          "klt_issue": issue_for(workload),
                          "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()},
-                         "overlap": pipelined},
+                         "overlap": pipelined and not more, "streams": 1 + len(more)},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
             "lk_accum": args.accum,

@@ -91,11 +91,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v + (row > 0 ? r0 : 0u) + (row > 1 ? r1 : 0u) + (row > 2 ? r2 : 0u);
 }
 
-// CLAHE_CalcLut_Body for one tile, by one wavefront: h = the tile's 256 bins.
-__device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, int lane, uint8_t* out) {
-    uint32_t h4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) h4[i] = h[4 * lane + i];
+// CLAHE_CalcLut_Body for one tile, by one wavefront: h4 = the lane's bins
+// 4*lane .. 4*lane+3 of the tile's histogram.
+__device__ __forceinline__ void tile_lut4(uint32_t (&h4)[4], const ClaheGeom& g, int lane, uint8_t* out) {
     if (g.clip > 0) {
         const uint32_t clip = (uint32_t)g.clip;
         uint32_t cl = 0;
@@ -134,6 +132,23 @@ __device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, 
     for (int i = 0; i < 4; ++i) packed |= sat_round_u8((float)(base + c4[i]) * g.lut_scale) << (8 * i);
     reinterpret_cast<uint32_t*>(out)[lane] = packed;
 }
+// the same from the tile's 256 bins h (one dword each)
+__device__ __forceinline__ void tile_lut(const uint32_t* h, const ClaheGeom& g, int lane, uint8_t* out) {
+    uint32_t h4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h4[i] = h[4 * lane + i];
+    tile_lut4(h4, g, lane, out);
+}
+
+// fused_kernel's tile histograms (an A/B build switch):
+// CLAHE_PACK 0 = one dword per bin; 1 / 2 = two 16-bit bins per dword (a tile
+// holds at most 1,647 + pad pixels), in 1 / 2 copies (lanes 0-31 / 32-63)
+#ifndef CLAHE_PACK
+#define CLAHE_PACK 0
+#endif
+constexpr int HPK = CLAHE_PACK;
+constexpr int HSTR = HPK ? 129 : HROW;  // dwords per tile histogram
+constexpr int HCOPY = HPK ? HPK : 1;
 
 // cv::cvtColor(COLOR_BGR2GRAY), 8-bit (OpenCV 4.x RGB2Gray<uchar>, tracking.cc:111-113)
 __device__ __forceinline__ uint32_t bgr_gray(uint32_t b, uint32_t g, uint32_t r) {
@@ -475,8 +490,9 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
                                                      uint32_t* __restrict__ hist_img) {
     extern __shared__ float4 smf[];
     uint32_t* tab = reinterpret_cast<uint32_t*>(smf);                      // (tiles_x + 1) * TROW entries
-    uint32_t* hs = tab + (g.tiles_x + 1) * TROW;  // tiles_x histograms, HROW apart
-    uint32_t* lrb = hs + (g.tiles_x + 1) * HROW;   // 2 x tiles_x * 64 dwords: LUT rows by parity
+    uint32_t* hs = tab + (g.tiles_x + 1) * TROW;  // tiles_x (+1 scratch) histograms, HSTR apart, HCOPY copies
+    const int hcs = (g.tiles_x + 1) * HSTR;        // dwords per copy
+    uint32_t* lrb = hs + hcs * HCOPY;              // 2 x tiles_x * 64 dwords: LUT rows by parity
     uint32_t* ih = lrb + 2 * g.tiles_x * 64;       // 256: in-image counts (histogram check)
     const int nb = g.tiles_y + 1;
     const int img = blockIdx.x / nseg, seg = blockIdx.x - img * nseg;
@@ -490,7 +506,24 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
     uint8_t* dd = dst + (int64_t)img * dst_img_stride;
     const float inv_th = 1.0f / g.th, inv_tw = 1.0f / g.tw;
     const int ew = g.tiles_x * g.tw;
-    for (int i = t; i < g.tiles_x * HROW; i += nthr) hs[i] = 0;
+    for (int i = t; i < hcs * HCOPY; i += nthr) hs[i] = 0;
+    // this lane's histogram copy; one bin count of value v into tile offset ho
+    uint32_t* const hmine = hs + ((HPK == 2 && (lane & 32)) ? hcs : 0);
+    auto hadd = [&](uint32_t* h, int ho, uint32_t v) {
+        if constexpr (HPK)
+            atomicAdd(&h[ho + (int)(v >> 1)], 1u << ((v & 1u) << 4));
+        else
+            atomicAdd(&h[ho + (int)v], 1u);
+    };
+    auto hget = [&](int tx, int b) -> uint32_t {  // bin b of tile tx, all copies
+        uint32_t n = 0;
+#pragma unroll
+        for (int c = 0; c < HCOPY; ++c) {
+            const uint32_t d = hs[c * hcs + tx * HSTR + (HPK ? (b >> 1) : b)];
+            n += HPK ? ((d >> ((b & 1) << 4)) & 0xffffu) : d;
+        }
+        return n;
+    };
     if (hist_img)
         for (int i = t; i < 256; i += nthr) ih[i] = 0;
     // column terms: the histogram bin offset (-1 past the image) and the blend terms
@@ -502,7 +535,7 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int x = x0 + j;
-        const int hoff = (x < g.w ? div_small(x, g.tw, inv_tw) : g.tiles_x) * HROW;
+        const int hoff = (x < g.w ? div_small(x, g.tw, inv_tw) : g.tiles_x) * HSTR;
         const float txf = (float)x * inv_tw - 0.5f;
         const int tx1 = (int)floorf(txf);
         const float xa = txf - (float)tx1;
@@ -579,14 +612,14 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t v = ((j < 4 ? px[i].x : px[i].y) >> (8 * (j & 3))) & 255u;
-                atomicAdd(&hs[(kh[j] >> 16) + v], 1u);
+                hadd(hmine, (int)(kh[j] >> 16), v);
             }
         }
         if (hist_img && count_img) {
             __syncthreads();
             for (int b = t; b < 256; b += nthr) {
                 uint32_t sum = 0;
-                for (int tx = 0; tx < g.tiles_x; ++tx) sum += hs[tx * HROW + b];
+                for (int tx = 0; tx < g.tiles_x; ++tx) sum += hget(tx, b);
                 ih[b] += sum;
             }
             __syncthreads();
@@ -596,21 +629,37 @@ __global__ void __launch_bounds__(1024) fused_kernel(const uint8_t* __restrict__
             const int pc = ew - g.w;
             for (int i = t; i < rows_in * pc; i += nthr) {
                 const int r = i / pc, x = g.w + (i - r * pc);
-                atomicAdd(&hs[div_small(x, g.tw, inv_tw) * HROW + pixel(y0 + r, refl101(x, g.w))], 1u);
+                hadd(hs, div_small(x, g.tw, inv_tw) * HSTR, pixel(y0 + r, refl101(x, g.w)));
             }
         }
         const int pr = g.th - rows_in;
         for (int i = t; i < pr * ew; i += nthr) {
             const int r = i / ew, x = i - r * ew;
             const int sy = refl101(y0 + rows_in + r, g.h);
-            atomicAdd(&hs[div_small(x, g.tw, inv_tw) * HROW + pixel(sy, refl101(x, g.w))], 1u);
+            hadd(hs, div_small(x, g.tw, inv_tw) * HSTR, pixel(sy, refl101(x, g.w)));
         }
         __syncthreads();
         uint32_t* lr = lrb + (k & 1) * g.tiles_x * 64;
         for (int tx = wave; tx < g.tiles_x; tx += nwave) {
-            tile_lut(hs + tx * HROW, g, lane, reinterpret_cast<uint8_t*>(lr + tx * 64));
+            if constexpr (HPK) {
+                uint32_t h4[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) hs[tx * HROW + 4 * lane + q] = 0;
+                for (int c = 0; c < HCOPY; ++c) {
+                    uint32_t* h = hs + c * hcs + tx * HSTR + 2 * lane;
+                    const uint32_t d0 = h[0], d1 = h[1];
+                    h4[0] += d0 & 0xffffu;
+                    h4[1] += d0 >> 16;
+                    h4[2] += d1 & 0xffffu;
+                    h4[3] += d1 >> 16;
+                    h[0] = 0;
+                    h[1] = 0;
+                }
+                tile_lut4(h4, g, lane, reinterpret_cast<uint8_t*>(lr + tx * 64));
+            } else {
+                tile_lut(hs + tx * HROW, g, lane, reinterpret_cast<uint8_t*>(lr + tx * 64));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) hs[tx * HROW + 4 * lane + q] = 0;
+            }
         }
         __syncthreads();
     };
@@ -765,7 +814,7 @@ constexpr int FUSED_MIN_BATCH = 8;
 
 // fused_kernel's LDS: the fp32 table, the histograms, two LUT rows, the image histogram
 size_t fused_lds(const ClaheGeom& g) {
-    return (size_t)(g.tiles_x + 1) * TROW * 4 + ((size_t)(g.tiles_x + 1) * HROW + 2 * g.tiles_x * 64 + 256) * 4;
+    return (size_t)(g.tiles_x + 1) * TROW * 4 + ((size_t)(g.tiles_x + 1) * HSTR * HCOPY + 2 * g.tiles_x * 64 + 256) * 4;
 }
 
 struct FusedPlan {

@@ -138,3 +138,35 @@ def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
     for key, o in outs.items():
         for name, a, b in zip(("next", "back", "flags", "kept", "n_kept"), o, outs[(0, 4096)]):
             _assert_same(a, b, f"lpp/superchunk {key} {name}")
+
+
+@pytest.mark.parametrize("n_ctx", [2, 3])
+def test_bench_multi_context_run_equals_step(ctx, gvx_mod, n_ctx):
+    """The headline's default run (bench.KltWorkload.run with further contexts:
+    step t on context t % n_ctx, each with its own stream, pyramid scratch and
+    output buffers, no waits between the streams) gives, on every context's
+    outputs, the bits of the single launch checked against the oracle above."""
+    import torch
+    wl = _workload(1280, 560, 150)
+    p = gvx_mod.KltParams.default(max_level=3)
+    wl.step(ctx, p)
+    ctx.sync()
+    ref = [t.cpu().numpy() for t in (wl.N, wl.B, wl.F, wl.K, wl.NK)]
+    more = tuple(gvx_mod.Context(0) for _ in range(n_ctx - 1))
+    try:
+        outs = [dict(N=wl.N, B=wl.B, F=wl.F, K=wl.K, NK=wl.NK)] + [wl._outs(i) for i in range(1, n_ctx)]
+        for o in outs:
+            for k in ("N", "B"):
+                o[k].fill_(np.nan)
+            o["NK"].fill_(-1)
+        torch.cuda.synchronize()
+        wl.run(ctx, p, 2 * n_ctx + 1, False, more=more)
+        for c in (ctx,) + more:
+            c.sync()
+        for i, o in enumerate(outs):
+            got = [o[k].cpu().numpy() for k in ("N", "B", "F", "K", "NK")]
+            for name, a, b in zip(("next", "back", "flags", "kept_idx", "n_kept"), got, ref):
+                _assert_same(a, b, f"context {i} {name}")
+    finally:
+        for c in more:
+            c.close()

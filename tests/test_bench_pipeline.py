@@ -72,3 +72,21 @@ def test_eager_run_is_one_call_per_step():
     ctx = _Ctx()
     wl.run(ctx, _Params(), 4, False)
     assert [c[0] for c in ctx.calls] == ["klt_fb_batch_init_dev"] * 4
+
+
+def test_multi_context_run_round_robin():
+    """--streams N: step t runs on context t % N, the first context into the
+    workload's own buffers and every other one into buffers of its own."""
+    wl = _workload()
+    ctxs = [_Ctx(), _Ctx(), _Ctx()]
+    steps = []
+    wl.run(ctxs[0], _Params(), 7, True, lambda: steps.append(1), more=tuple(ctxs[1:]))
+    assert len(steps) == 7
+    assert [len(c.calls) for c in ctxs] == [3, 2, 2]
+    for c in ctxs:
+        assert all(name == "klt_fb_batch_init_dev" for name, _ in c.calls)
+    # output pointers (N, B, F, K, NK: args 8..12): one set per context
+    sets = [{tuple(a[8:13]) for _, a in c.calls} for c in ctxs]
+    assert all(len(s) == 1 for s in sets)
+    assert len(set.union(*sets)) == 3
+    assert sets[0] == {(wl.N.data_ptr(), wl.B.data_ptr(), wl.F.data_ptr(), wl.K.data_ptr(), wl.NK.data_ptr())}

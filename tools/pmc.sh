@@ -2,7 +2,10 @@
 # One rocprofv3 --pmc pass per counter group over a short bench run (no trace
 # domains combined with --pmc).  Usage: tools/pmc.sh <tag> "<ctr ctr ..>" ["<ctr ..>" ...]
 # Summarise with: python3 tools/pmc_summary.py gpurun_out/<tag>
-# PMC_BENCH_ARGS overrides the bench arguments (default: the configs[1] batch alone -- --no-pre skips the single-pair and CLAHE launches, whose per-dispatch averages would mix with the batch launches; --no-sequence: under --pmc the sequence leg's torch set-up kernels abort the queue, r05_m1).
+# PMC_BENCH_ARGS overrides the bench arguments (default: the whole default line but the
+# CPU baselines, sequence leg included -- r06: its torch synthesis now synchronises every
+# 64 frames, the backlog that made rocprofv3's counter collection abort the queue in r05_m1).
+# tools/traffic.py takes each kernel's largest-grid (batch) dispatches.
 set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
 T=$1
@@ -13,5 +16,5 @@ i=0
 for grp in "$@"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/$T/p$i \
-     -- python3 $R/bench.py ${PMC_BENCH_ARGS:---steps 3 --warmup 1 --no-cpu --no-pre --no-factors --no-sequence} > $R/gpurun_out/$T/p$i.log 2>&1
+     -- python3 $R/bench.py ${PMC_BENCH_ARGS:---steps 3 --warmup 1 --no-cpu} > $R/gpurun_out/$T/p$i.log 2>&1
 done

@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -- python3 $R/$PROG > $O/p$i.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $O/p$i -- python3 $R/$PROG > $O/p$i.log 2>&1
 done
 cd $R
 python3 tools/pmc_summary.py $O > $O/pmc_summary.txt 2>&1 || true

@@ -7,7 +7,9 @@ import glob
 import sys
 
 
-def load(root):
+def load(root, by_grid=False):
+    """{kernel: {counter: average per dispatch}}; by_grid: keys "name@grid" (the
+    same kernel launched at several sizes, e.g. the batch and a single frame)."""
     # rows of one pass (one rocprofv3 run, its own file) are summed per dispatch;
     # a counter collected in several passes (SQ_WAVES is in every SQ group) is
     # averaged over them -- summing it across passes doubled SQ_WAVES and halved
@@ -17,6 +19,8 @@ def load(root):
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"].replace("(anonymous namespace)", "anon")
             name = kn.split("(")[0].split("<")[0].split("::")[-1] or kn[:40]
+            if by_grid:
+                name = f"{name}@{r['Grid_Size']}"
             acc[name][(r["Counter_Name"], r["Dispatch_Id"])][f] += float(r["Counter_Value"])
     out = {}
     for k, d in acc.items():

@@ -26,7 +26,14 @@ ap.add_argument("--workload", default="klt_fb_batch 256x1280x560 N150 L3")
 ap.add_argument("--pairs", type=int, default=256)
 ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
 a = ap.parse_args()
-res = load(a.pmc_dir)
+# the batch launch of each kernel: the largest grid (a full default line also
+# launches them per frame and per pair)
+res = {}
+for key, d in load(a.pmc_dir, by_grid=True).items():
+    name, grid = key.rsplit("@", 1)
+    if name not in res or int(grid) > res[name][0]:
+        res[name] = (int(grid), d)
+res = {k: v[1] for k, v in res.items()}
 kern = {}
 step = 0.0
 for name, n in list(PER_STEP.items()) + [(k, v) for k, v in OPTIONAL.items() if k in res]:
