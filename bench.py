@@ -634,6 +634,9 @@ def main():
                          "klt_issue": issue_for(workload),
                          "algorithmic_bytes_per_step": B * Pn, "algorithmic_bytes_per_pair": B,
                          "device_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in fam.items()},
+                         "device_ms_note": ("each kernel's own start-stop events summed over its launches; with "
+                                            "several streams the kernels overlap, so these add to more than the "
+                                            "span" if more or pipelined else "back to back: they add to the span"),
                          "overlap": pipelined and not more, "streams": 1 + len(more)},
             "cpu_baseline": cpu,
             "kept_fraction": round(kept_frac, 4),
