@@ -51,8 +51,9 @@ out = {
     "clock_ghz": round(cyc / (sum(durs) / len(durs)) / 1e9, 3) if durs else None,
     "kernel_us_under_pmc": round(sum(durs) / len(durs) * 1e6, 1) if durs else None,
     "source": os.path.relpath(a.pmc_dir),
-    "commit": subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
-                             cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip(),
+    "commit": os.environ.get("GVX_COMMIT") or subprocess.run(
+        ["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+        cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip(),
     "counters": {k: d[k] for k in sorted(d)},
 }
 json.dump(out, open(a.out, "w"), indent=1)

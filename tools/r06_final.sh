@@ -17,6 +17,8 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O
 python3 -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); f=d['factors']; print('bench', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['device_ms_per_step'], f['preint_steps_per_s'], d['sequence']['value'], d['single_pair']['us_per_pair_eager'], d['preprocess']['roofline']['frac'])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -- python3 $R/bench.py --steps 20 --warmup 5 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
+python3 $R/tools/trace_span.py $O/prof/*/*_kernel_trace.csv > $O/trace_span.json && cat $O/trace_span.json
+cp $O/prof/*/*_kernel_stats.csv $O/kernel_stats.csv && gzip -9 $O/prof/*/*_kernel_trace.csv
 echo "kernel trace done"
 cd $R
 ( while sleep 45; do echo "pmc running $(date +%T)"; done ) & TICK=$!
@@ -27,6 +29,10 @@ if [ $rc -eq 0 ]; then
 fi
 kill $TICK
 [ $rc -eq 0 ] || { echo "pmc failed rc=$rc"; tail -20 $O/pmc/p1.log; exit 1; }
+python3 tools/traffic.py $O/pmc --out $O/pmc_traffic.json > /dev/null && python3 tools/issue.py $O/lkpmc --out $O/pmc_issue.json
+python3 tools/pmc_kernel.py $O/lkpmc klt_kernel > $O/lkpmc_klt.txt 2>&1 || true
+gzip -9 $O/pmc/*/*/*.csv $O/lkpmc/*/*/*.csv 2>/dev/null || true
+du -sh $O
 echo "pmc done"
 for c in 3 4 5; do
   timeout -k 10 400 python -u bench.py --config $c --steps 20 --warmup 5 > $O/bench_config$c.json 2> $O/bench_config$c.err || { tail -20 $O/bench_config$c.err; exit 1; }

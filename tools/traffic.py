@@ -44,11 +44,14 @@ for name, n in list(PER_STEP.items()) + [(k, v) for k, v in OPTIONAL.items() if 
     kern[name] = {"bytes_per_launch": b, "fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
                   "launches_per_step": n}
     step += n * b
-try:
-    commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
-                            cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip()
-except OSError:
-    commit = ""
+# the measured code's commit: GVX_COMMIT (the GPU box has no .git), else git HEAD
+commit = os.environ.get("GVX_COMMIT", "")
+if not commit:
+    try:
+        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                                cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip()
+    except OSError:
+        commit = ""
 out = {"workload": a.workload, "pairs_per_step": a.pairs, "bytes_per_step": step, "commit": commit,
        "bytes_per_pair": step / a.pairs, "kernels": kern, "source": os.path.relpath(a.pmc_dir),
        "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md HBM"}
