@@ -476,16 +476,19 @@ def main():
     # a running tracker sees, not during the clock's ramp from idle.
     t_side = time.perf_counter()
     legs = side_legs_before_headline(args)
+    progress("side legs")
     accum_cost = accum_leg(ctx, step, gvx, L, steps=max(5, args.steps // 4)) if "lk_accum" in legs else None
     pre = preprocess_leg(ctx, dI, dJ, Pn, W, H, args.steps) if "preprocess" in legs else None
     pipelined = args.overlap
     more = tuple(gvx.Context(local) for _ in range(max(1, args.streams) - 1))
+    progress("settle")
     if "settle" in legs:
         wl.run(ctx, params, SETTLE_STEPS, pipelined, more=more)
         for c in (ctx,) + more:
             c.sync()
     t_side = time.perf_counter() - t_side
     side_ranks = ranks_that_ran(accum_cost is not None, dist, dev)
+    progress("warm-up and timed steps")
     wl.run(ctx, params, args.warmup, pipelined, collect, more=more)
     for c in more:
         c.sync()
@@ -525,6 +528,7 @@ def main():
         c.profile(False)
         c.close()
     elapsed = max_over_ranks(elapsed, dist, dev)
+    progress("single pair")
     single = single_pair_leg(ctx, dI, dJ, dP, dQ, W, H, N, params, reps=max(200, 5 * args.steps)) \
         if world == 1 and not args.no_pre else None
     pcie = None
@@ -550,11 +554,13 @@ def main():
 
     # the metric's second half (BASELINE.json: factor-Jacobian eval/s), timed in
     # the same run: configs[3]'s factor batch (its own line under "factors")
+    progress("factors")
     factors = None if args.no_factors else factor_leg(args, ctx, dev, dist, world, rank,
                                                       steps=max(10, args.steps // 2), window_extras=False)
     # the north_star scaling workload, timed in the same run at every N: one
     # configs[4] sequence per GPU replayed on the device, then every rank's
     # per-frame tracks gathered to rank 0 over RCCL (its own line under "sequence")
+    progress("sequence")
     seq = None if args.no_sequence else sequence_leg(args, ctx, dev, dist, world, rank, args.seq_frames)
     kept_frac = float(dNK.float().mean().item()) / N
     total_pairs = world * Pn * args.steps
@@ -1442,6 +1448,12 @@ def spawn_ranks(n):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.setdefault("OMP_NUM_THREADS", "4")
     return subprocess.run(cmd, env=env).returncode
+
+
+def progress(what):
+    """GVX_BENCH_TRACE=1: one stderr line per leg (where a run under a profiler stalls)."""
+    if os.environ.get("GVX_BENCH_TRACE"):
+        print(f"[bench {time.strftime('%H:%M:%S')}] {what}", file=sys.stderr, flush=True)
 
 
 def side_legs_before_headline(args):

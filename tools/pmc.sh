@@ -18,6 +18,6 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/$T/p$i \
+  GVX_BENCH_TRACE=1 timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/$T/p$i \
      -- python3 $R/bench.py ${PMC_BENCH_ARGS:---steps 3 --warmup 1 --no-cpu --streams 1} > $R/gpurun_out/$T/p$i.log 2>&1
 done

@@ -23,7 +23,7 @@ echo "kernel trace done"
 cd $R
 ( while sleep 45; do echo "pmc running $(date +%T)"; done ) & TICK=$!
 rc=0
-bash tools/pmc.sh $T/pmc FETCH_SIZE WRITE_SIZE || rc=$?
+PMC_BENCH_ARGS="${TRAFFIC_ARGS:---steps 3 --warmup 1 --no-cpu --streams 1 --no-overlap --no-sequence}" bash tools/pmc.sh $T/pmc FETCH_SIZE WRITE_SIZE || rc=$?
 if [ $rc -eq 0 ]; then
   bash tools/pmc_prog.sh $T/lkpmc "tools/lk_pmc.py 30 10" "SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" || rc=$?
 fi
@@ -38,3 +38,14 @@ for c in 3 4 5; do
   timeout -k 10 400 python -u bench.py --config $c --steps 20 --warmup 5 > $O/bench_config$c.json 2> $O/bench_config$c.err || { tail -20 $O/bench_config$c.err; exit 1; }
   tail -c 300 $O/bench_config$c.json; echo
 done
+if [ -n "$DIAG" ]; then
+  # one counter pass over the whole default line (sequence leg included), with the
+  # bench's leg progress on stderr: where a stall under counter collection sits
+  ( while sleep 45; do echo "pmc full line running $(date +%T)"; done ) & TICK=$!
+  rc=0
+  PMC_BENCH_ARGS="--steps 3 --warmup 1 --no-cpu --streams 1" bash tools/pmc.sh $T/pmcfull FETCH_SIZE || rc=$?
+  kill $TICK
+  grep "^\[bench" $O/pmcfull/p1.log || true
+  echo "full-line pmc rc=$rc"
+  gzip -9 $O/pmcfull/*/*/*.csv 2>/dev/null || true
+fi
