@@ -15,6 +15,7 @@ Usage: python3 tools/issue.py gpurun_out/<tag>/lkpmc [--kernel klt_kernel]"""
 import argparse
 import csv
 import glob
+import gzip
 import json
 import os
 import subprocess
@@ -36,8 +37,8 @@ need = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_WAVES", "G
 if d is None or any(k not in d for k in need):
     sys.exit(f"{a.kernel}: need {need} in {a.pmc_dir}")
 durs = []
-for f in glob.glob(f"{a.pmc_dir}/**/*kernel_trace.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
+for f in glob.glob(f"{a.pmc_dir}/**/*kernel_trace.csv*", recursive=True):
+    for r in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
         if a.kernel in r["Kernel_Name"]:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
 cyc = d["GRBM_GUI_ACTIVE"] / 8.0

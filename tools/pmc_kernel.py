@@ -6,6 +6,7 @@ output directory, per wave, with the gfx950 quad-cycle correction for SQ_*CYCLES
 import collections
 import csv
 import glob
+import gzip
 import sys
 
 root, name = sys.argv[1], sys.argv[2]
@@ -13,8 +14,8 @@ root, name = sys.argv[1], sys.argv[2]
 # several passes (SQ_WAVES, in every group) is averaged over them.  Through r05
 # it was summed, which doubled SQ_WAVES and halved every per-wave figure.
 raw = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
+for f in glob.glob(f"{root}/**/*counter_collection.csv*", recursive=True):
+    for r in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
         if name not in r["Kernel_Name"]:
             continue
         key = (int(r["Grid_Size"]), r["Dispatch_Id"])

@@ -4,6 +4,7 @@ Applies the gfx950 corrections of MI355X_MICROARCH.md: FETCH_SIZE reads half
 import collections
 import csv
 import glob
+import gzip
 import sys
 
 
@@ -15,8 +16,10 @@ def load(root, by_grid=False):
     # averaged over them -- summing it across passes doubled SQ_WAVES and halved
     # every per-wave figure through r05
     acc = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
-    for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
+    files = glob.glob(f"{root}/**/*counter_collection.csv", recursive=True) + \
+        glob.glob(f"{root}/**/*counter_collection.csv.gz", recursive=True)
+    for f in files:
+        for r in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
             kn = r["Kernel_Name"].replace("(anonymous namespace)", "anon")
             name = kn.split("(")[0].split("<")[0].split("::")[-1] or kn[:40]
             if by_grid:

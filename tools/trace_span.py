@@ -9,6 +9,7 @@ timed compaction's end, and each kernel's own duration (mean over the K steps),
 to set beside the bench line's device_span_ms_per_step / device_ms_per_step.
     python3 tools/trace_span.py <kernel_trace.csv> [K] [W]"""
 import csv
+import gzip
 import json
 import sys
 
@@ -19,7 +20,7 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 acc = {"stream_kernel": [], "klt_kernel<3, 0>": [], "compact_kernel": []}
 grids = {"stream_kernel": None, "klt_kernel<3, 0>": None, "compact_kernel": None}
-rows = list(csv.DictReader(open(path)))
+rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
 for r in rows:
     for k in acc:
         if k in r["Kernel_Name"]:
