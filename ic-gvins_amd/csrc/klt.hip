@@ -1497,6 +1497,9 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
     // fp32-order window sums: one region per point group
     __shared__ __attribute__((aligned(16))) float accs[ACC ? KLT_WPB * PPW : 1][ACC_FLOATS];
     KLT_WAVE_STAMP;
+#ifdef KLT_PRIO
+    __builtin_amdgcn_s_setprio(KLT_PRIO);  // A/B
+#endif
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wpp = (a.n_pts + PPW - 1) / PPW;  // waves per pair (launch capacity)
     const int n_waves = a.n_pairs * wpp;

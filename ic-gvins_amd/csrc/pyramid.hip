@@ -616,6 +616,9 @@ __global__ void __launch_bounds__(64 * WPB, STREAM_OCC) stream_kernel(StreamSrc 
 #ifdef GVX_KLT_TRACE
     WaveStamp wave_stamp_(gvx_pyr_trace_buf);
 #endif
+#ifdef PYR_PRIO
+    __builtin_amdgcn_s_setprio(PYR_PRIO);  // A/B: the pass's waves issue first on a shared SIMD
+#endif
     const int lane = threadIdx.x & 63;
     const int nblk = (n_units + WPB - 1) / WPB;
     const int unit = xcd_swizzle(blockIdx.x, nblk) * WPB + (WPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0);
