@@ -225,25 +225,30 @@ def cpu_preint_baseline(segs, states, iewn, threads, budget_s=2.0):
                       f"one segment per call, {threads} thread(s), {dt:.1f} s"}
 
 
+def _record_for(pattern, workload):
+    """The profiles/<pattern> JSON record measured on this workload, or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            return d
+    return None
+
+
 def traffic_for(workload):
-    """PMC HBM bytes per step measured on this workload (tools/traffic.py)."""
-    f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        d = json.load(open(f))
-    except (OSError, ValueError):
-        return None
-    return d if d.get("workload") == workload else None
+    """PMC HBM bytes per step measured on this workload (tools/traffic.py:
+    profiles/pmc_traffic.json for configs[1], pmc_traffic_*.json for others)."""
+    return _record_for("pmc_traffic*.json", workload)
 
 
 def issue_for(workload):
     """LK's VALU-issue fraction on this workload (tools/issue.py: one PMC pass,
     profiles/pmc_issue.json), or None."""
-    f = os.path.join(ROOT, "profiles", "pmc_issue.json")
-    try:
-        d = json.load(open(f))
-    except (OSError, ValueError):
-        return None
-    if d.get("workload") != workload:
+    d = _record_for("pmc_issue*.json", workload)
+    if d is None:
         return None
     return {k: d[k] for k in ("valu_busy", "resident_waves_per_simd", "max_waves_per_simd", "valu_insts_per_wave",
                               "clock_ghz", "source", "commit") if k in d}

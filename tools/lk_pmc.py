@@ -3,7 +3,7 @@
 LK/FB + compaction) for PMC passes of klt_kernel: K steps at the given LK
 iteration cap (default 30, the reference's criteria; 0 = the window
 extractions and level set-up alone, so iterations = full - capped).
-    python3 tools/lk_pmc.py [max_iter] [steps]"""
+    python3 tools/lk_pmc.py [max_iter] [steps] [3 = configs[2] geometry]"""
 import os
 import sys
 
@@ -15,10 +15,12 @@ import bench  # noqa: E402
 
 it = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+# geometry: configs[1] by default; "3" = configs[2] (1920x1200, 500 points, maxLevel 4)
+W_, H_, N_, L_ = (1920, 1200, 500, 4) if len(sys.argv) > 3 and sys.argv[3] == "3" else (1280, 560, 150, 3)
 dev = torch.device("cuda", 0)
 ctx = gvx.Context(0)
-wl = bench.KltWorkload(256, 1280, 560, 150, dev)
-p = gvx.KltParams.default(max_level=3, max_iter=it)
+wl = bench.KltWorkload(256, W_, H_, N_, dev)
+p = gvx.KltParams.default(max_level=L_, max_iter=it)
 for _ in range(k):
     wl.step(ctx, p)
 ctx.sync()
