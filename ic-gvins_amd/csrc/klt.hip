@@ -1188,6 +1188,21 @@ __device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X,
 // phase's wave; `resolve(nx, ny)` supplies it before the first level.  (Resolving
 // it after the top level's extraction, to hide the load behind the extraction's
 // own, costs 5 spilled VGPRs at 128.)  A whole-chain call resolves nothing.
+// KLT_LONE: when one group of the three is left iterating a level, the wave
+// finishes that point with one unit per lane over all 64 lanes (lone mode, in
+// lk_group3) instead of 21 lanes doing three units each.  Bit-identical (the
+// parity suite passes on it), but slower on the configs[1] headline: 0.455-0.457
+// against 0.427-0.431 ms per step (profiles/r06_ab, r06_a11).  The switch, the
+// J-row reload and the state hand-off cost more than the 17 % of wave-iterations
+// that run one group save.  Off.
+#ifndef KLT_LONE
+#define KLT_LONE 0
+#endif
+#if KLT_LONE
+__device__ __forceinline__ uint64_t gmask3(int g) {
+    return g == 0 ? (1ull << G3) - 1 : g == 1 ? ((1ull << G3) - 1) << G3 : ~0ull << (2 * G3);
+}
+#endif
 struct NoResolve {
     __device__ void operator()(float&, float&) const {}
 };
@@ -1319,10 +1334,42 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
         int cinx = INT_MIN, ciny = INT_MIN;
-        uint32_t jr[4][4];  // the lane's four J rows as spread byte pairs
+        uint32_t jr[4][4] = {};  // the lane's four J rows as spread byte pairs (defined: an undefined
+                                 // start lets the rows live across the levels, spilled around the extraction)
         bool more = cfg.max_iter > 0;
         int j = 0;
+#if KLT_LONE
+        // lone mode needs every lane: all three groups start the level's iterations
+        const bool lone_ok = __builtin_amdgcn_ballot_w64(true) == ~0ull;
+#endif
         while (more) {
+#if KLT_LONE
+            if (lone_ok) {
+                const uint64_t m = __builtin_amdgcn_ballot_w64(true);
+                const int g = grp3(__builtin_ctzll(m));
+                if ((m & ~gmask3(g)) == 0) {
+                    // one group left: its state goes through the (idle) tile, not
+                    // through registers live out of the loop
+                    const int k = lane_v() - G3 * g;
+                    if (k == 0) {
+                        win[0] = __builtin_bit_cast(uint32_t, nextx);
+                        win[1] = __builtin_bit_cast(uint32_t, nexty);
+                        win[2] = __builtin_bit_cast(uint32_t, pdx);
+                        win[3] = __builtin_bit_cast(uint32_t, pdy);
+                        win[4] = (uint32_t)j;
+                        win[5] = __builtin_bit_cast(uint32_t, A11);
+                        win[6] = __builtin_bit_cast(uint32_t, A12);
+                        win[7] = __builtin_bit_cast(uint32_t, A22);
+                        win[8] = __builtin_bit_cast(uint32_t, D);
+                    }
+                    if (k < G3) {
+                        win[32 + k] = (uint32_t)c1;
+                        win[64 + k] = (uint32_t)c2;
+                    }
+                    break;
+                }
+            }
+#endif
             const float fnx = floorf(nextx), fny = floorf(nexty);
             const int fxi = (int)fnx, fyi = (int)fny;
             const int inx = min(max(fxi, -WIN), W - 1), iny = min(max(fyi, -WIN), H - 1);
@@ -1398,6 +1445,96 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
             pdy = dy;
             more = !oob && !conv && !osc && ++j < cfg.max_iter;
         }
+#if KLT_LONE
+        if (lone_ok && __builtin_amdgcn_ballot_w64(more)) {
+            // Lone mode: group lg's point, unit k = lane (window rows k / 3,
+            // segment k % 3; lane 63 has none) read from its owner lane's slot.
+            // The same integer partials in another arrangement, so the same exact
+            // sums and the same fp32 steps; every lane carries the point's state.
+            const int lg = grp3(__builtin_ctzll(__builtin_amdgcn_ballot_w64(more))), sl = G3 * lg;
+            const int k = min(lane_v(), 62), lr = k / 3, ls = k - 3 * lr;
+            const bool live = lane_v() < 63;
+            const v4u* uo = units + (sl + 3 * (lr / 3) + ls);
+            const int slot = lr - 3 * (lr / 3);
+            const int loff = __mul24(lr, pitch) + 7 * ls;
+            const auto rdf = [&](float v) {
+                return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), sl));
+            };
+            const auto wf = [&](int i) { return __builtin_bit_cast(float, win[i]); };
+            wave_lds_sync();
+            const int lc1 = lane_v() < G3 ? (int)win[32 + min(lane_v(), G3 - 1)] : 0;
+            const int lc2 = lane_v() < G3 ? (int)win[64 + min(lane_v(), G3 - 1)] : 0;
+            const float LA11 = wf(5), LA12 = wf(6), LA22 = wf(7), LD = wf(8);
+            float lx = wf(0), ly = wf(1), lpdx = wf(2), lpdy = wf(3);
+            int lj = (int)win[4];
+            float lnx = rdf(nx), lny = rdf(ny);
+            int lst = __builtin_amdgcn_readlane(status, sl);
+            int lcx = INT_MIN, lcy = INT_MIN;
+            uint32_t h0[4], h1[4];
+            bool lmore = true;
+            while (lmore) {
+                const float fnx = floorf(lx), fny = floorf(ly);
+                const int fxi = (int)fnx, fyi = (int)fny;
+                const int inx = min(max(fxi, -WIN), W - 1), iny = min(max(fyi, -WIN), H - 1);
+                const bool oob = inx != fxi || iny != fyi;
+                uint32_t J0, J1;
+                weights(lx - fnx, ly - fny, J0, J1);
+                if (inx != lcx || iny != lcy) {
+                    const bool fast = !raw || (inx >= 3 && inx + 26 <= W && iny >= 0 && iny + 22 <= H);
+                    if (fast) {
+                        const int off = loff + (PJ.o0 + iny * PJ.pitch + inx);
+                        const int al = off & ~3;
+                        const uint32_t sh = (uint32_t)off & 3u;
+                        const v3u w0 = __builtin_amdgcn_raw_buffer_load_b96(PJ.rs, al, 0, 0);
+                        const v3u w1 = __builtin_amdgcn_raw_buffer_load_b96(PJ.rs, al, PJ.pitch, 0);
+                        spread_row(w0.x, w0.y, w0.z, sh, h0);
+                        spread_row(w1.x, w1.y, w1.z, sh, h1);
+                    } else {
+                        fill_win_active(win, PJ, W, H, inx, iny, WIN + 1);
+                        uint32_t t[2];
+                        read_win<2>(win, lr, 7 * ls, t);
+                        spread_row2(t, h0);
+                        read_win<2>(win, lr + 1, 7 * ls, t);
+                        spread_row2(t, h1);
+                    }
+                    lcx = inx;
+                    lcy = iny;
+                }
+                int b1 = -lc1, b2 = -lc2;
+                const v4u* ul = uo;
+                asm volatile("" : "+v"(ul));  // the slot reads stay in the loop (registers)
+                if ((int)J1 < 0)
+                    match_grad_h<true>(ul, slot, h0, h1, J0, J1, b1, b2);
+                else
+                    match_grad_h<false>(ul, slot, h0, h1, J0, J1, b1, b2);
+                b1 = live ? b1 : 0;
+                b2 = live ? b2 : 0;
+                float fb1, fb2;
+                group_sums_f32_fast<64>(b1, b2, fb1, fb2);
+                fb1 *= FLT_SCALE;
+                fb2 *= FLT_SCALE;
+                const float dx = (LA12 * fb2 - LA22 * fb1) * LD;
+                const float dy = (LA12 * fb1 - LA11 * fb2) * LD;
+                const float tx = lx + dx, ty = ly + dy;
+                const bool conv = __builtin_fma((double)dx, (double)dx, (double)dy * (double)dy) <= cfg.crit_eps;
+                const bool osc = !conv && lj > 0 && fabsf(dx + lpdx) < 0.01f && fabsf(dy + lpdy) < 0.01f;
+                const float ux = osc ? (tx + halfw) - dx * 0.5f : tx + halfw;
+                const float uy = osc ? (ty + halfw) - dy * 0.5f : ty + halfw;
+                lnx = oob ? lnx : ux;
+                lny = oob ? lny : uy;
+                lx = oob ? lx : tx;
+                ly = oob ? ly : ty;
+                lst = (oob && l == 0) ? 0 : lst;
+                lpdx = dx;
+                lpdy = dy;
+                lmore = !oob && !conv && !osc && ++lj < cfg.max_iter;
+            }
+            const bool mine = grp3(lane_v()) == lg;
+            nx = mine ? lnx : nx;
+            ny = mine ? lny : ny;
+            status = mine ? lst : status;
+        }
+#endif
         if (status && l == 0) {
             const float exf = nx - halfw, eyf = ny - halfw;
             const float fex = floorf(exf), fey = floorf(eyf);
