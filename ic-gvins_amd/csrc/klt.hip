@@ -390,18 +390,23 @@ __device__ __forceinline__ void spread_row(uint32_t x, uint32_t y, uint32_t z, u
 __device__ __forceinline__ void spread_row2(const uint32_t (&r)[2], uint32_t (&h)[4]) {
     spread_row(r[0], r[1], r[1], 0, h);
 }
-__device__ __forceinline__ void j_pairs_h(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t W0, uint32_t W1,
+// the seven pixel pairs of a spread row (the odd ones are shifted pairs)
+__device__ __forceinline__ void spread7(const uint32_t (&h)[4], uint32_t (&p)[7]) {
+#pragma unroll
+    for (int t = 0; t < 7; ++t) p[t] = spread_pair(h, t);
+}
+__device__ __forceinline__ void j_pairs_p(const uint32_t (&p0)[7], const uint32_t (&p1)[7], uint32_t W0, uint32_t W1,
                                           uint32_t (&jp)[4]) {
     constexpr uint32_t RND = 1u << (W_BITS - 6 + 7);
     uint32_t X[8];
 #pragma unroll
-    for (int t = 0; t < 7; ++t) X[t] = udot2(spread_pair(h1, t), W1, udot2k(spread_pair(h0, t), W0, RND));
+    for (int t = 0; t < 7; ++t) X[t] = udot2(p1[t], W1, udot2k(p0[t], W0, RND));
     X[7] = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) jp[k] = __builtin_amdgcn_perm(X[2 * k + 1], X[2 * k], 0x07060302u);  // (X0 >> 16, X1 >> 16)
 }
-// the signed form (w11 < 0) from the spread rows: plain bytes are the pairs >> 7
-__device__ __forceinline__ void j_pairs_h_signed(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t W0,
+// the signed form (w11 < 0) from the spread pairs: plain bytes are the pairs >> 7
+__device__ __forceinline__ void j_pairs_p_signed(const uint32_t (&p0)[7], const uint32_t (&p1)[7], uint32_t W0,
                                                  uint32_t W1, uint32_t (&jp)[4]) {
     constexpr int RND = 1 << (W_BITS - 6);
     const auto plain = [](uint32_t v) {
@@ -409,11 +414,24 @@ __device__ __forceinline__ void j_pairs_h_signed(const uint32_t (&h0)[4], const 
     };
     int jv[8];
 #pragma unroll
-    for (int t = 0; t < 7; ++t)
-        jv[t] = dot2(plain(spread_pair(h1, t)), W1, dot2k(plain(spread_pair(h0, t)), W0, RND)) >> (W_BITS - 5);
+    for (int t = 0; t < 7; ++t) jv[t] = dot2(plain(p1[t]), W1, dot2k(plain(p0[t]), W0, RND)) >> (W_BITS - 5);
     jv[7] = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) jp[k] = pack16(jv[2 * k], jv[2 * k + 1]);
+}
+__device__ __forceinline__ void j_pairs_h(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t W0, uint32_t W1,
+                                          uint32_t (&jp)[4]) {
+    uint32_t p0[7], p1[7];
+    spread7(h0, p0);
+    spread7(h1, p1);
+    j_pairs_p(p0, p1, W0, W1, jp);
+}
+__device__ __forceinline__ void j_pairs_h_signed(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t W0,
+                                                 uint32_t W1, uint32_t (&jp)[4]) {
+    uint32_t p0[7], p1[7];
+    spread7(h0, p0);
+    spread7(h1, p1);
+    j_pairs_p_signed(p0, p1, W0, W1, jp);
 }
 // an iteration's products of one unit: b1 += sum J Ix, b2 += sum J Iy (the I
 // side of b = sum (J - I) I' is the level's constant, subtracted once)
@@ -1070,19 +1088,27 @@ __device__ __forceinline__ void fill_win_active(uint32_t* win, const Plane& P, i
 // The J side of match_unit_h for unit slot s: b1 += sum J Ix, b2 += sum J Iy over
 // its pixels (the gradients read from the slot; I is not needed)
 template <bool SIGNED>
-__device__ __forceinline__ void match_grad_h(const v4u* ust, int s, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
+__device__ __forceinline__ void match_grad_p(const v4u* ust, int s, const uint32_t (&p0)[7], const uint32_t (&p1)[7],
                                              uint32_t W0, uint32_t W1, int& b1, int& b2) {
     const v4u gx = ust[(3 * s + 1) * 64], gy = ust[(3 * s + 2) * 64];
     uint32_t jp[4];
     if constexpr (SIGNED)
-        j_pairs_h_signed(h0, h1, W0, W1, jp);
+        j_pairs_p_signed(p0, p1, W0, W1, jp);
     else
-        j_pairs_h(h0, h1, W0, W1, jp);
+        j_pairs_p(p0, p1, W0, W1, jp);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         b1 = dot2(jp[k], gx[k], b1);
         b2 = dot2(jp[k], gy[k], b2);
     }
+}
+template <bool SIGNED>
+__device__ __forceinline__ void match_grad_h(const v4u* ust, int s, const uint32_t (&h0)[4], const uint32_t (&h1)[4],
+                                             uint32_t W0, uint32_t W1, int& b1, int& b2) {
+    uint32_t p0[7], p1[7];
+    spread7(h0, p0);
+    spread7(h1, p1);
+    match_grad_p<SIGNED>(ust, s, p0, p1, W0, W1, b1, b2);
 }
 
 // A lane's three units from its six source rows d[r] (bytes X .. X+11, X =
@@ -1334,8 +1360,9 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
         nexty -= halfw;
         float pdx = 0.f, pdy = 0.f;
         int cinx = INT_MIN, ciny = INT_MIN;
-        uint32_t jr[4][4] = {};  // the lane's four J rows as spread byte pairs (defined: an undefined
-                                 // start lets the rows live across the levels, spilled around the extraction)
+        // the lane's four J rows as their seven spread pixel pairs, formed once per
+        // reload (defined: an undefined start lets the rows live across the levels)
+        uint32_t jr[4][7] = {};
         bool more = cfg.max_iter > 0;
         int j = 0;
 #if KLT_LONE
@@ -1386,7 +1413,11 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
 #pragma unroll
                     for (int r = 0; r < 4; ++r) w[r] = __builtin_amdgcn_raw_buffer_load_b96(PJ.rs, al, r * PJ.pitch, 0);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) spread_row(w[r].x, w[r].y, w[r].z, sh, jr[r]);
+                    for (int r = 0; r < 4; ++r) {
+                        uint32_t h[4];
+                        spread_row(w[r].x, w[r].y, w[r].z, sh, h);
+                        spread7(h, jr[r]);
+                    }
                 } else {
                     const int g = grp3(lane_v());
                     uint32_t nj[4][4];
@@ -1407,9 +1438,7 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
                         }
                     }
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) jr[r][q] = nj[r][q];
+                    for (int r = 0; r < 4; ++r) spread7(nj[r], jr[r]);
                 }
                 cinx = inx;
                 ciny = iny;
@@ -1420,10 +1449,10 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
             int b1 = -c1, b2 = -c2;
             if (__builtin_amdgcn_ballot_w64((int)J1 < 0)) {
 #pragma unroll
-                for (int s = 0; s < 3; ++s) match_grad_h<true>(ust, s, jr[s], jr[s + 1], J0, J1, b1, b2);
+                for (int s = 0; s < 3; ++s) match_grad_p<true>(ust, s, jr[s], jr[s + 1], J0, J1, b1, b2);
             } else {
 #pragma unroll
-                for (int s = 0; s < 3; ++s) match_grad_h<false>(ust, s, jr[s], jr[s + 1], J0, J1, b1, b2);
+                for (int s = 0; s < 3; ++s) match_grad_p<false>(ust, s, jr[s], jr[s + 1], J0, J1, b1, b2);
             }
             float fb1, fb2;
             gsums_f32_fast3(b1, b2, fb1, fb2, ga);
