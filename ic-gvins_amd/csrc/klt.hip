@@ -1126,12 +1126,15 @@ __device__ __forceinline__ void extract_triple(const uint32_t (&d)[6][3], int X,
     for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int k = 0; k < 5; ++k) E[r][k] = bpair(d[r], 2 * k);
-    uint32_t cm[4];
+    // column masks for border windows, formed only when the wave holds one
+    uint32_t cm[4] = {~0u, ~0u, ~0u, ~0u};
+    if (__builtin_amdgcn_ballot_w64(!interior)) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const bool lo = (unsigned)(X + 2 * k + 1) < (unsigned)W;
-        const bool hi = (unsigned)(X + 2 * k + 2) < (unsigned)W;
-        cm[k] = (lo ? 0xffffu : 0u) | (hi ? 0xffff0000u : 0u);
+        for (int k = 0; k < 4; ++k) {
+            const bool lo = (unsigned)(X + 2 * k + 1) < (unsigned)W;
+            const bool hi = (unsigned)(X + 2 * k + 2) < (unsigned)W;
+            cm[k] = (lo ? 0xffffu : 0u) | (hi ? 0xffff0000u : 0u);
+        }
     }
     int iv[7], ix[7], iy[7];
     a11 = a12 = a22 = 0;
@@ -1361,8 +1364,13 @@ __device__ __forceinline__ void lk_group3(const uint8_t* __restrict__ I, const u
         float pdx = 0.f, pdy = 0.f;
         int cinx = INT_MIN, ciny = INT_MIN;
         // the lane's four J rows as their seven spread pixel pairs, formed once per
-        // reload (defined: an undefined start lets the rows live across the levels)
-        uint32_t jr[4][7] = {};
+        // reload.  Defined here by an empty asm: an undefined start lets the rows live
+        // across the levels (spills at 128 VGPRs), and zeros cost a move per register
+        uint32_t jr[4][7];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) asm volatile("" : "=v"(jr[r][t]));
         bool more = cfg.max_iter > 0;
         int j = 0;
 #if KLT_LONE
