@@ -202,6 +202,8 @@ gvx_status gvx_create(int32_t device, gvx_ctx** out) {
         if (pw) c->pyr_wpb = std::atoi(pw) == 4 ? 4 : 1;
         const char* po = std::getenv("GVX_PYR_ORDER");
         if (po) c->pyr_order = std::atoi(po) != 0;
+        const char* fc = std::getenv("GVX_FUSED_COMPACT");
+        if (fc) c->fused_compact = std::atoi(fc) != 0;
     }
     *out = c;
     return GVX_OK;
@@ -504,13 +506,12 @@ static gvx_status klt_single(gvx_ctx* c, uint64_t prev_id, uint64_t next_id, con
     a.cam_w = cam_w;
     a.cam_h = cam_h;
     const Level0 l0{fp.pyr + lay.off[0], fn.pyr + lay.off[0], 0, 0, PAD * lay.pitch[0] + PAD, lay.pitch[0], 0};
-    e = launch_klt(c, a, lay, fp.pyr, fn.pyr, 0, 0, l0, d_prev, d_next, mode ? d_back : nullptr, d_flags,
-                   d_err);
-    if (e != hipSuccess) return hip_err(c, e, "klt kernel");
-    if (mode == 1) {
-        e = launch_compact(c, 1, n, d_flags, d_kept, d_nkept);
-        if (e != hipSuccess) return hip_err(c, e, "compact kernel");
-    }
+    if (mode == 1)
+        e = launch_klt_compact(c, a, lay, fp.pyr, fn.pyr, 0, 0, l0, d_prev, d_next, d_back, d_flags, d_err, d_kept,
+                               d_nkept);
+    else
+        e = launch_klt(c, a, lay, fp.pyr, fn.pyr, 0, 0, l0, d_prev, d_next, nullptr, d_flags, d_err);
+    if (e != hipSuccess) return hip_err(c, e, "klt kernels");
     // one D2H of next | back | err | kept | n_kept | flags
     const size_t tail = 2 * fb_bytes + sizeof(float) * n + sizeof(int32_t) * (n + 1) + n;
     e = hipMemcpyAsync(h_next, d_next, tail, hipMemcpyDeviceToHost, c->stream);
@@ -593,11 +594,9 @@ static gvx_status klt_batch_on_pyramids(gvx_ctx* c, const PyrLayout& lay, int32_
     // reads the initial flow
     a.init_xy = d_init_xy;
     const Level0 l0{d_prev, d_next, (int64_t)w * h, (int64_t)w * h, 0, w, 1};
-    e = launch_klt(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, l0, d_prev_xy, d_next_xy, d_back_xy,
-                   d_flags, nullptr);
-    if (e != hipSuccess) return hip_err(c, e, "klt kernel");
-    e = launch_compact(c, n_pairs, n_pts, d_flags, d_kept_idx, d_n_kept);
-    return hip_err(c, e, "compact kernel");
+    e = launch_klt_compact(c, a, lay, pyr_prev, pyr_next, lay.bytes, lay.bytes, l0, d_prev_xy, d_next_xy,
+                           d_back_xy, d_flags, nullptr, d_kept_idx, d_n_kept);
+    return hip_err(c, e, "klt kernels");
 }
 
 static gvx_status check_batch(gvx_ctx* c, int32_t n_pairs, int32_t w, int32_t h, const uint8_t* d_prev,

@@ -113,6 +113,9 @@ struct gvx_ctx {
     // pyramid pass (stream_kernel): waves per workgroup (1 or 4) and work order
     // (1: edge strips first); GVX_PYR_WPB / GVX_PYR_ORDER at creation (A/B)
     int pyr_wpb = 1, pyr_order = 0;
+    // small fwd + bwd launches (one point per wave) compact inside the LK launch
+    // instead of a compact_kernel launch; GVX_FUSED_COMPACT=0 at creation: off (A/B)
+    bool fused_compact = true;
     // GVX_SIDE_LOW_PRIO=1 at creation: the branch stream at the lowest priority,
     // the context stream at the highest (work on the branch fills the gaps); 2:
     // the other way round; 0 (default): both at the default priority
@@ -229,6 +232,13 @@ struct KltArgs {
     const int32_t* n_dev = nullptr;
     // initial flow read from here instead of next_xy (which is then output only)
     const float* init_xy = nullptr;
+    // compaction inside the LK launch (one point per wave, mode 1, no n_dev):
+    // per pair ceil(n_pts / 64) keep-bit words and an arrival count, zero at
+    // launch; the last wave of a pair writes kept_idx / n_kept (compact_kernel's
+    // result) and zeroes them again (klt.hip fused_compact)
+    unsigned long long* cmask = nullptr;
+    int32_t* kept_idx = nullptr;
+    int32_t* n_kept = nullptr;
 };
 
 // Level 0 of pair i: prev plane at prev + i*prev_stride, pixel (x, y) at byte
@@ -250,6 +260,13 @@ hipError_t launch_klt(gvx_ctx* c, const KltArgs& a, const PyrLayout& lay, const 
                       float* err);
 hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* flags, int32_t* kept_idx,
                           int32_t* n_kept);
+// fwd + bwd + FB (a.mode must be 1) and the compaction: inside the LK launch
+// when it runs one point per wave (c->fused_compact), else launch_klt +
+// launch_compact
+hipError_t launch_klt_compact(gvx_ctx* c, KltArgs a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                              const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                              const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy,
+                              uint8_t* flags, float* err, int32_t* kept_idx, int32_t* n_kept);
 
 // ---- clahe.hip ----
 // CLAHE_Impl::apply geometry for an h x w 8-bit image (oracle/clahe.c).

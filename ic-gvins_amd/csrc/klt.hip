@@ -1650,6 +1650,49 @@ template <int PPW>
 constexpr int klt_tiles() {
     return PPW == 3 ? 1 : PPW;
 }
+// reduceVector (tracking.cc:831-839) inside the LK launch, one point per wave
+// (the live tracker's pair: 150 waves, where a compact_kernel launch of its own
+// cost ~4 us of a ~43 us pair).  Lane 0 ORs the wave's keep bit into its pair's
+// words, then counts the wave in.  Both are returning agent-scope atomics,
+// performed where every XCD sees them, and the count is issued only after the
+// OR has returned, so the wave that counts the pair's n_pts-th arrival sees
+// every bit.  That wave lists the set bits in point order (compact_kernel's
+// kept_idx / n_kept) and zeroes the words and the count for the next launch
+// (graph replays included).  No release fence: the other outputs are not read
+// inside the launch.
+__device__ __forceinline__ void fused_compact(const KltArgs& a, int pair, int pt, bool keep) {
+    const int nw = (a.n_pts + 63) >> 6;
+    unsigned long long* m = a.cmask + (int64_t)pair * (nw + 1);
+    bool last = false;
+    if (lane_v() == 0) {
+        if (keep) {
+            const unsigned long long o = __hip_atomic_fetch_or(m + (pt >> 6), 1ull << (pt & 63), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("; keep bit in: %0" ::"v"(o) : "memory");  // its return before the count
+        }
+        last = __hip_atomic_fetch_add(m + nw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned long long)(a.n_pts - 1);
+    }
+    if (__builtin_amdgcn_ballot_w64(last) == 0) return;
+    const int lane = lane_v();
+    // the words read by read-modify-write atomics like the ones that set them (an
+    // OR of a literal 0 would compile to an atomic load)
+    unsigned long long zero = 0, mine = 0;
+    asm volatile("" : "+v"(zero));
+    if (lane < nw) mine = __hip_atomic_fetch_or(m + lane, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t* out = a.kept_idx + (int64_t)pair * a.n_pts;
+    int base = 0;
+    for (int w = 0; w < nw; ++w) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, w);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), w);
+        const unsigned long long word = ((unsigned long long)hi << 32) | lo;
+        if ((word >> lane) & 1ull) out[base + __popcll(word & ((1ull << lane) - 1ull))] = 64 * w + lane;
+        base += __popcll(word);
+    }
+    if (lane == 0) a.n_kept[pair] = base;
+    if (lane <= nw) __hip_atomic_exchange(m + lane, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 #ifdef GVX_KLT_TRACE
 // Diagnostic build only (tools/lk_residency.py): every wave of the batch
 // layout stamps itself (gvx_internal.h WaveStamp) into gvx_klt_trace_buf.
@@ -1755,13 +1798,14 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
     else
         lk_group<PPW, ACC>(J, I, pb, lay, cfg, nx, ny, bx, by, st2, e2, wv_wins, wv_units, wv_accs);
     gp = point(writer);
+    bool keep = false;
     if (writer) {
         const float p0x = pxy[2 * gp], p0y = pxy[2 * gp + 1];
         const double B = a.border;
         const bool on_border = nx < B || ny < B || nx > (a.cam_w - B) || ny > (a.cam_h - B);
         const double ddx = (double)(bx - p0x), ddy = (double)(by - p0y);
         const double dist = __dsqrt_rn(ddx * ddx + ddy * ddy);
-        const bool keep = st && st2 && !on_border && dist < a.fb_thresh;
+        keep = st && st2 && !on_border && dist < a.fb_thresh;
         next_xy[2 * gp] = nx;
         next_xy[2 * gp + 1] = ny;
         if (back_xy) {
@@ -1770,6 +1814,9 @@ __global__ void __launch_bounds__(64 * KLT_WPB, (klt_occupancy<PPW, ACC>())) klt
         }
         flags[gp] = (uint8_t)((st ? 1 : 0) | (st2 ? 2 : 0) | (keep ? 4 : 0));
         if (err_out) err_out[gp] = e;
+    }
+    if constexpr (PPW == 1) {
+        if (a.cmask) fused_compact(a, pair, wg - pair * wpp, keep);
     }
 }
 
@@ -2090,6 +2137,39 @@ hipError_t launch_compact(gvx_ctx* c, int n_pairs, int n_pts, const uint8_t* fla
                           int32_t* n_kept) {
     if (n_pairs <= 0) return hipSuccess;
     return launch_timed(c, "compact", compact_kernel, dim3(n_pairs), dim3(256), 0, n_pts, flags, kept_idx, n_kept);
+}
+
+hipError_t launch_klt_compact(gvx_ctx* c, KltArgs a, const PyrLayout& lay, const uint8_t* pyr_prev,
+                              const uint8_t* pyr_next, int64_t prev_pair_stride, int64_t next_pair_stride,
+                              const Level0& l0, const float* prev_xy, float* next_xy, float* back_xy,
+                              uint8_t* flags, float* err, int32_t* kept_idx, int32_t* n_kept) {
+    a.mode = 1;
+    const int64_t total = (int64_t)a.n_pairs * a.n_pts;
+    if (c->fused_compact && total > 0 && klt_ppw(total) == 1 && !a.n_dev) {
+        // one set of words per stream: a launch on the branch stream must not share them
+        const std::string name = std::string("klt_cmask") + (c->stream == c->main ? "" : "_side");
+        const size_t bytes = sizeof(unsigned long long) * (size_t)a.n_pairs * ((a.n_pts + 63) / 64 + 1);
+        const bool failed_before = c->capture_failed;
+        unsigned long long* m = (unsigned long long*)scratch(c, name, bytes);
+        if (m) {
+            DevBuf& db = c->dev[name];
+            if (db.fresh) {  // zero once; every launch leaves them zero
+                const hipError_t e = hipMemsetAsync(db.p, 0, db.bytes, c->stream);
+                if (e != hipSuccess) return e;
+                db.fresh = false;
+            }
+            a.cmask = m;
+            a.kept_idx = kept_idx;
+            a.n_kept = n_kept;
+            return launch_klt(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                              next_xy, back_xy, flags, err);
+        }
+        c->capture_failed = failed_before;  // not a failure: the two-launch form needs no buffer
+    }
+    const hipError_t e = launch_klt(c, a, lay, pyr_prev, pyr_next, prev_pair_stride, next_pair_stride, l0, prev_xy,
+                                    next_xy, back_xy, flags, err);
+    if (e != hipSuccess) return e;
+    return launch_compact(c, a.n_pairs, a.n_pts, flags, kept_idx, n_kept);
 }
 
 }  // namespace gvx

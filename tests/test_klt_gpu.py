@@ -347,3 +347,32 @@ def test_three_point_wave_groups_leave_at_different_times(ctx, orc, gvx_mod, pha
         _assert_same(g["flags"][i], flags, f"pair {i} flags")
         _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"pair {i} kept")
         assert (flags[0::3] | flags[1::3] | flags[2::3]).any() and not o["st_f"].all()
+
+
+@pytest.mark.parametrize("n_pairs,n_pts", [(1, 1), (3, 64), (5, 65), (2, 130), (27, 150)])
+def test_fused_compaction_matches_two_launches(ctx, orc, gvx_mod, monkeypatch, n_pairs, n_pts):
+    """One point per wave (n_pairs * n_pts <= 4096): the LK launch compacts by
+    itself (klt.hip fused_compact).  Its kept_idx / n_kept must equal the
+    compact_kernel launch's (a context made with GVX_FUSED_COMPACT=0) over
+    repeated launches -- the keep words and arrival counts are left zero for the
+    next one -- and, for the first pairs, the oracle's reduceVector."""
+    monkeypatch.setenv("GVX_FUSED_COMPACT", "0")
+    ref = gvx_mod.Context(0)
+    monkeypatch.delenv("GVX_FUSED_COMPACT")
+    try:
+        for rep in range(3):
+            I, J, prev, init = synth.make_batch(n_pairs, 320, 140, n_pts, seed=100 + 7 * rep + n_pts)
+            g = ctx.klt_fb_batch(I, J, prev, init)
+            r = ref.klt_fb_batch(I, J, prev, init)
+            for k in g:
+                if k != "kept":  # entries past n_kept are whatever the buffer held
+                    _assert_same(g[k], r[k], f"rep {rep} {k}")
+            for i in range(n_pairs):
+                _assert_same(g["kept"][i][:g["n_kept"][i]], r["kept"][i][:r["n_kept"][i]], f"rep {rep} pair {i}")
+            for i in range(min(n_pairs, 2)):
+                o = orc.klt_fb(I[i], J[i], prev[i], init[i], reuse_pyramids=True)
+                assert g["n_kept"][i] == len(o["kept_idx"])
+                _assert_same(g["kept"][i][:g["n_kept"][i]], o["kept_idx"], f"rep {rep} pair {i} kept")
+            assert int(np.sum(g["n_kept"])) > 0
+    finally:
+        ref.close()
