@@ -235,26 +235,33 @@ __device__ __forceinline__ bool lane_in(uint64_t m) { return (m >> __lane_id()) 
 // wave-uniform soffset, so a row load costs no VALU address arithmetic.
 constexpr int SRC_BIAS = 64;
 typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
-template <bool GATHER>
-__device__ __forceinline__ uint4 src_row16(const uint8_t* __restrict__ S, int pitch, int h, int x, const Gather& g,
-                                           int y, const __amdgpu_buffer_rsrc_t& srs) {
-    if constexpr (!GATHER) {
-        const v4u_t w = __builtin_amdgcn_raw_buffer_load_b128(srs, x + SRC_BIAS, refl(y, h) * pitch, 0);
-        return make_uint4(w.x, w.y, w.z, w.w);
-    }
-    const uint8_t* row = S + (int64_t)refl(y, h) * pitch;
-    if constexpr (GATHER) {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x + g.dx);  // 4-byte aligned
-        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+// GATHER: 0 = interior strip; 1 / 2 = the strip holds the left / right edge of an
+// unpadded source; 3 = both (a source narrower than a strip).  Every lane loads
+// through the buffer view (edge strips at their clamped column x = xc, so no
+// per-row address arithmetic), and an edge strip then shifts the dwords of the
+// lanes the Gather masks name: the left edge has only r = -1 lanes, the right
+// edge only r = 1 / 2 lanes (r06_pp: the three-way selects of every row of
+// both edge strips were a fifth of their instructions).
+template <int GATHER>
+__device__ __forceinline__ uint4 src_row16(int pitch, int h, int x, const Gather& g, int y,
+                                           const __amdgpu_buffer_rsrc_t& srs) {
+    const v4u_t w = __builtin_amdgcn_raw_buffer_load_b128(srs, x + SRC_BIAS, refl(y, h) * pitch, 0);
+    if constexpr (GATHER == 0) return make_uint4(w.x, w.y, w.z, w.w);
+    const uint32_t d0 = w.x, d1 = w.y, d2 = w.z, d3 = w.w;
+    if constexpr (GATHER == 1) {
         const uint32_t el = __builtin_amdgcn_perm(d0, d0, 0x01020303u);  // columns -4..-1 <- (3,) 3, 2, 1
-        const uint32_t er = __builtin_amdgcn_perm(d3, d3, 0x00000102u);  // columns +16.. <- +14, +13, +12
-        const bool L = lane_in(g.m_left), R1 = lane_in(g.m_1), R2 = lane_in(g.m_2);
-        return make_uint4(L ? el : R1 ? d1 : R2 ? d2 : d0, L ? d0 : R1 ? d2 : R2 ? d3 : d1,
-                          L ? d1 : R1 ? d3 : R2 ? er : d2, L ? d2 : R1 ? er : R2 ? er : d3);
-    } else {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(row + x);  // 4-byte aligned
-        return make_uint4(q[0], q[1], q[2], q[3]);
+        const bool L = lane_in(g.m_left);
+        return make_uint4(L ? el : d0, L ? d0 : d1, L ? d1 : d2, L ? d2 : d3);
     }
+    const uint32_t er = __builtin_amdgcn_perm(d3, d3, 0x00000102u);  // columns +16.. <- +14, +13, +12
+    const bool R1 = lane_in(g.m_1), R2 = lane_in(g.m_2);
+    if constexpr (GATHER == 2)
+        return make_uint4(R1 ? d1 : R2 ? d2 : d0, R1 ? d2 : R2 ? d3 : d1, R1 ? d3 : R2 ? er : d2,
+                          R1 || R2 ? er : d3);
+    const uint32_t el = __builtin_amdgcn_perm(d0, d0, 0x01020303u);
+    const bool L = lane_in(g.m_left);
+    return make_uint4(L ? el : R1 ? d1 : R2 ? d2 : d0, L ? d0 : R1 ? d2 : R2 ? d3 : d1,
+                      L ? d1 : R1 ? d3 : R2 ? er : d2, L ? d2 : R1 ? er : R2 ? er : d3);
 }
 // Strip 0 of an unpadded source: level-1 columns -8..-1 (lanes 0, 1) are the
 // REFLECT_101 copies of columns 8..1 (lanes 2..4), taken with DPP row shifts.
@@ -309,65 +316,53 @@ __device__ __forceinline__ uint32_t fix_sel2(int lane, int c0, int w) {
 struct DownLevels {
     int64_t off[3];
     int32_t pitch[3], w[3], h[3];
-    int32_t sides[3];  // 1: the pass writes the level's side bands (w, h >= RING_MIN)
 };
 
-// SKIP (tools/pyr_micro.hip only): bit k-1 set = level-k outputs are folded
+// SKIP (tools/pyr_probe.hip only): bit k-1 set = level-k outputs are folded
 // into a register instead of stored (to time the store traffic).
 #ifndef STREAM_OCC
 #define STREAM_OCC 4
 #endif
-// One wave's walk over its (strip, band).  GATHER: this strip touches an edge
-// of an unpadded source (per-lane REFLECT_101 gathers); SIDES: it holds source
-// columns of some level's side bands.  Both are wave-uniform, so the kernel
-// branches once into one of three instances and the loop has no per-row path
+// One wave's walk over its (strip, band).  GATHER (wave-uniform, one instance
+// each): 0 = an interior strip, 1 / 2 / 3 = the strip holds the left / right /
+// both edges of an unpadded source (src_row16).  The loop has no per-row path
 // choice (loads stay in flight across iterations).
-// One output store of stream_walk: pixel column `col` of padded row `row` of a
-// level whose column 0 of padded row 0 is d.ptr (byte d.off of the image's
-// pyramid).  Lanes that own no output (own == false) must not write the level:
-// BUF (interior strips) stores through a buffer view at an offset past the
-// pyramid, which the bounds check drops -- a 32-bit offset and no select of a
-// 64-bit address per store: 1,262 -> 655 VALU per 8 level-1 rows, pyramid pass
-// -2 % (profiles/r04_v24/); otherwise a flat store, those lanes writing the
-// wave's trash line.  The edge-strip instances keep the flat form: with buffer
-// stores they spill at the kernel's 128 registers and ran 2.3x slower.
-struct PyrDst {
-    __amdgpu_buffer_rsrc_t rs;
-    uint8_t* ptr;
-    int off;
-    uint8_t* tl;
-};
+// Stores: pixel column `col` of padded row `row` of a level whose column 0 of
+// padded row 0 is byte `off` of the image's pyramid, through a buffer view of
+// the pyramid; lanes that own no output (own == false) store at an offset past
+// it, which the bounds check drops -- a 32-bit offset per store and no 64-bit
+// address (r04_v24).  The pass writes each level's rows and their top / bottom
+// REFLECT_101 ring rows; the side bands come from ring_kernel (r06: written here,
+// they took the edge strips' waves to ~2x the interior strips' instructions:
+// 64-bit flat stores, which the buffer form would have spilled).
 constexpr int PYR_OOB = 0x7fffffff;
-template <bool BUF, typename T>
-__device__ __forceinline__ void pyr_store(const PyrDst& d, bool own, int col, int row, int pitch, T v) {
-    if constexpr (BUF) {
-        const int o = own ? d.off + col + row * pitch : PYR_OOB;
-        if constexpr (sizeof(T) == 4)
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, d.rs, o, 0, 0);
-        else if constexpr (sizeof(T) == 2)
-            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, d.rs, o, 0, 0);
-        else
-            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, d.rs, o, 0, 0);
-    } else {
-        *reinterpret_cast<T*>(own ? d.ptr + col + (int64_t)row * pitch : d.tl) = v;
-    }
+template <typename T>
+__device__ __forceinline__ void pyr_store(const __amdgpu_buffer_rsrc_t& rs, int off, bool own, int col, int row,
+                                          int pitch, T v) {
+    const int o = own ? off + col + row * pitch : PYR_OOB;
+    if constexpr (sizeof(T) == 4)
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, o, 0, 0);
+    else if constexpr (sizeof(T) == 2)
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, rs, o, 0, 0);
+    else
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, rs, o, 0, 0);
 }
 
-template <int NL, bool GATHER, bool SIDES, int SKIP>
+template <int NL, int GATHER, int SKIP>
 __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                             const DownLevels& L, int st, int bd, int img, int band, int lane,
-                                            uint8_t* __restrict__ tl, bool side1, bool side2, bool side3) {
+                                            uint8_t* __restrict__ tl) {
     const uint8_t* S = img < src.n_a ? src.a + img * src.img_stride : src.b + (img - src.n_a) * src.img_stride;
     uint8_t* P = pyr + img * pyr_bytes;
-    // interior strips store through a buffer view of the image's pyramid (pyr_store)
-    constexpr bool BUF = !SIDES;
+    // stores go through a buffer view of the image's pyramid (pyr_store)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)pyr_bytes, 0x00020000);
     const int w0 = src.w, h0 = src.h, sp = src.pitch;
     const int x0 = ST_COLS * st + 8 * lane - 20;  // this lane's 16 source bytes
-    // padded sources: lanes past the ring read inside it (their outputs are unused)
-    const int xs = src.raw ? x0 : min(x0, w0 + 16);
+    // padded sources: lanes past the ring read inside it (their outputs are unused);
+    // edge strips of an unpadded source load at the clamped column xc = x0 + dx
     Gather g{};
-    if constexpr (GATHER) g = make_gather(x0, w0);
+    if constexpr (GATHER != 0) g = make_gather(x0, w0);
+    const int xs = GATHER != 0 ? x0 + g.dx : src.raw ? x0 : min(x0, w0 + 16);
     const __amdgpu_buffer_rsrc_t srs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(S - SRC_BIAS), (short)0, 0x7fffffff, 0x00020000);
     const bool own_lane = lane >= 2 && lane < 62;
@@ -393,10 +388,6 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     // the last source row the walk needs: the prefetch and the trip count's
     // round-up re-read it (a cache hit) instead of fetching rows past the band
     const int ylast = 2 * (r1s + n1 - 1) + 2;
-    // level-1 side bands as dwords: the left band always (ring dword [-a-4, -a-1]
-    // from lanes a, a+4), the right one when w1 % 4 == 0 ([2w1-4-a, 2w1-1-a] from
-    // lanes a-4, a); otherwise the right band byte by byte
-    const bool r1dw = (w1 & 3) == 0;
 
     // rolling state: horizontal sums of source rows 2r1-2 .. 2r1+2 (hr[0..4]),
     // level-2 horizontal sums of level-1 rows (g2[0..4], newest last), level-3
@@ -404,7 +395,7 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     uint2 hr[5];
     uint32_t g2[5] = {0, 0, 0, 0, 0}, g3[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16<GATHER>(S, sp, h0, xs, g, 2 * r1s - 2 + k, srs));
+    for (int k = 0; k < 3; ++k) hr[k] = hsum_row(src_row16<GATHER>(sp, h0, xs, g, 2 * r1s - 2 + k, srs));
     // source rows 2r1+1, 2r1+2 of level-1 row r1 = r1s+k live in slot k % RS;
     // they are fetched PF iterations ahead (2*PF rows x 1 KB in flight per wave).
     // PF = 4 at 4 waves per SIMD (99 VGPRs) measured 0.230 ms per 512 images
@@ -419,66 +410,43 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     uint4 pa[RS], pb[RS];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-        pa[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 1, ylast), srs);
-        pb[k] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1s + k) + 2, ylast), srs);
+        pa[k] = src_row16<GATHER>(sp, h0, xs, g, min(2 * (r1s + k) + 1, ylast), srs);
+        pb[k] = src_row16<GATHER>(sp, h0, xs, g, min(2 * (r1s + k) + 2, ylast), srs);
     }
     // Loads are issued unconditionally and stores branch only on wave-uniform
     // row conditions (rows of the band, mirrored ring rows): on gfx9 stores and
     // loads share vmcnt, and a store under a lane-divergent branch would make the
     // compiler wait for all earlier stores before using a prefetched row; a
     // uniform branch costs at most one extra counted op at the join.  Lanes that
-    // own no output (lanes 0/1/62/63, columns past the level, no ring column)
-    // store to this lane's dword of the wave's trash line.
+    // own no output (lanes 0/1/62/63, columns past the level) store out of bounds.
     uint32_t nsink = 0;
     auto body = [&](int k, auto slot_c) {
         constexpr int slot = decltype(slot_c)::value;
         const int r1 = r1s + k;
         hr[3] = hsum_row(pa[slot]);
         hr[4] = hsum_row(pb[slot]);
-        pa[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 1, ylast), srs);
-        pb[(slot + PF) % RS] = src_row16<GATHER>(S, sp, h0, xs, g, min(2 * (r1 + PF) + 2, ylast), srs);
+        pa[(slot + PF) % RS] = src_row16<GATHER>(sp, h0, xs, g, min(2 * (r1 + PF) + 1, ylast), srs);
+        pb[(slot + PF) % RS] = src_row16<GATHER>(sp, h0, xs, g, min(2 * (r1 + PF) + 2, ylast), srs);
         // level-1 row r1
         uint32_t l1 = hibytes(vsum2(hr[0].x, hr[1].x, hr[2].x, hr[3].x, hr[4].x),
                               vsum2(hr[0].y, hr[1].y, hr[2].y, hr[3].y, hr[4].y));
         hr[0] = hr[2];
         hr[1] = hr[3];
         hr[2] = hr[4];
-        if constexpr (GATHER) {
+        if constexpr (GATHER == 1 || GATHER == 3) {
             if (st == 0) l1 = left_mirror_l1(l1, lane);  // wave-uniform
         }
         if (fix1) l1 = __builtin_amdgcn_perm(l1, wave_shr1(l1), sel1);
         if (r1 >= o1lo && r1 < o1hi) {  // wave-uniform: rows of the band
             const int a = c1 + 4 * (lane - 2);
             const bool ok = own_lane && a < w1;
-            const PyrDst rb{rs, P + L.off[0] + PAD, (int)L.off[0] + PAD, tl};  // column 0 of padded row 0
+            const int ob = (int)L.off[0] + PAD;  // column 0 of padded row 0
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
             if constexpr ((SKIP & 1) != 0) {
                 nsink ^= l1;
             } else {
-                pyr_store<BUF, uint32_t>(rb, ok, a, r1 + PAD, p1, l1);
-                if (mr != r1) pyr_store<BUF, uint32_t>(rb, ok, a, mr + PAD, p1, l1);
-                if constexpr (SIDES) {
-                    if (side1) {  // wave-uniform
-                        const uint32_t nx = wave_shl1(l1), pv = wave_shr1(l1);
-                        const bool lw = own_lane && a <= PAD - 4;
-                        const bool rw = r1dw && own_lane && a >= w1 - PAD && a <= w1 - 4;
-                        const uint32_t v = lw ? __builtin_amdgcn_perm(nx, l1, 0x01020304u)
-                                              : __builtin_amdgcn_perm(l1, pv, 0x03040506u);
-                        const int col = lw ? -a - 4 : 2 * w1 - 4 - a;
-                        pyr_store<BUF, uint32_t>(rb, lw || rw, col, r1 + PAD, p1, v);
-                        if (mr != r1)
-                            pyr_store<BUF, uint32_t>(rb, lw || rw, col, mr + PAD, p1, v);
-                        if (!r1dw) {  // odd widths: the right band byte by byte
-#pragma unroll
-                            for (int b = 0; b < 4; ++b) {
-                                const int c = a + b, rc = ring_col(c, w1);
-                                const bool wb = own_lane && rc > 0;
-                                pyr_store<BUF, uint8_t>(rb, wb, rc, r1 + PAD, p1, (uint8_t)(l1 >> (8 * b)));
-                                if (mr != r1) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p1, (uint8_t)(l1 >> (8 * b)));
-                            }
-                        }
-                    }
-                }
+                pyr_store<uint32_t>(rs, ob, ok, a, r1 + PAD, p1, l1);
+                if (mr != r1) pyr_store<uint32_t>(rs, ob, ok, a, mr + PAD, p1, l1);
             }
         }
         if constexpr (NL > 1) {
@@ -512,26 +480,13 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                 if (k >= 4 && r2 >= o2lo && r2 < o2hi) {
                     const int a = c2 + 2 * (lane - 2);
                     const bool ok = own_lane && a < w2;
-                    const PyrDst rb{rs, P + L.off[1] + PAD, (int)L.off[1] + PAD, tl};
+                    const int ob = (int)L.off[1] + PAD;
                     const int mr = mirror_row(r2, h2);
                     if constexpr ((SKIP & 2) != 0) {
                         nsink ^= l2 << 7;
                     } else {
-                        pyr_store<BUF, uint16_t>(rb, ok, a, r2 + PAD, p2, (uint16_t)l2);
-                        if (mr != r2)
-                            pyr_store<BUF, uint16_t>(rb, ok, a, mr + PAD, p2, (uint16_t)l2);
-                        if constexpr (SIDES) {
-                            if (side2) {  // wave-uniform
-#pragma unroll
-                                for (int b = 0; b < 2; ++b) {
-                                    const int rc = ring_col(a + b, w2);
-                                    const bool wb = own_lane && rc != 0;
-                                    const uint8_t v8 = (uint8_t)(l2 >> (8 * b));
-                                    pyr_store<BUF, uint8_t>(rb, wb, rc, r2 + PAD, p2, v8);
-                                    if (mr != r2) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p2, v8);
-                                }
-                            }
-                        }
+                        pyr_store<uint16_t>(rs, ob, ok, a, r2 + PAD, p2, (uint16_t)l2);
+                        if (mr != r2) pyr_store<uint16_t>(rs, ob, ok, a, mr + PAD, p2, (uint16_t)l2);
                     }
                 }
                 if constexpr (NL > 2) {
@@ -555,22 +510,14 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
                         const int a = c3 + (lane - 2);
                         const bool ok = own_lane && a < w3;
-                        const PyrDst rb{rs, P + L.off[2] + PAD, (int)L.off[2] + PAD, tl};
+                        const int ob = (int)L.off[2] + PAD;
                         const int mr = mirror_row(r3, h3);
                         const uint8_t v8 = (uint8_t)(s3 >> 8);
                         if constexpr ((SKIP & 4) != 0) {
                             nsink ^= s3 << 13;
                         } else if (k >= 12 && r3 >= o3lo && r3 < o3hi) {
-                            pyr_store<BUF, uint8_t>(rb, ok, a, r3 + PAD, p3, v8);
-                            if (mr != r3) pyr_store<BUF, uint8_t>(rb, ok, a, mr + PAD, p3, v8);
-                            if constexpr (SIDES) {
-                                if (side3) {  // wave-uniform
-                                    const int rc = ring_col(a, w3);
-                                    const bool wb = own_lane && rc != 0;
-                                    pyr_store<BUF, uint8_t>(rb, wb, rc, r3 + PAD, p3, v8);
-                                    if (mr != r3) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p3, v8);
-                                }
-                            }
+                            pyr_store<uint8_t>(rs, ob, ok, a, r3 + PAD, p3, v8);
+                            if (mr != r3) pyr_store<uint8_t>(rs, ob, ok, a, mr + PAD, p3, v8);
                         }
                     }
                 }
@@ -635,25 +582,24 @@ __global__ void __launch_bounds__(64 * WPB, STREAM_OCC) stream_kernel(StreamSrc 
         bd = rest % n_bands;
         img = rest / n_bands;
     }
-    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
+    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (SKIP probes only)
     // wave-uniform strip classes: source columns past an edge of an unpadded
-    // level 0 (lanes 0 / 63 read x0 = 480*st - 20 / 480*st + 484, 16 bytes), and
-    // owned columns (240 / 120 / 60 per strip) that some side band copies
-    const bool gather = src.raw && (st == 0 || ST_COLS * st + 8 * 63 - 20 + 16 > src.w);
-    const int c1 = (ST_COLS / 2) * st;
-    const bool side1 = L.sides[0] && (st == 0 || c1 + ST_COLS / 2 > L.w[0] - 1 - PAD);
-    const bool side2 = NL > 1 && L.sides[1] && (st == 0 || c1 / 2 + ST_COLS / 4 > L.w[1] - 1 - PAD);
-    const bool side3 = NL > 2 && L.sides[2] && (st == 0 || c1 / 4 + ST_COLS / 8 > L.w[2] - 1 - PAD);
-    if (gather)
-        stream_walk<NL, true, true, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, side1, side2, side3);
-    else if (side1 || side2 || side3)
-        stream_walk<NL, false, true, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, side1, side2, side3);
+    // level 0 (lanes 0 / 63 read x0 = 480*st - 20 / 480*st + 484, 16 bytes)
+    const bool gl = src.raw && st == 0, gr = src.raw && ST_COLS * st + 8 * 63 - 20 + 16 > src.w;
+    if (gl && gr)
+        stream_walk<NL, 3, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
+    else if (gl)
+        stream_walk<NL, 1, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
+    else if (gr)
+        stream_walk<NL, 2, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
     else
-        stream_walk<NL, false, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+        stream_walk<NL, 0, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
 }
 
-// Side bands of a pass's level written by the pass itself (wide and tall enough)
-__host__ __device__ inline bool pass_writes_sides(int w, int h) { return w >= RING_MIN && h >= RING_MIN; }
+// Levels whose top / bottom ring rows the pass writes (mirror_row): tall enough
+// that every ring row is a single-bounce copy.  ring_kernel then writes only
+// their side bands (every padded row); shorter levels get their whole ring there.
+__host__ __device__ inline bool pass_writes_rows(int h) { return h >= RING_MIN; }
 
 // band height: BAND level-1 rows per wave when the batch fills the chip; a
 // small batch (the live tracker's single frame or pair) takes narrower bands
@@ -675,14 +621,13 @@ hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrL
         D.pitch[k] = lay.pitch[l0 + 1 + k];
         D.w[k] = lay.w[l0 + 1 + k];
         D.h[k] = lay.h[l0 + 1 + k];
-        D.sides[k] = pass_writes_sides(D.w[k], D.h[k]);
     }
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
     const int band = stream_band(n_strips, D.h[0], n_img, c->n_cu);
     const int n_bands = (D.h[0] + band - 1) / band;
     const int n_units = n_strips * n_bands * n_img;
-    // the lanes without an output store to their wave's trash line: the kernel
-    // must not run without it (a scratch buffer cannot grow inside a capture)
+    // the SKIP probe builds fold outputs into a per-wave trash line (a scratch
+    // buffer cannot grow inside a capture, so it is sized here)
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
     if (!trash) return hipErrorOutOfMemory;
     if (c->pyr_wpb == 4)
@@ -695,12 +640,13 @@ hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrL
 
 
 // ------------------------------------------------------------------ rings
-// Full REFLECT_101 rings of the levels too small for the streaming pass to
-// write them (narrower or shorter than RING_MIN: the ring reflects more than
-// once), all images in one launch.  Item = one ring dword: the top / bottom PAD
-// rows over the padded width, then per interior row the left PAD columns and
-// the right columns [w, w+PAD) (dword aligned; bytes of the last interior dword
-// rewrite their own value).
+// REFLECT_101 rings the streaming pass does not write, all images in one
+// launch: for levels the pass writes the top / bottom ring rows of
+// (pass_writes_rows), the side bands of every padded row; for shorter levels
+// (the ring reflects more than once) the whole ring.  Item = one ring dword:
+// [whole ring only: the top / bottom PAD rows over the padded width, then] per
+// padded row the left PAD columns and the right columns [w, w+PAD) (dword
+// aligned; bytes of the last interior dword rewrite their own value).
 struct RingLevels {
     int32_t n;                  // levels
     int64_t off[MAX_LEVELS];
@@ -708,6 +654,7 @@ struct RingLevels {
     int32_t dw[MAX_LEVELS];     // dwords per padded row (top/bottom bands)
     int32_t rd0[MAX_LEVELS];    // first dword (padded col / 4) of the right band
     int32_t rdn[MAX_LEVELS];    // dwords of the right band
+    int32_t sides[MAX_LEVELS];  // 1: side bands only, over all h + 2*PAD padded rows
     int32_t items[MAX_LEVELS];  // ring dwords of the level
 };
 
@@ -736,7 +683,7 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
     const int w = R.w[l], h = R.h[l], pitch = R.pitch[l];
     uint8_t* base = pyr + (int64_t)blockIdx.y * pyr_bytes + R.off[l];
     int prow, pcol;  // padded row, padded byte column of the dword
-    const int nb = 2 * PAD * R.dw[l];
+    const int nb = R.sides[l] ? 0 : 2 * PAD * R.dw[l];
     if (j < nb) {
         const int r = j / R.dw[l];
         prow = r < PAD ? r : h + r;
@@ -745,21 +692,19 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
         j -= nb;
         const int per = PAD / 4 + R.rdn[l];
         const int r = j / per, c = j - r * per;
-        prow = PAD + r;
+        prow = R.sides[l] ? r : PAD + r;
         pcol = c < PAD / 4 ? 4 * c : 4 * (R.rd0[l] + c - PAD / 4);
     }
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(base + (int64_t)(refl(prow - PAD, h) + PAD) * pitch);
     *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = ring_dword(rw, pcol, w);
 }
 
-// Rings of the levels lo..hi whose side bands the streaming pass did not write
-// (no launch when it wrote them all).
+// The rings of levels lo..hi the streaming pass left (ring_kernel).
 hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst) {
     RingLevels R{};
     int most = 0;
     for (int lv = lo; lv <= hi; ++lv) {
         const int w = lay.w[lv];
-        if (pass_writes_sides(w, lay.h[lv])) continue;
         const int k = R.n++;
         R.off[k] = lay.off[lv];
         R.pitch[k] = lay.pitch[lv];
@@ -768,7 +713,9 @@ hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int
         R.dw[k] = (w + 2 * PAD + 3) / 4;
         R.rd0[k] = (w + PAD) / 4;
         R.rdn[k] = (w + 2 * PAD + 3) / 4 - R.rd0[k];
-        R.items[k] = 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
+        R.sides[k] = pass_writes_rows(lay.h[lv]);
+        R.items[k] = R.sides[k] ? (lay.h[lv] + 2 * PAD) * (PAD / 4 + R.rdn[k])
+                                : 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
         most = R.items[k] > most ? R.items[k] : most;
     }
     if (R.n == 0) return hipSuccess;

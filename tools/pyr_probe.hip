@@ -243,7 +243,6 @@ int main(int argc, char** argv) {
         D.pitch[k] = lay.pitch[1 + k];
         D.w[k] = lay.w[1 + k];
         D.h[k] = lay.h[1 + k];
-        D.sides[k] = pass_writes_sides(D.w[k], D.h[k]);
     }
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
     const int band = stream_band(n_strips, D.h[0], NIMG, 256);
