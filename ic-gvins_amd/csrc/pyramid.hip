@@ -316,6 +316,7 @@ __device__ __forceinline__ uint32_t fix_sel2(int lane, int c0, int w) {
 struct DownLevels {
     int64_t off[3];
     int32_t pitch[3], w[3], h[3];
+    int32_t sides[3];  // SIDES passes: 1 = the pass writes the level's side bands (w, h >= RING_MIN)
 };
 
 // SKIP (tools/pyr_probe.hip only): bit k-1 set = level-k outputs are folded
@@ -327,34 +328,50 @@ struct DownLevels {
 // each): 0 = an interior strip, 1 / 2 / 3 = the strip holds the left / right /
 // both edges of an unpadded source (src_row16).  The loop has no per-row path
 // choice (loads stay in flight across iterations).
+// Side bands.  A batch that fills the chip (the default, SIDES = false): the
+// pass writes each level's rows and their top / bottom REFLECT_101 ring rows,
+// and ring_kernel the side bands (r06: written here they took the edge strips'
+// waves to ~2x the interior strips' instructions, 64-bit flat stores that the
+// buffer form would have spilled; pass + sides 0.179 -> 0.166 ms at configs[1],
+// profiles/r06_sb1).  A small launch (SIDES = true: the live tracker's pair or
+// frame, whose pass is latency-bound and where another launch costs ~1 us) also
+// writes the side bands here, from the lanes that hold their source pixels.
 // Stores: pixel column `col` of padded row `row` of a level whose column 0 of
-// padded row 0 is byte `off` of the image's pyramid, through a buffer view of
-// the pyramid; lanes that own no output (own == false) store at an offset past
-// it, which the bounds check drops -- a 32-bit offset per store and no 64-bit
-// address (r04_v24).  The pass writes each level's rows and their top / bottom
-// REFLECT_101 ring rows; the side bands come from ring_kernel (r06: written here,
-// they took the edge strips' waves to ~2x the interior strips' instructions:
-// 64-bit flat stores, which the buffer form would have spilled).
+// padded row 0 is d.ptr (byte d.off of the image's pyramid).  Lanes that own no
+// output (own == false) must not write the level: BUF stores through a buffer
+// view at an offset past the pyramid, which the bounds check drops (a 32-bit
+// offset per store, r04_v24); the SIDES instances keep the flat form, those
+// lanes writing the wave's trash line.
+struct PyrDst {
+    __amdgpu_buffer_rsrc_t rs;
+    uint8_t* ptr;
+    int off;
+    uint8_t* tl;
+};
 constexpr int PYR_OOB = 0x7fffffff;
-template <typename T>
-__device__ __forceinline__ void pyr_store(const __amdgpu_buffer_rsrc_t& rs, int off, bool own, int col, int row,
-                                          int pitch, T v) {
-    const int o = own ? off + col + row * pitch : PYR_OOB;
-    if constexpr (sizeof(T) == 4)
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, o, 0, 0);
-    else if constexpr (sizeof(T) == 2)
-        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, rs, o, 0, 0);
-    else
-        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, rs, o, 0, 0);
+template <bool BUF, typename T>
+__device__ __forceinline__ void pyr_store(const PyrDst& d, bool own, int col, int row, int pitch, T v) {
+    if constexpr (BUF) {
+        const int o = own ? d.off + col + row * pitch : PYR_OOB;
+        if constexpr (sizeof(T) == 4)
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, d.rs, o, 0, 0);
+        else if constexpr (sizeof(T) == 2)
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, d.rs, o, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, d.rs, o, 0, 0);
+    } else {
+        *reinterpret_cast<T*>(own ? d.ptr + col + (int64_t)row * pitch : d.tl) = v;
+    }
 }
 
-template <int NL, int GATHER, int SKIP>
+template <int NL, int GATHER, bool SIDES, int SKIP>
 __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __restrict__ pyr, int64_t pyr_bytes,
                                             const DownLevels& L, int st, int bd, int img, int band, int lane,
-                                            uint8_t* __restrict__ tl) {
+                                            uint8_t* __restrict__ tl, bool side1, bool side2, bool side3) {
     const uint8_t* S = img < src.n_a ? src.a + img * src.img_stride : src.b + (img - src.n_a) * src.img_stride;
     uint8_t* P = pyr + img * pyr_bytes;
     // stores go through a buffer view of the image's pyramid (pyr_store)
+    constexpr bool BUF = !SIDES;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (int)pyr_bytes, 0x00020000);
     const int w0 = src.w, h0 = src.h, sp = src.pitch;
     const int x0 = ST_COLS * st + 8 * lane - 20;  // this lane's 16 source bytes
@@ -378,6 +395,10 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     if (NL > 2) w3 = L.w[2], h3 = L.h[2], p3 = L.pitch[2], c3 = (ST_COLS / 8) * st;
     const uint32_t sel1 = fix1 ? fix_sel4(lane, c1, w1) : 0u;
     const uint32_t sel2 = fix2 ? fix_sel2(lane, c2, w2) : 0u;
+    // level-1 side bands as dwords: the left band always (ring dword [-a-4, -a-1]
+    // from lanes a, a+4), the right one when w1 % 4 == 0 ([2w1-4-a, 2w1-1-a] from
+    // lanes a-4, a); otherwise the right band byte by byte
+    const bool r1dw = (w1 & 3) == 0;
     // level-1 rows walked: everything the band's deepest owned rows depend on
     // (band: a multiple of 4, so r1s = 2 mod 4 and the level-2 / level-3 schedule below holds)
     const int r1s = band * bd - (NL == 3 ? 6 : NL == 2 ? 2 : 0);
@@ -418,7 +439,8 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
     // loads share vmcnt, and a store under a lane-divergent branch would make the
     // compiler wait for all earlier stores before using a prefetched row; a
     // uniform branch costs at most one extra counted op at the join.  Lanes that
-    // own no output (lanes 0/1/62/63, columns past the level) store out of bounds.
+    // own no output (lanes 0/1/62/63, columns past the level, no ring column)
+    // store out of bounds (BUF) or to this lane's dword of the wave's trash line.
     uint32_t nsink = 0;
     auto body = [&](int k, auto slot_c) {
         constexpr int slot = decltype(slot_c)::value;
@@ -440,13 +462,35 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
         if (r1 >= o1lo && r1 < o1hi) {  // wave-uniform: rows of the band
             const int a = c1 + 4 * (lane - 2);
             const bool ok = own_lane && a < w1;
-            const int ob = (int)L.off[0] + PAD;  // column 0 of padded row 0
+            const PyrDst rb{rs, P + L.off[0] + PAD, (int)L.off[0] + PAD, tl};  // column 0 of padded row 0
             const int mr = mirror_row(r1, h1);  // the ring row holding this row's REFLECT_101 copy
             if constexpr ((SKIP & 1) != 0) {
                 nsink ^= l1;
             } else {
-                pyr_store<uint32_t>(rs, ob, ok, a, r1 + PAD, p1, l1);
-                if (mr != r1) pyr_store<uint32_t>(rs, ob, ok, a, mr + PAD, p1, l1);
+                pyr_store<BUF, uint32_t>(rb, ok, a, r1 + PAD, p1, l1);
+                if (mr != r1) pyr_store<BUF, uint32_t>(rb, ok, a, mr + PAD, p1, l1);
+                if constexpr (SIDES) {
+                    if (side1) {  // wave-uniform
+                        const uint32_t nx = wave_shl1(l1), pv = wave_shr1(l1);
+                        const bool lw = own_lane && a <= PAD - 4;
+                        const bool rw = r1dw && own_lane && a >= w1 - PAD && a <= w1 - 4;
+                        const uint32_t v = lw ? __builtin_amdgcn_perm(nx, l1, 0x01020304u)
+                                              : __builtin_amdgcn_perm(l1, pv, 0x03040506u);
+                        const int col = lw ? -a - 4 : 2 * w1 - 4 - a;
+                        pyr_store<BUF, uint32_t>(rb, lw || rw, col, r1 + PAD, p1, v);
+                        if (mr != r1)
+                            pyr_store<BUF, uint32_t>(rb, lw || rw, col, mr + PAD, p1, v);
+                        if (!r1dw) {  // odd widths: the right band byte by byte
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) {
+                                const int c = a + b, rc = ring_col(c, w1);
+                                const bool wb = own_lane && rc > 0;
+                                pyr_store<BUF, uint8_t>(rb, wb, rc, r1 + PAD, p1, (uint8_t)(l1 >> (8 * b)));
+                                if (mr != r1) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p1, (uint8_t)(l1 >> (8 * b)));
+                            }
+                        }
+                    }
+                }
             }
         }
         if constexpr (NL > 1) {
@@ -480,13 +524,26 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                 if (k >= 4 && r2 >= o2lo && r2 < o2hi) {
                     const int a = c2 + 2 * (lane - 2);
                     const bool ok = own_lane && a < w2;
-                    const int ob = (int)L.off[1] + PAD;
+                    const PyrDst rb{rs, P + L.off[1] + PAD, (int)L.off[1] + PAD, tl};
                     const int mr = mirror_row(r2, h2);
                     if constexpr ((SKIP & 2) != 0) {
                         nsink ^= l2 << 7;
                     } else {
-                        pyr_store<uint16_t>(rs, ob, ok, a, r2 + PAD, p2, (uint16_t)l2);
-                        if (mr != r2) pyr_store<uint16_t>(rs, ob, ok, a, mr + PAD, p2, (uint16_t)l2);
+                        pyr_store<BUF, uint16_t>(rb, ok, a, r2 + PAD, p2, (uint16_t)l2);
+                        if (mr != r2)
+                            pyr_store<BUF, uint16_t>(rb, ok, a, mr + PAD, p2, (uint16_t)l2);
+                        if constexpr (SIDES) {
+                            if (side2) {  // wave-uniform
+#pragma unroll
+                                for (int b = 0; b < 2; ++b) {
+                                    const int rc = ring_col(a + b, w2);
+                                    const bool wb = own_lane && rc != 0;
+                                    const uint8_t v8 = (uint8_t)(l2 >> (8 * b));
+                                    pyr_store<BUF, uint8_t>(rb, wb, rc, r2 + PAD, p2, v8);
+                                    if (mr != r2) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p2, v8);
+                                }
+                            }
+                        }
                     }
                 }
                 if constexpr (NL > 2) {
@@ -510,14 +567,22 @@ __device__ __forceinline__ void stream_walk(const StreamSrc& src, uint8_t* __res
                         const uint32_t s3 = g3[0] + g3[4] + 4 * (g3[1] + g3[3]) + 6 * g3[2] + 128;
                         const int a = c3 + (lane - 2);
                         const bool ok = own_lane && a < w3;
-                        const int ob = (int)L.off[2] + PAD;
+                        const PyrDst rb{rs, P + L.off[2] + PAD, (int)L.off[2] + PAD, tl};
                         const int mr = mirror_row(r3, h3);
                         const uint8_t v8 = (uint8_t)(s3 >> 8);
                         if constexpr ((SKIP & 4) != 0) {
                             nsink ^= s3 << 13;
                         } else if (k >= 12 && r3 >= o3lo && r3 < o3hi) {
-                            pyr_store<uint8_t>(rs, ob, ok, a, r3 + PAD, p3, v8);
-                            if (mr != r3) pyr_store<uint8_t>(rs, ob, ok, a, mr + PAD, p3, v8);
+                            pyr_store<BUF, uint8_t>(rb, ok, a, r3 + PAD, p3, v8);
+                            if (mr != r3) pyr_store<BUF, uint8_t>(rb, ok, a, mr + PAD, p3, v8);
+                            if constexpr (SIDES) {
+                                if (side3) {  // wave-uniform
+                                    const int rc = ring_col(a, w3);
+                                    const bool wb = own_lane && rc != 0;
+                                    pyr_store<BUF, uint8_t>(rb, wb, rc, r3 + PAD, p3, v8);
+                                    if (mr != r3) pyr_store<BUF, uint8_t>(rb, wb, rc, mr + PAD, p3, v8);
+                                }
+                            }
                         }
                     }
                 }
@@ -555,7 +620,7 @@ __device__ uint64_t* gvx_pyr_trace_buf;  // diagnostic build only (tools/pyr_res
 // interior waves.  edge_first = 0: strip-major within a band, the r05 order.
 // WPB waves per workgroup: 1 frees a finished wave's slot at once (a 4-wave
 // workgroup held its slots until its slowest wave ended, 17 us apart on average).
-template <int NL, int SKIP = 0, int WPB = 1>
+template <int NL, int SKIP = 0, int WPB = 1, bool SIDES = false>
 __global__ void __launch_bounds__(64 * WPB, STREAM_OCC) stream_kernel(StreamSrc src, uint8_t* __restrict__ pyr,
                                                                   int64_t pyr_bytes, DownLevels L, int n_strips,
                                                                   int n_bands, int n_units, int band,
@@ -582,24 +647,45 @@ __global__ void __launch_bounds__(64 * WPB, STREAM_OCC) stream_kernel(StreamSrc 
         bd = rest % n_bands;
         img = rest / n_bands;
     }
-    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (SKIP probes only)
+    uint8_t* const tl = trash + (int64_t)unit * 256 + 4 * lane;  // this wave's own line (no sharing)
     // wave-uniform strip classes: source columns past an edge of an unpadded
-    // level 0 (lanes 0 / 63 read x0 = 480*st - 20 / 480*st + 484, 16 bytes)
+    // level 0 (lanes 0 / 63 read x0 = 480*st - 20 / 480*st + 484, 16 bytes), and
+    // (SIDES) owned columns (240 / 120 / 60 per strip) that some side band copies
     const bool gl = src.raw && st == 0, gr = src.raw && ST_COLS * st + 8 * 63 - 20 + 16 > src.w;
-    if (gl && gr)
-        stream_walk<NL, 3, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
-    else if (gl)
-        stream_walk<NL, 1, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
-    else if (gr)
-        stream_walk<NL, 2, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
-    else
-        stream_walk<NL, 0, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl);
+    if constexpr (SIDES) {
+        const int c1 = (ST_COLS / 2) * st;
+        const bool side1 = L.sides[0] && (st == 0 || c1 + ST_COLS / 2 > L.w[0] - 1 - PAD);
+        const bool side2 = NL > 1 && L.sides[1] && (st == 0 || c1 / 2 + ST_COLS / 4 > L.w[1] - 1 - PAD);
+        const bool side3 = NL > 2 && L.sides[2] && (st == 0 || c1 / 4 + ST_COLS / 8 > L.w[2] - 1 - PAD);
+        // one edge instance for both sides (fewer instances, fewer SGPRs spilled)
+        if (gl || gr)
+            stream_walk<NL, 3, true, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, side1, side2, side3);
+        else if (side1 || side2 || side3)
+            stream_walk<NL, 0, true, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, side1, side2, side3);
+        else
+            stream_walk<NL, 0, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+    } else {
+        if (gl && gr)
+            stream_walk<NL, 3, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+        else if (gl)
+            stream_walk<NL, 1, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+        else if (gr)
+            stream_walk<NL, 2, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+        else
+            stream_walk<NL, 0, false, SKIP>(src, pyr, pyr_bytes, L, st, bd, img, band, lane, tl, false, false, false);
+    }
 }
 
 // Levels whose top / bottom ring rows the pass writes (mirror_row): tall enough
 // that every ring row is a single-bounce copy.  ring_kernel then writes only
 // their side bands (every padded row); shorter levels get their whole ring there.
 __host__ __device__ inline bool pass_writes_rows(int h) { return h >= RING_MIN; }
+// SIDES passes also write the side bands of levels wide and tall enough
+__host__ __device__ inline bool pass_writes_sides(int w, int h) { return w >= RING_MIN && h >= RING_MIN; }
+// Launches smaller than the chip's wave slots (4 per SIMD) are latency-bound:
+// their pass writes the side bands itself (one launch fewer); larger ones leave
+// them to ring_kernel
+inline bool stream_sides(int n_units, int n_cu) { return n_units < 16 * n_cu; }
 
 // band height: BAND level-1 rows per wave when the batch fills the chip; a
 // small batch (the live tracker's single frame or pair) takes narrower bands
@@ -613,23 +699,31 @@ inline int stream_band(int n_strips, int h1, int n_img, int n_cu) {
     return std::min(band, ((h1 + n_bands - 1) / n_bands + 3) / 4 * 4);
 }
 
+// *sides: whether the pass wrote the side bands of the levels pass_writes_sides names
 template <int NL>
-hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrLayout& lay, int l0, uint8_t* dst) {
+hipError_t launch_stream(gvx_ctx* c, const StreamSrc& src, int n_img, const PyrLayout& lay, int l0, uint8_t* dst,
+                         bool* sides) {
     DownLevels D{};
     for (int k = 0; k < NL; ++k) {
         D.off[k] = lay.off[l0 + 1 + k];
         D.pitch[k] = lay.pitch[l0 + 1 + k];
         D.w[k] = lay.w[l0 + 1 + k];
         D.h[k] = lay.h[l0 + 1 + k];
+        D.sides[k] = pass_writes_sides(D.w[k], D.h[k]);
     }
     const int n_strips = (D.w[0] + ST_COLS / 2 - 1) / (ST_COLS / 2);
     const int band = stream_band(n_strips, D.h[0], n_img, c->n_cu);
     const int n_bands = (D.h[0] + band - 1) / band;
     const int n_units = n_strips * n_bands * n_img;
-    // the SKIP probe builds fold outputs into a per-wave trash line (a scratch
-    // buffer cannot grow inside a capture, so it is sized here)
+    *sides = stream_sides(n_units, c->n_cu);
+    // the SIDES instances' lanes without an output store to their wave's trash
+    // line: the kernel must not run without it (a scratch buffer cannot grow
+    // inside a capture)
     uint8_t* trash = (uint8_t*)scratch(c, "pyr_trash", (size_t)n_units * 256);
     if (!trash) return hipErrorOutOfMemory;
+    if (*sides)
+        return launch_timed(c, "pyramid", stream_kernel<NL, 0, 1, true>, dim3(N_XCD * xcd_per(n_units)), dim3(64),
+                            0, src, dst, lay.bytes, D, n_strips, n_bands, n_units, band, trash, c->pyr_order);
     if (c->pyr_wpb == 4)
         return launch_timed(c, "pyramid", stream_kernel<NL, 0, 4>, dim3(N_XCD * xcd_per((n_units + 3) / 4)),
                             dim3(256), 0, src, dst, lay.bytes, D, n_strips, n_bands, n_units, band, trash,
@@ -699,12 +793,15 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
     *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = ring_dword(rw, pcol, w);
 }
 
-// The rings of levels lo..hi the streaming pass left (ring_kernel).
-hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst) {
+// The rings of levels lo..hi the streaming pass left (ring_kernel); pass_sides:
+// the pass wrote the side bands of the levels pass_writes_sides names (none left).
+hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst,
+                        bool pass_sides) {
     RingLevels R{};
     int most = 0;
     for (int lv = lo; lv <= hi; ++lv) {
         const int w = lay.w[lv];
+        if (pass_sides && pass_writes_sides(w, lay.h[lv])) continue;
         const int k = R.n++;
         R.off[k] = lay.off[lv];
         R.pitch[k] = lay.pitch[lv];
@@ -802,11 +899,12 @@ hipError_t launch_build_pyramids(gvx_ctx* c, const uint8_t* src, int64_t img_str
         s.w = lay.w[l];
         s.h = lay.h[l];
         s.raw = l == 0 && raw;
-        const hipError_t e = nl == 3   ? launch_stream<3>(c, s, n_img, lay, l, dst)
-                             : nl == 2 ? launch_stream<2>(c, s, n_img, lay, l, dst)
-                                       : launch_stream<1>(c, s, n_img, lay, l, dst);
+        bool sides = false;
+        const hipError_t e = nl == 3   ? launch_stream<3>(c, s, n_img, lay, l, dst, &sides)
+                             : nl == 2 ? launch_stream<2>(c, s, n_img, lay, l, dst, &sides)
+                                       : launch_stream<1>(c, s, n_img, lay, l, dst, &sides);
         if (e != hipSuccess) return e;
-        const hipError_t er = launch_rings(c, n_img, lay, l + 1, l + nl, dst);
+        const hipError_t er = launch_rings(c, n_img, lay, l + 1, l + nl, dst, sides);
         if (er != hipSuccess) return er;
         l += nl;
     }
