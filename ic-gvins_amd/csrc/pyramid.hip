@@ -117,12 +117,17 @@ __device__ __forceinline__ uint2 hsum4(const uint32_t* row, int g) {
 // Vertical taps on packed u16 pairs: (a + 4b + 6c + 4d + e + 128) per half.
 // Every partial sum stays < 2^16 (inputs <= 4080, result <= 65408), so the two
 // halves never interact.
+// Five packed ops: the compiler's own form of the same sum takes six (it turns
+// the multiply by 4 into a shift and an add), so the two multiply-adds are
+// written out.
 __device__ __forceinline__ uint32_t vsum2(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
     typedef unsigned short v2u __attribute__((ext_vector_type(2)));
-    const v2u A = __builtin_bit_cast(v2u, a), B = __builtin_bit_cast(v2u, b), C = __builtin_bit_cast(v2u, c),
-              D = __builtin_bit_cast(v2u, d), E = __builtin_bit_cast(v2u, e);
-    const v2u r = A + E + (B + D) * (unsigned short)4 + C * (unsigned short)6 + (unsigned short)128;
-    return __builtin_bit_cast(uint32_t, r);
+    const uint32_t ae = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, a) + __builtin_bit_cast(v2u, e));
+    const uint32_t bd = __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, b) + __builtin_bit_cast(v2u, d));
+    uint32_t t, r;
+    asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(bd), "v"(ae));
+    asm("v_pk_mad_u16 %0, %1, 6, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(c), "v"(t));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, r) + (unsigned short)128);
 }
 // high bytes of the four u16 lanes of (lo, hi) = the (s + 128) >> 8 results
 __device__ __forceinline__ uint32_t hibytes(uint32_t lo, uint32_t hi) {
@@ -181,11 +186,14 @@ __device__ __forceinline__ int ring_col(int c, int w) {
     return (c >= 1 && c <= PAD) ? -c : (c >= w - 1 - PAD && c <= w - 2) ? 2 * w - 2 - c : 0;
 }
 
+// (bound_ctrl: a lane without a source lane reads 0, so no `old` operand has to
+// be zeroed first -- one v_mov_b32_dpp instead of two moves; every lane of the
+// pass is active)
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane L <- lane L-1
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
 }
 __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane L <- lane L+1
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
 }
 
 // Source of a pass: images [0, n_a) at a + i*img_stride, the rest at
@@ -266,10 +274,10 @@ __device__ __forceinline__ uint4 src_row16(int pitch, int h, int x, const Gather
 // Strip 0 of an unpadded source: level-1 columns -8..-1 (lanes 0, 1) are the
 // REFLECT_101 copies of columns 8..1 (lanes 2..4), taken with DPP row shifts.
 __device__ __forceinline__ uint32_t left_mirror_l1(uint32_t l1, int lane) {
-    const uint32_t s1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l1, 0x101, 0xf, 0xf, false);  // row_shl:1
-    const uint32_t s2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l1, 0x102, 0xf, 0xf, false);  // row_shl:2
+    const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)l1, 0x101, 0xf, 0xf, true);  // row_shl:1
+    const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)l1, 0x102, 0xf, 0xf, true);  // row_shl:2
     const uint32_t v = __builtin_amdgcn_perm(s2, s1, 0x01020304u);  // lane L: columns of lanes L+1, L+2 reversed
-    const uint32_t v2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x102, 0xf, 0xf, false);
+    const uint32_t v2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x102, 0xf, 0xf, true);
     return lane == 1 ? v : lane == 0 ? v2 : l1;
 }
 
