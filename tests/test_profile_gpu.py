@@ -23,16 +23,27 @@ def _with_profile(ctx, on, fn):
     return out, fams
 
 
-def test_klt_batch_profiled_launch_bits(ctx):
+@pytest.mark.parametrize("n_pts", [96, 1100])
+def test_klt_batch_profiled_launch_bits(ctx, n_pts):
+    """96 points a pair: one point per wave, the compaction inside the LK launch (no
+    compact launch); 1,100: three points per wave, a compact_kernel launch."""
     from gvx import synth
-    I, J, P, Q = synth.make_batch(4, 640, 280, 96, seed=synth.SEED, distinct=4)
+    I, J, P, Q = synth.make_batch(4, 640, 280, n_pts, seed=synth.SEED, distinct=4)
     off, _ = _with_profile(ctx, False, lambda: ctx.klt_fb_batch(I, J, P, Q))
     on, fams = _with_profile(ctx, True, lambda: ctx.klt_fb_batch(I, J, P, Q))
     for k in off:
+        if k == "kept":  # past n_kept: whatever the buffer held
+            for i in range(len(off["n_kept"])):
+                m = int(off["n_kept"][i])
+                assert np.array_equal(np.asarray(off[k][i][:m]), np.asarray(on[k][i][:m])), k
+            continue
         assert np.array_equal(np.asarray(off[k]), np.asarray(on[k])), k
-    for f in ("pyramid", "klt", "compact"):
+    fused = 4 * n_pts <= 4096
+    for f in ("pyramid", "klt") + (() if fused else ("compact",)):
         ms, n = fams[f]
         assert n >= 1 and ms > 0.0, (f, ms, n)
+    if fused:
+        assert fams["compact"][1] == 0
 
 
 def test_factor_kernels_profiled_launch_bits(ctx, gvx_mod):
