@@ -801,15 +801,66 @@ __global__ void __launch_bounds__(256) ring_kernel(uint8_t* __restrict__ pyr, in
     *reinterpret_cast<uint32_t*>(base + (int64_t)prow * pitch + pcol) = ring_dword(rw, pcol, w);
 }
 
-// The rings of levels lo..hi the streaming pass left (ring_kernel); pass_sides:
-// the pass wrote the side bands of the levels pass_writes_sides names (none left).
+// Side bands of levels whose rows (ring rows included) the pass wrote, w a
+// multiple of 4 and >= 36 (every side byte a single-bounce copy of an interior
+// byte): the 32 ring bytes of a (padded row, side) are the 32 interior bytes next
+// to the edge, reversed.  Eight lanes per (row, side), one output dword each: a
+// dword pair of the mirrored row and one v_perm with a fixed selector, so a wave
+// reads and writes 32-byte runs.  (ring_kernel's generic one-dword items took
+// 33 us for configs[1]'s 512 images, profiles/r06_m8; one lane per (row, side)
+// with 16-byte accesses was slower still, 64 rows per wave instruction.)
+struct SideLevels {
+    int32_t n;
+    int64_t off[3];
+    int32_t pitch[3], w[3], h[3];
+};
+__host__ __device__ inline bool side_fast(int w) { return (w & 3) == 0 && w >= 36; }
+// Grid (items, images, levels): the level is wave-uniform, so the buffer view is
+// an SGPR operand (a per-lane level would make every access a waterfall loop).
+__global__ void __launch_bounds__(256) side_kernel(uint8_t* __restrict__ pyr, int64_t pyr_bytes, SideLevels S) {
+    // a wave: 8 padded rows x 8 dwords of one side (the branch below is wave-uniform)
+    const int k = blockIdx.z;
+    const int t = blockIdx.x * 256 + threadIdx.x, q = t & 7, side = (t >> 6) & 1;
+    const int prow = (t >> 7) * 8 + ((t >> 3) & 7), w = S.w[k], h = S.h[k], pitch = S.pitch[k];
+    if (prow >= h + 2 * PAD) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        pyr + (int64_t)blockIdx.y * pyr_bytes + S.off[k], (short)0, (h + 2 * PAD) * pitch, 0x00020000);
+    const int so = (refl(prow - PAD, h) + PAD) * pitch, dof = prow * pitch;
+    typedef uint32_t v2u_t __attribute__((ext_vector_type(2)));
+    if (side == 0) {
+        // left: padded col 4q+b <- col 64-4q-b (D[t] = cols 32+4t .. 35+4t: D[8-q] byte 0,
+        // D[7-q] bytes 3, 2, 1)
+        const v2u_t d = __builtin_amdgcn_raw_buffer_load_b64(rs, so + PAD + 4 * (7 - q), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(d.y, d.x, 0x01020304u), rs, dof + 4 * q, 0, 0);
+    } else {
+        // right: padded col e+4q+b <- col e-2-4q-b, e = PAD + w (D[t] = dword (e-36)/4 + t:
+        // D[8-q] bytes 2, 1, 0, D[7-q] byte 3)
+        const int e = PAD + w;
+        const v2u_t d = __builtin_amdgcn_raw_buffer_load_b64(rs, so + e - 36 + 4 * (7 - q), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(d.x, d.y, 0x07000102u), rs, dof + e + 4 * q, 0,
+                                              0);
+    }
+}
+
+// The rings of levels lo..hi the streaming pass left (side_kernel, ring_kernel);
+// pass_sides: the pass wrote the side bands of the levels pass_writes_sides
+// names (none left).
 hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int hi, uint8_t* dst,
                         bool pass_sides) {
     RingLevels R{};
+    SideLevels S{};
     int most = 0;
     for (int lv = lo; lv <= hi; ++lv) {
         const int w = lay.w[lv];
         if (pass_sides && pass_writes_sides(w, lay.h[lv])) continue;
+        if (pass_writes_rows(lay.h[lv]) && side_fast(w) && S.n < 3) {
+            const int k = S.n++;
+            S.off[k] = lay.off[lv];
+            S.pitch[k] = lay.pitch[lv];
+            S.w[k] = w;
+            S.h[k] = lay.h[lv];
+            continue;
+        }
         const int k = R.n++;
         R.off[k] = lay.off[lv];
         R.pitch[k] = lay.pitch[lv];
@@ -822,6 +873,13 @@ hipError_t launch_rings(gvx_ctx* c, int n_img, const PyrLayout& lay, int lo, int
         R.items[k] = R.sides[k] ? (lay.h[lv] + 2 * PAD) * (PAD / 4 + R.rdn[k])
                                 : 2 * PAD * R.dw[k] + lay.h[lv] * (PAD / 4 + R.rdn[k]);
         most = R.items[k] > most ? R.items[k] : most;
+    }
+    if (S.n > 0) {
+        int most_s = 0;  // padded rows of the tallest level
+        for (int k = 0; k < S.n; ++k) most_s = std::max(most_s, S.h[k] + 2 * PAD);
+        const hipError_t e = launch_timed(c, "pyramid", side_kernel, dim3((128 * ((most_s + 7) / 8) + 255) / 256, n_img, S.n),
+                                          dim3(256), 0, dst, lay.bytes, S);
+        if (e != hipSuccess) return e;
     }
     if (R.n == 0) return hipSuccess;
     dim3 grid((most + 255) / 256, n_img, R.n);

@@ -7,6 +7,6 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -2 $O/tests.log
 timeout -k 10 60 ./tools/pyr_probe 40 q > $O/probe.txt 2>&1; head -4 $O/probe.txt
 V=$PWD/ic-gvins_amd/gvx/variants
-CFGS="head|GVX_LIB=$V/libgvx_head2.so|;tree||" bash tools/r06_ab.sh $TAG ${ROUNDS:-3}
+CFGS="head|GVX_LIB=$V/libgvx_head3.so|;tree||;head_nov|GVX_LIB=$V/libgvx_head3.so|--no-overlap --streams 1;tree_nov||--no-overlap --streams 1" bash tools/r06_ab.sh $TAG ${ROUNDS:-3}
 for f in gpurun_out/$TAG/b_*.json; do python3 -c "
 import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f'.split('/')[-1], d.get('single_pair',{}).get('us_per_pair_eager'), d.get('single_pair',{}).get('us_per_pair_graph'))"; done
