@@ -1,7 +1,7 @@
 """The headline's timed region in a rocprofv3 --kernel-trace of the driver's
 command (bench.py --steps K --warmup W, default line): the batch launches of
-stream_kernel (pyramid pass; since r06 followed by ring_kernel, the side
-bands), klt_kernel<3, 0> (LK) and compact_kernel in order, the timed K steps being the K after the LK side leg (28 exact-order
+stream_kernel (pyramid pass; since r06 followed by side_kernel / ring_kernel,
+the side bands), klt_kernel<3, 0> (LK) and compact_kernel in order, the timed K steps being the K after the LK side leg (28 exact-order
 steps), the settle leg (bench.SETTLE_STEPS) and the W warm-up steps.
 
 Prints per step: the span from the first timed pyramid pass's start to the last
@@ -18,7 +18,7 @@ SETTLE = 40
 path = sys.argv[1]
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-acc = {"stream_kernel": [], "ring_kernel": [], "klt_kernel<3, 0>": [], "compact_kernel": []}
+acc = {"stream_kernel": [], "side_kernel": [], "ring_kernel": [], "klt_kernel<3, 0>": [], "compact_kernel": []}
 rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
 for r in rows:
     for k in acc:
@@ -41,7 +41,8 @@ lo, hi = timed_lk[0][0], timed_lk[-1][1]
 w_last = lk[t0i - 1][0]
 pyr = [x for x in batch["stream_kernel"] if x[0] > w_last and x[1] <= hi]
 pyr = pyr[-K:]
-ring = [x for x in batch["ring_kernel"] if x[0] > w_last and x[1] <= hi][-K:]
+ring = [x for x in batch["ring_kernel"] if x[0] > w_last and x[1] <= hi][-K:] + \
+    [x for x in batch["side_kernel"] if x[0] > w_last and x[1] <= hi][-K:]
 cmp_ = [x for x in batch["compact_kernel"] if x[0] >= timed_lk[0][0]][:K]
 start = min(pyr[0][0], lo)
 end = max(hi, cmp_[-1][1])

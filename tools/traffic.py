@@ -19,7 +19,7 @@ from pmc_summary import load  # noqa: E402
 # pass and a ring pass ran beside it, which are counted when present); one LK
 # launch for fwd+bwd; one compaction.
 PER_STEP = {"stream_kernel": 1, "klt_kernel": 1, "compact_kernel": 1}
-OPTIONAL = {"edge_kernel": 1, "ring_kernel": 1}
+OPTIONAL = {"edge_kernel": 1, "ring_kernel": 1, "side_kernel": 1}  # r06: the side bands of large launches
 ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
 ap.add_argument("--workload", default="klt_fb_batch 256x1280x560 N150 L3")
