@@ -54,6 +54,7 @@ def test_bench_launch_bit_exact(ctx, orc, gvx_mod, w, h, n, L, mode):
     assert wl.n_pairs * n > 4096  # the batched (three / two points per wave) instance
     wl.N.fill_(np.nan)
     wl.NK.fill_(-1)
+    __import__("torch").cuda.synchronize()  # torch fills on its stream; gvx launches on its own
     wl.step(ctx, gvx_mod.KltParams.default(max_level=L, accum=mode))
     ctx.sync()
     nxt, back = wl.N.cpu().numpy(), wl.B.cpu().numpy()
@@ -126,6 +127,7 @@ def test_bench_launch_phases_same_bits(ctx, gvx_mod, w, h, n, L):
             wl.F.fill_(255)
             wl.K.fill_(-1)
             wl.NK.fill_(-1)
+            __import__("torch").cuda.synchronize()  # torch fills on its stream; gvx launches on its own
             wl.step(ctx, p)
             ctx.sync()
             got = [a.cpu().numpy() for a in (wl.N, wl.B, wl.F, wl.K, wl.NK)]

@@ -40,6 +40,7 @@ def _run(ctx, gvx_mod, frames, w, h, params=None, pitch=None, chan=1):
     src = torch.from_numpy(host).cuda()
     dst = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
     means = torch.zeros(n, dtype=torch.float64, device="cuda")
+    __import__("torch").cuda.synchronize()  # torch fills on its stream; gvx launches on its own
     ctx.clahe_batch_dev(n, w, h, src.data_ptr(), dst.data_ptr(), params=params, d_hist_mean=means.data_ptr(),
                         src_img_stride=h * pitch, src_stride=pitch)
     ctx.sync()

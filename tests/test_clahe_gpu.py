@@ -57,6 +57,7 @@ def test_clahe_batch_dev_strided_and_in_place(ctx, orc, gvx_mod):
     src = torch.from_numpy(host).cuda()
     dst = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
     means = torch.zeros(n, dtype=torch.float64, device="cuda")
+    __import__("torch").cuda.synchronize()  # torch fills on its stream; gvx launches on its own
     ctx.clahe_batch_dev(n, w, h, src.data_ptr(), dst.data_ptr(), d_hist_mean=means.data_ptr(),
                         src_img_stride=h * pitch, src_stride=pitch)
     ctx.sync()
@@ -157,6 +158,7 @@ def test_clahe_batch_dev_bgr(ctx, orc, gvx_mod):
     src = torch.from_numpy(np.stack(imgs)).cuda()
     dst = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
     means = torch.zeros(n, dtype=torch.float64, device="cuda")
+    __import__("torch").cuda.synchronize()  # torch fills on its stream; gvx launches on its own
     p = gvx_mod.ClaheParams.default(channels=3)
     ctx.clahe_batch_dev(n, w, h, src.data_ptr(), dst.data_ptr(), params=p, d_hist_mean=means.data_ptr(),
                         src_img_stride=3 * w * h, src_stride=3 * w)

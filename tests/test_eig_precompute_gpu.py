@@ -26,6 +26,7 @@ def _detect(ctx, gvx_mod, fid, pts_xy):
     n = torch.tensor([len(pts_xy)], dtype=torch.int32, device=dev)
     corners = torch.zeros((64 * 64, 2), dtype=torch.float32, device=dev)
     nc = torch.zeros(1, dtype=torch.int32, device=dev)
+    __import__("torch").cuda.synchronize()  # torch fills on its stream; gvx launches on its own
     ctx.track_frame_dev(fid, fid, False, pts.data_ptr(), vel.data_ptr(), init.data_ptr(), n.data_ptr(), N, W, H,
                         klt=kp, detect=dp, d_corners=corners.data_ptr(), d_n_corners=nc.data_ptr())
     ctx.sync()

@@ -16,10 +16,12 @@ def test_graph_replay_matches_eager(ctx, gvx_mod):
     dI, dJ, dP, dQ = (torch.from_numpy(a).to(dev) for a in (I, J, P, Q))
 
     def outputs():
-        return dict(N=torch.empty_like(dQ), B=torch.empty_like(dQ),
-                    F=torch.zeros((1, N), dtype=torch.uint8, device=dev),
-                    K=torch.full((1, N), -7, dtype=torch.int32, device=dev),
-                    NK=torch.full((1,), -7, dtype=torch.int32, device=dev))
+        o = dict(N=torch.empty_like(dQ), B=torch.empty_like(dQ),
+                 F=torch.zeros((1, N), dtype=torch.uint8, device=dev),
+                 K=torch.full((1, N), -7, dtype=torch.int32, device=dev),
+                 NK=torch.full((1,), -7, dtype=torch.int32, device=dev))
+        torch.cuda.synchronize()  # torch fills on its stream; gvx launches on its own
+        return o
 
     eager, replay = outputs(), outputs()
     params = gvx_mod.KltParams.default()
@@ -73,6 +75,7 @@ def test_stale_graph_refused(gvx_mod):
         d = {k: torch.from_numpy(a).to(dev) for k, a in zip("IJPQ", (I, J, P, Q))}
         d.update(N=d["Q"].clone(), B=torch.empty_like(d["Q"]), F=torch.zeros((n, N), dtype=torch.uint8, device=dev),
                  K=torch.zeros((n, N), dtype=torch.int32, device=dev), NK=torch.zeros((n,), dtype=torch.int32, device=dev))
+        torch.cuda.synchronize()  # torch fills on its stream; gvx launches on its own
         return d
 
     def enqueue(d, n):
