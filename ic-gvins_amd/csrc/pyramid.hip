@@ -163,8 +163,13 @@ __device__ __forceinline__ uint32_t hibytes(uint32_t lo, uint32_t hi) {
 //    lane, built with a DPP neighbour and a v_perm; levels 2 and 3: bytes).
 //    Levels narrower or shorter than RING_MIN take their ring from ring_kernel.
 constexpr int ST_COLS = 480;  // source columns owned per strip
+// Level-1 rows per band when the batch fills the chip.  72 (r06, profiles/r06_bd):
+// beside LK in the three-stream step, 72-96-row bands beat 40 by 1-2 % (fewer
+// warm-up rows, 6,144 instead of 10,752 waves at configs[1]), though the pass
+// alone is 5 % slower (0.169 against 0.161 ms); 140 loses (its long waves hold
+// LK out of the SIMDs).
 #ifndef STREAM_BAND
-#define STREAM_BAND 40
+#define STREAM_BAND 72
 #endif
 constexpr int BAND = STREAM_BAND;  // level-1 rows owned per band (level k: BAND >> (k-1))
 
