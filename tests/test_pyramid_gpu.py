@@ -91,7 +91,7 @@ def test_batched_pyramid_large_launch_bit_exact(ctx, orc, w, h, L, stride):
     ring_kernel (pyramid.hip stream_sides).  Enough images for that mode, three
     distinct ones tiled; the first three and the last are checked, rings included."""
     w1, h1 = (w + 1) // 2, (h + 1) // 2
-    units = -(-w1 // 240) * -(-h1 // 40)  # strips x 40-row bands per image
+    units = -(-w1 // 240) * -(-h1 // 72)  # strips x bands per image (pyramid.hip STREAM_BAND 72)
     n = max(3, -(-16 * 256 * 5 // 4 // units))  # 1.25x the large-launch threshold at 256 CUs
     rng = np.random.default_rng(w * 17 + h)
     base = np.stack([synth.make_image(w, h, rng) for _ in range(3)])
